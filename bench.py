@@ -1,0 +1,194 @@
+"""Benchmark of the DGPPO hot path on MI355X (driver contract: one JSON line from rank 0).
+
+Workload (BASELINE.json metric "env-steps/sec + PPO-updates/sec, LidarSpread n=8 x4096 envs"):
+LidarSpread, n=8 agents, 3 obstacles, 32 rays, 4096 parallel envs per GPU.  One bench "step" is
+one episode of the rollout hot path: env reset + T=128 fused env steps over all 4096 envs, with
+synthetic random actions already resident in HBM, writing the full (B, T+1) graph rollout buffer
+(the reference's `collect` minus the policy).  `value` = env transitions per second over all
+ranks.  Multi-GPU: envs are sharded (rank r owns envs [r*B, (r+1)*B)), no data-path collective —
+weak scaling.
+
+roofline: the dominant kernel is the env-step kernel (HBM-bound).  Algorithmic bytes per env
+transition = 8,856 B; per launch = 8,856 * 4096.  Its average duration is measured
+live with HIP events around back-to-back step launches on the launch stream.
+cpu_baseline: the NumPy oracle (oracle/env.py, single thread) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec + PPO-updates/sec, LidarSpread n=8 ×4096 envs, 1/2/4/8 GPU"
+ENV_ID, N_AGENTS, N_OBS, B_PER_GPU, T = "LidarSpread", 8, 3, 4096, 128
+BYTES_PER_ENV_STEP = 8856  # SURVEY.md §8(d), LidarSpread n8 O3
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def cpu_baseline(budget_s=12.0):
+    """NumPy oracle (1 thread, vectorised over envs) on a bounded sample of the same workload."""
+    from oracle import env as O
+
+    spec = O.Spec(ENV_ID, N_AGENTS, N_OBS)
+    Bs = 1024
+    ag, gl, third = O.env_reset(spec, 1, Bs)
+    g = O.initial_graph(spec, ag, gl, third)
+    rng = np.random.default_rng(0)
+    states = g["states"]
+    n_steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n_steps < T:
+        a = rng.uniform(-1, 1, (Bs, N_AGENTS, 2)).astype(np.float32)
+        out = O.env_step(spec, states, third, a)
+        states = out["states"]
+        n_steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(Bs * n_steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/env.py NumPy fp32, {Bs} envs x {n_steps} LidarSpread n=8 steps "
+                      f"({dt:.1f} s, reset excluded), 1 thread"}
+
+
+def read_pmc_traffic():
+    fn = os.path.join(ROOT, "profiles", "env_step_pmc.json")
+    if os.path.exists(fn):
+        try:
+            return json.load(open(fn)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dgppo_fov_amd.env import make_env
+    from dgppo_fov_amd.trainer.rollout import RolloutEngine
+
+    env = make_env(ENV_ID, N_AGENTS, num_obs=N_OBS, device=dev)
+    eng = RolloutEngine(env, B_PER_GPU, T, dev, env_offset=rank * B_PER_GPU)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    eng.actions.uniform_(-1.0, 1.0, generator=gen)  # synthetic actions, resident before timing
+    use_graph = not args.no_graph
+    if use_graph:
+        eng.capture()
+    for w in range(args.warmup):
+        eng.run(key=w)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        eng.run(key=10_000 + s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- live kernel timing for the roofline: back-to-back step launches on the launch stream ----
+    stream = torch.cuda.current_stream(dev)
+    n_launch = 4 * T
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g_step = None
+    cur = eng.graph_at(0)
+    outs = [eng.graph_at(1), eng.graph_at(2)]
+
+    def step_loop():
+        c = cur
+        for i in range(n_launch):
+            o = outs[i & 1]
+            c = env.step_into(c if i == 0 else outs[(i - 1) & 1], eng.actions[:, i % T], o, eng.rewards[:, i % T],
+                              eng.costs[:, i % T])
+
+    # ping-pong between two buffers: step i reads buffer (i-1)&1, writes i&1
+    step_loop()
+    torch.cuda.synchronize(dev)
+    if use_graph:
+        g_step = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_step):
+            step_loop()
+    kern_ms = []
+    for rep in range(3):
+        ev0.record(stream)
+        if g_step is not None:
+            g_step.replay()
+        else:
+            step_loop()
+        ev1.record(stream)
+        ev1.synchronize()
+        kern_ms.append(ev0.elapsed_time(ev1) / n_launch)
+    step_ms = float(np.median(kern_ms))
+
+    env_steps = args.steps * B_PER_GPU * T * world
+    value = env_steps / elapsed
+    bytes_per_launch = BYTES_PER_ENV_STEP * B_PER_GPU
+    achieved = bytes_per_launch / (step_ms * 1e-3) / 1e9
+    traffic = read_pmc_traffic()
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (Philox-sampled resets, uniform random actions in HBM)",
+            "config": {
+                "workload": f"{ENV_ID} n={N_AGENTS} obs={N_OBS} rays=32 top_k=8, {B_PER_GPU} envs/GPU, "
+                            f"1 step = reset + T={T} fused env steps into the (B,T+1) rollout buffer",
+                "env": ENV_ID, "num_agents": N_AGENTS, "n_obs": N_OBS, "n_env_per_gpu": B_PER_GPU, "T": T,
+                "hip_graph": use_graph, "parallelism": f"dp{world} (env-sharded, no collective)",
+            },
+            "env_step_kernel_us": round(step_ms * 1e3, 3),
+            "ppo_updates_per_s": None,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "env_step_kernel<LIDAR,SPREAD,4,256>",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": None if args.no_cpu_baseline or world > 1 else cpu_baseline(),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

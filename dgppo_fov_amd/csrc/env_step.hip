@@ -1,0 +1,882 @@
+// Fused env-step / env-reset kernels for gfx950 (MI355X): hot path (1) of DGPPO.
+//
+// One workgroup owns one environment for the whole transition, so every intermediate (agent
+// states, obstacle records, per-ray hit distances, sorted hits) lives in LDS and each env touches
+// HBM exactly once per input byte and once per output byte:
+//   read : current graph states (agents, goals, lidar hits / MPE obstacles), obstacle records,
+//          actions                                                       (~1 KB per env, n=8)
+//   write: next graph nodes, edges, states, receivers, senders, reward, cost (~8.4 KB per env)
+// The step is HBM-bound (~9 flop/B against a 20 flop/B fp32 ridge), so the design
+// goal is coalesced streaming stores: lane-contiguous dword stores for nodes/states/indices and
+// one dwordx4 store per edge row.
+//
+// Reference semantics (all in the reference's fp32 operation order, see include/dgppo_hip.h):
+//   dynamics     lidar_env/base.py:142-149, mpe/base.py:129-135, lidar_bicycle_target.py:92-111
+//   lidar        env/utils.py:49-79 (get_lidar), 115-136 (raytracing), env/obstacle.py:62-105
+//   reward       lidar_spread.py:35-52, lidar_target.py:35-52, mpe_spread.py:32-49, mpe_target.py:32-49
+//   cost         lidar_env/base.py:180-207, mpe/base.py:164-191
+//   graph        lidar_env/base.py:227-271, mpe/base.py:211-241, utils/graph.py:35-44, 212-247
+//   reset        lidar_env/base.py:89-124, lidar_bicycle_target.py:60-90, mpe/base.py:81-127,
+//                env/utils.py:139-244
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dgppo_hip.h"
+#include "math32.h"
+
+#pragma clang fp contract(off)
+
+namespace dgppo {
+
+constexpr int kMaxAgents = 64;
+constexpr int kMaxObs = 16;
+constexpr int kMaxRays = 128;
+
+__device__ __forceinline__ float clampf_nan(float x, float lo, float hi) {
+  // jnp.clip = minimum(maximum(x, lo), hi): NaN propagates (v_max/v_min_f32 would drop it)
+  x = x < lo ? lo : x;
+  return x > hi ? hi : x;
+}
+__device__ __forceinline__ float min_nan(float a, float b) {
+  // jnp.min / jnp.minimum semantics: NaN wins
+  return (a != a || a < b) ? a : b;
+}
+__device__ __forceinline__ float norm2(float dx, float dy) { return sqrtf(dx * dx + dy * dy); }
+
+// ---- LDS carve (floats) -------------------------------------------------------------------------
+struct Carve {
+  int cur, curhit, obst, evec, act, nxt, alpha, hpt, hits, isin, red, samp, dist, total;
+  __host__ __device__ Carve(int n, int sd, int O, int R, int k, bool lidar) {
+    int off = 0;
+    auto take = [&](int nf) { int o = off; off += (nf + 3) & ~3; return o; };
+    cur = take(2 * n * sd + (lidar ? 0 : O * sd));  // agents, goals (+ MPE obstacle rows)
+    curhit = take(lidar ? n * k * 2 : 0);
+    obst = take(lidar ? O * DGPPO_OBST_FIELDS : 0);
+    evec = take(lidar ? O * 8 : 0);
+    act = take(n * 2);
+    nxt = take(n * sd);
+    alpha = take(lidar ? n * R * 2 : 0);  // 64-bit sort keys
+    hpt = take(lidar ? n * R * 2 : 0);
+    hits = take(lidar ? n * k * 2 : 0);
+    isin = take(n);
+    red = take(5 * n);  // d2goal, far, |a|^2, cost0, cost1
+    samp = take(4 * n);  // reset: sampled positions / goals (n, 2) each
+    dist = take(2 * n * n + n * (k > O ? k : O));  // step: pairwise distance tasks
+    total = off;
+  }
+};
+
+// Sizes: compile-time where a specialisation fixes them (0 / -1 = read from cfg at run time)
+template <int NA, int NO, int NR, int NK>
+struct Dims {
+  int n, O, R, k;
+  __device__ __forceinline__ explicit Dims(const dgppo_env_cfg& c)
+      : n(NA > 0 ? NA : c.n_agents), O(NO >= 0 ? NO : c.n_obs), R(NR > 0 ? NR : c.n_rays), k(NK > 0 ? NK : c.top_k) {}
+};
+
+struct GraphOut {
+  float* nodes;
+  float* edges;
+  float* states;
+  int32_t* recv;
+  int32_t* send;
+};
+
+// ---- Rectangle helpers (env/obstacle.py) ------------------------------------------------------
+__device__ __forceinline__ bool rect_inside(const float* rec, float px, float py, float r) {
+  const float rel_x = px - rec[0];
+  const float rel_y = py - rec[1];
+  const float c = rec[5], s = rec[6];
+  const float rel_xx = fabsf(rel_x * c + rel_y * s) - rec[2] / 2.0f;
+  const float rel_yy = fabsf(rel_x * s - rel_y * c) - rec[3] / 2.0f;
+  const bool down = (rel_xx < r) && (rel_yy < 0.0f);
+  const bool up = (rel_xx < 0.0f) && (rel_yy < r);
+  const bool corner = (rel_xx > 0.0f) && (rel_yy > 0.0f);
+  const bool circle = sqrtf(rel_xx * rel_xx + rel_yy * rel_yy) < r;
+  return down || up || (corner && circle);
+}
+
+// Rectangle.raytracing for one ray against the 4 edges of one obstacle.
+//
+// Exactly the reference's result, with most IEEE divisions skipped: an edge whose alpha or beta is
+// PROVABLY outside [0, 1] contributes exactly 1e6 in the reference (valid = 0 -> 0*alpha + 1e6), so
+// for it we only need the numerators and det, not the quotients.  The screens below are
+// conservative (1.001 margin on the ratio, 1e-30 floor against underflow to -0, finite numerators
+// only); everything else -- including det == 0 and NaN inputs, which make the reference's alpha NaN --
+// takes the full divide-and-compare path.  The per-ray terms ax = x1-x2, ay = y1-y2 and per-edge
+// vectors (x4-x3, y4-y3) are exactly the reference's sub-expressions, hoisted.
+__device__ __forceinline__ float rect_raytrace(const float* rec, const float* evec, float x1, float y1, float ax,
+                                               float ay) {
+  float best = 0.0f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x3 = rec[8 + 2 * e], y3 = rec[9 + 2 * e];
+    const float exe = evec[2 * e], eye = evec[2 * e + 1];  // x4 - x3, y4 - y3
+    const float px = x1 - x3, py = y1 - y3;
+    const float det = ax * eye - ay * exe;
+    const float na = eye * px - exe * py;
+    const float nb = (-ay) * px + ax * py;
+    const float adet = fabsf(det);
+    float a;
+    if (!(adet > 0.0f)) {
+      a = __builtin_nanf("");  // det == 0 (sign 0) or NaN: the reference's alpha is NaN
+    } else {
+      const float cl = adet < 1e-7f ? 1e-7f : (adet > 1e7f ? 1e7f : adet);
+      const float detc = det < 0.0f ? -cl : cl;
+      const float lim = cl * 1.001f;
+      const float ana = fabsf(na), anb = fabsf(nb);
+      const bool finite = ana <= 3.0e38f && anb <= 3.0e38f;
+      const bool neg_d = detc < 0.0f;
+      const bool out = finite && (ana > lim || anb > lim || (ana >= 1e-30f && ((na < 0.0f) != neg_d)) ||
+                                  (anb >= 1e-30f && ((nb < 0.0f) != neg_d)));
+      if (out) {
+        a = 1e6f;
+      } else {
+        const float alpha = na / detc;
+        const float beta = nb / detc;
+        const bool valid = (alpha <= 1.0f) && (alpha >= 0.0f) && (beta <= 1.0f) && (beta >= 0.0f);
+        a = valid ? alpha + 0.0f : (alpha != alpha ? alpha : 1e6f);
+      }
+    }
+    best = e == 0 ? a : min_nan(best, a);
+  }
+  return best;
+}
+
+// ---- graph writer: nxt (agents), goal rows, hits / obstacle rows, all in LDS ------------------
+template <int ENGINE, int GOAL, int SD, class D>
+__device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d, const float* nxt,
+                                            const float* goal, const float* third, GraphOut out, bool edges_vec4,
+                                            int tid, int nthr) {
+  constexpr int ND = SD + 3;
+  constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
+  const int n = d.n, O = d.O, k = d.k;
+  const int n_third = mpe ? O : (O > 0 ? n * k : 0);
+  const int N = 2 * n + n_third + 1;
+  const int n_ag = GOAL == DGPPO_GOAL_SPREAD ? n * n : n;
+  const int E = n * n + n_ag + (mpe ? n * O : n_third);
+  const int pad = N - 1;
+  const float comm = cfg.comm_radius;
+
+  // nodes (N, ND): [state | obs, goal, agent one-hot]; lidar hit rows carry [hx, hy, 0...]
+#pragma unroll 1
+  for (int idx = tid; idx < N * ND; idx += nthr) {
+    const int r = idx / ND;
+    const int c = idx - r * ND;
+    float v = 0.0f;
+    if (r < n) {
+      v = c < SD ? nxt[r * SD + c] : (c == SD + 2 ? 1.0f : 0.0f);
+    } else if (r < 2 * n) {
+      v = c < SD ? goal[(r - n) * SD + c] : (c == SD + 1 ? 1.0f : 0.0f);
+    } else if (r < 2 * n + n_third) {
+      const int h = r - 2 * n;
+      if (mpe) v = c < SD ? third[h * SD + c] : (c == SD ? 1.0f : 0.0f);
+      else v = c < 2 ? third[h * 2 + c] : (c == SD ? 1.0f : 0.0f);
+    }
+    out.nodes[idx] = v;
+  }
+  // states (N, SD); pad row is -1
+#pragma unroll 1
+  for (int idx = tid; idx < N * SD; idx += nthr) {
+    const int r = idx / SD;
+    const int c = idx - r * SD;
+    float v;
+    if (r < n) v = nxt[r * SD + c];
+    else if (r < 2 * n) v = goal[(r - n) * SD + c];
+    else if (r < 2 * n + n_third) {
+      const int h = r - 2 * n;
+      v = mpe ? third[h * SD + c] : (c < 2 ? third[h * 2 + c] : 0.0f);
+    } else v = -1.0f;
+    out.states[idx] = v;
+  }
+  // edges: [agent-agent n*n][agent-goal][agent-lidar n*k | agent-obstacle n*O]
+  const int n_aa = n * n;
+#pragma unroll 1
+  for (int e = tid; e < E; e += nthr) {
+    float f0, f1, f2, f3;
+    int rv, sv;
+    if (e < n_aa) {
+      const int i = e / n, j = e - (e / n) * n;
+      const float* si = nxt + i * SD;
+      const float* sj = nxt + j * SD;
+      if (ENGINE == DGPPO_ENGINE_BICYCLE) {  // state2feat = [x, y, v cos, v sin]
+        f0 = si[0] - sj[0];
+        f1 = si[1] - sj[1];
+        f2 = si[4] * si[2] - sj[4] * sj[2];
+        f3 = si[4] * si[3] - sj[4] * sj[3];
+      } else {
+        f0 = si[0] - sj[0];
+        f1 = si[1] - sj[1];
+        f2 = si[2] - sj[2];
+        f3 = si[3] - sj[3];
+      }
+      float d = norm2(si[0] - sj[0], si[1] - sj[1]);
+      if (i == j) d = d + cfg.c_self_dist;
+      const bool m = d < comm;
+      rv = m ? i : pad;
+      sv = m ? j : pad;
+    } else if (e < n_aa + n_ag) {
+      const int q = e - n_aa;
+      int i, j;
+      if (GOAL == DGPPO_GOAL_SPREAD) {
+        i = q / n;
+        j = q - i * n;
+      } else {
+        i = q;
+        j = q;
+      }
+      const float* si = nxt + i * SD;
+      const float* gj = goal + j * SD;
+      if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+        f0 = si[0] - gj[0];
+        f1 = si[1] - gj[1];
+        f2 = si[4] * si[2] - gj[4] * gj[2];
+        f3 = si[4] * si[3] - gj[4] * gj[3];
+      } else {
+        f0 = si[0] - gj[0];
+        f1 = si[1] - gj[1];
+        f2 = si[2] - gj[2];
+        f3 = si[3] - gj[3];
+      }
+      rv = i;
+      sv = n + j;
+    } else {
+      const int q = e - n_aa - n_ag;
+      if (mpe) {  // agent-obstacle block (n, O), mask ||p_i - o|| < comm_radius
+        const int i = q / O, o = q - (q / O) * O;
+        const float* si = nxt + i * SD;
+        const float* so = third + o * SD;
+        f0 = si[0] - so[0];
+        f1 = si[1] - so[1];
+        f2 = si[2] - so[2];
+        f3 = si[3] - so[3];
+        const bool m = norm2(si[0] - so[0], si[1] - so[1]) < comm;
+        rv = m ? i : pad;
+        sv = m ? 2 * n + o : pad;
+      } else {  // agent-lidar blocks (1, k) per agent, mask ||p_i - hit|| < comm_radius - 0.1
+        const int i = q / k, h = q - (q / k) * k;
+        const float* si = nxt + i * SD;
+        f0 = si[0] - third[(i * k + h) * 2 + 0];
+        f1 = si[1] - third[(i * k + h) * 2 + 1];
+        f2 = 0.0f;
+        f3 = 0.0f;
+        const bool m = norm2(f0, f1) < cfg.c_lidar_active;
+        rv = m ? i : pad;
+        sv = m ? 2 * n + i * k + h : pad;
+      }
+    }
+    if (edges_vec4) {
+      reinterpret_cast<float4*>(out.edges)[e] = make_float4(f0, f1, f2, f3);
+    } else {
+      out.edges[4 * e + 0] = f0;
+      out.edges[4 * e + 1] = f1;
+      out.edges[4 * e + 2] = f2;
+      out.edges[4 * e + 3] = f3;
+    }
+    out.recv[e] = rv;
+    out.send[e] = sv;
+  }
+}
+
+// ---- lidar: per-ray hit distance, then a stable NaN-last rank -> top-k hits -------------------
+// jnp.argsort (stable, NaN last, -0 == +0) as one 64-bit key per ray: high word = the alpha bits
+// mapped to an unsigned total order (every NaN -> 0xFFFFFFFF, -0 -> +0), low word = ray index.
+__device__ __forceinline__ uint64_t sort_key(float a, int r) {
+  uint32_t u = __float_as_uint(a + 0.0f);  // -0 -> +0
+  uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  if (a != a) ord = 0xFFFFFFFFu;
+  return ((uint64_t)ord << 32) | (uint32_t)r;
+}
+
+template <int SD, class D>
+__device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, float* lds, const Carve& cv, int tid,
+                                           int nthr) {
+  const int n = d.n, R = d.R, k = d.k, O = d.O;
+  const float* nxt = lds + cv.nxt;
+  const float* obst = lds + cv.obst;
+  const float* evec = lds + cv.evec;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(lds + cv.alpha);
+  float* hpt = lds + cv.hpt;
+#pragma unroll 1
+  for (int p = tid; p < n * R; p += nthr) {
+    asm volatile("" ::: "memory");  // keep obstacle LDS reads inside the loop (no LICM register blow-up)
+    const int i = p / R, r = p - (p / R) * R;
+    const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
+    const float ex = sx + ray_dirs[2 * r + 0];
+    const float ey = sy + ray_dirs[2 * r + 1];
+    const float ax = sx - ex, ay = sy - ey;
+    float a = 0.0f;
+    for (int o = 0; o < O; ++o) {
+      const float ao = rect_raytrace(obst + o * DGPPO_OBST_FIELDS, evec + o * 8, sx, sy, ax, ay);
+      a = o == 0 ? ao : min_nan(a, ao);
+    }
+    a = a * (1.0f - lds[cv.isin + i]);
+    keys[p] = sort_key(a, r);
+    hpt[2 * p + 0] = sx + (ex - sx) * a;
+    hpt[2 * p + 1] = sy + (ey - sy) * a;
+  }
+  __syncthreads();
+  float* hits = lds + cv.hits;
+#pragma unroll 1
+  for (int p = tid; p < n * R; p += nthr) {
+    const int i = p / R;
+    const uint64_t key = keys[p];
+    const uint64_t* row = keys + i * R;
+    int rank = 0;
+#pragma unroll 8
+    for (int j = 0; j < R; ++j) rank += row[j] < key ? 1 : 0;
+    if (rank < k) {
+      hits[(i * k + rank) * 2 + 0] = hpt[2 * p + 0];
+      hits[(i * k + rank) * 2 + 1] = hpt[2 * p + 1];
+    }
+  }
+}
+
+// per-obstacle edge vectors (x4 - x3, y4 - y3) of Rectangle.raytracing, e -> points[e-1] - points[e]
+__device__ __forceinline__ void stage_edge_vectors(int O, float* lds, const Carve& cv, int tid, int nthr) {
+  for (int q = tid; q < O * 8; q += nthr) {
+    const int o = q >> 3, e = (q >> 1) & 3, c = q & 1;
+    const float* rec = lds + cv.obst + o * DGPPO_OBST_FIELDS;
+    const int e4 = (e + 3) & 3;
+    lds[cv.evec + q] = rec[8 + 2 * e4 + c] - rec[8 + 2 * e + c];
+  }
+}
+
+__device__ __forceinline__ void agent_is_inside(int O, float* lds, const Carve& cv, int SD, int i) {
+  const float* obst = lds + cv.obst;
+  const float px = lds[cv.nxt + i * SD + 0], py = lds[cv.nxt + i * SD + 1];
+  bool in = false;
+  for (int o = 0; o < O; ++o) in = in || rect_inside(obst + o * DGPPO_OBST_FIELDS, px, py, 0.0f);
+  lds[cv.isin + i] = in ? 1.0f : 0.0f;
+}
+
+// ---- the step kernel --------------------------------------------------------------------------
+// Phases (one barrier each), every phase spread over the whole workgroup:
+//   A  stage current rows, obstacles, clipped actions in LDS
+//   B  task list: per-agent dynamics + |a|^2, and one pairwise distance per lane (agent-agent,
+//      goal-agent, agent-hit / agent-obstacle) on the pre-step graph
+//   C  per-agent row minima -> cost and reward terms; is-inside on the next state
+//   D  reward/cost stores, ray cast of the next state (keys + hit points), stable rank -> top-k
+//   E  stream the next graph out
+template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
+__global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
+  const Dims<NA, NO, NR, NK> d(cfg);
+  const int n = d.n, O = d.O, k = d.k;
+  const bool lidar = !mpe && O > 0;
+  const Carve cv(n, SD, O, d.R, k, !mpe);
+  const int tid = threadIdx.x;
+  const int64_t env = blockIdx.x;
+
+  // ---- A ------------------------------------------------------------------------------------
+  const float* st = io.states + env * io.states_stride;
+  const int n_cur = (2 * n + (mpe ? O : 0)) * SD;  // type_states(0), (1) [, (2) for MPE]
+  for (int idx = tid; idx < n_cur; idx += BLOCK) lds[cv.cur + idx] = st[idx];
+  if (lidar) {
+    for (int idx = tid; idx < n * k * 2; idx += BLOCK) {  // type_states(2)[:, :2] = current hits
+      const int h = idx >> 1, c = idx & 1;
+      lds[cv.curhit + idx] = st[(2 * n + h) * SD + c];
+    }
+    const float* ob = io.obstacles + env * io.obstacles_stride;
+    for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) lds[cv.obst + idx] = ob[idx];
+  }
+  const float* ac = io.action + env * io.action_stride;
+  for (int idx = tid; idx < 2 * n; idx += BLOCK) lds[cv.act + idx] = clampf_nan(ac[idx], -1.0f, 1.0f);
+  __syncthreads();
+
+  // ---- B ------------------------------------------------------------------------------------
+  const float* cur = lds + cv.cur;
+  const float* goal = lds + cv.cur + n * SD;
+  float* dist = lds + cv.dist;
+  const int n_aa = n * n;
+  const int n_ga = GOAL == DGPPO_GOAL_SPREAD ? n * n : n;
+  const int n_t3 = lidar ? n * k : (mpe ? n * O : 0);
+  const int n_task = n + n_aa + n_ga + n_t3;
+#pragma unroll 1
+  for (int q = tid; q < n_task; q += BLOCK) {
+    if (q < n) {  // dynamics (lidar_env/base.py:142-149 / bicycle 92-111), then clip_state
+      const int i = q;
+      const float* x = cur + i * SD;
+      const float* a = lds + cv.act + 2 * i;
+      float y[SD];
+      if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+        const float theta = atan2_32(x[3], x[2]);
+        const float theta_next = theta + ((x[4] * a[0]) * cfg.dt) * 10.0f;
+        float st_, ct_, sn_, cn_;
+        sincos32(theta, &st_, &ct_);
+        sincos32(theta_next, &sn_, &cn_);
+        y[0] = x[0] + (x[4] * ct_) * cfg.dt;
+        y[1] = x[1] + (x[4] * st_) * cfg.dt;
+        y[2] = cn_;
+        y[3] = sn_;
+        y[4] = x[4] + (a[1] * cfg.dt) * 10.0f;
+      } else {
+        y[0] = x[2] * cfg.dt + x[0];
+        y[1] = x[3] * cfg.dt + x[1];
+        y[2] = (a[0] * 10.0f) * cfg.dt + x[2];
+        y[3] = (a[1] * 10.0f) * cfg.dt + x[3];
+      }
+#pragma unroll
+      for (int c = 0; c < SD; ++c) lds[cv.nxt + i * SD + c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+      const float an = norm2(a[0], a[1]);
+      lds[cv.red + 2 * n + i] = an * an;
+      continue;
+    }
+    int t = q - n;
+    if (t < n_aa) {  // agent-agent distance with the eye * 1e6 diagonal (lidar_env/base.py:185-187)
+      const int i = t / n, j = t - (t / n) * n;
+      float dj = norm2(cur[i * SD] - cur[j * SD], cur[i * SD + 1] - cur[j * SD + 1]);
+      if (i == j) dj = dj + 1e6f;
+      dist[t] = dj;
+      continue;
+    }
+    t -= n_aa;
+    if (t < n_ga) {  // goal j to agent i (spread, goal-major) or own goal (target)
+      int gj, ai;
+      if (GOAL == DGPPO_GOAL_SPREAD) {
+        gj = t / n;
+        ai = t - gj * n;
+      } else {
+        gj = t;
+        ai = t;
+      }
+      dist[n_aa + t] = norm2(goal[gj * SD] - cur[ai * SD], goal[gj * SD + 1] - cur[ai * SD + 1]);
+      continue;
+    }
+    t -= n_ga;
+    if (lidar) {  // current hit h of agent i: ||hit - p_i|| (lidar_env/base.py:194-197)
+      const int i = t / k;
+      const float* hc = lds + cv.curhit + 2 * t;
+      dist[2 * n_aa + t] = norm2(hc[0] - cur[i * SD], hc[1] - cur[i * SD + 1]);
+    } else {  // MPE: ||p_i - o|| (mpe/base.py:179-181)
+      const int i = t / O, o = t - (t / O) * O;
+      const float* ob = cur + 2 * n * SD + o * SD;
+      dist[2 * n_aa + t] = norm2(cur[i * SD] - ob[0], cur[i * SD + 1] - ob[1]);
+    }
+  }
+  if (lidar) stage_edge_vectors(O, lds, cv, tid, BLOCK);
+  __syncthreads();
+
+  // ---- C ------------------------------------------------------------------------------------
+  for (int i = tid; i < n; i += BLOCK) {
+    float md = dist[i * n];
+    for (int j = 1; j < n; ++j) md = min_nan(md, dist[i * n + j]);
+    float dg;
+    if (GOAL == DGPPO_GOAL_SPREAD) {  // goal i's nearest agent
+      dg = dist[n_aa + i * n];
+      for (int j = 1; j < n; ++j) dg = min_nan(dg, dist[n_aa + i * n + j]);
+    } else {
+      dg = dist[n_aa + i];
+    }
+    lds[cv.red + i] = dg;
+    lds[cv.red + n + i] = dg > cfg.dist2goal ? 1.0f : 0.0f;
+    float c0 = cfg.c_agent_cost - md;
+    float c1 = 0.0f;
+    const int m3 = lidar ? k : (mpe ? O : 0);
+    if (m3 > 0) {
+      const float* row = dist + 2 * n_aa + i * m3;
+      float mo = row[0];
+      for (int h = 1; h < m3; ++h) mo = min_nan(mo, row[h]);
+      c1 = cfg.c_obs_cost - mo;
+    }
+    c0 = c0 <= 0.0f ? c0 - 0.5f : c0 + 0.5f;
+    c1 = c1 <= 0.0f ? c1 - 0.5f : c1 + 0.5f;
+    if (mpe) {  // jnp.clip(cost, a_min=-1.0)
+      c0 = c0 < -1.0f ? -1.0f : c0;
+      c1 = c1 < -1.0f ? -1.0f : c1;
+    } else {
+      c0 = clampf_nan(c0, -1.0f, 1.0f);
+      c1 = clampf_nan(c1, -1.0f, 1.0f);
+    }
+    lds[cv.red + 3 * n + i] = c0;
+    lds[cv.red + 4 * n + i] = c1;
+    if (lidar) agent_is_inside(O, lds, cv, SD, i);
+  }
+  __syncthreads();
+
+  // ---- D ------------------------------------------------------------------------------------
+  if (tid == 0) {
+    float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
+    for (int i = 0; i < n; ++i) {
+      sd_ = sd_ + lds[cv.red + i];
+      sf = sf + lds[cv.red + n + i];
+      sa = sa + lds[cv.red + 2 * n + i];
+    }
+    const float nn = (float)n;
+    float r = 0.0f - (sd_ / nn) * 0.01f;
+    r = r - (sf / nn) * 0.001f;
+    r = r - (sa / nn) * 0.0001f;
+    io.reward[env * io.reward_stride] = r;
+  }
+  for (int idx = tid; idx < 2 * n; idx += BLOCK) {
+    const int i = idx >> 1, h = idx & 1;
+    io.cost[env * io.cost_stride + idx] = lds[cv.red + (3 + h) * n + i];
+  }
+  if (lidar) {
+    lidar_scan<SD>(d, io.ray_dirs, lds, cv, tid, BLOCK);
+    __syncthreads();
+  }
+
+  // ---- E ------------------------------------------------------------------------------------
+  GraphOut out;
+  out.nodes = io.nodes + env * io.nodes_stride;
+  out.edges = io.edges + env * io.edges_stride;
+  out.states = io.out_states + env * io.out_states_stride;
+  out.recv = io.receivers + env * io.edge_index_stride;
+  out.send = io.senders + env * io.edge_index_stride;
+  const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
+  const float* third = mpe ? cur + 2 * n * SD : lds + cv.hits;
+  write_graph<ENGINE, GOAL, SD>(cfg, d, lds + cv.nxt, goal, third, out, vec4, tid, BLOCK);
+}
+
+// ---- reset ------------------------------------------------------------------------------------
+// Thread 0 runs the reference's sequential rejection sampler for its env (reset is once per
+// episode, amortised over T = 128 steps); then the whole workgroup ray-casts and writes the graph.
+__device__ bool inside_any(const float* obst, int O, float px, float py, float r) {
+  bool in = false;
+  for (int o = 0; o < O; ++o) in = in || rect_inside(obst + o * DGPPO_OBST_FIELDS, px, py, r);
+  return in;
+}
+
+__device__ void make_rectangle(float* rec, float cx, float cy, float w, float h, float th) {
+  float s, c;
+  sincos32(th, &s, &c);
+  const float hw = w / 2.0f, hh = h / 2.0f;
+  const float bx[4] = {hw, -hw, -hw, hw};
+  const float by[4] = {hh, hh, -hh, -hh};
+  rec[0] = cx;
+  rec[1] = cy;
+  rec[2] = w;
+  rec[3] = h;
+  rec[4] = th;
+  rec[5] = c;
+  rec[6] = s;
+  rec[7] = 0.0f;
+  for (int p = 0; p < 4; ++p) {
+    rec[8 + 2 * p] = (c * bx[p] + (-s) * by[p]) + cx;
+    rec[9 + 2 * p] = (s * bx[p] + c * by[p]) + cy;
+  }
+}
+
+// get_node_goal_rng (env/utils.py:139-244), dim 2, max_travel None; pos/goal are (n, 2) in LDS
+__device__ void node_goal_rng(Rng& rng, float side, int n, float min_dist, float r_in, const float* obst, int O,
+                              float* pos, float* gl) {
+  constexpr int kMaxIter = 1024;
+  for (int i = 0; i < 2 * n; ++i) {
+    pos[i] = 0.0f;
+    gl[i] = 0.0f;
+  }
+  int agent_id = 0;
+  while (agent_id < n) {
+    float cx = rng.uniform(0.0f, side), cy = rng.uniform(0.0f, side);
+    int it = 0;
+    for (;;) {
+      float dmin = 0.0f;
+      for (int j = 0; j < n; ++j) {
+        const float d = norm2(pos[2 * j] - cx, pos[2 * j + 1] - cy);
+        dmin = j == 0 ? d : min_nan(dmin, d);
+      }
+      const bool collide = dmin <= min_dist;
+      const bool in = inside_any(obst, O, cx, cy, r_in);
+      if (!(collide || in) || it >= kMaxIter) break;
+      ++it;
+      cx = rng.uniform(0.0f, side);
+      cy = rng.uniform(0.0f, side);
+    }
+    const int it_agent = it;
+    pos[2 * agent_id] = cx;
+    pos[2 * agent_id + 1] = cy;
+    float gx = rng.uniform(0.0f, side), gy = rng.uniform(0.0f, side);
+    it = 0;
+    for (;;) {
+      float dmin = 0.0f;
+      for (int j = 0; j < n; ++j) {
+        const float d = norm2(gl[2 * j] - gx, gl[2 * j + 1] - gy);
+        dmin = j == 0 ? d : min_nan(dmin, d);
+      }
+      const bool collide = dmin <= min_dist;
+      const bool in = inside_any(obst, O, gx, gy, r_in);
+      const bool outside = gx < 0.0f || gy < 0.0f || gx > side || gy > side;
+      if (!(collide || in || outside) || it >= kMaxIter) break;
+      ++it;
+      gx = rng.uniform(0.0f, side);
+      gy = rng.uniform(0.0f, side);
+    }
+    gl[2 * agent_id] = gx;
+    gl[2 * agent_id + 1] = gy;
+    ++agent_id;
+    if (it_agent >= kMaxIter || it >= kMaxIter) {  // no solution: start over (utils.py:229-232)
+      agent_id = 0;
+      for (int i = 0; i < 2 * n; ++i) {
+        pos[i] = 0.0f;
+        gl[i] = 0.0f;
+      }
+    }
+  }
+}
+
+template <int ENGINE, int GOAL, int SD, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgppo_env_reset_io io) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const bool mpe = ENGINE == DGPPO_ENGINE_MPE;
+  const Dims<0, -1, 0, 0> d(cfg);
+  const int n = d.n, O = d.O, k = d.k;
+  const bool lidar = !mpe && O > 0;
+  const Carve cv(n, SD, O, cfg.n_rays, k, !mpe);
+  const int tid = threadIdx.x;
+  const int64_t env = blockIdx.x;
+  float* nxt = lds + cv.nxt;            // sampled agent states
+  float* goal = lds + cv.cur + n * SD;  // sampled goal states
+  float* third = lds + cv.cur + 2 * n * SD;  // MPE obstacle states
+  float* obst = lds + cv.obst;
+  if (tid == 0) {
+    Rng rng(io.seed_ptr ? *io.seed_ptr : io.seed, (uint32_t)(io.env_offset + env));
+    const float area = cfg.area_size;
+    float* pos = lds + cv.samp;
+    float* gl = pos + 2 * n;
+    if (!mpe && O > 0) {
+      float tmp[4 * kMaxObs + kMaxObs];
+      for (int o = 0; o < O; ++o) {
+        tmp[2 * o] = rng.uniform(0.0f, area);
+        tmp[2 * o + 1] = rng.uniform(0.0f, area);
+      }
+      for (int o = 0; o < O; ++o) {
+        tmp[2 * O + 2 * o] = rng.uniform(cfg.obs_len_lo, cfg.obs_len_hi);
+        tmp[2 * O + 2 * o + 1] = rng.uniform(cfg.obs_len_lo, cfg.obs_len_hi);
+      }
+      for (int o = 0; o < O; ++o) tmp[4 * O + o] = rng.uniform(cfg.obs_theta_lo, cfg.obs_theta_hi);
+      for (int o = 0; o < O; ++o)
+        make_rectangle(obst + o * DGPPO_OBST_FIELDS, tmp[2 * o], tmp[2 * o + 1], tmp[2 * O + 2 * o],
+                       tmp[2 * O + 2 * o + 1], tmp[4 * O + o]);
+    }
+    node_goal_rng(rng, area, n, cfg.c_min_dist, cfg.c_inside_r, obst, mpe ? 0 : O, pos, gl);
+    for (int i = 0; i < n; ++i) {
+      for (int c = 0; c < SD; ++c) {
+        nxt[i * SD + c] = c < 2 ? pos[2 * i + c] : 0.0f;
+        goal[i * SD + c] = c < 2 ? gl[2 * i + c] : 0.0f;
+      }
+    }
+    if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+      for (int i = 0; i < n; ++i) {
+        float s, c;
+        sincos32(rng.uniform(0.0f, 6.28318548202514648438f), &s, &c);
+        nxt[i * SD + 2] = c;
+        nxt[i * SD + 3] = s;
+      }
+    }
+    if (mpe) {  // obstacles (mpe/base.py:92-118); the reference loop is unbounded, we cap it
+      for (int o = 0; o < O; ++o) {
+        float cx = rng.uniform(0.0f, area), cy = rng.uniform(0.0f, area);
+        for (int it = 0; it < (1 << 16); ++it) {
+          float da = 0.0f, dg = 0.0f;
+          for (int j = 0; j < n; ++j) {
+            const float d1 = norm2(pos[2 * j] - cx, pos[2 * j + 1] - cy);
+            const float d2 = norm2(gl[2 * j] - cx, gl[2 * j + 1] - cy);
+            da = j == 0 ? d1 : min_nan(da, d1);
+            dg = j == 0 ? d2 : min_nan(dg, d2);
+          }
+          const bool bad = da <= cfg.c_mpe_obs_agent || dg <= cfg.c_mpe_obs_goal || cx < cfg.c_mpe_obs_lo ||
+                           cy < cfg.c_mpe_obs_lo || cx > cfg.c_mpe_obs_hi || cy > cfg.c_mpe_obs_hi;
+          if (!bad) break;
+          cx = rng.uniform(cfg.c_mpe_obs_lo, cfg.c_mpe_obs_hi);
+          cy = rng.uniform(cfg.c_mpe_obs_lo, cfg.c_mpe_obs_hi);
+        }
+        for (int c = 0; c < SD; ++c) third[o * SD + c] = c == 0 ? cx : (c == 1 ? cy : 0.0f);
+      }
+    }
+  }
+  __syncthreads();
+  if (lidar) {
+    float* ob = io.obstacles + env * io.obstacles_stride;
+    for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) ob[idx] = obst[idx];
+    for (int i = tid; i < n; i += BLOCK) agent_is_inside(O, lds, cv, SD, i);
+    stage_edge_vectors(O, lds, cv, tid, BLOCK);
+    __syncthreads();
+    lidar_scan<SD>(d, io.ray_dirs, lds, cv, tid, BLOCK);
+    __syncthreads();
+  }
+  GraphOut out;
+  out.nodes = io.nodes + env * io.nodes_stride;
+  out.edges = io.edges + env * io.edges_stride;
+  out.states = io.out_states + env * io.out_states_stride;
+  out.recv = io.receivers + env * io.edge_index_stride;
+  out.send = io.senders + env * io.edge_index_stride;
+  const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
+  write_graph<ENGINE, GOAL, SD>(cfg, d, nxt, goal, mpe ? third : lds + cv.hits, out, vec4, tid, BLOCK);
+}
+
+// ---- host dispatch --------------------------------------------------------------------------
+static int validate(const dgppo_env_cfg* c) {
+  if (!c) return DGPPO_EINVAL;
+  if (c->engine < 0 || c->engine > 2 || c->goal_mode < 0 || c->goal_mode > 1) return DGPPO_EINVAL;
+  if (c->n_agents < 1 || c->n_agents > kMaxAgents || c->n_obs < 0 || c->n_obs > kMaxObs) return DGPPO_EINVAL;
+  const int sd = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : 4;
+  if (c->state_dim != sd || c->node_dim != sd + 3) return DGPPO_EINVAL;
+  if (c->engine != DGPPO_ENGINE_MPE && c->n_obs > 0) {
+    if (c->n_rays < 1 || c->n_rays > kMaxRays || c->top_k < 1 || c->top_k > c->n_rays) return DGPPO_EINVAL;
+  }
+  return 0;
+}
+
+// ---- launch helpers ---------------------------------------------------------------------------
+template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
+static void launch_step(const dgppo_env_cfg& c, const dgppo_env_step_io& io, size_t shmem, hipStream_t s) {
+  hipLaunchKernelGGL((env_step_kernel<ENGINE, GOAL, SD, BLOCK, NA, NO, NR, NK>), dim3((unsigned)io.n_env),
+                     dim3(BLOCK), shmem, s, c, io);
+}
+
+template <int ENGINE, int GOAL, int SD>
+static void dispatch_step_sized(const dgppo_env_cfg& c, const dgppo_env_step_io& io, size_t shmem, hipStream_t s) {
+  const int n = c.n_agents, O = c.n_obs, R = c.n_rays, k = c.top_k;
+  if (ENGINE == DGPPO_ENGINE_MPE) {
+    if (n == 3 && O == 3) return launch_step<ENGINE, GOAL, SD, 64, 3, 3, 0, 0>(c, io, shmem, s);
+    if (n == 3 && O == 0) return launch_step<ENGINE, GOAL, SD, 64, 3, 0, 0, 0>(c, io, shmem, s);
+    return launch_step<ENGINE, GOAL, SD, 64, 0, -1, 0, 0>(c, io, shmem, s);
+  }
+  if (R == 32 && k == 8) {  // the BASELINE.json Lidar configs: compile-time sizes
+    if (n == 8 && O == 3) return launch_step<ENGINE, GOAL, SD, 256, 8, 3, 32, 8>(c, io, shmem, s);
+    if (n == 32 && O == 8) return launch_step<ENGINE, GOAL, SD, 256, 32, 8, 32, 8>(c, io, shmem, s);
+  }
+  if (n * R >= 256) return launch_step<ENGINE, GOAL, SD, 256, 0, -1, 0, 0>(c, io, shmem, s);
+  return launch_step<ENGINE, GOAL, SD, 128, 0, -1, 0, 0>(c, io, shmem, s);
+}
+
+static void dispatch_step(const dgppo_env_cfg& c, const dgppo_env_step_io& io, size_t shmem, hipStream_t s) {
+  const bool spread = c.goal_mode == DGPPO_GOAL_SPREAD;
+  switch (c.engine) {
+    case DGPPO_ENGINE_MPE:
+      return spread ? dispatch_step_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
+                    : dispatch_step_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
+    case DGPPO_ENGINE_BICYCLE:
+      return spread ? dispatch_step_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, io, shmem, s)
+                    : dispatch_step_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, io, shmem, s);
+    default:
+      return spread ? dispatch_step_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
+                    : dispatch_step_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
+  }
+}
+
+template <int ENGINE, int GOAL, int SD>
+static void dispatch_reset_sized(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s) {
+  const dim3 grid((unsigned)io.n_env);
+  if (ENGINE == DGPPO_ENGINE_MPE)
+    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 64>), grid, dim3(64), shmem, s, c, io);
+  else if (c.n_agents * c.n_rays >= 256)
+    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 256>), grid, dim3(256), shmem, s, c, io);
+  else
+    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 128>), grid, dim3(128), shmem, s, c, io);
+}
+
+static void dispatch_reset(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s) {
+  const bool spread = c.goal_mode == DGPPO_GOAL_SPREAD;
+  switch (c.engine) {
+    case DGPPO_ENGINE_MPE:
+      return spread ? dispatch_reset_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
+                    : dispatch_reset_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
+    case DGPPO_ENGINE_BICYCLE:
+      return spread ? dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, io, shmem, s)
+                    : dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, io, shmem, s);
+    default:
+      return spread ? dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
+                    : dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
+  }
+}
+
+}  // namespace dgppo
+
+using namespace dgppo;
+
+extern "C" int dgppo_abi_version(void) { return DGPPO_ABI_VERSION; }
+
+extern "C" const char* dgppo_build_info(void) {
+  return "libdgppo_hip gfx950 abi=" "1" " env_step+env_reset (fp-contract=off)";
+}
+
+extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
+  if (!c) return DGPPO_EINVAL;
+  const bool mpe = c->engine == DGPPO_ENGINE_MPE;
+  const int n = c->n_agents;
+  c->state_dim = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : 4;
+  c->node_dim = c->state_dim + 3;
+  const int n_ag = c->goal_mode == DGPPO_GOAL_SPREAD ? n * n : n;
+  if (mpe) {
+    c->n_nodes = 2 * n + c->n_obs + 1;
+    c->n_edges = n * n + n_ag + n * c->n_obs;
+  } else {
+    const int hits = c->n_obs > 0 ? n * c->top_k : 0;
+    c->n_nodes = 2 * n + hits + 1;
+    c->n_edges = n * n + n_ag + hits;
+  }
+  const float a = c->area_size;
+  if (c->engine == DGPPO_ENGINE_BICYCLE) {
+    const float lo[5] = {0.f, 0.f, -1.f, -1.f, -0.5f}, hi[5] = {a, a, 1.f, 1.f, 0.5f};
+    for (int i = 0; i < 5; ++i) { c->state_lo[i] = lo[i]; c->state_hi[i] = hi[i]; }
+  } else {
+    const float v = mpe ? 1.0f : 0.5f;
+    const float lo[5] = {0.f, 0.f, -v, -v, 0.f}, hi[5] = {a, a, v, v, 0.f};
+    for (int i = 0; i < 5; ++i) { c->state_lo[i] = lo[i]; c->state_hi[i] = hi[i]; }
+  }
+  const double r = c->car_radius, orr = c->obs_radius, cr = c->comm_radius;
+  if (c->c_agent_cost == 0.f) c->c_agent_cost = (float)(r * 2);
+  if (c->c_obs_cost == 0.f) c->c_obs_cost = (float)(mpe ? r + orr : r);
+  if (c->c_self_dist == 0.f) c->c_self_dist = (float)(cr + 1);
+  if (c->c_lidar_active == 0.f) c->c_lidar_active = (float)(cr - 0.1);
+  const double md = mpe ? 2 * r : 2.2 * r;
+  if (c->c_min_dist == 0.f) c->c_min_dist = (float)md;
+  if (c->c_inside_r == 0.f) c->c_inside_r = (float)(md / 2);
+  if (c->c_mpe_obs_agent == 0.f) c->c_mpe_obs_agent = (float)(r + orr);
+  if (c->c_mpe_obs_goal == 0.f) c->c_mpe_obs_goal = (float)(r * 2 + orr);
+  if (c->c_mpe_obs_lo == 0.f) c->c_mpe_obs_lo = (float)(r * 3);
+  if (c->c_mpe_obs_hi == 0.f) c->c_mpe_obs_hi = (float)(c->area_size - r * 3);
+  return validate(c);
+}
+
+extern "C" int dgppo_ray_table(int32_t n_rays, float sense_range, float* out) {
+  if (n_rays < 1 || !out) return DGPPO_EINVAL;
+  // jnp.linspace(start, stop, R): start * (1 - i/div) + stop * (i/div), endpoint = stop
+  const float start = (float)(-M_PI);
+  const float stop = (float)(M_PI - 2 * M_PI / n_rays);
+  for (int i = 0; i < n_rays; ++i) {
+    float th;
+    if (n_rays == 1) th = start;
+    else if (i == n_rays - 1) th = stop;
+    else {
+      const float step = (float)i / (float)(n_rays - 1);
+      th = start * (1.0f - step) + stop * step;
+    }
+    float s, c;
+    sincos32(th, &s, &c);
+    out[2 * i + 0] = c * sense_range;
+    out[2 * i + 1] = s * sense_range;
+  }
+  return 0;
+}
+
+extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io* io, void* stream) {
+  if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
+  if (io->n_env == 0) return 0;
+  if (!io->states || !io->action || !io->nodes || !io->edges || !io->out_states || !io->receivers ||
+      !io->senders || !io->reward || !io->cost)
+    return DGPPO_EINVAL;
+  const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
+  if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
+                 cfg->engine != DGPPO_ENGINE_MPE);
+  const size_t shmem = (size_t)cv.total * sizeof(float);
+  dispatch_step(*cfg, *io, shmem, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {
+  if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
+  if (io->n_env == 0) return 0;
+  if (!io->nodes || !io->edges || !io->out_states || !io->receivers || !io->senders) return DGPPO_EINVAL;
+  const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
+  if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
+                 cfg->engine != DGPPO_ENGINE_MPE);
+  const size_t shmem = (size_t)cv.total * sizeof(float);
+  dispatch_reset(*cfg, *io, shmem, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,3 @@
+from .base import MPE, MPEEnvState
+from .mpe_spread import MPESpread
+from .mpe_target import MPETarget

@@ -1,0 +1,106 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol include/dgppo_hip.h
+declares, the ctypes mirrors have the C layout, and the host-side helpers agree with the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from dgppo_fov_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dgppo_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(dgppo_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_entry_points():
+    fns = declared_functions()
+    assert "dgppo_env_step" in fns and "dgppo_env_reset" in fns
+    assert set(fns) == set(_lib.SIGNATURES), (fns, sorted(_lib.SIGNATURES))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.dgppo_abi_version() == 1
+    assert b"gfx950" in lib.dgppo_build_info()
+
+
+def _c_layout(struct, fields):
+    code = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    code.append(f'printf("%zu\\n", sizeof({struct}));')
+    for f in fields:
+        code.append(f'printf("%zu\\n", offsetof({struct}, {f}));')
+    code.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        exe = os.path.join(d, "t")
+        open(c, "w").write("\n".join(code))
+        subprocess.check_call(["gcc", "-std=c99", c, "-o", exe])
+        out = subprocess.check_output([exe]).decode().split()
+    return [int(x) for x in out]
+
+
+@pytest.mark.parametrize("pystruct,cname", [(_lib.EnvCfg, "dgppo_env_cfg"), (_lib.EnvStepIO, "dgppo_env_step_io"),
+                                            (_lib.EnvResetIO, "dgppo_env_reset_io")])
+def test_ctypes_mirror_matches_c_layout(pystruct, cname):
+    names = [f[0] for f in pystruct._fields_]
+    got = _c_layout(cname, names)
+    assert got[0] == ctypes.sizeof(pystruct)
+    for name, off in zip(names, got[1:]):
+        assert getattr(pystruct, name).offset == off, name
+
+
+def test_cfg_finalize_sizes_and_einval():
+    from dgppo_fov_amd.env import make_env
+
+    e = make_env("LidarSpread", 8, num_obs=3)
+    assert (e.n_nodes, e.n_edges, e.node_dim) == (81, 192, 7)
+    bad = _lib.EnvCfg()
+    ctypes.memmove(ctypes.byref(bad), ctypes.byref(e.cfg), ctypes.sizeof(bad))
+    bad.n_agents = 0
+    assert _lib.load().dgppo_env_cfg_finalize(ctypes.byref(bad)) == _lib.DGPPO_EINVAL
+    bad.n_agents = 8
+    bad.top_k = 64  # > n_rays
+    assert _lib.load().dgppo_env_cfg_finalize(ctypes.byref(bad)) == _lib.DGPPO_EINVAL
+
+
+def test_ray_table_matches_oracle():
+    from dgppo_fov_amd.env.base import ray_table
+    from oracle import env as O
+
+    for R in (1, 8, 32, 33):
+        np.testing.assert_array_equal(ray_table(R, 0.5).numpy(), O.ray_table(R, 0.5))
+
+
+def test_derived_constants_follow_python_float_arithmetic():
+    from dgppo_fov_amd.env import make_env
+
+    e = make_env("LidarSpread", 4, num_obs=3)
+    F = np.float32
+    assert F(e.cfg.c_lidar_active) == F(0.5 - 1e-1)
+    assert F(e.cfg.c_min_dist) == F(2.2 * 0.05)
+    assert F(e.cfg.c_inside_r) == F(2.2 * 0.05 / 2)
+    m = make_env("MPESpread", 3, num_obs=3)
+    assert F(m.cfg.c_mpe_obs_lo) == F(3 * 0.05) and F(m.cfg.c_mpe_obs_hi) == F(1.5 - 3 * 0.05)
+
+
+def test_step_without_gpu_raises_not_silently_falls_back():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from dgppo_fov_amd.env import make_env
+
+    e = make_env("LidarSpread", 2, num_obs=1, device="cpu")
+    with pytest.raises(Exception):
+        e.reset(0, n_env=1)

@@ -1,0 +1,198 @@
+"""Hand-derived known-answer tests that pin the NumPy oracle (oracle/env.py, oracle/math32.py).
+
+The reference ships no tests or golden vectors and JAX is absent, so these
+closed-form cases are what pins the restatement (parity unpinned against the reference itself)."""
+import numpy as np
+import pytest
+
+from oracle import env as O
+from oracle import math32 as M
+
+F = np.float32
+
+
+# ---- math32 ------------------------------------------------------------------------------------
+def test_philox_random123_kat():
+    # Random123 kat_vectors for philox4x32-10
+    assert [int(x) for x in M.philox4x32(0, 0, 0, 0, 0, 0)] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    f = 0xFFFFFFFF
+    assert [int(x) for x in M.philox4x32(f, f, f, f, f, f)] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    got = M.philox4x32(0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344, 0xA4093822, 0x299F31D0)
+    assert [int(x) for x in got] == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_uniform_map_matches_jax_definition():
+    # jax.random.uniform: bitcast((bits >> 9) | 0x3f800000) - 1, then max(lo, u*(hi-lo)+lo)
+    assert M.bits_to_unit(np.uint32(0)) == 0.0
+    assert M.bits_to_unit(np.uint32(0xFFFFFFFF)) == F(1.0) - F(2.0 ** -23)
+    u = M.uniform(np.uint32(0x80000000), 0.0, 1.5)
+    assert u == F(0.5) * F(1.5)
+
+
+def test_sincos_atan2_accuracy():
+    x = np.linspace(-7, 7, 100001).astype(F)
+    s, c = M.sincos(x)
+    assert np.max(np.abs(s - np.sin(x.astype(np.float64)))) < 1.2e-7
+    assert np.max(np.abs(c - np.cos(x.astype(np.float64)))) < 1.2e-7
+    y = np.random.default_rng(0).uniform(-1, 1, (2, 50000)).astype(F)
+    a = M.atan2(y[0], y[1])
+    assert np.max(np.abs(a - np.arctan2(y[0].astype(np.float64), y[1].astype(np.float64)))) < 4e-7
+    assert M.atan2(F(0), F(1)) == 0 and abs(M.atan2(F(1), F(0)) - np.pi / 2) < 2e-7
+
+
+# ---- geometry ------------------------------------------------------------------------------------
+def test_ray_thetas_linspace():
+    th = O.ray_thetas(32)
+    assert th.dtype == F and th.shape == (32,)
+    np.testing.assert_allclose(th, np.linspace(-np.pi, np.pi - 2 * np.pi / 32, 32), atol=3e-7)
+    assert th[0] == F(-np.pi) and th[-1] == F(np.pi - 2 * np.pi / 32)
+
+
+def test_rectangle_corners_axis_aligned():
+    rec = O.make_rectangles(np.array([[0.8, 0.5]], F), np.array([0.2], F), np.array([0.4], F), np.array([0.0], F))
+    pts = rec[0, 8:].reshape(4, 2)
+    np.testing.assert_allclose(pts, [[0.9, 0.7], [0.7, 0.7], [0.7, 0.3], [0.9, 0.3]], atol=1e-7)
+    assert rec[0, 5] == 1.0 and rec[0, 6] == 0.0
+
+
+def test_inside_with_radius():
+    rec = O.make_rectangles(np.array([0.5, 0.5], F), F(0.2), F(0.2), F(0.0))
+    assert O.inside_rect(F(0.5), F(0.5), rec, 0.0)
+    assert not O.inside_rect(F(0.65), F(0.5), rec, 0.0)
+    assert O.inside_rect(F(0.65), F(0.5), rec, 0.06)  # within r of the right edge
+    # corner region: (0.63, 0.63) is 0.03*sqrt(2)=0.0424 from the corner
+    assert not O.inside_rect(F(0.63), F(0.63), rec, 0.04)
+    assert O.inside_rect(F(0.63), F(0.63), rec, 0.05)
+
+
+def _lidar_one(pos, rec, k=8):
+    hits, alpha = O.lidar(np.asarray(pos, F)[None, None], np.asarray(rec, F)[None], O.ray_table(32, 0.5), k)
+    return hits[0, 0], alpha[0, 0]
+
+
+def test_ray_hits_square_at_known_alpha():
+    rec = O.make_rectangles(np.array([[0.8, 0.5]], F), np.array([0.2], F), np.array([0.2], F), np.array([0.0], F))
+    hits, alpha = _lidar_one([0.5, 0.5], rec)
+    # ray 16 has theta = 0 (up to fp32 rounding of linspace): enters the square at x = 0.7
+    assert abs(alpha[16] - 0.4) < 1e-6
+    np.testing.assert_allclose(hits[0], [0.7, 0.5], atol=1e-6)
+    # only rays pointing at the square hit; all others report alpha = 1e6
+    assert np.sum(alpha < 1) >= 3 and np.sum(alpha == F(1e6)) == 32 - np.sum(alpha < 1)
+
+
+def test_no_hit_gives_far_points_in_ray_order():
+    rec = O.make_rectangles(np.array([[1.4, 1.4]], F), np.array([0.1], F), np.array([0.1], F), np.array([0.0], F))
+    hits, alpha = _lidar_one([0.2, 0.2], rec)
+    assert np.all(alpha == F(1e6))
+    tab = O.ray_table(32, 0.5)
+    # stable argsort of equal keys = rays 0..7, hit = start + (end - start) * 1e6
+    for h in range(8):
+        ex = F(0.2) + tab[h, 0]
+        np.testing.assert_array_equal(hits[h, 0], F(0.2) + (ex - F(0.2)) * F(1e6))
+
+
+def test_agent_inside_obstacle_gives_start_points():
+    rec = O.make_rectangles(np.array([[0.5, 0.5]], F), np.array([0.3], F), np.array([0.3], F), np.array([0.3], F))
+    hits, alpha = _lidar_one([0.5, 0.5], rec)
+    assert np.all(alpha == 0)
+    np.testing.assert_array_equal(hits, np.full((8, 2), 0.5, F))
+
+
+# ---- cost / reward / dynamics ---------------------------------------------------------------------
+def test_agent_cost_margin():
+    spec = O.Spec("LidarSpread", 2, 0)
+    agent = np.zeros((2, 2, 4), F)
+    agent[0, 1, 0] = 0.08  # d = 0.08 -> 0.1 - 0.08 = 0.02 > 0 -> +0.5
+    agent[1, 1, 0] = 0.3  # d = 0.3 -> -0.2 -> -0.7
+    c = O.get_cost_lidar(spec, agent, None)
+    np.testing.assert_allclose(c[0, :, 0], [0.52, 0.52], atol=1e-6)
+    np.testing.assert_allclose(c[1, :, 0], [-0.7, -0.7], atol=1e-6)
+    assert np.all(c[..., 1] == F(-0.5))  # no obstacles: 0 - 0.5
+
+
+def test_mpe_cost_has_no_upper_clip():
+    spec = O.Spec("MPESpread", 2, 1)
+    agent = np.zeros((1, 2, 4), F)
+    agent[0, 1, 0] = 1.0
+    obs = np.zeros((1, 1, 4), F)  # obstacle on agent 0 -> 0.1 - 0 + 0.5 = 0.6
+    c = O.get_cost_mpe(spec, agent, obs)
+    assert abs(c[0, 0, 1] - 0.6) < 1e-6
+
+
+def test_double_integrator_and_clip():
+    spec = O.Spec("LidarSpread", 1, 0)
+    x = np.array([[[0.5, 0.5, 0.2, -0.1]]], F)
+    a = np.array([[[1.0, -0.5]]], F)
+    y = O.step_double_integrator(spec, x, a)
+    np.testing.assert_allclose(y[0, 0], [0.5 + 0.2 * 0.03, 0.5 - 0.1 * 0.03, 0.5, -0.25], atol=1e-7)
+
+
+def test_bicycle_heading_update():
+    spec = O.Spec("LidarBicycleTarget", 1, 0)
+    x = np.array([[[0.5, 0.5, 1.0, 0.0, 0.4]]], F)  # heading 0, v = 0.4
+    a = np.array([[[1.0, 0.0]]], F)
+    y = O.step_bicycle(spec, x, a)
+    th = 0.4 * 1.0 * 0.03 * 10
+    np.testing.assert_allclose(y[0, 0], [0.5 + 0.4 * 0.03, 0.5, np.cos(th), np.sin(th), 0.4], atol=2e-7)
+
+
+def test_spread_reward_at_goals():
+    spec = O.Spec("LidarSpread", 2, 0)
+    agent = np.zeros((1, 2, 4), F)
+    agent[0, :, :2] = [[0.2, 0.2], [0.9, 0.9]]
+    goal = agent.copy()[:, ::-1]  # goals permuted: spread matches each goal to its nearest agent
+    a = np.array([[[0.6, 0.8], [0.0, 0.0]]], F)  # |a|^2 = 1 and 0
+    r = O.get_reward(spec, agent, goal, a)
+    assert abs(r[0] - (-0.0001 * 0.5)) < 1e-9
+
+
+# ---- graph layout ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("eid,n,obs,N,E", [
+    ("MPETarget", 3, 0, 7, 12), ("MPESpread", 3, 3, 10, 27), ("LidarSpread", 8, 3, 81, 192),
+    ("LidarBicycleTarget", 8, 3, 81, 136), ("LidarSpread", 32, 8, 321, 2304)])
+def test_graph_sizes_match_survey(eid, n, obs, N, E):
+    s = O.Spec(eid, n, obs)
+    assert (s.n_nodes, s.n_edges) == (N, E)
+
+
+def test_graph_layout_lidar_spread():
+    spec = O.Spec("LidarSpread", 2, 1, top_k=2)
+    agent = np.zeros((1, 2, 4), F)
+    agent[0, 0, :2] = [0.1, 0.1]
+    agent[0, 1, :2] = [0.3, 0.1]  # d = 0.2 < 0.5: connected
+    goal = np.zeros((1, 2, 4), F)
+    goal[0, :, :2] = [[1.0, 1.0], [1.2, 1.0]]
+    hits = np.array([[[[0.15, 0.1], [5.0, 5.0]], [[0.3, 0.2], [0.3, 0.9]]]], F)  # (1, n, k, 2)
+    g = O.build_graph(spec, agent, goal, hits)
+    N, pad = spec.n_nodes, spec.n_nodes - 1
+    assert N == 2 + 2 + 4 + 1
+    np.testing.assert_array_equal(g["nodes"][0, 0], np.array([0.1, 0.1, 0, 0, 0, 0, 1], F))
+    np.testing.assert_array_equal(g["nodes"][0, 2], np.array([1.0, 1.0, 0, 0, 0, 1, 0], F))
+    np.testing.assert_array_equal(g["nodes"][0, 4], np.array([0.15, 0.1, 0, 0, 1, 0, 0], F))
+    np.testing.assert_array_equal(g["nodes"][0, pad], np.zeros(7))
+    np.testing.assert_array_equal(g["states"][0, pad], -np.ones(4))
+    # agent-agent: self edges masked to the pad node, 0<->1 connected
+    np.testing.assert_array_equal(g["receivers"][0, :4], [pad, 0, 1, pad])
+    np.testing.assert_array_equal(g["senders"][0, :4], [pad, 1, 0, pad])
+    # agent-goal (spread): all four present
+    np.testing.assert_array_equal(g["receivers"][0, 4:8], [0, 0, 1, 1])
+    np.testing.assert_array_equal(g["senders"][0, 4:8], [2, 3, 2, 3])
+    # agent-lidar: agent 0 hit 0 at d=0.05 (active), hit 1 far (masked); agent 1: d=0.1 and 0.8
+    np.testing.assert_array_equal(g["receivers"][0, 8:], [0, pad, 1, pad])
+    np.testing.assert_array_equal(g["senders"][0, 8:], [4, pad, 6, pad])
+    np.testing.assert_allclose(g["edges"][0, 8], [-0.05, 0, 0, 0], atol=1e-7)
+
+
+def test_reset_invariants():
+    spec = O.Spec("LidarSpread", 4, 3)
+    ag, gl, ob = O.env_reset(spec, 7, 6)
+    md = F(2.2 * 0.05)
+    for b in range(6):
+        p = ag[b, :, :2]
+        d = np.linalg.norm(p[:, None] - p[None], axis=-1) + np.eye(4) * 10
+        assert d.min() > md
+        for i in range(4):
+            assert not O.inside_rect(p[i, 0], p[i, 1], ob[b], F(2.2 * 0.05 / 2)).any()
+        assert np.all((p >= 0) & (p <= 1.5))
+        assert np.all(ag[b, :, 2:] == 0)
+        assert np.all((ob[b, :, 2:4] >= 0.1) & (ob[b, :, 2:4] <= 0.3))
