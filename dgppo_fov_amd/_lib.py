@@ -93,6 +93,62 @@ class EnvResetIO(ctypes.Structure):
     ]
 
 
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32), ("batch", ctypes.c_int32),
+        ("trans_a", ctypes.c_int32), ("trans_b", ctypes.c_int32),
+        ("A", c_f32p), ("lda", ctypes.c_int64), ("stride_a", ctypes.c_int64),
+        ("B", c_f32p), ("ldb", ctypes.c_int64), ("stride_b", ctypes.c_int64),
+        ("C", c_f32p), ("ldc", ctypes.c_int64), ("stride_c", ctypes.c_int64),
+        ("a_grp", ctypes.c_int32), ("b_grp", ctypes.c_int32), ("c_grp", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("a_gstride", ctypes.c_int64), ("b_gstride", ctypes.c_int64), ("c_gstride", ctypes.c_int64),
+        ("bias", c_f32p),
+        ("addend", c_f32p), ("ld_add", ctypes.c_int64), ("stride_add", ctypes.c_int64),
+        ("add_grp", ctypes.c_int32), ("pad2_", ctypes.c_int32), ("add_gstride", ctypes.c_int64),
+        ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
+        ("relu", ctypes.c_int32),
+        ("split_k", ctypes.c_int32),
+        ("workspace", c_f32p),
+    ]
+
+
+class GnnAttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("G", ctypes.c_int32), ("N", ctypes.c_int32), ("E", ctypes.c_int32), ("n_agents", ctypes.c_int32),
+        ("D", ctypes.c_int32), ("F", ctypes.c_int32), ("H", ctypes.c_int32), ("C", ctypes.c_int32),
+        ("cand", c_f32p), ("receivers", c_f32p), ("senders", c_f32p),
+        ("x", c_f32p), ("x_gstride", ctypes.c_int64),
+        ("ef", c_f32p), ("ef_gstride", ctypes.c_int64),
+        ("q", c_f32p), ("qt", c_f32p), ("bk", c_f32p),
+        ("attn", c_f32p), ("xcat", c_f32p),
+        ("dxcat", c_f32p), ("dqt", c_f32p), ("dq", c_f32p), ("dbeta", c_f32p),
+        ("dx", c_f32p), ("dx_gstride", ctypes.c_int64),
+        ("scale", ctypes.c_float),
+    ]
+
+
+class TanhNormalArgs(ctypes.Structure):
+    _fields_ = [
+        ("rows", ctypes.c_int64),
+        ("A", ctypes.c_int32), ("mode", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("mean", c_f32p), ("std_raw", c_f32p),
+        ("std_shift", ctypes.c_float), ("std_min", ctypes.c_float),
+        ("noise", c_f32p), ("action", c_f32p), ("action_out", c_f32p), ("std_out", c_f32p),
+        ("log_pi", c_f32p), ("entropy", c_f32p), ("entropy_eps", c_f32p),
+        ("dlog_pi", c_f32p), ("dentropy", c_f32p), ("dmean", c_f32p), ("dstd_raw", c_f32p),
+    ]
+
+
+class GaeArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_h", ctypes.c_int32),
+        ("hs", c_f32p), ("l", c_f32p), ("Vh", c_f32p), ("Vl", c_f32p), ("Qh", c_f32p), ("Ql", c_f32p),
+        ("gamma", ctypes.c_float), ("lambda", ctypes.c_float),
+    ]
+
+
+_V, _I64, _I32, _F32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
+
 # symbol -> (restype, argtypes); must match include/dgppo_hip.h (checked by tests/test_capi.py)
 SIGNATURES = {
     "dgppo_abi_version": (ctypes.c_int, []),
@@ -101,6 +157,28 @@ SIGNATURES = {
     "dgppo_ray_table": (ctypes.c_int, [ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]),
     "dgppo_env_step": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvStepIO), ctypes.c_void_p]),
     "dgppo_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvResetIO), ctypes.c_void_p]),
+    "dgppo_gemm_workspace_floats": (ctypes.c_int64, [ctypes.POINTER(GemmArgs)]),
+    "dgppo_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), ctypes.c_void_p]),
+    "dgppo_gnn_attn_fwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
+    "dgppo_gnn_attn_bwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
+    "dgppo_relu_bwd": (ctypes.c_int, [_V, _V, _I64, _V]),
+    "dgppo_layernorm_fwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _I64, _I32, _I32, _F32, _V]),
+    "dgppo_layernorm_bwd_workspace_floats": (ctypes.c_int64, [_I64, _I32]),
+    "dgppo_layernorm_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _I32, _V, _V]),
+    "dgppo_colsum_workspace_floats": (ctypes.c_int64, [_I64, _I32]),
+    "dgppo_colsum": (ctypes.c_int, [_V, _I64, _I32, _I64, _I32, _I64, _V, _F32, _F32, _V, _V]),
+    "dgppo_gru_fwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, _I32, _V]),
+    "dgppo_gru_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _V]),
+    "dgppo_agent_mean_fwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),
+    "dgppo_agent_mean_bwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),
+    "dgppo_tanh_normal": (ctypes.c_int, [ctypes.POINTER(TanhNormalArgs), ctypes.c_void_p]),
+    "dgppo_loss_workspace_floats": (ctypes.c_int64, []),
+    "dgppo_ppo_loss": (ctypes.c_int, [_V, _V, _V, _V, _I64, _F32, _F32, _V, _V, _V, _V, _V]),
+    "dgppo_l2_loss": (ctypes.c_int, [_V, _V, _I64, _V, _V, _V, _V]),
+    "dgppo_gae": (ctypes.c_int, [ctypes.POINTER(GaeArgs), ctypes.c_void_p]),
+    "dgppo_grad_norm": (ctypes.c_int, [_V, _I64, _V, _V, _V]),
+    "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, _F32, _F32, _F32, _F32, _V]),
+    "dgppo_normal": (ctypes.c_int, [_V, _I64, _V, ctypes.c_uint64, ctypes.c_uint64, _V]),
 }
 
 _LIB = None

@@ -1,0 +1,255 @@
+"""The three DGPPO networks with explicit forward/backward:
+
+  ActorNet  PPOPolicy / TanhNormal / PolicyNet (dgppo/algo/module/policy.py:20-212):
+            GraphTransformerGNN(2 layers, 32 -> 64, 3 heads) -> MLP(64,64)+LN -> GRUCell(64) ->
+            ScaleHid Dense(64, init x0.01, no activation) -> mean Dense(2), std Dense(2) ->
+            std = softplus(x + log(e^0.5 - 1)) + 1e-5 -> Independent(TanhTransformed(Normal)).
+  VlNet     ValueNet(decompose=False) = RStateFn (dgppo/algo/module/value.py:15-44): GNN(2 layers)
+            -> mean over agents -> MLP -> GRUCell -> Dense(1).
+  VhNet     DGPPO's ValueNet(n_out=n_cost, gnn_layers=1, decompose=True, use_global_info=False) =
+            DecRStateFn (value.py:47-79, dgppo.py:83-95): GNN(1 layer) -> MLP -> GRUCell fed the
+            ACTOR's stored carry -> Dense(n_cost).
+
+Rows are always ordered (graph, agent).  Sequences (the 16-step truncated-BPTT chunks of
+informarl.py:365-367 / 409-413) are (sequence s, step t) graph-major, carries start at zero.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ... import _lib
+from ...nn import kernels as K
+from ...nn.layers import GNN, Dense, GraphBatch, GRUCell, MLPHead, ParamSpace
+
+STD_DEV_INIT_INV = math.log(math.exp(0.5) - 1.0)  # TanhNormal.std_dev_init_inv (policy.py:54-59)
+STD_DEV_MIN = 1e-5
+
+
+class _Net:
+    modules: list
+
+    def init_host(self, seed: int):
+        rng = np.random.default_rng(seed)
+        for m in self.modules:
+            m.init_host(rng)
+
+    @property
+    def n_params(self):
+        return self.ps.size
+
+
+class ActorNet(_Net):
+    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 0, gnn_layers: int = 2, action_dim: int = 2):
+        self.n, self.A = n_agents, action_dim
+        ps = self.ps = ParamSpace()
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers)
+        self.head = MLPHead(ps, "head")
+        self.gru = GRUCell(ps, "gru")
+        self.scale_hid = Dense(ps, "ScaleHid", 64, 64, scale=0.01)
+        self.mean = Dense(ps, "OutputDenseMean", 64, action_dim)
+        self.std = Dense(ps, "OutputDenseStdTrans", 64, action_dim)
+        self.modules = [self.gnn, self.head, self.gru, self.scale_hid, self.mean, self.std]
+        ps.build(device)
+        self.init_host(seed)
+        self.device = torch.device(device)
+
+    # flax-layout import / export (checkpoint interop and oracle tests)
+    def flax(self):
+        return {"gnn": self.gnn.flax(), "head": self.head.flax(), "gru": self.gru.flax(),
+                "ScaleHid": self.scale_hid.flax(), "OutputDenseMean": self.mean.flax(),
+                "OutputDenseStdTrans": self.std.flax()}
+
+    def load_flax(self, d):
+        self.gnn.load_flax(d["gnn"]), self.head.load_flax(d["head"]), self.gru.load_flax(d["gru"])
+        self.scale_hid.load_flax(d["ScaleHid"]), self.mean.load_flax(d["OutputDenseMean"])
+        self.std.load_flax(d["OutputDenseStdTrans"])
+
+    def _trunk(self, g: GraphBatch):
+        z, gc = self.gnn.fwd(g)
+        y, hc = self.head.fwd(z)
+        return y, (gc, hc)
+
+    def _outputs(self, h2):
+        rows = h2.shape[0]
+        s = self.scale_hid.fwd(h2, rows)
+        mu = self.mean.fwd(s, rows)
+        sr = self.std.fwd(s, rows)
+        return s, mu, sr
+
+    def act(self, g: GraphBatch, h: torch.Tensor, mode: int, noise=None, action_out=None, log_pi_out=None,
+            h_out=None):
+        """One policy step for G graphs: mode 0 = deterministic (get_action: tanh(mean)),
+        1 = sample_action with standard-normal `noise` (G*n, A).  Returns (action, log_pi, h_new)."""
+        rows = g.G * self.n
+        y, _ = self._trunk(g)
+        h2 = h_out if h_out is not None else torch.empty_like(h)
+        hn, _ = self.gru.fwd(y, h)
+        h2.copy_(hn)
+        _, mu, sr = self._outputs(h2)
+        action = action_out if action_out is not None else torch.empty((rows, self.A), device=h.device)
+        log_pi = log_pi_out if log_pi_out is not None else torch.empty(rows, device=h.device)
+        a = _lib.TanhNormalArgs()
+        a.rows, a.A, a.mode, a.n_agents = rows, self.A, mode, self.n
+        a.mean, a.std_raw = K._p(mu), K._p(sr)
+        a.std_shift, a.std_min = STD_DEV_INIT_INV, STD_DEV_MIN
+        a.noise = K._p(noise)
+        a.action_out, a.log_pi = K._p(action), K._p(log_pi)
+        K.tanh_normal(a, h.device)
+        return action, log_pi, h2
+
+    def eval_seq_fwd(self, g: GraphBatch, S: int, L: int, actions: torch.Tensor, entropy_eps: torch.Tensor):
+        """eval_action over S sequences of L steps (scan_eval_action, informarl.py:387-403), zero
+        initial carries.  actions (S*L*n, A) rows (s, t, agent).  Returns log_pi, entropy (S*L*n,)."""
+        n, dev = self.n, actions.device
+        y, tc = self._trunk(g)  # (S*L*n, 64)
+        y4 = y.view(S, L, n, 64)
+        h = torch.zeros((S * n, 64), device=dev)
+        Hs = torch.empty((S, L, n, 64), device=dev)
+        gcs = []
+        for t in range(L):
+            x_t = y4[:, t].contiguous().view(S * n, 64)
+            h, c = self.gru.fwd(x_t, h)
+            gcs.append(c)
+            Hs[:, t].copy_(h.view(S, n, 64))
+        H2 = Hs.view(S * L * n, 64)
+        s, mu, sr = self._outputs(H2)
+        rows = S * L * n
+        log_pi = torch.empty(rows, device=dev)
+        ent = torch.empty(rows, device=dev)
+        a = _lib.TanhNormalArgs()
+        a.rows, a.A, a.mode, a.n_agents = rows, self.A, 2, n
+        a.mean, a.std_raw, a.action = K._p(mu), K._p(sr), K._p(actions)
+        a.std_shift, a.std_min = STD_DEV_INIT_INV, STD_DEV_MIN
+        a.log_pi, a.entropy, a.entropy_eps = K._p(log_pi), K._p(ent), K._p(entropy_eps)
+        K.tanh_normal(a, dev)
+        cache = (g, S, L, tc, gcs, H2, s, mu, sr, actions, entropy_eps)
+        return log_pi, ent, cache
+
+    def eval_seq_bwd(self, cache, dlog_pi, dentropy):
+        g, S, L, tc, gcs, H2, s, mu, sr, actions, entropy_eps = cache
+        n, dev = self.n, dlog_pi.device
+        rows = S * L * n
+        dmu = torch.empty_like(mu)
+        dsr = torch.empty_like(sr)
+        a = _lib.TanhNormalArgs()
+        a.rows, a.A, a.mode, a.n_agents = rows, self.A, 2, n
+        a.mean, a.std_raw, a.action = K._p(mu), K._p(sr), K._p(actions)
+        a.std_shift, a.std_min = STD_DEV_INIT_INV, STD_DEV_MIN
+        a.entropy_eps = K._p(entropy_eps)
+        a.dlog_pi, a.dentropy, a.dmean, a.dstd_raw = K._p(dlog_pi), K._p(dentropy), K._p(dmu), K._p(dsr)
+        K.tanh_normal(a, dev)
+        ds = self.mean.bwd(s, dmu, rows)
+        self.std.bwd(s, dsr, rows, dx_out=ds, accumulate=True)
+        dH2 = self.scale_hid.bwd(H2, ds, rows)
+        self._bptt(dH2.view(S, L, n, 64), gcs, S, L, tc, g)
+
+    def _bptt(self, dHs, gcs, S, L, tc, g):
+        n, dev = self.n, dHs.device
+        dY = torch.empty((S, L, n, 64), device=dev)
+        dh = torch.zeros((S * n, 64), device=dev)
+        for t in range(L - 1, -1, -1):
+            dtot = dHs[:, t].contiguous().view(S * n, 64) + dh
+            dx, dh = self.gru.bwd(gcs[t], dtot)
+            dY[:, t].copy_(dx.view(S, n, 64))
+        gc, hc = tc
+        dz = self.head.bwd(hc, dY.view(S * L * n, 64))
+        self.gnn.bwd(gc, dz, g)
+
+
+class VlNet(_Net):
+    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 1, gnn_layers: int = 2):
+        self.n = n_agents
+        ps = self.ps = ParamSpace()
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers)
+        self.head = MLPHead(ps, "head")
+        self.gru = GRUCell(ps, "gru")
+        self.out = Dense(ps, "out", 64, 1)
+        self.modules = [self.gnn, self.head, self.gru, self.out]
+        ps.build(device)
+        self.init_host(seed)
+        self.device = torch.device(device)
+
+    def flax(self):
+        return {"gnn": self.gnn.flax(), "head": self.head.flax(), "gru": self.gru.flax(), "out": self.out.flax()}
+
+    def load_flax(self, d):
+        self.gnn.load_flax(d["gnn"]), self.head.load_flax(d["head"]), self.gru.load_flax(d["gru"])
+        self.out.load_flax(d["out"])
+
+    def seq_fwd(self, g: GraphBatch, S: int, L: int, h0=None, keep_cache=True):
+        """scan_Vl (informarl.py:281-293) over S sequences of L graphs.  Returns values (S, L),
+        final carries (S, 64) and the cache for seq_bwd."""
+        n, dev = self.n, g.nodes.device
+        G = S * L
+        z, gc = self.gnn.fwd(g)  # (G*n, 64)
+        zm = torch.empty((G, 64), device=dev)
+        K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
+        y, hc = self.head.fwd(zm)
+        y3 = y.view(S, L, 64)
+        h = torch.zeros((S, 64), device=dev) if h0 is None else h0
+        Hs = torch.empty((S, L, 64), device=dev)
+        gcs = []
+        for t in range(L):
+            h, c = self.gru.fwd(y3[:, t].contiguous(), h)
+            if keep_cache:
+                gcs.append(c)
+            Hs[:, t].copy_(h)
+        v = self.out.fwd(Hs.view(G, 64), G)
+        cache = (g, S, L, gc, z, hc, gcs, Hs) if keep_cache else None
+        return v.view(S, L), h, cache
+
+    def seq_bwd(self, cache, dv):
+        g, S, L, gc, z, hc, gcs, Hs = cache
+        n, dev = self.n, dv.device
+        G = S * L
+        dH = self.out.bwd(Hs.view(G, 64), dv.reshape(G, 1).contiguous(), G).view(S, L, 64)
+        dY = torch.empty((S, L, 64), device=dev)
+        dh = torch.zeros((S, 64), device=dev)
+        for t in range(L - 1, -1, -1):
+            dx, dh = self.gru.bwd(gcs[t], dH[:, t].contiguous() + dh)
+            dY[:, t].copy_(dx)
+        dzm = self.head.bwd(hc, dY.view(G, 64))
+        dz = torch.empty_like(z)
+        K.agent_mean_bwd(dzm, dz, G, n, 64, n * 64)
+        self.gnn.bwd(gc, dz, g)
+
+
+class VhNet(_Net):
+    def __init__(self, node_dim: int, n_agents: int, n_cost: int, device, seed: int = 2, gnn_layers: int = 1):
+        self.n, self.n_cost = n_agents, n_cost
+        ps = self.ps = ParamSpace()
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers)
+        self.head = MLPHead(ps, "head")
+        self.gru = GRUCell(ps, "gru")
+        self.out = Dense(ps, "out", 64, n_cost)
+        self.modules = [self.gnn, self.head, self.gru, self.out]
+        ps.build(device)
+        self.init_host(seed)
+        self.device = torch.device(device)
+
+    def flax(self):
+        return {"gnn": self.gnn.flax(), "head": self.head.flax(), "gru": self.gru.flax(), "out": self.out.flax()}
+
+    def load_flax(self, d):
+        self.gnn.load_flax(d["gnn"]), self.head.load_flax(d["head"]), self.gru.load_flax(d["gru"])
+        self.out.load_flax(d["out"])
+
+    def fwd(self, g: GraphBatch, h: torch.Tensor, keep_cache=True):
+        """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, 64): (G*n, n_cost)."""
+        rows = g.G * self.n
+        z, gc = self.gnn.fwd(g)
+        y, hc = self.head.fwd(z)
+        h2, rc = self.gru.fwd(y, h)
+        out = self.out.fwd(h2, rows)
+        return out, ((g, gc, hc, rc, h2) if keep_cache else None)
+
+    def bwd(self, cache, dout):
+        g, gc, hc, rc, h2 = cache
+        rows = g.G * self.n
+        dh2 = self.out.bwd(h2, dout, rows)
+        dy, _ = self.gru.bwd(rc, dh2)
+        dz = self.head.bwd(hc, dy)
+        self.gnn.bwd(gc, dz, g)

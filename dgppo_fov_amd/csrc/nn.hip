@@ -1,0 +1,901 @@
+// Hot path (2) kernels besides the GEMM: the GraphTransformer attention core, LayerNorm(+ReLU),
+// GRU cell, agent mean, TanhNormal head, PPO / L2 losses, Dec-OCP GAE, global-norm clip + Adam,
+// and Philox normal noise.  All fp32; forward and backward for everything that carries gradients.
+//
+// GraphTransformer (dgppo/nn/gnn.py:78-117).  In every DGPPO env graph only agent nodes receive
+// messages (all other edges are masked to the pad node), so per receiving agent i and head h:
+//   logit_c = (q_h . k_c) / sqrt(F),  k_c = x_{s_c} Wk_h + bk_h
+//           = (qt_h . x_{s_c} + q_h . bk_h) / sqrt(F),  with qt_h = Wk_h q_h   (D-dim, not F-dim)
+//   sum_c a_c (v_c + e_c) = xbar_h Wv_h + sig_h bv_h + ebar_h We_h
+//           with xbar_h = sum_c a_c x_{s_c}, ebar_h = sum_c a_c ef_c, sig_h = sum_c a_c
+// i.e. the per-edge K/V/E projections of the reference collapse into per-agent dense products
+// (GEMMs over all agents of the batch, dgppo_gemm) plus this O(C * H * D) gather core.  The
+// result equals the reference's up to fp32 rounding.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/dgppo_hip.h"
+
+namespace dgppo {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float softplusf_(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+
+constexpr int kMaxCand = 128;
+constexpr int kMaxHD = 3 * 64;
+
+// ---- GraphTransformer attention core ---------------------------------------------------------
+// One wave per graph; agents processed in order (so the sender-gradient accumulation of the
+// backward is a deterministic, conflict-free per-lane column update in LDS).
+struct AttnLds {
+  float qt[kMaxHD];             // H*D
+  float beta[4];
+  float a[kMaxCand * 3];        // [c][h]
+  int s[kMaxCand];              // sender node (or -1)
+  int e[kMaxCand];              // edge id
+  float g[kMaxHD + 3 * 4 + 4];  // backward: dxbar (H*D) | debar (H*4) | dsig (H)
+  float dl[kMaxCand * 3];       // backward: scaled dlogit [c][h]
+};
+
+__device__ void attn_candidates(const dgppo_gnn_attn_args& p, int g, int i, AttnLds& L, int lane) {
+  const int32_t* recv = p.receivers + (int64_t)g * p.E;
+  const int32_t* send = p.senders + (int64_t)g * p.E;
+  for (int c = lane; c < p.C; c += 64) {
+    const int e = p.cand[i * p.C + c];
+    int s = -1;
+    if (e >= 0 && recv[e] == i) s = send[e];
+    L.s[c] = s;
+    L.e[c] = e;
+  }
+}
+
+__global__ __launch_bounds__(64) void gnn_attn_fwd_kernel(dgppo_gnn_attn_args p) {
+  __shared__ AttnLds L;
+  const int g = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int H = p.H, D = p.D, F = p.F, C = p.C;
+  const float* xg = p.x + (int64_t)g * p.x_gstride;
+  const float* efg = p.ef + (int64_t)g * p.ef_gstride;
+  const int W = H * (D + 5);
+  for (int i = 0; i < p.n_agents; ++i) {
+    const int64_t row = (int64_t)g * p.n_agents + i;
+    for (int t = lane; t < H * D; t += 64) L.qt[t] = p.qt[row * H * D + t];
+    for (int h = 0; h < H; ++h) {  // beta_h = q_h . bk_h
+      float acc = 0.0f;
+      for (int f = lane; f < F; f += 64) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
+      acc = wave_sum(acc);
+      if (lane == 0) L.beta[h] = acc;
+    }
+    attn_candidates(p, g, i, L, lane);
+    __syncthreads();
+    // logits (one candidate per lane), then softmax per head over valid candidates
+    float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int c = lane; c < C; c += 64) {
+      const int s = L.s[c];
+      for (int h = 0; h < H; ++h) {
+        float lg = -INFINITY;
+        if (s >= 0) {
+          const float* xs = xg + (int64_t)s * D;
+          float acc = 0.0f;
+          for (int d = 0; d < D; ++d) acc += L.qt[h * D + d] * xs[d];
+          lg = (acc + L.beta[h]) * p.scale;
+        }
+        L.a[c * 3 + h] = lg;
+        mx[h] = fmaxf(mx[h], lg);
+      }
+    }
+    float sm[3];
+    for (int h = 0; h < H; ++h) mx[h] = wave_max(mx[h]);
+    __syncthreads();
+    for (int h = 0; h < H; ++h) sm[h] = 0.0f;
+    for (int c = lane; c < C; c += 64) {
+      for (int h = 0; h < H; ++h) {
+        const float ex = L.s[c] >= 0 ? expf(L.a[c * 3 + h] - mx[h]) : 0.0f;
+        L.a[c * 3 + h] = ex;
+        sm[h] += ex;
+      }
+    }
+    for (int h = 0; h < H; ++h) sm[h] = wave_sum(sm[h]);
+    __syncthreads();
+    for (int c = lane; c < C; c += 64) {
+      for (int h = 0; h < H; ++h) {
+        const float a = L.a[c * 3 + h] / sm[h];
+        L.a[c * 3 + h] = a;
+        if (p.attn) p.attn[(row * H + h) * C + c] = a;
+      }
+    }
+    __syncthreads();
+    // xbar_h[d] (lane = d), ebar_h[j], sig_h
+    float* out = p.xcat + row * W;
+    for (int d = lane; d < D; d += 64) {
+      float acc[3] = {0.0f, 0.0f, 0.0f};
+      for (int c = 0; c < C; ++c) {
+        const int s = L.s[c];
+        if (s < 0) continue;
+        const float xv = xg[(int64_t)s * D + d];
+        for (int h = 0; h < H; ++h) acc[h] += L.a[c * 3 + h] * xv;
+      }
+      for (int h = 0; h < H; ++h) out[h * D + d] = acc[h];
+    }
+    if (lane < H * 4) {
+      const int h = lane >> 2, j = lane & 3;
+      float acc = 0.0f;
+      for (int c = 0; c < C; ++c)
+        if (L.s[c] >= 0) acc += L.a[c * 3 + h] * efg[(int64_t)L.e[c] * 4 + j];
+      out[H * D + lane] = acc;
+    }
+    if (lane < H) {
+      float acc = 0.0f;
+      for (int c = 0; c < C; ++c)
+        if (L.s[c] >= 0) acc += L.a[c * 3 + lane];
+      out[H * D + H * 4 + lane] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void gnn_attn_bwd_kernel(dgppo_gnn_attn_args p) {
+  __shared__ AttnLds L;
+  extern __shared__ __attribute__((aligned(16))) float dxs[];  // (N, D) sender gradients
+  const int g = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int H = p.H, D = p.D, F = p.F, C = p.C, N = p.N;
+  const float* xg = p.x + (int64_t)g * p.x_gstride;
+  const float* efg = p.ef + (int64_t)g * p.ef_gstride;
+  const int W = H * (D + 5);
+  const bool want_dx = p.dx != nullptr;
+  if (want_dx)
+    for (int t = lane; t < N * D; t += 64) dxs[t] = 0.0f;
+  for (int i = 0; i < p.n_agents; ++i) {
+    const int64_t row = (int64_t)g * p.n_agents + i;
+    for (int t = lane; t < H * D; t += 64) L.qt[t] = p.qt[row * H * D + t];
+    for (int t = lane; t < W; t += 64) L.g[t] = p.dxcat[row * W + t];
+    attn_candidates(p, g, i, L, lane);
+    for (int t = lane; t < C * H; t += 64) {
+      const int c = t / H, h = t - (t / H) * H;
+      L.a[c * 3 + h] = p.attn[(row * H + h) * C + c];
+    }
+    __syncthreads();
+    // da_c,h = dxbar_h . x_s + debar_h . ef_e + dsig_h ; softmax backward -> dlogit
+    float dot[3] = {0.0f, 0.0f, 0.0f};
+    float da_[2][3];
+    int k = 0;
+    for (int c = lane; c < C; c += 64, ++k) {
+      const int s = L.s[c];
+      for (int h = 0; h < H; ++h) {
+        float v = 0.0f;
+        if (s >= 0) {
+          const float* xs = xg + (int64_t)s * D;
+          for (int d = 0; d < D; ++d) v += L.g[h * D + d] * xs[d];
+          const float* ef = efg + (int64_t)L.e[c] * 4;
+          for (int j = 0; j < 4; ++j) v += L.g[H * D + h * 4 + j] * ef[j];
+          v += L.g[H * D + H * 4 + h];
+        }
+        da_[k][h] = v;
+        dot[h] += L.a[c * 3 + h] * v;
+      }
+    }
+    for (int h = 0; h < H; ++h) dot[h] = wave_sum(dot[h]);
+    k = 0;
+    float dbeta[3] = {0.0f, 0.0f, 0.0f};
+    for (int c = lane; c < C; c += 64, ++k) {
+      for (int h = 0; h < H; ++h) {
+        const float dlg = L.s[c] >= 0 ? L.a[c * 3 + h] * (da_[k][h] - dot[h]) * p.scale : 0.0f;
+        L.dl[c * 3 + h] = dlg;
+        dbeta[h] += dlg;
+      }
+    }
+    for (int h = 0; h < H; ++h) dbeta[h] = wave_sum(dbeta[h]);
+    if (lane < H) p.dbeta[row * H + lane] = lane == 0 ? dbeta[0] : (lane == 1 ? dbeta[1] : dbeta[2]);
+    for (int t = lane; t < H * F; t += 64) {
+      const int h = t / F;
+      p.dq[row * H * F + t] = (h == 0 ? dbeta[0] : (h == 1 ? dbeta[1] : dbeta[2])) * p.bk[t];
+    }
+    __syncthreads();
+    // dqt_h[d] = sum_c dl_c,h x_s[d];  sender grads  dx_s[d] += sum_h a_c,h dxbar_h[d] + dl_c,h qt_h[d]
+    for (int d = lane; d < D; d += 64) {
+      float acc[3] = {0.0f, 0.0f, 0.0f};
+      for (int c = 0; c < C; ++c) {
+        const int s = L.s[c];
+        if (s < 0) continue;
+        const float xv = xg[(int64_t)s * D + d];
+        float contrib = 0.0f;
+        for (int h = 0; h < H; ++h) {
+          acc[h] += L.dl[c * 3 + h] * xv;
+          contrib += L.a[c * 3 + h] * L.g[h * D + d] + L.dl[c * 3 + h] * L.qt[h * D + d];
+        }
+        if (want_dx) dxs[s * D + d] += contrib;
+      }
+      for (int h = 0; h < H; ++h) p.dqt[row * H * D + h * D + d] = acc[h];
+    }
+    __syncthreads();
+  }
+  if (want_dx) {
+    float* dxg = p.dx + (int64_t)g * p.dx_gstride;
+    for (int t = lane; t < N * D; t += 64) dxg[t] += dxs[t];
+  }
+}
+
+// ---- LayerNorm (+ReLU) over rows of width F (flax LayerNorm, eps 1e-6, fast variance) --------
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* x, const float* scale, const float* bias,
+                                                            float* y, float* mean_out, float* rstd_out,
+                                                            int64_t rows, int F, int relu, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * F;
+  float s = 0.0f, s2 = 0.0f;
+  for (int f = lane; f < F; f += 64) {
+    const float v = xr[f];
+    s += v;
+    s2 += v * v;
+  }
+  s = wave_sum(s);
+  s2 = wave_sum(s2);
+  const float mean = s / F;
+  float var = s2 / F - mean * mean;
+  var = var > 0.0f ? var : 0.0f;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  for (int f = lane; f < F; f += 64) {
+    float v = (xr[f] - mean) * rstd * scale[f] + bias[f];
+    if (relu) v = v > 0.0f ? v : 0.0f;
+    y[r * F + f] = v;
+  }
+  if (lane == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+// dx (overwrite), and per-block partial sums of dscale / dbias -> part[(block, 2, F)]
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* x, const float* y, const float* dy,
+                                                            const float* scale, const float* mean_in,
+                                                            const float* rstd_in, float* dx, float* part,
+                                                            int64_t rows, int F, int relu, int rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];  // 4 waves x 2F
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int t = threadIdx.x; t < 8 * F; t += 256) acc[t] = 0.0f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int64_t r = r0 + wave; r < r0 + rows_per_block && r < rows; r += 4) {
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float s1 = 0.0f, s2 = 0.0f;
+    for (int f = lane; f < F; f += 64) {
+      float g = dy[r * F + f];
+      if (relu && !(y[r * F + f] > 0.0f)) g = 0.0f;
+      const float xh = (x[r * F + f] - mean) * rstd;
+      acc[wave * 2 * F + f] += g * xh;
+      acc[wave * 2 * F + F + f] += g;
+      const float gx = g * scale[f];
+      s1 += gx;
+      s2 += gx * xh;
+    }
+    s1 = wave_sum(s1) / F;
+    s2 = wave_sum(s2) / F;
+    for (int f = lane; f < F; f += 64) {
+      float g = dy[r * F + f];
+      if (relu && !(y[r * F + f] > 0.0f)) g = 0.0f;
+      const float xh = (x[r * F + f] - mean) * rstd;
+      dx[r * F + f] = rstd * (g * scale[f] - s1 - xh * s2);
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * F; t += 256)
+    part[(int64_t)blockIdx.x * 2 * F + t] = acc[t] + acc[2 * F + t] + acc[4 * F + t] + acc[6 * F + t];
+}
+
+// ---- column sums (deterministic two-level) ----------------------------------------------------
+// part[b][c] = sum of rows [b*rpb, (b+1)*rpb) of x (grouped row addressing as in the GEMM)
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int64_t rows, int cols, int64_t ld,
+                                                             int grp, int64_t gstride, float* part,
+                                                             int64_t rows_per_block) {
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    float s = 0.0f;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t off = grp > 0 ? (r / grp) * gstride + (r % grp) * ld : r * ld;
+      s += x[off + c];
+    }
+    part[(int64_t)blockIdx.x * cols + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nparts, int cols, int64_t pstride,
+                                                           float* out, float alpha, float beta) {
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < cols; c += gridDim.x * 256) {
+    float s = 0.0f;
+    for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * pstride + c];
+    out[c] = alpha * s + (beta != 0.0f ? beta * out[c] : 0.0f);
+  }
+}
+
+// ---- GRU cell (flax GRUCell) ------------------------------------------------------------------
+// gi = x Wi + bi (rows, 3H: r|z|n), gh = h Wh (rows, 3H, no bias), bhn (H)
+__global__ __launch_bounds__(256) void gru_fwd_kernel(const float* gi, const float* gh, const float* bhn,
+                                                      const float* h, float* hn_out, int64_t rows, int H) {
+  const int64_t total = rows * H;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / H;
+    const int j = (int)(t - r * H);
+    const float* a = gi + r * 3 * H;
+    const float* b = gh + r * 3 * H;
+    const float rg = sigmoidf_(a[j] + b[j]);
+    const float zg = sigmoidf_(a[H + j] + b[H + j]);
+    const float ng = tanhf(a[2 * H + j] + rg * (b[2 * H + j] + bhn[j]));
+    hn_out[t] = (1.0f - zg) * ng + zg * h[t];
+  }
+}
+
+// dgi, dgh (overwrite), dh (+= direct path)
+__global__ __launch_bounds__(256) void gru_bwd_kernel(const float* gi, const float* gh, const float* bhn,
+                                                      const float* h, const float* dhn, float* dgi, float* dgh,
+                                                      float* dh, int64_t rows, int H) {
+  const int64_t total = rows * H;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / H;
+    const int j = (int)(t - r * H);
+    const float* a = gi + r * 3 * H;
+    const float* b = gh + r * 3 * H;
+    const float rg = sigmoidf_(a[j] + b[j]);
+    const float zg = sigmoidf_(a[H + j] + b[H + j]);
+    const float hnp = b[2 * H + j] + bhn[j];
+    const float ng = tanhf(a[2 * H + j] + rg * hnp);
+    const float g = dhn[t];
+    const float dz = g * (h[t] - ng);
+    const float dn = g * (1.0f - zg);
+    const float dn_pre = dn * (1.0f - ng * ng);
+    const float dr = dn_pre * hnp;
+    const float dr_pre = dr * rg * (1.0f - rg);
+    const float dz_pre = dz * zg * (1.0f - zg);
+    float* ai = dgi + r * 3 * H;
+    float* bi = dgh + r * 3 * H;
+    ai[j] = dr_pre;
+    ai[H + j] = dz_pre;
+    ai[2 * H + j] = dn_pre;
+    bi[j] = dr_pre;
+    bi[H + j] = dz_pre;
+    bi[2 * H + j] = dn_pre * rg;
+    dh[t] += g * zg;
+  }
+}
+
+// ---- mean over the n agents of each graph: (G, n, F) <-> (G, F) ------------------------------
+__global__ __launch_bounds__(256) void agent_mean_fwd_kernel(const float* x, float* y, int64_t G, int n, int F,
+                                                             int64_t x_gstride) {
+  const int64_t total = G * F;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t g = t / F;
+    const int f = (int)(t - g * F);
+    float s = 0.0f;
+    for (int i = 0; i < n; ++i) s += x[g * x_gstride + (int64_t)i * F + f];
+    y[t] = s / n;
+  }
+}
+
+__global__ __launch_bounds__(256) void agent_mean_bwd_kernel(const float* dy, float* dx, int64_t G, int n, int F,
+                                                             int64_t dx_gstride) {
+  const int64_t total = G * n * F;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t g = t / ((int64_t)n * F);
+    const int64_t rem = t - g * n * F;
+    const int i = (int)(rem / F), f = (int)(rem - (int64_t)(rem / F) * F);
+    dx[g * dx_gstride + (int64_t)i * F + f] = dy[g * F + f] / n;
+  }
+}
+
+// ---- TanhNormal head (distribution.py:10-66 + tfp Normal / Tanh / Independent) ----------------
+__device__ __forceinline__ float log_ndtr_f(float z) {
+  if (z > -10.0f) return logf(0.5f * erfcf(-z * 0.70710678118654752f));
+  // asymptotic series for the far left tail
+  const float z2 = z * z;
+  const float s = 1.0f - 1.0f / z2 + 3.0f / (z2 * z2) - 15.0f / (z2 * z2 * z2);
+  return -0.5f * z2 - logf(-z) - 0.91893853320467274f + logf(s);
+}
+// d/dz log Phi(z) = phi(z) / Phi(z)
+__device__ __forceinline__ float dlog_ndtr_f(float z) {
+  const float lp = -0.5f * z * z - 0.91893853320467274f;
+  return expf(lp - log_ndtr_f(z));
+}
+__device__ __forceinline__ float tanh_fldj_f(float x) {  // 2 (log 2 - x - softplus(-2x))
+  return 2.0f * (0.69314718055994531f - x - softplusf_(-2.0f * x));
+}
+
+__global__ __launch_bounds__(256) void tanh_normal_kernel(dgppo_tanh_normal_args p) {
+  constexpr float kThr = 0.999f;
+  const float inv_t = atanhf(kThr);
+  const float log_eps = logf(1.0f - kThr);
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < p.rows; r += (int64_t)gridDim.x * 256) {
+    float lp_sum = 0.0f, ent_sum = 0.0f;
+    for (int j = 0; j < p.A; ++j) {
+      const int64_t k = r * p.A + j;
+      const float mu = p.mean[k];
+      const float sraw = p.std_raw[k] + p.std_shift;
+      const float sd = softplusf_(sraw) + p.std_min;
+      if (p.std_out) p.std_out[k] = sd;
+      float a;
+      if (p.mode == 0) a = tanhf(mu);                         // mode(): tanh(mean)
+      else if (p.mode == 1) a = tanhf(mu + sd * p.noise[k]);  // sample
+      else a = p.action[k];                                   // evaluate given actions
+      if (p.mode <= 1 && p.action_out) p.action_out[k] = a;
+      // log_prob with the threshold clip
+      const float v = fminf(fmaxf(a, -kThr), kThr);
+      float lp, dmu, dsd;
+      if (v <= -kThr) {
+        const float w = (-inv_t - mu) / sd;
+        lp = log_ndtr_f(w) - log_eps;
+        const float lam = dlog_ndtr_f(w);
+        dmu = -lam / sd;
+        dsd = -lam * w / sd;
+      } else if (v >= kThr) {
+        const float u = (mu - inv_t) / sd;
+        lp = log_ndtr_f(u) - log_eps;
+        const float lam = dlog_ndtr_f(u);
+        dmu = lam / sd;
+        dsd = -lam * u / sd;
+      } else {
+        const float x = atanhf(v);
+        const float z = (x - mu) / sd;
+        lp = -0.5f * z * z - logf(sd) - 0.91893853320467274f - tanh_fldj_f(x);
+        dmu = z / sd;
+        dsd = (z * z - 1.0f) / sd;
+      }
+      lp_sum += lp;
+      float dmu_e = 0.0f, dsd_e = 0.0f;
+      if (p.entropy_eps) {  // entropy = N entropy + fldj(mu + sd * eps_fixed[agent])
+        const int agent = (int)(r % p.n_agents);
+        const float eps = p.entropy_eps[agent * p.A + j];
+        const float ysmp = mu + sd * eps;
+        ent_sum += 1.41893853320467274f + logf(sd) + tanh_fldj_f(ysmp);
+        const float dfl = -2.0f * tanhf(ysmp);
+        dmu_e = dfl;
+        dsd_e = 1.0f / sd + dfl * eps;
+      }
+      if (p.dmean) {  // backward: upstream dlog_pi[r], dentropy[r]
+        const float glp = p.dlog_pi ? p.dlog_pi[r] : 0.0f;
+        const float gen = p.dentropy ? p.dentropy[r] : 0.0f;
+        const float dsd_tot = glp * dsd + gen * dsd_e;
+        p.dmean[k] = glp * dmu + gen * dmu_e;
+        p.dstd_raw[k] = dsd_tot * sigmoidf_(sraw);
+      }
+    }
+    if (p.log_pi) p.log_pi[r] = lp_sum;
+    if (p.entropy) p.entropy[r] = ent_sum;
+  }
+}
+
+// ---- losses ------------------------------------------------------------------------------------
+// block partial sums: part[block*8 + q]
+__device__ __forceinline__ void block_sums(float* vals, int nv, float* part) {
+  __shared__ float red[8][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int q = 0; q < nv; ++q) {
+    const float s = wave_sum(vals[q]);
+    if (lane == 0) red[q][wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int q = threadIdx.x;
+    part[blockIdx.x * 8 + q] = red[q][0] + red[q][1] + red[q][2] + red[q][3];
+  }
+}
+
+// PPO clipped surrogate (informarl.py:428-438): grads into dlog_pi / dentropy; stats partials:
+// [sum max(l1,l2), sum entropy, sum (l2 > l1), sum |ratio - 1|]
+__global__ __launch_bounds__(256) void ppo_loss_kernel(const float* log_pi, const float* log_pi_old, const float* adv,
+                                                       const float* entropy, int64_t n, float clip_eps, float coef_ent,
+                                                       float* dlog_pi, float* dentropy, float* part) {
+  float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const float inv_n = 1.0f / (float)n;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const float r = expf(log_pi[t] - log_pi_old[t]);
+    const float A = adv[t];
+    const float l1 = -r * A;
+    const float rc = fminf(fmaxf(r, 1.0f - clip_eps), 1.0f + clip_eps);
+    const float l2 = -rc * A;
+    const float in_range = (r >= 1.0f - clip_eps && r <= 1.0f + clip_eps) ? 1.0f : 0.0f;
+    float g;
+    if (l1 > l2) g = -A * r;
+    else if (l1 < l2) g = -A * r * in_range;
+    else g = 0.5f * (-A * r) + 0.5f * (-A * r * in_range);  // jnp.maximum splits ties
+    dlog_pi[t] = g * inv_n;
+    dentropy[t] = -coef_ent * inv_n;
+    v[0] += fmaxf(l1, l2);
+    v[1] += entropy[t];
+    v[2] += l2 > l1 ? 1.0f : 0.0f;
+    v[3] += fabsf(r - 1.0f);
+  }
+  block_sums(v, 4, part);
+}
+
+// 0.5 * mean (pred - target)^2 (optax.l2_loss): grad = (pred - target) / n; partial [sum loss]
+__global__ __launch_bounds__(256) void l2_loss_kernel(const float* pred, const float* target, int64_t n,
+                                                      float* dpred, float* part) {
+  float v[1] = {0.0f};
+  const float inv_n = 1.0f / (float)n;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const float d = pred[t] - target[t];
+    dpred[t] = d * inv_n;
+    v[0] += 0.5f * d * d;
+  }
+  block_sums(v, 1, part);
+}
+
+__global__ __launch_bounds__(64) void partial_reduce_kernel(const float* part, int nparts, int nv, float* out,
+                                                            float scale) {
+  if (threadIdx.x < nv) {
+    float s = 0.0f;
+    for (int b = 0; b < nparts; ++b) s += part[b * 8 + threadIdx.x];
+    out[threadIdx.x] = s * scale;
+  }
+}
+
+// ---- Dec-OCP GAE (algo/utils.py:11-79), literal reverse scan; one workgroup per env ------------
+// lanes over the (T+1)-long rows; the carry rows live in LDS.
+__global__ __launch_bounds__(256) void gae_kernel(dgppo_gae_args p) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int T = p.T, n = p.n_agents, nh = p.n_h, Tp1 = T + 1;
+  const int K = n * nh;
+  float* vh_row = sh;                    // (T+1, K)
+  float* vl_row = vh_row + Tp1 * K;      // (T+1)
+  float* coef = vl_row + Tp1;            // (T+1)
+  float* red = coef + Tp1;               // (4 waves, K + 1)
+  const int64_t b = blockIdx.x;
+  const float* hs = p.hs + b * (int64_t)T * K;        // (T, n, nh)
+  const float* l = p.l + b * (int64_t)T;              // (T)
+  const float* Vh = p.Vh + b * (int64_t)Tp1 * K;      // (T+1, n, nh)
+  const float* Vl = p.Vl + b * (int64_t)Tp1;          // (T+1)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int t = tid; t < Tp1 * K; t += 256) vh_row[t] = t < K ? Vh[T * K + t] : 0.0f;
+  for (int t = tid; t < Tp1; t += 256) {
+    vl_row[t] = t == 0 ? Vl[T] : 0.0f;
+    coef[t] = t == 0 ? 1.0f : 0.0f;
+  }
+  __syncthreads();
+  const float gamma = p.gamma, lam = p.lambda;
+  for (int ii = T - 1; ii >= 0; --ii) {
+    // new rows (masked), weighted sums with the current coefficients
+    float acc[33];
+    for (int q = 0; q <= K; ++q) acc[q] = 0.0f;
+    const float lv = l[ii];
+    for (int t = tid; t < Tp1; t += 256) {
+      const bool m = t < ii + 1;
+      const float c = coef[t];
+      for (int a = 0; a < n; ++a) {
+        float hmax = hs[(int64_t)ii * K + a * nh];
+        for (int h = 1; h < nh; ++h) hmax = fmaxf(hmax, hs[(int64_t)ii * K + a * nh + h]);
+        for (int h = 0; h < nh; ++h) {
+          const int q = a * nh + h;
+          const float hv = hs[(int64_t)ii * K + q];
+          const float disc = (1.0f - gamma) * hmax + gamma * vh_row[t * K + q];
+          const float nv = m ? fmaxf(hv, disc) : 0.0f;
+          vh_row[t * K + q] = nv;
+          acc[q] += nv * c;
+        }
+      }
+      const float nl = m ? lv + gamma * vl_row[t] : 0.0f;
+      vl_row[t] = nl;
+      acc[K] += nl * c;
+    }
+    for (int q = 0; q <= K; ++q) {
+      const float s = wave_sum(acc[q]);
+      if (lane == 0) red[wave * (K + 1) + q] = s;
+    }
+    __syncthreads();
+    if (tid <= K) {
+      const float s = red[tid] + red[(K + 1) + tid] + red[2 * (K + 1) + tid] + red[3 * (K + 1) + tid];
+      if (tid < K) p.Qh[(b * T + ii) * K + tid] = s;
+      else p.Ql[b * T + ii] = s;
+    }
+    // row ii+1 <- current values; roll the coefficients
+    for (int q = tid; q < K; q += 256) vh_row[(ii + 1) * K + q] = Vh[(int64_t)ii * K + q];
+    if (tid == 0) vl_row[ii + 1] = Vl[ii];
+    __syncthreads();
+    float cprev = 0.0f;
+    for (int t = tid; t < Tp1; t += 256) cprev = t == 0 ? coef[T] : coef[t - 1];
+    __syncthreads();
+    for (int t = tid; t < Tp1; t += 256) {
+      float c = cprev;
+      if (t == 0) c = powf(lam, (float)(ii + 1));
+      if (t == 1) c = powf(lam, (float)ii) * (1.0f - lam);
+      coef[t] = c;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- global norm / finite check, clipped Adam (optax.adam + apply_if_finite) ------------------
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int64_t n, float* part) {
+  float v[2] = {0.0f, 0.0f};
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const float x = g[t];
+    v[0] += x * x;
+    v[1] += isfinite(x) ? 0.0f : 1.0f;
+  }
+  block_sums(v, 2, part);
+}
+
+// state[0] = global norm, state[1] = non-finite count, state[2] = adam step count (float)
+__global__ __launch_bounds__(64) void norm_final_kernel(const float* part, int nparts, float* state) {
+  if (threadIdx.x == 0) {
+    float s = 0.0f, nf = 0.0f;
+    for (int b = 0; b < nparts; ++b) {
+      s += part[b * 8 + 0];
+      nf += part[b * 8 + 1];
+    }
+    state[0] = sqrtf(s);
+    state[1] = nf;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* param, const float* grad, float* m, float* v, int64_t n,
+                                                   const float* state, float lr, float b1, float b2, float eps,
+                                                   float max_norm) {
+  if (state[1] != 0.0f) return;  // apply_if_finite: skip the whole update
+  const float gnorm = state[0];
+  const float c = fmaxf(max_norm, gnorm);
+  const float t = state[2] + 1.0f;
+  const float bc1 = 1.0f - powf(b1, t);
+  const float bc2 = 1.0f - powf(b2, t);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float g = (grad[i] / c) * max_norm;
+    const float mi = b1 * m[i] + (1.0f - b1) * g;
+    const float vi = b2 * v[i] + (1.0f - b2) * g * g;
+    m[i] = mi;
+    v[i] = vi;
+    param[i] = param[i] - lr * ((mi / bc1) / (sqrtf(vi / bc2) + eps));
+  }
+}
+
+__global__ void adam_count_kernel(float* state) {
+  if (threadIdx.x == 0 && state[1] == 0.0f) state[2] += 1.0f;
+}
+
+// ---- Philox normals (Box-Muller) ------------------------------------------------------------------
+__device__ __forceinline__ uint32_t philox_w(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                             uint32_t k1, int word) {
+  for (int rnd = 0; rnd < 10; ++rnd) {
+    if (rnd > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+  }
+  return word == 0 ? c0 : (word == 1 ? c1 : (word == 2 ? c2 : c3));
+}
+
+__global__ __launch_bounds__(256) void normal_kernel(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed,
+                                                     uint64_t stream_id) {
+  const uint64_t sd = seed_ptr ? *seed_ptr : seed;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const uint32_t c0 = (uint32_t)t, c1 = (uint32_t)(t >> 32);
+    const uint32_t a = philox_w(c0, c1, (uint32_t)stream_id, (uint32_t)(stream_id >> 32), (uint32_t)sd,
+                                (uint32_t)(sd >> 32), 0);
+    const uint32_t b = philox_w(c0, c1, (uint32_t)stream_id, (uint32_t)(stream_id >> 32), (uint32_t)sd,
+                                (uint32_t)(sd >> 32), 1);
+    const float u1 = ((a >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+    const float u2 = (b >> 8) * (1.0f / 16777216.0f);
+    out[t] = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958648f * u2);
+  }
+}
+
+__global__ __launch_bounds__(256) void relu_bwd_kernel(float* dy, const float* y, int64_t n) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256)
+    if (!(y[t] > 0.0f)) dy[t] = 0.0f;
+}
+
+static int grid_for(int64_t n) {
+  const int64_t b = (n + 255) / 256;
+  return (int)(b < 8192 ? (b < 1 ? 1 : b) : 8192);
+}
+
+}  // namespace dgppo
+
+using namespace dgppo;
+
+#define DG_STREAM(s) ((hipStream_t)(s))
+
+extern "C" int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* p, void* stream) {
+  if (!p || p->H < 1 || p->H > 3 || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > kMaxCand ||
+      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->q || !p->bk || !p->xcat || !p->cand)
+    return DGPPO_EINVAL;
+  if (p->G == 0) return 0;
+  hipLaunchKernelGGL(gnn_attn_fwd_kernel, dim3(p->G), dim3(64), 0, DG_STREAM(stream), *p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* p, void* stream) {
+  if (!p || p->H < 1 || p->H > 3 || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > kMaxCand ||
+      !p->attn || !p->dxcat || !p->dqt || !p->dq || !p->dbeta)
+    return DGPPO_EINVAL;
+  if (p->G == 0) return 0;
+  const size_t shmem = p->dx ? (size_t)p->N * p->D * sizeof(float) : 0;
+  if (shmem > 48 * 1024) return DGPPO_EINVAL;
+  hipLaunchKernelGGL(gnn_attn_bwd_kernel, dim3(p->G), dim3(64), shmem, DG_STREAM(stream), *p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_relu_bwd(float* dy, const float* y, int64_t n, void* stream) {
+  if (n < 0 || !dy || !y) return DGPPO_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), dy, y, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_layernorm_fwd(const float* x, const float* scale, const float* bias, float* y, float* mean,
+                                   float* rstd, int64_t rows, int32_t F, int32_t relu, float eps, void* stream) {
+  if (rows < 0 || F < 1 || !x || !scale || !bias || !y || !mean || !rstd) return DGPPO_EINVAL;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, DG_STREAM(stream), x,
+                     scale, bias, y, mean, rstd, rows, F, relu, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t dgppo_layernorm_bwd_workspace_floats(int64_t rows, int32_t F) {
+  const int64_t rpb = 64;
+  return ((rows + rpb - 1) / rpb) * 2 * F;
+}
+
+// dscale / dbias are ACCUMULATED (+=) so one call serves a whole parameter-gradient buffer
+extern "C" int dgppo_layernorm_bwd(const float* x, const float* y, const float* dy, const float* scale,
+                                   const float* mean, const float* rstd, float* dx, float* dscale, float* dbias,
+                                   int64_t rows, int32_t F, int32_t relu, float* workspace, void* stream) {
+  if (rows < 0 || F < 1 || !x || !dy || !scale || !dx || !dscale || !dbias || !workspace || (relu && !y))
+    return DGPPO_EINVAL;
+  if (rows == 0) return 0;
+  const int rpb = 64;
+  const int nb = (int)((rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), 8 * F * sizeof(float), DG_STREAM(stream), x, y, dy,
+                     scale, mean, rstd, dx, workspace, rows, F, relu, rpb);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(256), 0, DG_STREAM(stream), workspace, nb, F,
+                     (int64_t)2 * F, dscale, 1.0f, 1.0f);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(256), 0, DG_STREAM(stream), workspace + F, nb, F,
+                     (int64_t)2 * F, dbias, 1.0f, 1.0f);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t dgppo_colsum_workspace_floats(int64_t rows, int32_t cols) {
+  const int64_t rpb = 256;
+  return ((rows + rpb - 1) / rpb) * cols;
+}
+
+// out = alpha * colsum(x) + beta * out, deterministic
+extern "C" int dgppo_colsum(const float* x, int64_t rows, int32_t cols, int64_t ld, int32_t grp, int64_t gstride,
+                            float* out, float alpha, float beta, float* workspace, void* stream) {
+  if (rows < 0 || cols < 1 || !x || !out || !workspace) return DGPPO_EINVAL;
+  const int64_t rpb = 256;
+  const int nb = (int)((rows + rpb - 1) / rpb);
+  if (nb > 0)
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, DG_STREAM(stream), x, rows, cols, ld, grp,
+                       gstride, workspace, rpb);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, DG_STREAM(stream), workspace, nb,
+                     cols, (int64_t)cols, out, alpha, beta);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_gru_fwd(const float* gi, const float* gh, const float* bhn, const float* h, float* h_new,
+                             int64_t rows, int32_t H, void* stream) {
+  if (rows < 0 || H < 1 || !gi || !gh || !bhn || !h || !h_new) return DGPPO_EINVAL;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(gru_fwd_kernel, dim3(grid_for(rows * H)), dim3(256), 0, DG_STREAM(stream), gi, gh, bhn, h,
+                     h_new, rows, H);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_gru_bwd(const float* gi, const float* gh, const float* bhn, const float* h, const float* dh_new,
+                             float* dgi, float* dgh, float* dh, int64_t rows, int32_t H, void* stream) {
+  if (rows < 0 || H < 1 || !gi || !gh || !bhn || !h || !dh_new || !dgi || !dgh || !dh) return DGPPO_EINVAL;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(gru_bwd_kernel, dim3(grid_for(rows * H)), dim3(256), 0, DG_STREAM(stream), gi, gh, bhn, h,
+                     dh_new, dgi, dgh, dh, rows, H);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_agent_mean_fwd(const float* x, float* y, int64_t G, int32_t n, int32_t F, int64_t x_gstride,
+                                    void* stream) {
+  if (G < 0 || n < 1 || F < 1 || !x || !y) return DGPPO_EINVAL;
+  if (G == 0) return 0;
+  hipLaunchKernelGGL(agent_mean_fwd_kernel, dim3(grid_for(G * F)), dim3(256), 0, DG_STREAM(stream), x, y, G, n, F,
+                     x_gstride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_agent_mean_bwd(const float* dy, float* dx, int64_t G, int32_t n, int32_t F, int64_t dx_gstride,
+                                    void* stream) {
+  if (G < 0 || n < 1 || F < 1 || !dx || !dy) return DGPPO_EINVAL;
+  if (G == 0) return 0;
+  hipLaunchKernelGGL(agent_mean_bwd_kernel, dim3(grid_for(G * n * F)), dim3(256), 0, DG_STREAM(stream), dy, dx, G,
+                     n, F, dx_gstride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_tanh_normal(const dgppo_tanh_normal_args* p, void* stream) {
+  if (!p || p->rows < 0 || p->A < 1 || !p->mean || !p->std_raw || p->mode < 0 || p->mode > 2) return DGPPO_EINVAL;
+  if (p->mode == 1 && !p->noise) return DGPPO_EINVAL;
+  if (p->mode == 2 && !p->action) return DGPPO_EINVAL;
+  if (p->dmean && !p->dstd_raw) return DGPPO_EINVAL;
+  if (p->entropy_eps && p->n_agents < 1) return DGPPO_EINVAL;
+  if (p->rows == 0) return 0;
+  hipLaunchKernelGGL(tanh_normal_kernel, dim3(grid_for(p->rows)), dim3(256), 0, DG_STREAM(stream), *p);
+  return (int)hipGetLastError();
+}
+
+static const int kLossBlocks = 512;
+
+extern "C" int64_t dgppo_loss_workspace_floats(void) { return (int64_t)kLossBlocks * 8; }
+
+// stats out (4 floats): [mean max(l1,l2), mean entropy, clip_frac, total_variation_dist]
+extern "C" int dgppo_ppo_loss(const float* log_pi, const float* log_pi_old, const float* adv, const float* entropy,
+                              int64_t n, float clip_eps, float coef_ent, float* dlog_pi, float* dentropy, float* stats,
+                              float* workspace, void* stream) {
+  if (n < 1 || !log_pi || !log_pi_old || !adv || !entropy || !dlog_pi || !dentropy || !stats || !workspace)
+    return DGPPO_EINVAL;
+  hipLaunchKernelGGL(ppo_loss_kernel, dim3(kLossBlocks), dim3(256), 0, DG_STREAM(stream), log_pi, log_pi_old, adv,
+                     entropy, n, clip_eps, coef_ent, dlog_pi, dentropy, workspace);
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), workspace, kLossBlocks, 4,
+                     stats, 1.0f / (float)n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_l2_loss(const float* pred, const float* target, int64_t n, float* dpred, float* loss,
+                             float* workspace, void* stream) {
+  if (n < 1 || !pred || !target || !dpred || !loss || !workspace) return DGPPO_EINVAL;
+  hipLaunchKernelGGL(l2_loss_kernel, dim3(kLossBlocks), dim3(256), 0, DG_STREAM(stream), pred, target, n, dpred,
+                     workspace);
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), workspace, kLossBlocks, 1, loss,
+                     1.0f / (float)n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_gae(const dgppo_gae_args* p, void* stream) {
+  if (!p || p->B < 0 || p->T < 1 || p->T > 255 || p->n_agents < 1 || p->n_h < 1 || p->n_agents * p->n_h > 32 ||
+      !p->hs || !p->l || !p->Vh || !p->Vl || !p->Qh || !p->Ql)
+    return DGPPO_EINVAL;
+  if (p->B == 0) return 0;
+  const int K = p->n_agents * p->n_h;
+  const size_t shmem = ((size_t)(p->T + 1) * (K + 2) + 4 * (K + 1)) * sizeof(float);
+  hipLaunchKernelGGL(gae_kernel, dim3((unsigned)p->B), dim3(256), shmem, DG_STREAM(stream), *p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace, void* stream) {
+  if (n < 0 || !grad || !state || !workspace) return DGPPO_EINVAL;
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kLossBlocks), dim3(256), 0, DG_STREAM(stream), grad, n, workspace);
+  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), workspace, kLossBlocks, state);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr,
+                          float b1, float b2, float eps, float max_norm, void* stream) {
+  if (n < 0 || !param || !grad || !m || !v || !state) return DGPPO_EINVAL;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), param, grad, m, v, n, state, lr,
+                     b1, b2, eps, max_norm);
+  hipLaunchKernelGGL(adam_count_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), state);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_normal(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed, uint64_t stream_id,
+                            void* stream) {
+  if (n < 0 || !out) return DGPPO_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(normal_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), out, n, seed_ptr, seed,
+                     stream_id);
+  return (int)hipGetLastError();
+}

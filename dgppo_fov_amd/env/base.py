@@ -210,6 +210,27 @@ class MultiAgentEnv(ABC):
             self._dev_cache[key] = t.to(device)
         return self._dev_cache[key]
 
+    def agent_candidates(self, device=None) -> torch.Tensor:
+        """(n, C) int32: for each agent i, the edge ids of the padded layout whose receiver may be i
+        (agent-agent row i, its goal edge(s), its lidar hits / obstacle edges).  The GNN kernels
+        keep a candidate iff receivers[e] == i at run time (masked edges point at the pad node)."""
+        device = device or self.device
+        key = ("cand", str(device))
+        if key not in self._dev_cache:
+            n = self._num_agents
+            spread = self.GOAL_MODE == _lib.DGPPO_GOAL_SPREAD
+            n_ag = n * n if spread else n
+            mpe = self.ENGINE == _lib.DGPPO_ENGINE_MPE
+            k = self.n_obs if mpe else (int(self._params.get("top_k_rays", 0)) if self.n_obs > 0 else 0)
+            rows = []
+            for i in range(n):
+                r = [i * n + j for j in range(n)]
+                r += [n * n + i * n + j for j in range(n)] if spread else [n * n + i]
+                r += [n * n + n_ag + i * k + h for h in range(k)]
+                rows.append(r)
+            self._dev_cache[key] = torch.tensor(rows, dtype=torch.int32).to(device)
+        return self._dev_cache[key]
+
     # ---- buffers ----------------------------------------------------------------------------
     def empty_graph(self, batch_shape, device=None) -> GraphsTuple:
         """Allocate an uninitialised batched graph (the kernel fills every element)."""

@@ -1,0 +1,165 @@
+"""Typed wrappers over the hot-path-(2) C-ABI (include/dgppo_hip.h) for torch device tensors.
+
+Every function launches on torch's current stream and returns immediately; there is no CPU
+path (non-CUDA tensors raise NativeLibraryError)."""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from .. import _lib
+
+_WS = {}
+
+
+def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
+    """Grow-only scratch buffer per (device, slot); safe to reuse across sequential launches."""
+    key = (str(device), slot)
+    t = _WS.get(key)
+    if t is None or t.numel() < nfloats:
+        t = torch.empty(max(int(nfloats), 1024), dtype=torch.float32, device=device)
+        _WS[key] = t
+    return t
+
+
+def _p(t, off=0):
+    return 0 if t is None else int(t.data_ptr()) + 4 * int(off)
+
+
+def _stream(t):
+    return _lib.stream_handle(t.device)
+
+
+def _chk(rc, what):
+    _lib.check(rc, what)
+
+
+def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
+         a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
+         bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
+         alpha=1.0, beta=0.0, relu=False, split_k=None):
+    """C = alpha op(A) op(B) + beta C + bias + addend (see dgppo_gemm).  Element offsets/strides."""
+    lib = _lib.load()
+    _lib.require_gpu(C.device, "gemm")
+    g = _lib.GemmArgs()
+    g.M, g.N, g.K, g.batch = int(M), int(N), int(K), int(batch)
+    g.trans_a, g.trans_b = int(ta), int(tb)
+    g.A, g.lda, g.stride_a = _p(A, a_off), int(lda if lda is not None else (M if ta else K)), int(sa)
+    g.B, g.ldb, g.stride_b = _p(B, b_off), int(ldb if ldb is not None else (K if tb else N)), int(sb)
+    g.C, g.ldc, g.stride_c = _p(C, c_off), int(ldc if ldc is not None else N), int(sc)
+    g.a_grp, g.b_grp, g.c_grp = int(a_grp), int(b_grp), int(c_grp)
+    g.a_gstride, g.b_gstride, g.c_gstride = int(a_gs), int(b_gs), int(c_gs)
+    g.bias = _p(bias)
+    g.addend, g.ld_add, g.stride_add = _p(addend, add_off), int(ld_add if ld_add is not None else N), 0
+    g.add_grp, g.add_gstride = int(add_grp), int(add_gs)
+    g.alpha, g.beta, g.relu = float(alpha), float(beta), int(relu)
+    if split_k is None:
+        tiles = math.ceil(M / 64) * math.ceil(N / 64) * batch
+        split_k = max(1, min(math.ceil(K / 512), 1024 // max(tiles, 1))) if K >= 2048 else 1
+    g.split_k = int(split_k)
+    ws = None
+    if g.split_k > 1:
+        ws = workspace(lib.dgppo_gemm_workspace_floats(ctypes.byref(g)), C.device, "gemm")
+    g.workspace = _p(ws)
+    _chk(lib.dgppo_gemm(ctypes.byref(g), _stream(C)), "dgppo_gemm")
+
+
+def colsum(x, rows, cols, out, *, ld=None, grp=0, gs=0, x_off=0, alpha=1.0, beta=0.0):
+    lib = _lib.load()
+    ws = workspace(lib.dgppo_colsum_workspace_floats(int(rows), int(cols)), out.device, "colsum")
+    _chk(lib.dgppo_colsum(_p(x, x_off), int(rows), int(cols), int(ld if ld is not None else cols), int(grp), int(gs),
+                          _p(out), float(alpha), float(beta), _p(ws), _stream(out)), "dgppo_colsum")
+
+
+def relu_bwd_(dy, y):
+    _chk(_lib.load().dgppo_relu_bwd(_p(dy), _p(y), int(dy.numel()), _stream(dy)), "dgppo_relu_bwd")
+
+
+def layernorm_fwd(x, scale, bias, y, mean, rstd, relu=True, eps=1e-6):
+    rows, F = x.shape
+    _chk(_lib.load().dgppo_layernorm_fwd(_p(x), _p(scale), _p(bias), _p(y), _p(mean), _p(rstd), int(rows), int(F),
+                                         int(relu), float(eps), _stream(x)), "dgppo_layernorm_fwd")
+
+
+def layernorm_bwd(x, y, dy, scale, mean, rstd, dx, dscale, dbias, relu=True):
+    lib = _lib.load()
+    rows, F = x.shape
+    ws = workspace(lib.dgppo_layernorm_bwd_workspace_floats(int(rows), int(F)), x.device, "ln")
+    _chk(lib.dgppo_layernorm_bwd(_p(x), _p(y), _p(dy), _p(scale), _p(mean), _p(rstd), _p(dx), _p(dscale), _p(dbias),
+                                 int(rows), int(F), int(relu), _p(ws), _stream(x)), "dgppo_layernorm_bwd")
+
+
+def gru_fwd(gi, gh, bhn, h, h_new):
+    rows, H = h.shape
+    _chk(_lib.load().dgppo_gru_fwd(_p(gi), _p(gh), _p(bhn), _p(h), _p(h_new), int(rows), int(H), _stream(h)),
+         "dgppo_gru_fwd")
+
+
+def gru_bwd(gi, gh, bhn, h, dh_new, dgi, dgh, dh):
+    rows, H = h.shape
+    _chk(_lib.load().dgppo_gru_bwd(_p(gi), _p(gh), _p(bhn), _p(h), _p(dh_new), _p(dgi), _p(dgh), _p(dh), int(rows),
+                                   int(H), _stream(h)), "dgppo_gru_bwd")
+
+
+def agent_mean_fwd(x, y, G, n, F, x_gstride):
+    _chk(_lib.load().dgppo_agent_mean_fwd(_p(x), _p(y), int(G), int(n), int(F), int(x_gstride), _stream(y)),
+         "dgppo_agent_mean_fwd")
+
+
+def agent_mean_bwd(dy, dx, G, n, F, dx_gstride):
+    _chk(_lib.load().dgppo_agent_mean_bwd(_p(dy), _p(dx), int(G), int(n), int(F), int(dx_gstride), _stream(dx)),
+         "dgppo_agent_mean_bwd")
+
+
+def gnn_attn(args: _lib.GnnAttnArgs, backward: bool, device):
+    lib = _lib.load()
+    fn = lib.dgppo_gnn_attn_bwd if backward else lib.dgppo_gnn_attn_fwd
+    _chk(fn(ctypes.byref(args), _lib.stream_handle(device)), "dgppo_gnn_attn")
+
+
+def tanh_normal(args: _lib.TanhNormalArgs, device):
+    _chk(_lib.load().dgppo_tanh_normal(ctypes.byref(args), _lib.stream_handle(device)), "dgppo_tanh_normal")
+
+
+def ppo_loss(log_pi, log_pi_old, adv, entropy, clip_eps, coef_ent, dlog_pi, dentropy, stats):
+    lib = _lib.load()
+    ws = workspace(lib.dgppo_loss_workspace_floats(), log_pi.device, "loss")
+    _chk(lib.dgppo_ppo_loss(_p(log_pi), _p(log_pi_old), _p(adv), _p(entropy), int(log_pi.numel()), float(clip_eps),
+                            float(coef_ent), _p(dlog_pi), _p(dentropy), _p(stats), _p(ws), _stream(log_pi)),
+         "dgppo_ppo_loss")
+
+
+def l2_loss(pred, target, dpred, loss):
+    lib = _lib.load()
+    ws = workspace(lib.dgppo_loss_workspace_floats(), pred.device, "loss")
+    _chk(lib.dgppo_l2_loss(_p(pred), _p(target), int(pred.numel()), _p(dpred), _p(loss), _p(ws), _stream(pred)),
+         "dgppo_l2_loss")
+
+
+def gae(hs, l, Vh, Vl, Qh, Ql, gamma, lam):
+    B, T, n, nh = hs.shape
+    a = _lib.GaeArgs()
+    a.B, a.T, a.n_agents, a.n_h = int(B), int(T), int(n), int(nh)
+    a.hs, a.l, a.Vh, a.Vl, a.Qh, a.Ql = _p(hs), _p(l), _p(Vh), _p(Vl), _p(Qh), _p(Ql)
+    a.gamma = float(gamma)
+    setattr(a, "lambda", float(lam))
+    _chk(_lib.load().dgppo_gae(ctypes.byref(a), _stream(hs)), "dgppo_gae")
+
+
+def grad_norm(grad, state):
+    lib = _lib.load()
+    ws = workspace(lib.dgppo_loss_workspace_floats(), grad.device, "norm")
+    _chk(lib.dgppo_grad_norm(_p(grad), int(grad.numel()), _p(state), _p(ws), _stream(grad)), "dgppo_grad_norm")
+
+
+def adam(param, grad, m, v, state, lr, b1=0.9, b2=0.999, eps=1e-8, max_norm=2.0):
+    _chk(_lib.load().dgppo_adam(_p(param), _p(grad), _p(m), _p(v), int(param.numel()), _p(state), float(lr),
+                                float(b1), float(b2), float(eps), float(max_norm), _stream(param)), "dgppo_adam")
+
+
+def normal_(out, seed=0, stream_id=0, seed_tensor=None):
+    _chk(_lib.load().dgppo_normal(_p(out), int(out.numel()), _p(seed_tensor), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                  int(stream_id) & 0xFFFFFFFFFFFFFFFF, _stream(out)), "dgppo_normal")
+    return out

@@ -1,0 +1,488 @@
+"""Network layers of the DGPPO actor / critics with explicit forward and backward passes.
+
+Counterparts of dgppo/nn/gnn.py (GraphTransformer, GraphTransformerGNN), dgppo/nn/mlp.py (MLP with
+LayerNorm), dgppo/nn/rnn.py + flax GRUCell, and flax Dense.  Parameters of a network live in ONE
+flat fp32 buffer (and gradients in a twin buffer), so gradient clipping, the finite check, Adam
+and the multi-GPU all-reduce are single launches over contiguous memory.  All arithmetic runs in
+libdgppo_hip.so (dgppo_gemm, dgppo_gnn_attn_*, dgppo_layernorm_*, dgppo_gru_*); torch only
+allocates.
+
+Kernel-side parameter layouts (converted from / to the flax layout by `to_flax` / `from_flax`):
+  Dense          W (in, out), b (out)                              == flax kernel, bias
+  GraphTransformer (D -> F, H heads)
+                 Wq (D, H*F), bq (H*F)                             == Dense_0 (query)
+                 Wkt (H, F, D), bk (H*F)   Wkt[h] = Dense_1.kernel[:, hF:(h+1)F]^T (key)
+                 Wcat (H*(D+5), F) = [Wv (H*D, F); We (H*4, F); bv (H, F)] stacked per head
+                   Wv[h*D + d] = Dense_2.kernel[d, hF:(h+1)F], We from Dense_3 (edge, no bias),
+                   bv[h] = Dense_2.bias[hF:(h+1)F]
+                 Wu (D, F), bu (F)                                 == Dense_4 (update)
+  GRUCell(64)    Wi (64, 192) = [ir | iz | in], bi (192), Wh (64, 192) = [hr | hz | hn], bhn (64)
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import kernels as K
+
+
+# ---- parameter space ------------------------------------------------------------------------
+class ParamSpace:
+    """Flat parameter + gradient buffers with named views."""
+
+    def __init__(self):
+        self.entries: List[Tuple[str, Tuple[int, ...], str]] = []
+        self.offsets: Dict[str, int] = {}
+        self.size = 0
+        self.flat = None
+        self.grad = None
+
+    def add(self, name: str, shape, init: str) -> str:
+        shape = tuple(int(s) for s in shape)
+        assert name not in self.offsets, name
+        self.offsets[name] = self.size
+        self.entries.append((name, shape, init))
+        self.size += int(np.prod(shape))
+        return name
+
+    def build(self, device):
+        self.flat = torch.zeros(self.size, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.size, dtype=torch.float32, device=device)
+        self._views = {}
+        for n, shape, _ in self.entries:
+            o, sz = self.offsets[n], int(np.prod(shape))
+            self._views[(n, False)] = self.flat[o:o + sz].view(shape)
+            self._views[(n, True)] = self.grad[o:o + sz].view(shape)
+        return self
+
+    def view(self, name: str, grad: bool = False) -> torch.Tensor:
+        return self._views[(name, bool(grad))]
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def swap_views(self):
+        """Exchange parameter and gradient views (lets the flax exporters export gradients)."""
+        for n, _, _ in self.entries:
+            self._views[(n, False)], self._views[(n, True)] = self._views[(n, True)], self._views[(n, False)]
+
+    def state_dict(self):
+        return {n: self.view(n).detach().cpu().clone() for n, _, _ in self.entries}
+
+    def load_state_dict(self, sd):
+        for n, shape, _ in self.entries:
+            self.view(n).copy_(torch.as_tensor(sd[n]).reshape(shape))
+
+
+# ---- host-side initialisers (one-time, not on the hot path) -----------------------------------
+def orthogonal(rng: np.random.Generator, shape, scale=1.0):
+    """flax.linen.initializers.orthogonal for a (in, out) kernel."""
+    n_rows, n_cols = shape
+    a = rng.standard_normal((max(n_rows, n_cols), min(n_rows, n_cols)))
+    q, r = np.linalg.qr(a)
+    q = q * np.sign(np.diag(r))
+    if n_rows < n_cols:
+        q = q.T
+    return (scale * q[:n_rows, :n_cols]).astype(np.float32)
+
+
+def lecun_normal(rng: np.random.Generator, shape):
+    """flax lecun_normal: truncated normal (2 sd) with variance 1 / fan_in."""
+    std = math.sqrt(1.0 / shape[0]) / 0.87962566103423978
+    x = rng.standard_normal(shape)
+    while True:
+        bad = np.abs(x) > 2
+        if not bad.any():
+            break
+        x[bad] = rng.standard_normal(bad.sum())
+    return (x * std).astype(np.float32)
+
+
+# ---- building blocks ----------------------------------------------------------------------
+class Dense:
+    def __init__(self, ps: ParamSpace, name: str, d_in: int, d_out: int, bias=True, init="orthogonal", scale=1.0):
+        self.ps, self.name, self.d_in, self.d_out, self.has_bias = ps, name, d_in, d_out, bias
+        self.init, self.scale = init, scale
+        ps.add(name + ".W", (d_in, d_out), init)
+        if bias:
+            ps.add(name + ".b", (d_out,), "zeros")
+
+    def W(self, g=False):
+        return self.ps.view(self.name + ".W", g)
+
+    def b(self, g=False):
+        return self.ps.view(self.name + ".b", g) if self.has_bias else None
+
+    def flax(self) -> dict:
+        d = {"kernel": self.W().detach().cpu().numpy()}
+        if self.has_bias:
+            d["bias"] = self.b().detach().cpu().numpy()
+        return d
+
+    def load_flax(self, d):
+        self.W().copy_(torch.as_tensor(np.asarray(d["kernel"], np.float32)))
+        if self.has_bias:
+            self.b().copy_(torch.as_tensor(np.asarray(d["bias"], np.float32)))
+
+    def init_host(self, rng):
+        if self.init == "orthogonal":
+            w = orthogonal(rng, (self.d_in, self.d_out), self.scale)
+        else:
+            w = lecun_normal(rng, (self.d_in, self.d_out))
+        self.W().copy_(torch.from_numpy(w))
+
+    def fwd(self, x, rows, out=None, relu=False):
+        y = out if out is not None else torch.empty((rows, self.d_out), device=x.device)
+        K.gemm(x, self.W(), y, rows, self.d_out, self.d_in, bias=self.b(), relu=relu)
+        return y
+
+    def bwd(self, x, dy, rows, need_dx=True, dx_out=None, accumulate=False):
+        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0)
+        if self.has_bias:
+            K.colsum(dy, rows, self.d_out, self.b(True), beta=1.0)
+        if not need_dx:
+            return None
+        dx = dx_out if dx_out is not None else torch.empty((rows, self.d_in), device=dy.device)
+        K.gemm(dy, self.W(), dx, rows, self.d_in, self.d_out, tb=True, ldb=self.d_out, beta=1.0 if accumulate else 0.0)
+        return dx
+
+
+class LayerNormReLU:
+    def __init__(self, ps: ParamSpace, name: str, F: int):
+        self.ps, self.name, self.F = ps, name, F
+        ps.add(name + ".scale", (F,), "ones")
+        ps.add(name + ".bias", (F,), "zeros")
+
+    def init_host(self, rng):
+        self.ps.view(self.name + ".scale").fill_(1.0)
+
+    def flax(self):
+        return {"scale": self.ps.view(self.name + ".scale").cpu().numpy(),
+                "bias": self.ps.view(self.name + ".bias").cpu().numpy()}
+
+    def load_flax(self, d):
+        self.ps.view(self.name + ".scale").copy_(torch.as_tensor(np.asarray(d["scale"], np.float32)))
+        self.ps.view(self.name + ".bias").copy_(torch.as_tensor(np.asarray(d["bias"], np.float32)))
+
+    def fwd(self, x):
+        rows = x.shape[0]
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, device=x.device)
+        rstd = torch.empty(rows, device=x.device)
+        K.layernorm_fwd(x, self.ps.view(self.name + ".scale"), self.ps.view(self.name + ".bias"), y, mean, rstd)
+        return y, (x, y, mean, rstd)
+
+    def bwd(self, cache, dy):
+        x, y, mean, rstd = cache
+        dx = torch.empty_like(x)
+        K.layernorm_bwd(x, y, dy, self.ps.view(self.name + ".scale"), mean, rstd, dx,
+                        self.ps.view(self.name + ".scale", True), self.ps.view(self.name + ".bias", True))
+        return dx
+
+
+class MLPHead:
+    """MLP(hid_sizes=(64, 64), relu, act_final=True, layernorm) (dgppo/nn/mlp.py:6-30)."""
+
+    def __init__(self, ps, name, d_in=64, hid=64):
+        self.d0 = Dense(ps, name + ".Dense_0", d_in, hid)
+        self.ln0 = LayerNormReLU(ps, name + ".LayerNorm_0", hid)
+        self.d1 = Dense(ps, name + ".Dense_1", hid, hid)
+        self.ln1 = LayerNormReLU(ps, name + ".LayerNorm_1", hid)
+
+    def init_host(self, rng):
+        for m in (self.d0, self.ln0, self.d1, self.ln1):
+            m.init_host(rng)
+
+    def flax(self):
+        return {"Dense_0": self.d0.flax(), "LayerNorm_0": self.ln0.flax(), "Dense_1": self.d1.flax(),
+                "LayerNorm_1": self.ln1.flax()}
+
+    def load_flax(self, d):
+        self.d0.load_flax(d["Dense_0"]), self.ln0.load_flax(d["LayerNorm_0"])
+        self.d1.load_flax(d["Dense_1"]), self.ln1.load_flax(d["LayerNorm_1"])
+
+    def fwd(self, x):
+        rows = x.shape[0]
+        h0 = self.d0.fwd(x, rows)
+        y0, c0 = self.ln0.fwd(h0)
+        h1 = self.d1.fwd(y0, rows)
+        y1, c1 = self.ln1.fwd(h1)
+        return y1, (x, y0, c0, c1)
+
+    def bwd(self, cache, dy, need_dx=True):
+        x, y0, c0, c1 = cache
+        rows = x.shape[0]
+        dh1 = self.ln1.bwd(c1, dy)
+        dy0 = self.d1.bwd(y0, dh1, rows)
+        dh0 = self.ln0.bwd(c0, dy0)
+        return self.d0.bwd(x, dh0, rows, need_dx)
+
+
+class GRUCell:
+    """flax.linen.GRUCell(features=64) (used through dgppo/nn/rnn.py:15-30)."""
+
+    def __init__(self, ps, name, d_in=64, H=64):
+        self.ps, self.name, self.d_in, self.H = ps, name, d_in, H
+        ps.add(name + ".Wi", (d_in, 3 * H), "lecun")
+        ps.add(name + ".bi", (3 * H,), "zeros")
+        ps.add(name + ".Wh", (H, 3 * H), "orthogonal")
+        ps.add(name + ".bhn", (H,), "zeros")
+
+    def v(self, k, g=False):
+        return self.ps.view(self.name + "." + k, g)
+
+    def init_host(self, rng):
+        H = self.H
+        wi = np.concatenate([lecun_normal(rng, (self.d_in, H)) for _ in range(3)], axis=1)
+        wh = np.concatenate([orthogonal(rng, (H, H)) for _ in range(3)], axis=1)
+        self.v("Wi").copy_(torch.from_numpy(wi))
+        self.v("Wh").copy_(torch.from_numpy(wh))
+
+    def flax(self):
+        H = self.H
+        wi, bi, wh, bhn = (self.v(k).cpu().numpy() for k in ("Wi", "bi", "Wh", "bhn"))
+        return {"ir": {"kernel": wi[:, :H], "bias": bi[:H]}, "iz": {"kernel": wi[:, H:2 * H], "bias": bi[H:2 * H]},
+                "in": {"kernel": wi[:, 2 * H:], "bias": bi[2 * H:]}, "hr": {"kernel": wh[:, :H]},
+                "hz": {"kernel": wh[:, H:2 * H]}, "hn": {"kernel": wh[:, 2 * H:], "bias": bhn}}
+
+    def load_flax(self, d):
+        wi = np.concatenate([d["ir"]["kernel"], d["iz"]["kernel"], d["in"]["kernel"]], 1).astype(np.float32)
+        bi = np.concatenate([d["ir"]["bias"], d["iz"]["bias"], d["in"]["bias"]]).astype(np.float32)
+        wh = np.concatenate([d["hr"]["kernel"], d["hz"]["kernel"], d["hn"]["kernel"]], 1).astype(np.float32)
+        self.v("Wi").copy_(torch.from_numpy(wi))
+        self.v("bi").copy_(torch.from_numpy(bi))
+        self.v("Wh").copy_(torch.from_numpy(wh))
+        self.v("bhn").copy_(torch.as_tensor(np.asarray(d["hn"]["bias"], np.float32)))
+
+    def fwd(self, x, h):
+        rows, H = h.shape[0], self.H
+        gi = torch.empty((rows, 3 * H), device=x.device)
+        gh = torch.empty((rows, 3 * H), device=x.device)
+        K.gemm(x, self.v("Wi"), gi, rows, 3 * H, self.d_in, bias=self.v("bi"))
+        K.gemm(h, self.v("Wh"), gh, rows, 3 * H, H)
+        hn = torch.empty_like(h)
+        K.gru_fwd(gi, gh, self.v("bhn"), h, hn)
+        return hn, (x, h, gi, gh)
+
+    def bwd(self, cache, dhn, need_dx=True):
+        """returns (dx, dh)"""
+        x, h, gi, gh = cache
+        rows, H = h.shape[0], self.H
+        dgi = torch.empty_like(gi)
+        dgh = torch.empty_like(gh)
+        dh = torch.zeros_like(h)
+        K.gru_bwd(gi, gh, self.v("bhn"), h, dhn, dgi, dgh, dh)
+        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0)
+        K.colsum(dgi, rows, 3 * H, self.v("bi", True), beta=1.0)
+        K.gemm(h, dgh, self.v("Wh", True), H, 3 * H, rows, ta=True, beta=1.0)
+        K.colsum(dgh, rows, H, self.v("bhn", True), ld=3 * H, x_off=2 * H, beta=1.0)
+        K.gemm(dgh, self.v("Wh"), dh, rows, H, 3 * H, tb=True, ldb=3 * H, beta=1.0)
+        dx = None
+        if need_dx:
+            dx = torch.empty_like(x)
+            K.gemm(dgi, self.v("Wi"), dx, rows, self.d_in, 3 * H, tb=True, ldb=3 * H)
+        return dx, dh
+
+
+class GraphTransformer:
+    """GraphTransformer layer (dgppo/nn/gnn.py:78-117) in the per-receiving-agent form."""
+
+    def __init__(self, ps, name, D, F, H=3):
+        self.ps, self.name, self.D, self.F, self.H = ps, name, D, F, H
+        ps.add(name + ".Wq", (D, H * F), "orthogonal")
+        ps.add(name + ".bq", (H * F,), "zeros")
+        ps.add(name + ".Wkt", (H, F, D), "orthogonal")
+        ps.add(name + ".bk", (H * F,), "zeros")
+        ps.add(name + ".Wcat", (H * (D + 5), F), "orthogonal")
+        ps.add(name + ".Wu", (D, F), "orthogonal")
+        ps.add(name + ".bu", (F,), "zeros")
+
+    def v(self, k, g=False):
+        return self.ps.view(self.name + "." + k, g)
+
+    # ---- flax layout conversion (Dense_0..Dense_4 of the reference) ----
+    def load_flax(self, d):
+        D, F, H = self.D, self.F, self.H
+        f32 = lambda a: np.asarray(a, np.float32)  # noqa: E731
+        self.v("Wq").copy_(torch.from_numpy(f32(d["Dense_0"]["kernel"])))
+        self.v("bq").copy_(torch.from_numpy(f32(d["Dense_0"]["bias"])))
+        wk = f32(d["Dense_1"]["kernel"]).reshape(D, H, F).transpose(1, 2, 0)  # (H, F, D)
+        self.v("Wkt").copy_(torch.from_numpy(np.ascontiguousarray(wk)))
+        self.v("bk").copy_(torch.from_numpy(f32(d["Dense_1"]["bias"])))
+        wv = f32(d["Dense_2"]["kernel"]).reshape(D, H, F).transpose(1, 0, 2).reshape(H * D, F)
+        we = f32(d["Dense_3"]["kernel"]).reshape(4, H, F).transpose(1, 0, 2).reshape(H * 4, F)
+        bv = f32(d["Dense_2"]["bias"]).reshape(H, F)
+        self.v("Wcat").copy_(torch.from_numpy(np.concatenate([wv, we, bv], 0)))
+        self.v("Wu").copy_(torch.from_numpy(f32(d["Dense_4"]["kernel"])))
+        self.v("bu").copy_(torch.from_numpy(f32(d["Dense_4"]["bias"])))
+
+    def flax(self):
+        D, F, H = self.D, self.F, self.H
+        wcat = self.v("Wcat").cpu().numpy()
+        wv, we, bv = wcat[:H * D], wcat[H * D:H * D + 4 * H], wcat[H * D + 4 * H:]
+        return {
+            "Dense_0": {"kernel": self.v("Wq").cpu().numpy(), "bias": self.v("bq").cpu().numpy()},
+            "Dense_1": {"kernel": self.v("Wkt").cpu().numpy().transpose(2, 0, 1).reshape(D, H * F),
+                        "bias": self.v("bk").cpu().numpy()},
+            "Dense_2": {"kernel": wv.reshape(H, D, F).transpose(1, 0, 2).reshape(D, H * F), "bias": bv.reshape(-1)},
+            "Dense_3": {"kernel": we.reshape(H, 4, F).transpose(1, 0, 2).reshape(4, H * F)},
+            "Dense_4": {"kernel": self.v("Wu").cpu().numpy(), "bias": self.v("bu").cpu().numpy()},
+        }
+
+    def init_host(self, rng):
+        D, F, H = self.D, self.F, self.H
+        d = {"Dense_0": {"kernel": orthogonal(rng, (D, H * F)), "bias": np.zeros(H * F, np.float32)},
+             "Dense_1": {"kernel": orthogonal(rng, (D, H * F)), "bias": np.zeros(H * F, np.float32)},
+             "Dense_2": {"kernel": orthogonal(rng, (D, H * F)), "bias": np.zeros(H * F, np.float32)},
+             "Dense_3": {"kernel": orthogonal(rng, (4, H * F))},
+             "Dense_4": {"kernel": orthogonal(rng, (D, F)), "bias": np.zeros(F, np.float32)}}
+        self.load_flax(d)
+
+    def _attn_args(self, X, g: "GraphBatch"):
+        a = K._lib.GnnAttnArgs()
+        G, N, D = X.shape
+        a.G, a.N, a.E, a.n_agents = G, N, g.E, g.n
+        a.D, a.F, a.H, a.C = D, self.F, self.H, g.C
+        a.cand, a.receivers, a.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
+        a.x, a.x_gstride = K._p(X), N * D
+        a.ef, a.ef_gstride = K._p(g.edges), g.E * 4
+        a.bk = K._p(self.v("bk"))
+        a.scale = 1.0 / math.sqrt(self.F)
+        return a
+
+    def fwd(self, X, g: "GraphBatch", last: bool):
+        """X (G, N, D) contiguous -> Y: (G*n, F) agent rows if last else (G, N, F)."""
+        G, N, D = X.shape
+        n, F, H, C = g.n, self.F, self.H, g.C
+        dev = X.device
+        R = G * n
+        Q = torch.empty((R, H * F), device=dev)
+        K.gemm(X, self.v("Wq"), Q, R, H * F, D, lda=D, a_grp=n, a_gs=N * D, bias=self.v("bq"))
+        QT = torch.empty((R, H * D), device=dev)
+        K.gemm(Q, self.v("Wkt"), QT, R, D, F, lda=H * F, sa=F, ldb=D, sb=F * D, ldc=H * D, sc=D, batch=H)
+        attn = torch.empty((R, H, C), device=dev)
+        xcat = torch.empty((R, H * (D + 5)), device=dev)
+        a = self._attn_args(X, g)
+        a.q, a.qt, a.attn, a.xcat = K._p(Q), K._p(QT), K._p(attn), K._p(xcat)
+        K.gnn_attn(a, False, dev)
+        M = torch.empty((R, F), device=dev)
+        K.gemm(xcat, self.v("Wcat"), M, R, F, H * (D + 5), alpha=1.0 / H)
+        if last:
+            Y = torch.empty((R, F), device=dev)
+            K.gemm(X, self.v("Wu"), Y, R, F, D, lda=D, a_grp=n, a_gs=N * D, bias=self.v("bu"), addend=M, relu=True)
+        else:
+            Y = torch.empty((G, N, F), device=dev)
+            K.gemm(X, self.v("Wu"), Y, R, F, D, lda=D, a_grp=n, a_gs=N * D, c_grp=n, c_gs=N * F,
+                   bias=self.v("bu"), addend=M, relu=True)
+            K.gemm(X, self.v("Wu"), Y, G * (N - n), F, D, lda=D, a_off=n * D, a_grp=N - n, a_gs=N * D,
+                   c_off=n * F, c_grp=N - n, c_gs=N * F, bias=self.v("bu"), relu=True)
+        return Y, (X, Q, QT, attn, xcat, Y, last)
+
+    def bwd(self, cache, dY, g: "GraphBatch", need_dx: bool):
+        X, Q, QT, attn, xcat, Y, last = cache
+        G, N, D = X.shape
+        n, F, H = g.n, self.F, self.H
+        R = G * n
+        W = H * (D + 5)
+        dev = X.device
+        K.relu_bwd_(dY, Y)  # dY := dZ
+        za = dict(lda=F) if last else dict(lda=F, a_grp=n, a_gs=N * F)
+        zb = dict(ldb=F) if last else dict(ldb=F, b_grp=n, b_gs=N * F)
+        dxcat = torch.empty((R, W), device=dev)
+        K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H, **za)
+        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0, **zb)
+        dQT = torch.empty((R, H * D), device=dev)
+        dQ = torch.empty((R, H * F), device=dev)
+        dbeta = torch.empty((R, H), device=dev)
+        dX = torch.zeros((G, N, D), device=dev) if need_dx else None
+        a = self._attn_args(X, g)
+        a.q, a.qt, a.attn = K._p(Q), K._p(QT), K._p(attn)
+        a.dxcat, a.dqt, a.dq, a.dbeta = K._p(dxcat), K._p(dQT), K._p(dQ), K._p(dbeta)
+        a.dx, a.dx_gstride = K._p(dX), N * D
+        K.gnn_attn(a, True, dev)
+        K.gemm(dbeta, Q, self.v("bk", True), 1, F, R, ta=True, lda=H, sa=1, ldb=H * F, sb=F, ldc=F, sc=F,
+               batch=H, beta=1.0)
+        K.gemm(Q, dQT, self.v("Wkt", True), F, D, R, ta=True, lda=H * F, sa=F, ldb=H * D, sb=D, ldc=D, sc=F * D,
+               batch=H, beta=1.0)
+        K.gemm(dQT, self.v("Wkt"), dQ, R, F, D, lda=H * D, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
+               batch=H, beta=1.0)
+        K.gemm(X, dQ, self.v("Wq", True), D, H * F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0)
+        K.colsum(dQ, R, H * F, self.v("bq", True), beta=1.0)
+        if last:
+            K.gemm(X, dY, self.v("Wu", True), D, F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0)
+            K.colsum(dY, R, F, self.v("bu", True), beta=1.0)
+        else:
+            K.gemm(X, dY, self.v("Wu", True), D, F, G * N, ta=True, lda=D, beta=1.0)
+            K.colsum(dY, G * N, F, self.v("bu", True), beta=1.0)
+        if need_dx:
+            if last:
+                K.gemm(dY, self.v("Wu"), dX, R, D, F, tb=True, ldb=F, c_grp=n, c_gs=N * D, ldc=D, beta=1.0)
+            else:
+                K.gemm(dY, self.v("Wu"), dX, G * N, D, F, tb=True, ldb=F, ldc=D, beta=1.0)
+            K.gemm(dQ, self.v("Wq"), dX, R, D, H * F, tb=True, ldb=H * F, c_grp=n, c_gs=N * D, ldc=D, beta=1.0)
+        return dX
+
+
+class GraphBatch:
+    """A batch of env graphs as the GNN kernels consume them (nodes/edges/receivers/senders contiguous
+    (G, ...)), plus the per-agent candidate-edge table of the env layout."""
+
+    @staticmethod
+    def from_graph(graph, env, flatten_dims=None):
+        """GraphsTuple with any leading batch dims -> GraphBatch over all graphs (row-major)."""
+        nd = graph.nodes.dim() - 2
+        G = int(np.prod(graph.nodes.shape[:nd]))
+        return GraphBatch(graph.nodes.reshape(G, *graph.nodes.shape[nd:]), graph.edges.reshape(G, *graph.edges.shape[nd:]),
+                          graph.receivers.reshape(G, -1), graph.senders.reshape(G, -1), env.num_agents,
+                          env.agent_candidates(graph.nodes.device))
+
+    def __init__(self, nodes, edges, receivers, senders, n_agents: int, cand: torch.Tensor):
+        self.nodes = nodes.contiguous()
+        self.edges = edges.contiguous()
+        self.receivers = receivers.contiguous()
+        self.senders = senders.contiguous()
+        self.G, self.N = self.nodes.shape[0], self.nodes.shape[1]
+        self.E = self.edges.shape[1]
+        self.n = int(n_agents)
+        self.cand = cand
+        self.C = int(cand.shape[1])
+
+
+class GNN:
+    """GraphTransformerGNN (dgppo/nn/gnn.py:127-142), msg_dim 32, out_dim 64, 3 heads, followed by
+    type_nodes(agent): returns the agent rows of the last layer, (G*n, out_dim)."""
+
+    def __init__(self, ps, name, node_dim, n_layers, msg_dim=32, out_dim=64, n_heads=3):
+        self.layers = []
+        d = node_dim
+        for i in range(n_layers):
+            od = out_dim if i == n_layers - 1 else msg_dim
+            self.layers.append(GraphTransformer(ps, f"{name}.GraphTransformer_{i}", d, od, n_heads))
+            d = od
+
+    def init_host(self, rng):
+        for L in self.layers:
+            L.init_host(rng)
+
+    def flax(self):
+        return [L.flax() for L in self.layers]
+
+    def load_flax(self, layers):
+        for L, d in zip(self.layers, layers):
+            L.load_flax(d)
+
+    def fwd(self, g: GraphBatch):
+        X = g.nodes
+        caches = []
+        for i, L in enumerate(self.layers):
+            X, c = L.fwd(X, g, i == len(self.layers) - 1)
+            caches.append(c)
+        return X, caches
+
+    def bwd(self, caches, dZ, g: GraphBatch):
+        d = dZ
+        for i in range(len(self.layers) - 1, -1, -1):
+            d = self.layers[i].bwd(caches[i], d, g, need_dx=i > 0)

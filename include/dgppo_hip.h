@@ -132,6 +132,150 @@ typedef struct dgppo_env_reset_io {
 
 int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream);
 
+/* ---- hot path (2): DGPPO update building blocks ------------------------------------------------
+ * Batched fp32 GEMM on the matrix cores (v_mfma_f32_32x32x2_f32):
+ *   C[b] = alpha * op(A[b]) op(B[b]) + beta * C[b] + bias[N] + addend[b]   (optional ReLU)
+ * op(A) = A (M,K) row-major, or trans_a: A stored (K,M); op(B) = B (K,N), or trans_b: stored (N,K).
+ * Every flax `nn.Dense` of the reference networks (dgppo/nn/mlp.py:15-30, nn/gnn.py:86-111,
+ * algo/module/policy.py:67-71, value.py:253,288, flax GRUCell) and its two backward GEMMs map here.
+ * split_k > 1 computes K in slices into `workspace` (dgppo_gemm_workspace_floats floats) and reduces
+ * them in a fixed order (bitwise-deterministic weight gradients, no float atomics). */
+/* Row grouping (a_grp/b_grp/c_grp/add_grp > 0): stored row r lives at (r / grp) * gstride + (r % grp) * ld,
+ * e.g. the n agent rows of every graph inside a (G, N, D) node tensor (grp = n, gstride = N*D).  Stored rows are M (A), K (trans_a A), K (B), N (trans_b B), M (C). */
+typedef struct dgppo_gemm_args {
+  int32_t M, N, K, batch;
+  int32_t trans_a, trans_b;
+  const float* A; int64_t lda, stride_a;
+  const float* B; int64_t ldb, stride_b;
+  float* C;       int64_t ldc, stride_c;
+  int32_t a_grp, b_grp, c_grp, pad_;
+  int64_t a_gstride, b_gstride, c_gstride;
+  const float* bias;                          /* (N) or NULL */
+  const float* addend; int64_t ld_add, stride_add; /* (M,N) per batch or NULL */
+  int32_t add_grp, pad2_; int64_t add_gstride;     /* addend row grouping (independent of C's) */
+  float alpha, beta;
+  int32_t relu;
+  int32_t split_k;
+  float* workspace;
+} dgppo_gemm_args;
+
+int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* args);
+int dgppo_gemm(const dgppo_gemm_args* args, void* stream);
+
+/* GraphTransformer attention core (dgppo/nn/gnn.py:78-117 + jraph.segment_softmax/segment_sum),
+ * per RECEIVING AGENT: only agents receive messages in the DGPPO env graphs, so with
+ * qt_h = Wk_h q_h the logits are (qt_h . x_s + q_h . bk_h) / sqrt(F) and the aggregated message is
+ * xbar_h Wv_h + sig_h bv_h + ebar_h We_h (see csrc/nn.hip).  fwd writes attn (G*n, H, C) and
+ * xcat (G*n, H*(D+5)) = [xbar (H*D) | ebar (H*4) | sig (H)]; bwd consumes dxcat and writes dqt,
+ * dq (= dbeta_h * bk_h), dbeta and ACCUMULATES sender-node gradients into dx (optional).
+ * cand (n, C): edge ids that may target agent i (checked against receivers at run time). */
+typedef struct dgppo_gnn_attn_args {
+  int32_t G, N, E, n_agents, D, F, H, C;
+  const int32_t* cand;
+  const int32_t* receivers;
+  const int32_t* senders;     /* (G, E) */
+  const float* x; int64_t x_gstride;   /* node features (G, N, D) */
+  const float* ef; int64_t ef_gstride; /* edge features (G, E, 4) */
+  const float* q;   /* (G*n, H*F) */
+  const float* qt;  /* (G*n, H*D) */
+  const float* bk;  /* (H*F) */
+  float* attn;      /* (G*n, H, C) */
+  float* xcat;      /* (G*n, H*(D+5)) */
+  const float* dxcat;
+  float* dqt;
+  float* dq;
+  float* dbeta;     /* (G*n, H) */
+  float* dx; int64_t dx_gstride;
+  float scale;      /* 1/sqrt(F) */
+} dgppo_gnn_attn_args;
+
+int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* args, void* stream);
+int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* args, void* stream);
+
+/* flax LayerNorm (+ReLU) over rows of width F (dgppo/nn/mlp.py:27-29); bwd accumulates dscale/dbias */
+int dgppo_layernorm_fwd(const float* x, const float* scale, const float* bias, float* y, float* mean, float* rstd,
+                        int64_t rows, int32_t F, int32_t relu, float eps, void* stream);
+int64_t dgppo_layernorm_bwd_workspace_floats(int64_t rows, int32_t F);
+int dgppo_layernorm_bwd(const float* x, const float* y, const float* dy, const float* scale, const float* mean,
+                        const float* rstd, float* dx, float* dscale, float* dbias, int64_t rows, int32_t F,
+                        int32_t relu, float* workspace, void* stream);
+
+/* dy *= (y > 0) in place (ReLU backward) */
+int dgppo_relu_bwd(float* dy, const float* y, int64_t n, void* stream);
+
+/* out = alpha * column_sums(x) + beta * out (deterministic; bias gradients) */
+int64_t dgppo_colsum_workspace_floats(int64_t rows, int32_t cols);
+int dgppo_colsum(const float* x, int64_t rows, int32_t cols, int64_t ld, int32_t grp, int64_t gstride, float* out,
+                 float alpha, float beta, float* workspace, void* stream);
+
+/* flax GRUCell (dgppo/nn/rnn.py:15-30): gi = x Wi + bi, gh = h Wh (r|z|n blocks), bhn = hn bias */
+int dgppo_gru_fwd(const float* gi, const float* gh, const float* bhn, const float* h, float* h_new, int64_t rows,
+                  int32_t H, void* stream);
+int dgppo_gru_bwd(const float* gi, const float* gh, const float* bhn, const float* h, const float* dh_new,
+                  float* dgi, float* dgh, float* dh, int64_t rows, int32_t H, void* stream);
+
+/* mean over the agents of each graph (RStateFn, dgppo/algo/module/value.py:29) */
+int dgppo_agent_mean_fwd(const float* x, float* y, int64_t G, int32_t n, int32_t F, int64_t x_gstride, void* stream);
+int dgppo_agent_mean_bwd(const float* dy, float* dx, int64_t G, int32_t n, int32_t F, int64_t dx_gstride,
+                         void* stream);
+
+/* TanhNormal head (dgppo/algo/module/policy.py:61-74, distribution.py:10-66): std = softplus(raw +
+ * std_shift) + std_min; mode 0 = tanh(mean), 1 = tanh(mean + std * noise), 2 = evaluate `action`.
+ * log_pi / entropy summed over the A action dims; entropy uses a fixed per-agent eps (n_agents, A).
+ * If dmean is set, writes the backward of (dlog_pi, dentropy) into dmean / dstd_raw. */
+typedef struct dgppo_tanh_normal_args {
+  int64_t rows;
+  int32_t A, mode, n_agents, pad_;
+  const float* mean;
+  const float* std_raw;
+  float std_shift, std_min;
+  const float* noise;
+  const float* action;
+  float* action_out;
+  float* std_out;
+  float* log_pi;
+  float* entropy;
+  const float* entropy_eps;
+  const float* dlog_pi;
+  const float* dentropy;
+  float* dmean;
+  float* dstd_raw;
+} dgppo_tanh_normal_args;
+
+int dgppo_tanh_normal(const dgppo_tanh_normal_args* args, void* stream);
+
+/* losses: PPO clipped surrogate + entropy bonus (dgppo/algo/informarl.py:428-438) and
+ * optax.l2_loss mean (informarl.py:374, dgppo.py:310); gradients are d(mean loss)/d(input) */
+int64_t dgppo_loss_workspace_floats(void);
+int dgppo_ppo_loss(const float* log_pi, const float* log_pi_old, const float* adv, const float* entropy, int64_t n,
+                   float clip_eps, float coef_ent, float* dlog_pi, float* dentropy, float* stats, float* workspace,
+                   void* stream);
+int dgppo_l2_loss(const float* pred, const float* target, int64_t n, float* dpred, float* loss, float* workspace,
+                  void* stream);
+
+/* compute_dec_ocp_gae (dgppo/algo/utils.py:11-79), one workgroup per env */
+typedef struct dgppo_gae_args {
+  int32_t B, T, n_agents, n_h;
+  const float* hs;  /* (B, T, n, nh) costs */
+  const float* l;   /* (B, T) */
+  const float* Vh;  /* (B, T+1, n, nh) */
+  const float* Vl;  /* (B, T+1) */
+  float* Qh;        /* (B, T, n, nh) */
+  float* Ql;        /* (B, T) */
+  float gamma, lambda;
+} dgppo_gae_args;
+
+int dgppo_gae(const dgppo_gae_args* args, void* stream);
+
+/* compute_norm_and_clip + optax.adam + apply_if_finite (dgppo/trainer/utils.py:105-118,
+ * informarl.py:131-137): state = [global norm, non-finite count, adam step] on the device */
+int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace, void* stream);
+int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, float b1,
+               float b2, float eps, float max_norm, void* stream);
+
+/* standard normal noise from Philox4x32-10 (Box-Muller); seed from *seed_ptr when non-NULL */
+int dgppo_normal(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed, uint64_t stream_id, void* stream);
+
 /* Library / device introspection */
 int dgppo_abi_version(void);
 const char* dgppo_build_info(void);

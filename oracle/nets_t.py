@@ -1,0 +1,169 @@
+"""float64 torch-CPU twin of oracle/nets.py used for GRADIENT checks (autograd on the reference's
+literal per-edge formulation).  TEST INFRASTRUCTURE ONLY; see oracle/__init__.py.
+
+Same param trees as oracle/nets.py (flax layout); every leaf is a float64 tensor that may require
+grad.  Function-for-function restatement of dgppo/nn/gnn.py:78-142, dgppo/nn/mlp.py:15-30,
+flax GRUCell, dgppo/algo/module/policy.py:61-74, value.py:15-79, distribution.py:10-66,
+informarl.py:357-457 and dgppo.py:296-321."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+T64 = torch.float64
+
+
+def to_t(tree, requires_grad=False):
+    if isinstance(tree, dict):
+        return {k: to_t(v, requires_grad) for k, v in tree.items()}
+    if isinstance(tree, (list, tuple)):
+        return [to_t(v, requires_grad) for v in tree]
+    t = torch.tensor(np.asarray(tree), dtype=T64)
+    if requires_grad:
+        t.requires_grad_(True)
+    return t
+
+
+def dense(x, p):
+    y = x @ p["kernel"]
+    return y + p["bias"] if "bias" in p else y
+
+
+def layernorm(x, p, eps=1e-6):
+    mean = x.mean(-1, keepdim=True)
+    var = torch.clamp((x * x).mean(-1, keepdim=True) - mean * mean, min=0.0)
+    return (x - mean) / torch.sqrt(var + eps) * p["scale"] + p["bias"]
+
+
+def mlp_head(x, p):
+    for i in range(2):
+        x = torch.relu(layernorm(dense(x, p[f"Dense_{i}"]), p[f"LayerNorm_{i}"]))
+    return x
+
+
+def gru_cell(p, h, x):
+    r = torch.sigmoid(dense(x, p["ir"]) + dense(h, p["hr"]))
+    z = torch.sigmoid(dense(x, p["iz"]) + dense(h, p["hz"]))
+    n = torch.tanh(dense(x, p["in"]) + r * dense(h, p["hn"]))
+    return (1.0 - z) * n + z * h
+
+
+def segment_softmax(logits, seg, num):
+    idx = seg[:, None].expand_as(logits)
+    mx = torch.full((num,) + logits.shape[1:], -math.inf, dtype=logits.dtype).scatter_reduce(
+        0, idx, logits, reduce="amax", include_self=True)
+    ex = torch.exp(logits - mx[seg].detach())
+    den = torch.zeros((num,) + logits.shape[1:], dtype=logits.dtype).index_add(0, seg, ex)
+    return ex / den[seg]
+
+
+def graph_transformer(p, nodes, edges, recv, send, n_heads, out_dim):
+    N = nodes.shape[0]
+    xs, xr = nodes[send], nodes[recv]
+    q = dense(xr, p["Dense_0"]).reshape(-1, n_heads, out_dim)
+    k = dense(xs, p["Dense_1"]).reshape(-1, n_heads, out_dim)
+    v = dense(xs, p["Dense_2"]).reshape(-1, n_heads, out_dim)
+    e = (edges @ p["Dense_3"]["kernel"]).reshape(-1, n_heads, out_dim)
+    attn = (q * k).sum(-1) / math.sqrt(out_dim)
+    attn = segment_softmax(attn, recv, N)[..., None]
+    msgs = (attn * (v + e)).mean(dim=1)
+    agg = torch.zeros((N, out_dim), dtype=nodes.dtype).index_add(0, recv, msgs)
+    return torch.relu(dense(nodes, p["Dense_4"]) + agg)
+
+
+def gnn(layers, graph, n_agents, out_dim=64, msg_dim=32, n_heads=3):
+    outs = []
+    L = len(layers)
+    nodes = torch.as_tensor(graph["nodes"], dtype=T64)
+    edges = torch.as_tensor(graph["edges"], dtype=T64)
+    recv = torch.as_tensor(graph["receivers"]).long()
+    send = torch.as_tensor(graph["senders"]).long()
+    for g in range(nodes.shape[0]):
+        x = nodes[g]
+        for i in range(L):
+            od = out_dim if i == L - 1 else msg_dim
+            x = graph_transformer(layers[i], x, edges[g], recv[g], send[g], n_heads, od)
+        outs.append(x[:n_agents])
+    return torch.stack(outs)
+
+
+STD_INIT_INV = math.log(math.exp(0.5) - 1.0)
+THRESH = 0.999
+
+
+def policy_dist(p, h2):
+    feats = dense(h2, p["ScaleHid"])
+    means = dense(feats, p["OutputDenseMean"])
+    stds = torch.nn.functional.softplus(dense(feats, p["OutputDenseStdTrans"]) + STD_INIT_INV) + 1e-5
+    return means, stds
+
+
+def tanh_fldj(x):
+    return 2.0 * (math.log(2.0) - x - torch.nn.functional.softplus(-2.0 * x))
+
+
+def tanh_normal_log_prob(a, mu, sd):
+    inv_t = math.atanh(THRESH)
+    log_eps = math.log(1.0 - THRESH)
+    left = torch.special.log_ndtr((-inv_t - mu) / sd) - log_eps
+    right = torch.special.log_ndtr((mu - inv_t) / sd) - log_eps
+    v = torch.clamp(torch.as_tensor(a, dtype=T64), -THRESH, THRESH)
+    x = torch.atanh(v)
+    z = (x - mu) / sd
+    inner = -0.5 * z * z - torch.log(sd) - 0.5 * math.log(2 * math.pi) - tanh_fldj(x)
+    lp = torch.where(v <= -THRESH, left, torch.where(v >= THRESH, right, inner))
+    return lp.sum(-1)
+
+
+def tanh_normal_entropy(mu, sd, eps_fixed):
+    ent = 0.5 + 0.5 * math.log(2 * math.pi) + torch.log(sd)
+    return (ent + tanh_fldj(mu + sd * torch.as_tensor(eps_fixed, dtype=T64))).sum(-1)
+
+
+def actor_eval_seq(p, graph, S, L, n, actions, eps_fixed):
+    """scan_eval_action over S sequences of L graphs (zero carries); graph batch ordered (s, t).
+    Returns log_pi, entropy (S, L, n)."""
+    y = mlp_head(gnn(p["gnn"], graph, n), p["head"]).reshape(S, L, n, 64)
+    h = torch.zeros((S, n, 64), dtype=T64)
+    hs = []
+    for t in range(L):
+        h = gru_cell(p["gru"], h, y[:, t])
+        hs.append(h)
+    H = torch.stack(hs, 1)
+    mu, sd = policy_dist(p, H)
+    act = torch.as_tensor(actions, dtype=T64).reshape(S, L, n, -1)
+    return tanh_normal_log_prob(act, mu, sd), tanh_normal_entropy(mu, sd, eps_fixed)
+
+
+def vl_seq(p, graph, S, L, n):
+    """scan_Vl over S sequences of L graphs with zero carries: values (S, L)."""
+    y = mlp_head(gnn(p["gnn"], graph, n).mean(1), p["head"]).reshape(S, L, 64)
+    h = torch.zeros((S, 64), dtype=T64)
+    vs = []
+    for t in range(L):
+        h = gru_cell(p["gru"], h, y[:, t])
+        vs.append(dense(h, p["out"])[:, 0])
+    return torch.stack(vs, 1)
+
+
+def vh(p, graph, h, n):
+    y = mlp_head(gnn(p["gnn"], graph, n), p["head"])
+    return dense(gru_cell(p["gru"], torch.as_tensor(h, dtype=T64), y), p["out"])
+
+
+def ppo_loss(log_pis, log_pis_old, A, entropy, clip_eps=0.25, coef_ent=1e-2):
+    ratio = torch.exp(log_pis - torch.as_tensor(log_pis_old, dtype=T64))
+    A = torch.as_tensor(A, dtype=T64)
+    l1 = -ratio * A
+    l2 = -torch.clamp(ratio, 1 - clip_eps, 1 + clip_eps) * A
+    return torch.maximum(l1, l2).mean() - coef_ent * entropy.mean()
+
+
+def grads(tree):
+    if isinstance(tree, dict):
+        return {k: grads(v) for k, v in tree.items()}
+    if isinstance(tree, list):
+        return [grads(v) for v in tree]
+    return None if tree.grad is None else tree.grad.detach().numpy()

@@ -51,7 +51,11 @@ def _c_layout(struct, fields):
 
 
 @pytest.mark.parametrize("pystruct,cname", [(_lib.EnvCfg, "dgppo_env_cfg"), (_lib.EnvStepIO, "dgppo_env_step_io"),
-                                            (_lib.EnvResetIO, "dgppo_env_reset_io")])
+                                            (_lib.EnvResetIO, "dgppo_env_reset_io"),
+                                            (_lib.GemmArgs, "dgppo_gemm_args"),
+                                            (_lib.GnnAttnArgs, "dgppo_gnn_attn_args"),
+                                            (_lib.TanhNormalArgs, "dgppo_tanh_normal_args"),
+                                            (_lib.GaeArgs, "dgppo_gae_args")])
 def test_ctypes_mirror_matches_c_layout(pystruct, cname):
     names = [f[0] for f in pystruct._fields_]
     got = _c_layout(cname, names)

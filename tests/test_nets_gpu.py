@@ -1,0 +1,174 @@
+"""GPU parity for hot path (2): the MFMA GEMM, and the actor / Vl / Vh networks (forward AND
+gradients) against the float64 per-edge reference formulation (oracle/nets_t.py, autograd).
+
+Tolerances (fp32 kernels vs float64 reference): forward outputs |gpu - ref| <= 1e-5 + 1e-5 |ref|;
+gradients |gpu - ref| <= 2e-5 * max|ref| + 1e-6 per parameter tensor (the kernels use a different
+but algebraically identical per-receiver formulation and different summation orders)."""
+import numpy as np
+import pytest
+import torch
+
+from dgppo_fov_amd.algo.module.nets import ActorNet, VhNet, VlNet
+from dgppo_fov_amd.env import make_env
+from dgppo_fov_amd.nn import kernels as K
+from dgppo_fov_amd.nn.layers import GraphBatch
+from oracle import nets_t as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol=1e-5, atol=1e-5, what=""):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = np.abs(a - b) - (atol + rtol * np.abs(b))
+    assert err.max() <= 0, f"{what}: max excess {err.max():.3e}, max abs err {np.abs(a - b).max():.3e}"
+
+
+def _grad_close(g, r, what):
+    g = np.asarray(g, np.float64)
+    r = np.asarray(r, np.float64)
+    scale = np.abs(r).max()
+    err = np.abs(g - r).max()
+    assert err <= 2e-5 * scale + 1e-6, f"{what}: max abs err {err:.3e} vs scale {scale:.3e}"
+
+
+def _walk(a, b, path=""):
+    if isinstance(a, dict):
+        for k in a:
+            yield from _walk(a[k], b[k], f"{path}/{k}")
+    elif isinstance(a, list):
+        for i, (x, y) in enumerate(zip(a, b)):
+            yield from _walk(x, y, f"{path}[{i}]")
+    else:
+        yield path, a, b
+
+
+# ---- GEMM ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("M,N,Kd,ta,tb,batch", [(1, 1, 1, 0, 0, 1), (70, 33, 17, 0, 0, 1), (64, 64, 64, 1, 0, 1),
+                                               (130, 5, 200, 0, 1, 1), (7, 96, 3000, 1, 0, 1),
+                                               (50, 40, 20, 1, 1, 3), (33, 192, 9000, 1, 0, 2)])
+def test_gemm_matches_float64(cuda, M, N, Kd, ta, tb, batch):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(batch, *((Kd, M) if ta else (M, Kd)), generator=g, dtype=torch.float64)
+    B = torch.randn(batch, *((N, Kd) if tb else (Kd, N)), generator=g, dtype=torch.float64)
+    C0 = torch.randn(batch, M, N, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    opA = A.transpose(1, 2) if ta else A
+    opB = B.transpose(1, 2) if tb else B
+    ref = torch.relu(0.5 * opA @ opB + 0.25 * C0 + bias)
+    Ad, Bd, Cd = A.float().to(cuda), B.float().to(cuda), C0.float().to(cuda).contiguous()
+    K.gemm(Ad, Bd, Cd, M, N, Kd, ta=bool(ta), tb=bool(tb), batch=batch, sa=A[0].numel(), sb=B[0].numel(),
+           sc=M * N, bias=bias.float().to(cuda), alpha=0.5, beta=0.25, relu=True)
+    torch.cuda.synchronize()
+    scale = (opA.abs() @ opB.abs()).max().item()
+    assert (Cd.double().cpu() - ref).abs().max().item() <= 2e-6 * scale + 1e-5
+
+
+def test_gemm_row_grouping(cuda):
+    """agent rows (first n of N per graph) as GEMM rows, in and out."""
+    G, N, n, D, F = 5, 9, 3, 6, 4
+    X = torch.randn(G, N, D, dtype=torch.float64)
+    W = torch.randn(D, F, dtype=torch.float64)
+    Y = torch.zeros(G, N, F, dtype=torch.float32, device=cuda)
+    K.gemm(X.float().to(cuda), W.float().to(cuda), Y, G * n, F, D, lda=D, a_grp=n, a_gs=N * D, c_grp=n, c_gs=N * F)
+    torch.cuda.synchronize()
+    ref = X[:, :n] @ W
+    assert (Y[:, :n].double().cpu() - ref).abs().max() < 1e-5
+    assert Y[:, n:].abs().max() == 0
+
+
+# ---- network fixtures ----------------------------------------------------------------------------
+def _graphs(cuda, eid, n, obs, S, L, seed=0):
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    g = env.reset(key=seed, n_env=S)
+    gs = []
+    rng = np.random.default_rng(seed)
+    for t in range(L):
+        gs.append(g)
+        a = torch.from_numpy(rng.uniform(-1, 1, (S, n, 2)).astype(np.float32)).to(cuda)
+        g = env.step(g, a).graph
+    stack = lambda f: torch.stack([getattr(x, f) for x in gs], 1).contiguous()  # noqa: E731
+    nodes, edges, recv, send = stack("nodes"), stack("edges"), stack("receivers"), stack("senders")
+    gb = GraphBatch(nodes.view(S * L, *nodes.shape[2:]), edges.view(S * L, *edges.shape[2:]),
+                    recv.view(S * L, -1), send.view(S * L, -1), n, env.agent_candidates(cuda))
+    host = dict(nodes=gb.nodes.cpu().numpy(), edges=gb.edges.cpu().numpy(), receivers=gb.receivers.cpu().numpy(),
+                senders=gb.senders.cpu().numpy())
+    return env, gb, host
+
+
+CASES = [("LidarSpread", 8, 3), ("MPETarget", 3, 0), ("MPESpread", 3, 3), ("LidarBicycleTarget", 4, 2)]
+
+
+@pytest.mark.parametrize("eid,n,obs", CASES)
+def test_actor_eval_seq_fwd_bwd(cuda, eid, n, obs):
+    S, L = 3, 4
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L)
+    net = ActorNet(env.node_dim, n, cuda, seed=3)
+    rng = np.random.default_rng(1)
+    actions = rng.uniform(-0.99, 0.99, (S * L * n, 2)).astype(np.float32)
+    actions[0] = [0.9995, -0.9999]  # both boundary branches of the clipped log_prob
+    eps = rng.standard_normal((n, 2)).astype(np.float32)
+    lp, ent, cache = net.eval_seq_fwd(gb, S, L, torch.from_numpy(actions).to(cuda), torch.from_numpy(eps).to(cuda))
+    p = R.to_t(net.flax(), requires_grad=True)
+    rlp, rent = R.actor_eval_seq(p, host, S, L, n, actions, eps)
+    torch.cuda.synchronize()
+    _close(lp.cpu().numpy(), rlp.detach().numpy().reshape(-1), what="log_pi")
+    _close(ent.cpu().numpy(), rent.detach().numpy().reshape(-1), what="entropy")
+    # gradients of an arbitrary scalar function of (log_pi, entropy)
+    w1 = rng.standard_normal(S * L * n)
+    w2 = rng.standard_normal(S * L * n)
+    (rlp.reshape(-1) * torch.tensor(w1) + rent.reshape(-1) * torch.tensor(w2)).sum().backward()
+    net.ps.zero_grad()
+    net.eval_seq_bwd(cache, torch.tensor(w1, dtype=torch.float32, device=cuda),
+                     torch.tensor(w2, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    net.ps.swap_views()
+    g = net.flax()
+    net.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(p)):
+        _grad_close(a, b, "actor grad " + path)
+
+
+@pytest.mark.parametrize("eid,n,obs", CASES[:2])
+def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
+    S, L = 3, 5
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=4)
+    net = VlNet(env.node_dim, n, cuda, seed=5)
+    v, _, cache = net.seq_fwd(gb, S, L)
+    p = R.to_t(net.flax(), requires_grad=True)
+    rv = R.vl_seq(p, host, S, L, n)
+    torch.cuda.synchronize()
+    _close(v.cpu().numpy(), rv.detach().numpy(), what="Vl")
+    w = np.random.default_rng(2).standard_normal((S, L))
+    (rv * torch.tensor(w)).sum().backward()
+    net.ps.zero_grad()
+    net.seq_bwd(cache, torch.tensor(w, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    net.ps.swap_views()
+    g = net.flax()
+    net.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(p)):
+        _grad_close(a, b, "Vl grad " + path)
+
+
+@pytest.mark.parametrize("eid,n,obs", CASES[:3])
+def test_vh_fwd_bwd(cuda, eid, n, obs):
+    S, L = 2, 3
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=6)
+    net = VhNet(env.node_dim, n, 2, cuda, seed=7)
+    h = np.random.default_rng(3).standard_normal((S * L * n, 64)).astype(np.float32) * 0.5
+    out, cache = net.fwd(gb, torch.from_numpy(h).to(cuda))
+    p = R.to_t(net.flax(), requires_grad=True)
+    rout = R.vh(p, host, h.reshape(S * L, n, 64), n)
+    torch.cuda.synchronize()
+    _close(out.cpu().numpy(), rout.detach().numpy().reshape(-1, 2), what="Vh")
+    w = np.random.default_rng(4).standard_normal(rout.shape)
+    (rout * torch.tensor(w)).sum().backward()
+    net.ps.zero_grad()
+    net.bwd(cache, torch.tensor(w.reshape(-1, 2), dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    net.ps.swap_views()
+    g = net.flax()
+    net.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(p)):
+        _grad_close(a, b, "Vh grad " + path)
