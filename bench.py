@@ -120,14 +120,11 @@ def main():
     cur = eng.graph_at(0)
     outs = [eng.graph_at(1), eng.graph_at(2)]
 
-    def step_loop():
-        c = cur
+    def step_loop():  # ping-pong: step i reads buffer (i-1)&1 (graph 0 for i = 0), writes i&1
         for i in range(n_launch):
-            o = outs[i & 1]
-            c = env.step_into(c if i == 0 else outs[(i - 1) & 1], eng.actions[:, i % T], o, eng.rewards[:, i % T],
-                              eng.costs[:, i % T])
+            src = cur if i == 0 else outs[(i - 1) & 1]
+            env.step_into(src, eng.actions[i % T], outs[i & 1], eng.rewards[i % T], eng.costs[i % T])
 
-    # ping-pong between two buffers: step i reads buffer (i-1)&1, writes i&1
     step_loop()
     torch.cuda.synchronize(dev)
     if use_graph:

@@ -147,6 +147,15 @@ class GaeArgs(ctypes.Structure):
     ]
 
 
+class AdvArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_h", ctypes.c_int32),
+        ("Ql", c_f32p), ("Vl", c_f32p), ("Vh", c_f32p),
+        ("dt", ctypes.c_float), ("alpha", ctypes.c_float), ("cbf_eps", ctypes.c_float), ("cbf_weight", ctypes.c_float),
+        ("A", c_f32p), ("safe_count", c_f32p),
+    ]
+
+
 _V, _I64, _I32, _F32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
 
 # symbol -> (restype, argtypes); must match include/dgppo_hip.h (checked by tests/test_capi.py)
@@ -176,6 +185,7 @@ SIGNATURES = {
     "dgppo_ppo_loss": (ctypes.c_int, [_V, _V, _V, _V, _I64, _F32, _F32, _V, _V, _V, _V, _V]),
     "dgppo_l2_loss": (ctypes.c_int, [_V, _V, _I64, _V, _V, _V, _V]),
     "dgppo_gae": (ctypes.c_int, [ctypes.POINTER(GaeArgs), ctypes.c_void_p]),
+    "dgppo_dgppo_advantages": (ctypes.c_int, [ctypes.POINTER(AdvArgs), ctypes.c_void_p]),
     "dgppo_grad_norm": (ctypes.c_int, [_V, _I64, _V, _V, _V]),
     "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, _F32, _F32, _F32, _F32, _V]),
     "dgppo_normal": (ctypes.c_int, [_V, _I64, _V, ctypes.c_uint64, ctypes.c_uint64, _V]),

@@ -1,0 +1,10 @@
+"""Algorithm registry (dgppo/algo/__init__.py:8-18)."""
+from .dgppo import DGPPO
+
+
+def make_algo(algo: str, **kwargs):
+    if algo == "dgppo":
+        return DGPPO(**kwargs)
+    if algo in ("informarl", "informarl_lagr", "hcbfcrpo"):
+        raise NotImplementedError(f"{algo} is not built on the MI355X path yet (DESIGN.md: next rows)")
+    raise ValueError(f"Unknown algorithm: {algo}")

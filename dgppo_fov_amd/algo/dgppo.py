@@ -1,0 +1,342 @@
+"""DGPPO (dgppo/algo/dgppo.py:25-321 + its bases informarl_lagr.py / informarl.py) on MI355X.
+
+Same public surface as the reference Algorithm (dgppo/algo/base.py:10-99): `params`, `config`,
+`init_rnn_state`, `act`, `step`, `collect`, `update`, `save`, `load`.  Every numeric step runs in
+libdgppo_hip.so:
+
+  collect      RolloutEngine (env reset + T x [actor step + fused env step]) in one hipGraph
+  update       det rollout (get_action) -> Vl scan (prepass) -> Vh on both rollouts ->
+               Dec-OCP GAE -> DGPPO advantages -> per minibatch: update_Vl, update_Vh,
+               update_policy (fwd+bwd through the GNN/MLP/GRU kernels, losses, global-norm clip,
+               finite check, Adam), dgppo.py:136-321 / informarl.py:357-457.
+
+Multi-GPU (torch.distributed over RCCL): each rank owns a shard of the envs; the minibatch is the
+k-th env chunk of every rank's local shuffle; the three nets' gradients live in ONE flat buffer
+and are all-reduced (mean) once per minibatch before clip + Adam, so replicas stay identical.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..env.base import MultiAgentEnv
+from ..nn import kernels as K
+from ..nn.layers import GraphBatch
+from ..trainer.data import Rollout
+from ..trainer.rollout import RolloutEngine
+from .module.nets import ActorNet, VhNet, VlNet
+
+
+class _Opt:
+    """optax.apply_if_finite(optax.adam(lr), 1e6) state + compute_norm_and_clip for one flat buffer."""
+
+    def __init__(self, ps, lr, max_norm, device):
+        self.ps, self.lr, self.max_norm = ps, lr, max_norm
+        self.m = torch.zeros_like(ps.flat)
+        self.v = torch.zeros_like(ps.flat)
+        self.state = torch.zeros(3, dtype=torch.float32, device=device)  # [norm, non-finite, count]
+
+    def step(self):
+        K.grad_norm(self.ps.grad, self.state)
+        K.adam(self.ps.flat, self.ps.grad, self.m, self.v, self.state, self.lr, max_norm=self.max_norm)
+
+
+class DGPPO:
+    def __init__(self, env: MultiAgentEnv, node_dim: int, edge_dim: int, state_dim: int, action_dim: int,
+                 n_agents: int, actor_gnn_layers: int = 2, Vl_gnn_layers: int = 2, Vh_gnn_layers: int = 1,
+                 gamma: float = 0.99, lr_actor: float = 3e-4, lr_Vl: float = 1e-3, lr_Vh: float = 1e-3,
+                 batch_size: int = 8192, epoch_ppo: int = 1, clip_eps: float = 0.25, gae_lambda: float = 0.95,
+                 coef_ent: float = 1e-2, max_grad_norm: float = 2.0, seed: int = 0, use_rnn: bool = True,
+                 rnn_layers: int = 1, rnn_step: int = 16, use_lstm: bool = False, alpha: float = 10.0,
+                 cbf_eps: float = 1e-2, cbf_weight: float = 1.0, train_steps: int = int(1e5),
+                 cbf_schedule: bool = True, device=None, **kwargs):
+        if not use_rnn or use_lstm or rnn_layers != 1:
+            raise NotImplementedError("the MI355X path implements the reference default: 1-layer GRU policy/critics")
+        self._env = env
+        self.device = torch.device(device) if device is not None else env.device
+        self._node_dim, self._edge_dim, self._action_dim, self._n_agents = node_dim, edge_dim, action_dim, n_agents
+        self.actor_gnn_layers, self.Vl_gnn_layers, self.Vh_gnn_layers = actor_gnn_layers, Vl_gnn_layers, Vh_gnn_layers
+        self.gamma, self.lr_actor, self.lr_Vl, self.lr_Vh = gamma, lr_actor, lr_Vl, lr_Vh
+        self.batch_size, self.epoch_ppo, self.clip_eps, self.gae_lambda = batch_size, epoch_ppo, clip_eps, gae_lambda
+        self.coef_ent, self.max_grad_norm, self.seed = coef_ent, max_grad_norm, seed
+        self.use_rnn, self.rnn_layers, self.rnn_step, self.use_lstm = use_rnn, rnn_layers, rnn_step, use_lstm
+        self.alpha, self.cbf_eps, self.cbf_weight, self.cbf_schedule = alpha, cbf_eps, cbf_weight, cbf_schedule
+        self.train_steps = int(train_steps)
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank() if self.world > 1 else 0
+
+        dev = self.device
+        self.actor = ActorNet(node_dim, n_agents, dev, seed=seed * 3 + 0, gnn_layers=actor_gnn_layers,
+                              action_dim=action_dim)
+        self.Vl = VlNet(node_dim, n_agents, dev, seed=seed * 3 + 1, gnn_layers=Vl_gnn_layers)
+        self.Vh = VhNet(node_dim, n_agents, env.n_cost, dev, seed=seed * 3 + 2, gnn_layers=Vh_gnn_layers)
+        # one flat gradient buffer for the three nets (one all-reduce per minibatch)
+        sizes = [self.Vl.ps.size, self.Vh.ps.size, self.actor.ps.size]
+        self.grad_flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+        off = 0
+        for net, sz in zip((self.Vl, self.Vh, self.actor), sizes):
+            net.ps.grad = self.grad_flat[off:off + sz]
+            net.ps.build_views()
+            off += sz
+        self.opt = {"Vl": _Opt(self.Vl.ps, lr_Vl, max_grad_norm, dev), "Vh": _Opt(self.Vh.ps, lr_Vh, max_grad_norm, dev),
+                    "policy": _Opt(self.actor.ps, lr_actor, max_grad_norm, dev)}
+        # the reference draws the entropy's tanh-Jacobian sample ONCE at trace time with a fixed key,
+        # identical for every vmapped env/step (distribution.py:37-43); here: a fixed (n, A) draw
+        self.entropy_eps = torch.from_numpy(
+            np.random.default_rng(10_000 + seed).standard_normal((n_agents, action_dim)).astype(np.float32)).to(dev)
+        self.init_rnn_state = torch.zeros((rnn_layers, n_agents, 1, 64), device=dev)
+        self.init_Vl_rnn_state = torch.zeros((rnn_layers, 1, 1, 64), device=dev)
+        self._engines = {}
+        self.key = np.random.default_rng(seed)
+        self.np_rng = np.random.default_rng(seed)
+
+    # ---- reference properties ------------------------------------------------------------------
+    @property
+    def node_dim(self):
+        return self._node_dim
+
+    @property
+    def edge_dim(self):
+        return self._edge_dim
+
+    @property
+    def action_dim(self):
+        return self._action_dim
+
+    @property
+    def n_agents(self):
+        return self._n_agents
+
+    @property
+    def config(self) -> dict:
+        return {
+            "cost_weight": 0.0, "actor_gnn_layers": self.actor_gnn_layers, "Vl_gnn_layers": self.Vl_gnn_layers,
+            "gamma": self.gamma, "lr_actor": self.lr_actor, "lr_Vl": self.lr_Vl, "batch_size": self.batch_size,
+            "epoch_ppo": self.epoch_ppo, "clip_eps": self.clip_eps, "gae_lambda": self.gae_lambda,
+            "coef_ent": self.coef_ent, "max_grad_norm": self.max_grad_norm, "seed": self.seed,
+            "use_rnn": self.use_rnn, "rnn_layers": self.rnn_layers, "rnn_step": self.rnn_step,
+            "use_lstm": self.use_lstm, "cost_schedule": False, "lr_Vh": self.lr_Vh,
+            "Vh_gnn_layers": self.Vh_gnn_layers, "alpha": self.alpha, "cbf_eps": self.cbf_eps,
+            "cbf_weight": self.cbf_weight, "cbf_schedule": self.cbf_schedule,
+        }
+
+    @property
+    def params(self) -> dict:
+        return {"policy": self.actor.ps.flat, "Vl": self.Vl.ps.flat, "Vh": self.Vh.ps.flat}
+
+    def cbf_weight_at(self, step: int) -> float:
+        """optax.piecewise_constant_schedule(cbf_weight, {0.5 T: 2, 0.75 T: 2}) (dgppo.py:73-80)."""
+        w = self.cbf_weight
+        if not self.cbf_schedule:
+            return w
+        if step >= int(self.train_steps * 0.5):
+            w *= 2
+        if step >= int(self.train_steps * 0.75):
+            w *= 2
+        return w
+
+    # ---- acting ----------------------------------------------------------------------------------
+    def _gb(self, graph) -> GraphBatch:
+        return GraphBatch.from_graph(graph, self._env)
+
+    def act(self, graph, rnn_state: torch.Tensor, params=None):
+        """get_action for a batch of graphs: rnn_state (B, 1, n, 1, 64) -> (action (B, n, A), rnn)."""
+        assert params is None or params is self.params
+        g = self._gb(graph)
+        B, n = g.G, self._n_agents
+        h = rnn_state.reshape(B * n, 64).contiguous()
+        a, _, h2 = self.actor.act(g, h, 0)
+        return a.view(B, n, -1), h2.view(B, 1, n, 1, 64)
+
+    def step(self, graph, rnn_state: torch.Tensor, key: int, params=None):
+        """sample_action: (action, log_pi (B, n), rnn)."""
+        g = self._gb(graph)
+        B, n = g.G, self._n_agents
+        noise = torch.empty((B * n, self._action_dim), device=self.device)
+        K.normal_(noise, seed=int(key))
+        a, lp, h2 = self.actor.act(g, rnn_state.reshape(B * n, 64).contiguous(), 1, noise=noise)
+        return a.view(B, n, -1), lp.view(B, n), h2.view(B, 1, n, 1, 64)
+
+    def _engine(self, n_env: int, mode: int) -> RolloutEngine:
+        k = (n_env, mode)
+        if k not in self._engines:
+            eng = RolloutEngine(self._env, n_env, self._env.max_episode_steps, self.device,
+                                env_offset=self.rank * n_env, actor=self.actor, mode=mode)
+            if os.environ.get("DGPPO_NO_GRAPH", "0") != "1":
+                eng.capture()
+            self._engines[k] = eng
+        return self._engines[k]
+
+    def collect(self, params, key, n_env: Optional[int] = None) -> Rollout:
+        """jit(vmap(rollout_fn))(params, keys): `key` is an int seed (or a sequence whose length is n_env)."""
+        if n_env is None:
+            n_env = len(key) if hasattr(key, "__len__") else 128
+        seed = int(np.asarray(key).reshape(-1)[0]) if hasattr(key, "__len__") else int(key)
+        return self._engine(n_env, RolloutEngine.MODE_SAMPLE).run(seed)
+
+    def det_rollout(self, n_env: int, key: int) -> Rollout:
+        return self._engine(n_env, RolloutEngine.MODE_DET).run(key)
+
+    # ---- update ------------------------------------------------------------------------------
+    def _graphs(self, graph, envs) -> GraphBatch:
+        """(Be, T, ...) graphs of the selected envs, env-major -> contiguous GraphBatch."""
+        sel = lambda x: x.index_select(0, envs) if not isinstance(envs, slice) else x[envs]  # noqa: E731
+        nodes, edges = sel(graph.nodes).contiguous(), sel(graph.edges).contiguous()
+        recv, send = sel(graph.receivers).contiguous(), sel(graph.senders).contiguous()
+        Be, T = nodes.shape[:2]
+        return GraphBatch(nodes.view(Be * T, *nodes.shape[2:]), edges.view(Be * T, *edges.shape[2:]),
+                          recv.view(Be * T, -1), send.view(Be * T, -1), self._n_agents,
+                          self._env.agent_candidates(self.device))
+
+    def _last_graph(self, next_graph, envs=slice(None)) -> GraphBatch:
+        ng = next_graph
+        return GraphBatch(ng.nodes[envs, -1], ng.edges[envs, -1], ng.receivers[envs, -1], ng.senders[envs, -1],
+                          self._n_agents, self._env.agent_candidates(self.device))
+
+    def _vh_all(self, rollout: Rollout, chunk: int):
+        """Vh on every (env, t) graph with the stored actor carries, plus the final Vh (dgppo.py:218-228)."""
+        B, T, n = rollout.rewards.shape[0], rollout.rewards.shape[1], self._n_agents
+        out = torch.empty((B, T + 1, n, self._env.n_cost), device=self.device)
+        for e0 in range(0, B, chunk):
+            e1 = min(B, e0 + chunk)
+            g = self._graphs(rollout.graph, slice(e0, e1))
+            h = rollout.rnn_states[e0:e1].reshape((e1 - e0) * T * n, 64).contiguous()
+            v, _ = self.Vh.fwd(g, h, keep_cache=False)
+            out[e0:e1, :T].copy_(v.view(e1 - e0, T, n, -1))
+            # final: act on next_graph[-1] from rnn_states[-1], then Vh with that carry
+            gl = self._last_graph(rollout.next_graph, slice(e0, e1))
+            h_last = rollout.rnn_states[e0:e1, -1].reshape((e1 - e0) * n, 64).contiguous()
+            _, _, h2 = self.actor.act(gl, h_last, 0)
+            vf, _ = self.Vh.fwd(gl, h2, keep_cache=False)
+            out[e0:e1, T].copy_(vf.view(e1 - e0, n, -1))
+        return out
+
+    def _allreduce_grads(self):
+        if self.world > 1:
+            dist.all_reduce(self.grad_flat, op=dist.ReduceOp.SUM)
+            self.grad_flat.mul_(1.0 / self.world)
+
+    def update(self, rollout: Rollout, step: int) -> dict:
+        env, dev = self._env, self.device
+        B, T = rollout.rewards.shape
+        n = self._n_agents
+        det = self.det_rollout(B, int(self.key.integers(0, 2 ** 62)))
+        assert B * T * self.world >= self.batch_size
+        chunk = max(1, min(B, 65536 // T))
+        info = {}
+        for _ in range(self.epoch_ppo):
+            # ---- prepass: Vl scan over the whole episode + final Vl (dgppo.py:203-216)
+            Vl = torch.empty((B, T + 1), device=dev)
+            for e0 in range(0, B, chunk):
+                e1 = min(B, e0 + chunk)
+                g = self._graphs(rollout.graph, slice(e0, e1))
+                v, hT, _ = self.Vl.seq_fwd(g, e1 - e0, T, keep_cache=False)
+                Vl[e0:e1, :T].copy_(v)
+                vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
+                                           keep_cache=False)
+                Vl[e0:e1, T].copy_(vf[:, 0])
+            Vh = self._vh_all(rollout, chunk)
+            Vh_det = self._vh_all(det, chunk)
+            # ---- GAE + advantages
+            costs = rollout.costs.contiguous()
+            l = (-rollout.rewards).contiguous()
+            Qh = torch.empty((B, T, n, env.n_cost), device=dev)
+            Ql = torch.empty((B, T), device=dev)
+            K.gae(costs, l, Vh, Vl, Qh, Ql, self.gamma, self.gae_lambda)
+            Qh_det = torch.empty_like(Qh)
+            Ql_det = torch.empty_like(Ql)
+            K.gae(det.costs.contiguous(), (-det.rewards).contiguous(), Vh_det, Vl, Qh_det, Ql_det, self.gamma,
+                  self.gae_lambda)
+            A = torch.empty((B, T, n), device=dev)
+            safe_cnt = torch.empty(B, device=dev)
+            K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, env.dt, self.alpha, self.cbf_eps, self.cbf_weight_at(step))
+            # ---- minibatches (dgppo.py:155-159, 275-289)
+            idx = np.arange(B)
+            self.np_rng.shuffle(idx)
+            mb_envs_global = self.batch_size // T
+            n_mb = (B * self.world) // mb_envs_global
+            batches = np.array_split(idx, n_mb)
+            L = self.rnn_step
+            S_per_env = T // L
+            for bi in batches:
+                envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
+                Bm = len(bi)
+                self.grad_flat.zero_()
+                # update_Vl (informarl.py:357-385)
+                g = self._graphs(rollout.graph, envs)
+                v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
+                tgt = Ql.index_select(0, envs).view(Bm * S_per_env, L)
+                dv = torch.empty_like(v)
+                vl_loss = torch.empty(1, device=dev)
+                K.l2_loss(v, tgt, dv, vl_loss)
+                self.Vl.seq_bwd(cache, dv)
+                del cache
+                # update_Vh (dgppo.py:296-321) on the deterministic rollout
+                gd = self._graphs(det.graph, envs)
+                hd = det.rnn_states.index_select(0, envs).reshape(Bm * T * n, 64).contiguous()
+                vh, cache = self.Vh.fwd(gd, hd)
+                dvh = torch.empty_like(vh)
+                vh_loss = torch.empty(1, device=dev)
+                K.l2_loss(vh, Qh_det.index_select(0, envs).reshape(-1, env.n_cost), dvh, vh_loss)
+                self.Vh.bwd(cache, dvh)
+                del cache
+                # update_policy (informarl.py:405-457)
+                acts = rollout.actions.index_select(0, envs).reshape(-1, self._action_dim).contiguous()
+                lp_old = rollout.log_pis.index_select(0, envs).reshape(-1).contiguous()
+                adv = A.index_select(0, envs).reshape(-1).contiguous()
+                lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
+                dlp = torch.empty_like(lp)
+                dent = torch.empty_like(ent)
+                stats = torch.empty(4, device=dev)
+                K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, stats)
+                self.actor.eval_seq_bwd(cache, dlp, dent)
+                del cache
+                # one all-reduce for the three nets, then clip + finite check + Adam per net
+                self._allreduce_grads()
+                for name in ("Vl", "Vh", "policy"):
+                    self.opt[name].step()
+                info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
+                        "Vh/loss_Vh": vh_loss, "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
+            safe = safe_cnt.sum()
+            if self.world > 1:
+                dist.all_reduce(safe)
+            info["eval/safe_data"] = safe / (B * self.world * T * n)
+        return self._finish_info(info)
+
+    def _finish_info(self, info) -> dict:
+        out = {}
+        st = info.pop("policy/stats", None)
+        for k, v in info.items():
+            out[k] = float(v.reshape(-1)[0].item()) if torch.is_tensor(v) else v
+        if st is not None:
+            s = st.cpu().numpy()
+            out["policy/loss"] = float(s[0] - self.coef_ent * s[1])
+            out["policy/entropy"], out["policy/clip_frac"], out["policy/total_variation_dist"] = \
+                float(s[1]), float(s[2]), float(0.5 * s[3])
+        for name, tag in (("Vl", "Vl/grad_norm"), ("Vh", "Vh/grad_Vh_norm"), ("policy", "policy/grad_norm")):
+            stv = self.opt[name].state.cpu().numpy()
+            out[tag] = float(stv[0])
+            out[{"Vl": "Vl/has_nan", "Vh": "Vh/grad_Vh_has_nan", "policy": "policy/has_nan"}[name]] = float(stv[1] > 0)
+        return out
+
+    # ---- checkpoints ---------------------------------------------------------------------------
+    def save(self, save_dir: str, step: int):
+        """models/<step>/{actor,Vl,Vh}.pt: params AND Adam state (the reference keeps params only)."""
+        d = os.path.join(save_dir, str(step))
+        os.makedirs(d, exist_ok=True)
+        for name, net, opt in (("actor", self.actor, self.opt["policy"]), ("Vl", self.Vl, self.opt["Vl"]),
+                               ("Vh", self.Vh, self.opt["Vh"])):
+            torch.save({"params": net.ps.flat.cpu(), "m": opt.m.cpu(), "v": opt.v.cpu(), "state": opt.state.cpu(),
+                        "layout": [(n, s) for n, s, _ in net.ps.entries]}, os.path.join(d, f"{name}.pt"))
+
+    def load(self, load_dir: str, step: int):
+        d = os.path.join(load_dir, str(step))
+        for name, net, opt in (("actor", self.actor, self.opt["policy"]), ("Vl", self.Vl, self.opt["Vl"]),
+                               ("Vh", self.Vh, self.opt["Vh"])):
+            ck = torch.load(os.path.join(d, f"{name}.pt"), weights_only=True)
+            net.ps.flat.copy_(ck["params"])
+            opt.m.copy_(ck["m"]), opt.v.copy_(ck["v"]), opt.state.copy_(ck["state"])

@@ -615,6 +615,56 @@ __global__ __launch_bounds__(256) void gae_kernel(dgppo_gae_args p) {
   }
 }
 
+// ---- DGPPO advantages (dgppo/algo/dgppo.py:239-259), one workgroup per env -------------------
+//   Al = norm_t(Ql - Vl) (population std + 1e-8), cbf = (Vh_{t+1} - Vh_t)/dt + alpha Vh_t,
+//   safe = all_h(cbf <= 0), A = -(where(safe, Al, 0) + max_h relu(cbf + eps) * w)
+__global__ __launch_bounds__(256) void dgppo_adv_kernel(dgppo_adv_args p) {
+  __shared__ float red[2][4];
+  const int64_t b = blockIdx.x;
+  const int T = p.T, n = p.n_agents, nh = p.n_h;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* Ql = p.Ql + b * T;
+  const float* Vl = p.Vl + b * (T + 1);
+  float s = 0.0f;
+  for (int t = tid; t < T; t += 256) s += Ql[t] - Vl[t];
+  s = wave_sum(s);
+  if (lane == 0) red[0][wave] = s;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / T;
+  float s2 = 0.0f;
+  for (int t = tid; t < T; t += 256) {
+    const float d = (Ql[t] - Vl[t]) - mean;
+    s2 += d * d;
+  }
+  s2 = wave_sum(s2);
+  if (lane == 0) red[1][wave] = s2;
+  __syncthreads();
+  const float sd = sqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / T);
+  const float* Vh = p.Vh + b * (int64_t)(T + 1) * n * nh;
+  float safe_cnt = 0.0f;
+  for (int q = tid; q < T * n; q += 256) {
+    const int t = q / n, i = q - (q / n) * n;
+    const float al = ((Ql[t] - Vl[t]) - mean) / (sd + 1e-8f);
+    bool safe = true;
+    float amax = 0.0f;
+    for (int h = 0; h < nh; ++h) {
+      const float v0 = Vh[((int64_t)t * n + i) * nh + h];
+      const float v1 = Vh[((int64_t)(t + 1) * n + i) * nh + h];
+      const float dv = (v1 - v0) / p.dt + p.alpha * v0;
+      safe = safe && (dv <= 0.0f);
+      const float ac = fmaxf(dv + p.cbf_eps, 0.0f);
+      amax = h == 0 ? ac : fmaxf(amax, ac);
+    }
+    p.A[(b * T + t) * n + i] = -((safe ? al : 0.0f) + amax * p.cbf_weight);
+    safe_cnt += safe ? 1.0f : 0.0f;
+  }
+  safe_cnt = wave_sum(safe_cnt);
+  __syncthreads();
+  if (lane == 0) red[0][wave] = safe_cnt;
+  __syncthreads();
+  if (tid == 0) p.safe_count[b] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+}
+
 // ---- global norm / finite check, clipped Adam (optax.adam + apply_if_finite) ------------------
 __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int64_t n, float* part) {
   float v[2] = {0.0f, 0.0f};
@@ -872,6 +922,15 @@ extern "C" int dgppo_gae(const dgppo_gae_args* p, void* stream) {
   const int K = p->n_agents * p->n_h;
   const size_t shmem = ((size_t)(p->T + 1) * (K + 2) + 4 * (K + 1)) * sizeof(float);
   hipLaunchKernelGGL(gae_kernel, dim3((unsigned)p->B), dim3(256), shmem, DG_STREAM(stream), *p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_dgppo_advantages(const dgppo_adv_args* p, void* stream) {
+  if (!p || p->B < 0 || p->T < 1 || p->n_agents < 1 || p->n_h < 1 || !p->Ql || !p->Vl || !p->Vh || !p->A ||
+      !p->safe_count)
+    return DGPPO_EINVAL;
+  if (p->B == 0) return 0;
+  hipLaunchKernelGGL(dgppo_adv_kernel, dim3((unsigned)p->B), dim3(256), 0, DG_STREAM(stream), *p);
   return (int)hipGetLastError();
 }
 

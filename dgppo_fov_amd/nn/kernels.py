@@ -163,3 +163,13 @@ def normal_(out, seed=0, stream_id=0, seed_tensor=None):
     _chk(_lib.load().dgppo_normal(_p(out), int(out.numel()), _p(seed_tensor), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                   int(stream_id) & 0xFFFFFFFFFFFFFFFF, _stream(out)), "dgppo_normal")
     return out
+
+
+def dgppo_advantages(Ql, Vl, Vh, A, safe_count, dt, alpha, cbf_eps, cbf_weight):
+    B, T = Ql.shape
+    _, _, n, nh = Vh.shape
+    a = _lib.AdvArgs()
+    a.B, a.T, a.n_agents, a.n_h = int(B), int(T), int(n), int(nh)
+    a.Ql, a.Vl, a.Vh, a.A, a.safe_count = _p(Ql), _p(Vl), _p(Vh), _p(A), _p(safe_count)
+    a.dt, a.alpha, a.cbf_eps, a.cbf_weight = float(dt), float(alpha), float(cbf_eps), float(cbf_weight)
+    _chk(_lib.load().dgppo_dgppo_advantages(ctypes.byref(a), _stream(Ql)), "dgppo_dgppo_advantages")

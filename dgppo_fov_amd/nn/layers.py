@@ -51,6 +51,9 @@ class ParamSpace:
     def build(self, device):
         self.flat = torch.zeros(self.size, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.size, dtype=torch.float32, device=device)
+        return self.build_views()
+
+    def build_views(self):
         self._views = {}
         for n, shape, _ in self.entries:
             o, sz = self.offsets[n], int(np.prod(shape))

@@ -1,59 +1,87 @@
 """Device-resident rollout driver: the reference's `rollout` / `test_rollout`
-(dgppo/trainer/utils.py:22-86: reset, then lax.scan of (actor, env.step) over T steps) as a
-fixed sequence of HIP launches over preallocated (B, T+1, ...) HBM buffers, optionally captured
-once into a hipGraph and replayed (one host call per episode instead of 2T+1 launches).
+(dgppo/trainer/utils.py:22-86: reset, then lax.scan of (actor, env.step) over T steps) as a fixed
+sequence of HIP launches over preallocated TIME-MAJOR HBM buffers, optionally captured once into
+a hipGraph and replayed (one host call per episode instead of ~25T launches).
 
-The actor is any callable `actor(graph_t, t)` that writes actions into `self.actions[:, t]`
-(and log-probs / carries into its own buffers) with device-side launches only; `None` keeps the
-actions already stored in `self.actions` (synthetic/random-action rollouts)."""
+Buffers are time-major, (T+1, B, ...), so the graph of step t is one contiguous (B, ...) block
+that the env-step and GNN kernels read and write without copies; the Rollout handed to the
+algorithm exposes the reference's (B, T, ...) leading dims as permuted views.
+
+Actor carry semantics follow the reference exactly:
+  stochastic `rollout`   rnn_states[t] = carry BEFORE acting on graph t (utils.py:186-192)
+  deterministic `test_rollout` rnn_states[t] = carry AFTER acting on graph t (utils.py:211-218)
+"""
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Optional
 
 import torch
 
 from ..env.base import MultiAgentEnv
+from ..nn import kernels as K
+from ..nn.layers import GraphBatch
 from ..utils.graph import GraphsTuple
 from .data import Rollout
 
 
 class RolloutEngine:
+    MODE_RANDOM, MODE_SAMPLE, MODE_DET = -1, 1, 0
+
     def __init__(self, env: MultiAgentEnv, n_env: int, T: Optional[int] = None, device=None, env_offset: int = 0,
-                 actor: Optional[Callable] = None):
+                 actor=None, mode: int = -1):
+        """actor: an ActorNet (or None); mode: MODE_SAMPLE (stochastic policy, sample_action),
+        MODE_DET (deterministic policy, get_action) or MODE_RANDOM (keep `self.actions` as given)."""
         self.env = env
         self.B = int(n_env)
         self.T = int(T or env.max_episode_steps)
         self.device = torch.device(device) if device is not None else env.device
         self.env_offset = int(env_offset)
         self.actor = actor
-        B, T, n = self.B, self.T, env.num_agents
-        self.buf = env.empty_graph((B, T + 1), self.device)
+        self.mode = mode if actor is not None else self.MODE_RANDOM
+        B, T, n, dev = self.B, self.T, env.num_agents, self.device
+        self.buf = env.empty_graph((T + 1, B), dev)
         nf = env._obstacle_fields()
-        self.obstacles = (torch.empty((B, max(env.n_obs, 1), nf), dtype=torch.float32, device=self.device)
-                          if nf else None)
-        self.actions = torch.zeros((B, T, n, env.action_dim), dtype=torch.float32, device=self.device)
-        self.rewards = torch.empty((B, T), dtype=torch.float32, device=self.device)
-        self.costs = torch.empty((B, T, n, env.n_cost), dtype=torch.float32, device=self.device)
-        self.dones = torch.zeros((B, T), dtype=torch.bool, device=self.device)
-        self.key = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.obstacles = (torch.empty((B, max(env.n_obs, 1), nf), dtype=torch.float32, device=dev) if nf else None)
+        self.actions = torch.zeros((T, B, n, env.action_dim), dtype=torch.float32, device=dev)
+        self.rewards = torch.empty((T, B), dtype=torch.float32, device=dev)
+        self.costs = torch.empty((T, B, n, env.n_cost), dtype=torch.float32, device=dev)
+        self.dones = torch.zeros((T, B), dtype=torch.bool, device=dev)
+        self.key = torch.zeros(1, dtype=torch.int64, device=dev)
+        if actor is not None:
+            self.rnn = torch.zeros((T + 1, B, n, 64), dtype=torch.float32, device=dev)
+            self.log_pis = torch.zeros((T, B, n), dtype=torch.float32, device=dev)
+            self.noise = torch.empty((B * n, env.action_dim), dtype=torch.float32, device=dev)
         self._hip_graph = None
 
     def graph_at(self, t: int) -> GraphsTuple:
         b = self.buf
-        return self.env._assemble(b.nodes[:, t], b.edges[:, t], b.states[:, t], b.receivers[:, t],
-                                  b.senders[:, t], self.obstacles)
+        return self.env._assemble(b.nodes[t], b.edges[t], b.states[t], b.receivers[t], b.senders[t], self.obstacles)
+
+    def _act(self, t: int):
+        env, b = self.env, self.buf
+        g = GraphBatch(b.nodes[t], b.edges[t], b.receivers[t], b.senders[t], env.num_agents,
+                       env.agent_candidates(self.device))
+        n = env.num_agents
+        h = self.rnn[t].view(self.B * n, 64)
+        if self.mode == self.MODE_SAMPLE:
+            K.normal_(self.noise, stream_id=t, seed_tensor=self.key)
+            self.actor.act(g, h, 1, noise=self.noise, action_out=self.actions[t].view(-1, env.action_dim),
+                           log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, 64))
+        else:
+            self.actor.act(g, h, 0, action_out=self.actions[t].view(-1, env.action_dim),
+                           h_out=self.rnn[t + 1].view(self.B * n, 64))
 
     def _run(self):
         env = self.env
         cur = env.reset(self.key, n_env=self.B, env_offset=self.env_offset, out=self.graph_at(0),
                         obstacles_out=self.obstacles)
         for t in range(self.T):
-            if self.actor is not None:
-                self.actor(cur, t)
-            cur = env.step_into(cur, self.actions[:, t], self.graph_at(t + 1), self.rewards[:, t], self.costs[:, t])
+            if self.mode != self.MODE_RANDOM:
+                self._act(t)
+            cur = env.step_into(cur, self.actions[t], self.graph_at(t + 1), self.rewards[t], self.costs[t])
 
     def capture(self):
-        """Record reset + T steps into one hipGraph (after one eager warm-up run)."""
+        """Record reset + T x (actor, step) into one hipGraph (after one eager warm-up run)."""
         self._run()
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
@@ -71,12 +99,20 @@ class RolloutEngine:
         return self.rollout()
 
     def rollout(self) -> Rollout:
-        b = self.buf
-        T = self.T
+        """(B, T, ...) views of the time-major buffers (Rollout of dgppo/trainer/data.py)."""
+        b, T = self.buf, self.T
 
         def view(sl):
-            return self.env._assemble(b.nodes[:, sl], b.edges[:, sl], b.states[:, sl], b.receivers[:, sl],
-                                      b.senders[:, sl], self.obstacles)
+            tr = lambda x: x[sl].transpose(0, 1)  # noqa: E731
+            return self.env._assemble(tr(b.nodes), tr(b.edges), tr(b.states), tr(b.receivers), tr(b.senders),
+                                      self.obstacles)
 
-        return Rollout(view(slice(0, T)), self.actions, None, self.rewards, self.costs, self.dones, None,
-                       view(slice(1, T + 1)))
+        rnn = None
+        log_pis = None
+        if self.actor is not None:
+            # (B, T, 1, n, 1, 64): rnn_states[t] = carry before (stochastic) / after (deterministic) step t
+            sl = slice(0, T) if self.mode == self.MODE_SAMPLE else slice(1, T + 1)
+            rnn = self.rnn[sl].transpose(0, 1).unsqueeze(2).unsqueeze(4)
+            log_pis = self.log_pis.transpose(0, 1) if self.mode == self.MODE_SAMPLE else None
+        return Rollout(view(slice(0, T)), self.actions.transpose(0, 1), rnn, self.rewards.transpose(0, 1),
+                       self.costs.transpose(0, 1), self.dones.transpose(0, 1), log_pis, view(slice(1, T + 1)))

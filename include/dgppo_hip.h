@@ -267,6 +267,21 @@ typedef struct dgppo_gae_args {
 
 int dgppo_gae(const dgppo_gae_args* args, void* stream);
 
+/* DGPPO advantages (dgppo/algo/dgppo.py:239-259): per env, Al = (Ql - Vl) normalised over T,
+ * CBF derivative of Vh, A = -(where(safe, Al, 0) + max_h relu(cbf + cbf_eps) * cbf_weight);
+ * safe_count[b] = number of safe (t, agent) pairs (for eval/safe_data). */
+typedef struct dgppo_adv_args {
+  int32_t B, T, n_agents, n_h;
+  const float* Ql;  /* (B, T) */
+  const float* Vl;  /* (B, T+1) */
+  const float* Vh;  /* (B, T+1, n, nh) */
+  float dt, alpha, cbf_eps, cbf_weight;
+  float* A;         /* (B, T, n) */
+  float* safe_count;/* (B) */
+} dgppo_adv_args;
+
+int dgppo_dgppo_advantages(const dgppo_adv_args* args, void* stream);
+
 /* compute_norm_and_clip + optax.adam + apply_if_finite (dgppo/trainer/utils.py:105-118,
  * informarl.py:131-137): state = [global norm, non-finite count, adam step] on the device */
 int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace, void* stream);
