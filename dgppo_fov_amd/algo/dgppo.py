@@ -91,6 +91,7 @@ class DGPPO:
         self.init_rnn_state = torch.zeros((rnn_layers, n_agents, 1, 64), device=dev)
         self.init_Vl_rnn_state = torch.zeros((rnn_layers, 1, 1, 64), device=dev)
         self._engines = {}
+        self.trace: Optional[dict] = None  # set to {} to record update intermediates (parity tests)
         self.key = np.random.default_rng(seed)
         self.np_rng = np.random.default_rng(seed)
 
@@ -254,6 +255,10 @@ class DGPPO:
             A = torch.empty((B, T, n), device=dev)
             safe_cnt = torch.empty(B, device=dev)
             K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, env.dt, self.alpha, self.cbf_eps, self.cbf_weight_at(step))
+            if self.trace is not None:
+                self.trace.update(det=det, Vl=Vl.clone(), Vh=Vh.clone(), Vh_det=Vh_det.clone(), Ql=Ql.clone(),
+                                  Qh=Qh.clone(), Qh_det=Qh_det.clone(), A=A.clone(), safe_cnt=safe_cnt.clone(),
+                                  mb=[])
             # ---- minibatches (dgppo.py:155-159, 275-289)
             idx = np.arange(B)
             self.np_rng.shuffle(idx)
@@ -261,6 +266,7 @@ class DGPPO:
             n_mb = (B * self.world) // mb_envs_global
             batches = np.array_split(idx, n_mb)
             L = self.rnn_step
+            assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
             S_per_env = T // L
             for bi in batches:
                 envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
@@ -297,6 +303,13 @@ class DGPPO:
                 del cache
                 # one all-reduce for the three nets, then clip + finite check + Adam per net
                 self._allreduce_grads()
+                if self.trace is not None:
+                    self.trace["mb"].append(dict(
+                        envs=bi.copy(), grad=self.grad_flat.clone(), vl_loss=vl_loss.clone(), vh_loss=vh_loss.clone(),
+                        stats=stats.clone(), before={k: o.ps.flat.clone() for k, o in self.opt.items()},
+                        m_before={k: o.m.clone() for k, o in self.opt.items()},
+                        v_before={k: o.v.clone() for k, o in self.opt.items()},
+                        state_before={k: o.state.clone() for k, o in self.opt.items()}))
                 for name in ("Vl", "Vh", "policy"):
                     self.opt[name].step()
                 info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),

@@ -64,7 +64,8 @@ class RolloutEngine:
         n = env.num_agents
         h = self.rnn[t].view(self.B * n, 64)
         if self.mode == self.MODE_SAMPLE:
-            K.normal_(self.noise, stream_id=t, seed_tensor=self.key)
+            # per-step, per-shard Philox stream: (env_offset, t) -> disjoint noise across ranks
+            K.normal_(self.noise, stream_id=(self.env_offset << 32) | t, seed_tensor=self.key)
             self.actor.act(g, h, 1, noise=self.noise, action_out=self.actions[t].view(-1, env.action_dim),
                            log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, 64))
         else:

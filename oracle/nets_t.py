@@ -137,15 +137,22 @@ def actor_eval_seq(p, graph, S, L, n, actions, eps_fixed):
     return tanh_normal_log_prob(act, mu, sd), tanh_normal_entropy(mu, sd, eps_fixed)
 
 
-def vl_seq(p, graph, S, L, n):
-    """scan_Vl over S sequences of L graphs with zero carries: values (S, L)."""
+def vl_seq(p, graph, S, L, n, h0=None, return_h=False):
+    """scan_Vl over S sequences of L graphs (zero carries unless h0 (S, 64)): values (S, L)."""
     y = mlp_head(gnn(p["gnn"], graph, n).mean(1), p["head"]).reshape(S, L, 64)
-    h = torch.zeros((S, 64), dtype=T64)
+    h = torch.zeros((S, 64), dtype=T64) if h0 is None else torch.as_tensor(h0, dtype=T64)
     vs = []
     for t in range(L):
         h = gru_cell(p["gru"], h, y[:, t])
         vs.append(dense(h, p["out"])[:, 0])
-    return torch.stack(vs, 1)
+    v = torch.stack(vs, 1)
+    return (v, h) if return_h else v
+
+
+def actor_carry(p, graph, h, n):
+    """act(): the policy GRU carry after one graph (policy.py:61-74), h (G, n, 64)."""
+    y = mlp_head(gnn(p["gnn"], graph, n), p["head"])
+    return gru_cell(p["gru"], torch.as_tensor(h, dtype=T64), y)
 
 
 def vh(p, graph, h, n):
@@ -167,3 +174,80 @@ def grads(tree):
     if isinstance(tree, list):
         return [grads(v) for v in tree]
     return None if tree.grad is None else tree.grad.detach().numpy()
+
+
+# ---- one DGPPO update (dgppo.py:136-321, informarl.py:357-457) ---------------------------------
+def _flat(graph, envs=None):
+    """(B, T, ...) host graph dict -> (B*T, ...) env-major (= chunk-major for any rnn_step)."""
+    out = {}
+    for k in ("nodes", "edges", "receivers", "senders"):
+        x = np.asarray(graph[k])
+        if envs is not None:
+            x = x[envs]
+        out[k] = x.reshape((-1,) + x.shape[2:])
+    return out
+
+
+def dgppo_prepass(pa, pl, ph, roll, det, n, dt, gamma, lam, alpha, cbf_eps, cbf_w):
+    """Vl / Vh / Dec-OCP GAE / merged advantage of DGPPO.update_inner (dgppo.py:200-283).
+    roll / det: dicts of host arrays: graph (B, T, ...) dict, last (B, ...) dict (next_graph[:, -1]),
+    rewards (B, T), costs (B, T, n, nh), rnn (B, T, n, 64) stored actor carries."""
+    from .nets import compute_dec_ocp_gae
+    B, T = roll["rewards"].shape
+    with torch.no_grad():
+        v, hT = vl_seq(pl, _flat(roll["graph"]), B, T, n, return_h=True)
+        vf = vl_seq(pl, _flat({k: x[:, None] for k, x in roll["last"].items()}), B, 1, n, h0=hT)
+        Vl = torch.cat([v, vf], 1).numpy()
+
+        def vh_all(r):
+            nh = r["costs"].shape[-1]
+            vhs = vh(ph, _flat(r["graph"]), np.asarray(r["rnn"]).reshape(B * T, n, 64), n).reshape(B, T, n, nh)
+            h2 = actor_carry(pa, _flat({k: x[:, None] for k, x in r["last"].items()}), r["rnn"][:, -1], n)
+            vfin = vh(ph, _flat({k: x[:, None] for k, x in r["last"].items()}), h2.numpy(), n)
+            return torch.cat([vhs, vfin.reshape(B, 1, n, nh)], 1).numpy()
+
+        Vh, Vh_det = vh_all(roll), vh_all(det)
+    Qh, Ql, Qh_det = [], [], []
+    for b in range(B):
+        qh, ql = compute_dec_ocp_gae(roll["costs"][b].astype(np.float64), -roll["rewards"][b].astype(np.float64),
+                                     Vh[b], Vl[b], gamma, lam)
+        qhd, _ = compute_dec_ocp_gae(det["costs"][b].astype(np.float64), -det["rewards"][b].astype(np.float64),
+                                     Vh_det[b], Vl[b], gamma, lam)
+        Qh.append(qh), Ql.append(ql), Qh_det.append(qhd)
+    Qh, Ql, Qh_det = np.stack(Qh), np.stack(Ql), np.stack(Qh_det)
+    Al = Ql - Vl[:, :T]
+    Al = (Al - Al.mean(1, keepdims=True)) / (Al.std(1, keepdims=True) + 1e-8)
+    deriv = (Vh[:, 1:] - Vh[:, :T]) / dt + alpha * Vh[:, :T]
+    Acbf = np.maximum(deriv + cbf_eps, 0.0)
+    is_safe = (deriv <= 0).min(-1)
+    A = -(np.where(is_safe, Al[:, :, None], 0.0) + Acbf.max(-1) * cbf_w)
+    return dict(Vl=Vl, Vh=Vh, Vh_det=Vh_det, Qh=Qh, Ql=Ql, Qh_det=Qh_det, A=A, deriv=deriv,
+                safe_data=is_safe.mean())
+
+
+def dgppo_minibatch_grads(pa, pl, ph, roll, det, envs, Ql, Qh_det, A, n, L, eps_fixed, clip_eps, coef_ent):
+    """Losses + autograd gradients of update_Vl / update_Vh / update_policy for one minibatch of
+    envs (targets Ql (B, T), Qh_det (B, T, n, nh) and advantages A (B, T, n) given).  pa/pl/ph must
+    be leaf trees with requires_grad."""
+    B, T = roll["rewards"].shape
+    Bm = len(envs)
+    S = Bm * (T // L)
+    g = _flat(roll["graph"], envs)
+    v = vl_seq(pl, g, S, L, n)
+    tgt = torch.as_tensor(Ql[envs].reshape(S, L), dtype=T64)
+    loss_vl = (0.5 * (v - tgt) ** 2).mean()
+    loss_vl.backward()
+    gd = _flat(det["graph"], envs)
+    nh = Qh_det.shape[-1]
+    out = vh(ph, gd, np.asarray(det["rnn"])[envs].reshape(Bm * T, n, 64), n)
+    loss_vh = (0.5 * (out - torch.as_tensor(Qh_det[envs].reshape(Bm * T, n, nh), dtype=T64)) ** 2).mean()
+    loss_vh.backward()
+    acts = np.asarray(roll["actions"])[envs].reshape(S * L * n, -1)
+    lp, ent = actor_eval_seq(pa, g, S, L, n, acts, eps_fixed)
+    lp_old = torch.as_tensor(np.asarray(roll["log_pis"])[envs].reshape(S, L, n), dtype=T64)
+    adv = torch.as_tensor(A[envs].reshape(S, L, n), dtype=T64)
+    loss_pi = ppo_loss(lp, lp_old, adv, ent, clip_eps, coef_ent)
+    loss_pi.backward()
+    ratio = torch.exp(lp - lp_old).detach()
+    return dict(Vl_loss=loss_vl.item(), Vh_loss=loss_vh.item(), policy_loss=loss_pi.item(),
+                entropy=ent.mean().item(), tv=0.5 * (ratio - 1).abs().mean().item())

@@ -1,0 +1,102 @@
+"""GPU parity for the policy rollout (trainer/utils.py:22-86 rollout / test_rollout as one
+captured hipGraph, trainer/rollout.py): every step's actor carry, tanh-normal action and log_pi
+against the float64 oracle (policy.py:61-74, 191-212, distribution.py), the env transition
+against the env kernel itself (bit-exact), and the carry-storage conventions of both rollouts.
+
+The sampling noise is the framework's Philox stream (the reference's threefry stream is not
+reproducible without JAX), regenerated here from (key, env_offset, t); its moments are checked.
+Tolerances: carries / actions / log_pi |gpu - ref| <= 3e-5 (1 + |ref|)."""
+import numpy as np
+import pytest
+import torch
+
+from dgppo_fov_amd.algo import make_algo
+from dgppo_fov_amd.env import make_env
+from dgppo_fov_amd.nn import kernels as K
+from dgppo_fov_amd.trainer.rollout import RolloutEngine
+from oracle import nets_t as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol, what):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = (np.abs(a - b) - tol * (1 + np.abs(b))).max()
+    assert err <= 0, f"{what}: max abs err {np.abs(a - b).max():.3e}"
+
+
+def test_normal_moments(cuda):
+    x = torch.empty(1 << 22, device=cuda)
+    K.normal_(x, seed=123, stream_id=5)
+    y = x.double()
+    assert abs(y.mean().item()) < 3e-3 and abs(y.std().item() - 1) < 3e-3
+    assert abs((y ** 4).mean().item() - 3) < 2e-2
+    z = torch.empty_like(x)
+    K.normal_(z, seed=123, stream_id=6)
+    assert abs(torch.corrcoef(torch.stack([x, z]))[0, 1].item()) < 3e-3
+    z2 = torch.empty_like(x)
+    K.normal_(z2, seed=123, stream_id=5)
+    assert torch.equal(x, z2)
+
+
+def _host_graph(eng, t):
+    b = eng.buf
+    return {k: getattr(b, k)[t].cpu().numpy() for k in ("nodes", "edges", "receivers", "senders")}
+
+
+@pytest.mark.parametrize("eid,n,obs,graph", [("LidarSpread", 3, 2, True), ("MPETarget", 3, 0, False),
+                                             ("LidarBicycleTarget", 2, 1, True)])
+def test_policy_rollout_matches_oracle(cuda, eid, n, obs, graph):
+    B, T = 3, 12
+    env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=n, batch_size=B * T, rnn_step=4, seed=2, device=cuda)
+    pa = R.to_t(algo.actor.flax())
+    for mode in (RolloutEngine.MODE_SAMPLE, RolloutEngine.MODE_DET):
+        eng = RolloutEngine(env, B, T, cuda, env_offset=0, actor=algo.actor, mode=mode)
+        if graph:
+            eng.capture()
+        roll = eng.run(11)
+        torch.cuda.synchronize()
+        rnn = eng.rnn.cpu().numpy()
+        assert np.abs(rnn[0]).max() == 0
+        noise = torch.empty((B * n, env.action_dim), device=cuda)
+        for t in range(T):
+            g = _host_graph(eng, t)
+            with torch.no_grad():
+                h2 = R.actor_carry(pa, g, rnn[t], n)
+                mu, sd = R.policy_dist(pa, h2)
+            _close(rnn[t + 1], h2.numpy(), 3e-5, f"carry t={t}")
+            a = eng.actions[t].cpu().numpy()
+            if mode == RolloutEngine.MODE_SAMPLE:
+                K.normal_(noise, seed=11, stream_id=t)
+                eps = noise.view(B, n, -1).double().cpu()
+                _close(a, torch.tanh(mu + sd * eps).numpy(), 3e-5, f"action t={t}")
+                lp = R.tanh_normal_log_prob(a.astype(np.float64), mu, sd)
+                _close(eng.log_pis[t].cpu().numpy(), lp.numpy(), 3e-5, f"log_pi t={t}")
+            else:
+                _close(a, torch.tanh(mu).numpy(), 3e-5, f"det action t={t}")
+            # env transition: graph t+1 is exactly env.step(graph t, action t)
+            nxt = env.step(eng.graph_at(t), eng.actions[t])
+            for k in ("nodes", "edges", "states", "receivers", "senders"):
+                assert torch.equal(getattr(nxt.graph, k), getattr(eng.graph_at(t + 1), k)), (t, k)
+            assert torch.equal(nxt.reward, eng.rewards[t]) and torch.equal(nxt.cost, eng.costs[t])
+        # storage conventions (utils.py:186-192 stochastic: carry before; 211-218 det: carry after)
+        want = slice(0, T) if mode == RolloutEngine.MODE_SAMPLE else slice(1, T + 1)
+        got = roll.rnn_states.reshape(B, T, n, 64).transpose(0, 1).cpu().numpy()
+        assert np.array_equal(got, rnn[want])
+        assert roll.graph.nodes.shape[:2] == (B, T) and roll.next_graph.nodes.shape[:2] == (B, T)
+        assert torch.equal(roll.next_graph.nodes[:, 0], roll.graph.nodes[:, 1])
+
+
+def test_rollout_shards_use_disjoint_noise(cuda):
+    env = make_env("MPETarget", 3, num_obs=0, max_step=4, device=cuda)
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=3, batch_size=8, rnn_step=4, seed=2, device=cuda)
+    acts = []
+    for off in (0, 2):
+        eng = RolloutEngine(env, 2, 4, cuda, env_offset=off, actor=algo.actor, mode=RolloutEngine.MODE_SAMPLE)
+        eng.run(5)
+        acts.append(eng.actions.clone())
+    assert not torch.equal(acts[0], acts[1])

@@ -1,0 +1,215 @@
+"""GPU parity for the DGPPO update (hot path 2 end to end): Dec-OCP GAE, merged DGPPO advantage,
+global-norm clip + apply_if_finite Adam, and one full `DGPPO.update` (prepass Vl/Vh on both rollouts,
+targets, advantages, Vl/Vh/policy losses and gradients, Adam) against the float64 restatement in
+oracle/nets.py + oracle/nets_t.py (dgppo.py:136-321, informarl.py:357-457, algo/utils.py:11-79).
+
+Tolerances (fp32 kernels vs float64): values / targets |gpu - ref| <= 3e-5 (1 + |ref|);
+advantages compared where every CBF-derivative component is farther than 1e-3 from the is_safe
+threshold (a sign decided by fp32 noise is not a parity failure); gradients within 2e-5 of the largest reference entry or 8x
+the error of the float32 evaluation of the same oracle; Adam results within 1e-6 absolute (lr-sized steps)."""
+import numpy as np
+import pytest
+import torch
+
+from dgppo_fov_amd.algo import make_algo
+from dgppo_fov_amd.env import make_env
+from dgppo_fov_amd.nn import kernels as K
+from oracle import nets as O
+from oracle import nets_t as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol, what):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = (np.abs(a - b) - tol * (1 + np.abs(b))).max()
+    assert err <= 0, f"{what}: max abs err {np.abs(a - b).max():.3e}"
+
+
+def _walk(a, b, path=""):
+    if isinstance(a, dict):
+        for k in a:
+            yield from _walk(a[k], b[k], f"{path}/{k}")
+    elif isinstance(a, list):
+        for i, (x, y) in enumerate(zip(a, b)):
+            yield from _walk(x, y, f"{path}[{i}]")
+    else:
+        yield path, a, b
+
+
+# ---- GAE -------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,T,n,nh", [(3, 1, 1, 1), (2, 32, 3, 2), (2, 128, 8, 2), (1, 255, 16, 2)])
+def test_gae_matches_oracle(cuda, B, T, n, nh):
+    rng = np.random.default_rng(T + n)
+    hs = rng.standard_normal((B, T, n, nh)).astype(np.float32)
+    l = rng.standard_normal((B, T)).astype(np.float32)
+    Vh = rng.standard_normal((B, T + 1, n, nh)).astype(np.float32)
+    Vl = rng.standard_normal((B, T + 1)).astype(np.float32)
+    Qh = torch.empty((B, T, n, nh), device=cuda)
+    Ql = torch.empty((B, T), device=cuda)
+    d = lambda x: torch.from_numpy(x).to(cuda)  # noqa: E731
+    K.gae(d(hs), d(l), d(Vh), d(Vl), Qh, Ql, 0.99, 0.95)
+    torch.cuda.synchronize()
+    for b in range(B):
+        qh, ql = O.compute_dec_ocp_gae(hs[b].astype(np.float64), l[b].astype(np.float64), Vh[b].astype(np.float64),
+                                       Vl[b].astype(np.float64), 0.99, 0.95)
+        _close(Qh[b].cpu().numpy(), qh, 2e-5, f"Qh[{b}]")
+        _close(Ql[b].cpu().numpy(), ql, 2e-5, f"Ql[{b}]")
+
+
+# ---- DGPPO advantage ---------------------------------------------------------------------------
+def test_dgppo_advantages_match_oracle(cuda):
+    B, T, n, nh = 3, 64, 4, 2
+    rng = np.random.default_rng(0)
+    Ql = rng.standard_normal((B, T)).astype(np.float32)
+    Vl = rng.standard_normal((B, T + 1)).astype(np.float32)
+    Vh = (rng.standard_normal((B, T + 1, n, nh)) * 0.05).astype(np.float32)
+    d = lambda x: torch.from_numpy(x).to(cuda)  # noqa: E731
+    A = torch.empty((B, T, n), device=cuda)
+    cnt = torch.empty(B, device=cuda)
+    dt, alpha, eps, w = 0.03, 10.0, 1e-2, 2.0
+    K.dgppo_advantages(d(Ql), d(Vl), d(Vh), A, cnt, dt, alpha, eps, w)
+    torch.cuda.synchronize()
+    Vh64 = Vh.astype(np.float64)
+    Al = Ql - Vl[:, :T].astype(np.float64)
+    Al = (Al - Al.mean(1, keepdims=True)) / (Al.std(1, keepdims=True) + 1e-8)
+    deriv = (Vh64[:, 1:] - Vh64[:, :T]) / dt + alpha * Vh64[:, :T]
+    safe = (deriv <= 0).min(-1)
+    ref = -(np.where(safe, Al[..., None], 0) + np.maximum(deriv + eps, 0).max(-1) * w)
+    robust = np.abs(deriv).min(-1) > 1e-3
+    _close(A.cpu().numpy()[robust], ref[robust], 2e-5, "A")
+    assert abs(cnt.sum().item() - safe.sum()) <= (~robust).sum()
+
+
+# ---- clip + apply_if_finite Adam ------------------------------------------------------------------
+@pytest.mark.parametrize("scale", [1e-3, 10.0])
+def test_adam_clip_matches_optax_restatement(cuda, scale):
+    rng = np.random.default_rng(5)
+    n = 70_001
+    p = rng.standard_normal(n).astype(np.float32)
+    m = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    v = (rng.random(n) * 1e-4).astype(np.float32)
+    g = (rng.standard_normal(n) * scale).astype(np.float32)
+    d = lambda x: torch.from_numpy(x.copy()).to(cuda)  # noqa: E731
+    P, M, V, G = d(p), d(m), d(v), d(g)
+    st = torch.tensor([0.0, 0.0, 4.0], device=cuda)
+    K.grad_norm(G, st)
+    K.adam(P, G, M, V, st, 1e-3, max_norm=2.0)
+    torch.cuda.synchronize()
+    (gc,), gn = O.clip_by_global_norm_ref([g], 2.0)
+    (rp,), (rm,), (rv,) = O.adam_step([p.astype(np.float64)], [gc], [m.astype(np.float64)], [v.astype(np.float64)],
+                                      4, 1e-3)
+    assert abs(st[0].item() - gn) <= 1e-5 * gn
+    assert st[1].item() == 0 and st[2].item() == 5
+    assert np.abs(P.cpu().numpy() - rp).max() <= 1e-6
+    _close(M.cpu().numpy(), rm, 1e-6, "m")
+    _close(V.cpu().numpy(), rv, 1e-6, "v")
+
+
+def test_adam_skips_nonfinite_update(cuda):
+    g = torch.ones(1000, device=cuda)
+    g[17] = float("nan")
+    p = torch.randn(1000, device=cuda)
+    p0 = p.clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    st = torch.zeros(3, device=cuda)
+    K.grad_norm(g, st)
+    K.adam(p, g, m, v, st, 1e-3)
+    torch.cuda.synchronize()
+    assert st[1].item() > 0 and st[2].item() == 0
+    assert torch.equal(p, p0) and m.abs().max() == 0 and v.abs().max() == 0
+
+
+# ---- one full DGPPO.update ---------------------------------------------------------------------
+def _host(r, n):
+    B, T = r.rewards.shape
+    f = lambda G, sl: {k: getattr(G, k)[sl].cpu().numpy() for k in ("nodes", "edges", "receivers", "senders")}  # noqa
+    return dict(graph=f(r.graph, slice(None)), last=f(r.next_graph, (slice(None), -1)),
+                rewards=r.rewards.cpu().numpy(), costs=r.costs.cpu().numpy(),
+                rnn=r.rnn_states.reshape(B, T, n, 64).cpu().numpy(), actions=r.actions.cpu().numpy(),
+                log_pis=None if r.log_pis is None else r.log_pis.cpu().numpy())
+
+
+def _net_trees(algo, grad=False):
+    out = []
+    for net in (algo.actor, algo.Vl, algo.Vh):
+        if grad:
+            net.ps.swap_views()
+        out.append(net.flax())
+        if grad:
+            net.ps.swap_views()
+    return out
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("MPESpread", 3, 3), ("LidarBicycleTarget", 2, 1)])
+def test_dgppo_update_matches_oracle(cuda, eid, n, obs):
+    B, T, L = 4, 32, 16
+    env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=n, batch_size=B * T, rnn_step=L, train_steps=100,
+                     seed=1, device=cuda)
+    roll = algo.collect(algo.params, 7, n_env=B)
+    pa, pl, ph = _net_trees(algo)
+    algo.trace = {}
+    info = algo.update(roll, 60)  # past 50% of train_steps: cbf weight doubled
+    torch.cuda.synchronize()
+    tr = algo.trace
+    hr, hd = _host(roll, n), _host(tr["det"], n)
+    cw = algo.cbf_weight_at(60)
+    assert cw == 2.0
+    ref = R.dgppo_prepass(R.to_t(pa), R.to_t(pl), R.to_t(ph), hr, hd, n, env.dt, algo.gamma, algo.gae_lambda,
+                          algo.alpha, algo.cbf_eps, cw)
+    for k in ("Vl", "Vh", "Vh_det"):
+        _close(tr[k].cpu().numpy(), ref[k], 3e-5, k)
+    for k in ("Ql", "Qh", "Qh_det"):
+        _close(tr[k].cpu().numpy(), ref[k], 1e-4, k)
+    robust = np.abs(ref["deriv"]).min(-1) > 1e-3
+    assert robust.mean() > 0.5
+    _close(tr["A"].cpu().numpy()[robust], ref["A"][robust], 1e-3, "A")
+    total = B * T * n
+    assert abs(info["eval/safe_data"] - ref["safe_data"]) <= (~robust).sum() / total + 1e-6
+
+    # gradients of the single minibatch, oracle fed the GPU's own targets / advantages; the same
+    # oracle evaluated in float32 gives the noise floor of an fp32 evaluation (ReLU gates and
+    # softmax weights decided by rounding make some tensors differ from float64 by far more than
+    # 2e-5 relative, identically for any fp32 implementation)
+    (mb,) = tr["mb"]
+    algo.grad_flat.copy_(mb["grad"])
+    gpu = _net_trees(algo, grad=True)
+    envs = np.asarray(mb["envs"])
+    refs = {}
+    try:
+        for dt in (torch.float64, torch.float32):
+            R.T64 = dt
+            ts = [R.to_t(x, requires_grad=True) for x in (pa, pl, ph)]
+            losses = R.dgppo_minibatch_grads(*ts, hr, hd, envs, tr["Ql"].double().cpu().numpy(),
+                                             tr["Qh_det"].double().cpu().numpy(), tr["A"].double().cpu().numpy(),
+                                             n, L, algo.entropy_eps.cpu().numpy(), algo.clip_eps, algo.coef_ent)
+            refs[dt] = ([R.grads(t) for t in ts], losses)
+    finally:
+        R.T64 = torch.float64
+    losses = refs[torch.float64][1]
+    _close(info["Vl/loss"], losses["Vl_loss"], 1e-5, "Vl loss")
+    _close(info["Vh/loss_Vh"], losses["Vh_loss"], 1e-5, "Vh loss")
+    _close(info["policy/loss"], losses["policy_loss"], 1e-5, "policy loss")
+    _close(info["policy/entropy"], losses["entropy"], 1e-5, "entropy")
+    for tag, g, r64, r32 in zip(("actor", "Vl", "Vh"), gpu, refs[torch.float64][0], refs[torch.float32][0]):
+        for (path, a, b), (_, c, _) in zip(_walk(g, r64), _walk(r32, r64)):
+            b = np.asarray(b, np.float64)
+            err = np.abs(np.asarray(a, np.float64) - b).max()
+            floor = np.abs(np.asarray(c, np.float64) - b).max()
+            assert err <= 2e-5 * np.abs(b).max() + 1e-6 + 8 * floor, f"{tag} grad {path}: {err:.3e} (fp32 floor {floor:.3e})"
+
+    # clip + Adam on exactly those gradients
+    off = 0
+    for name, net in (("Vl", algo.Vl), ("Vh", algo.Vh), ("policy", algo.actor)):
+        sz = net.ps.size
+        g = mb["grad"][off:off + sz].double().cpu().numpy()
+        off += sz
+        (gc,), gn = O.clip_by_global_norm_ref([g], algo.max_grad_norm)
+        key = {"Vl": "Vl/grad_norm", "Vh": "Vh/grad_Vh_norm", "policy": "policy/grad_norm"}[name]
+        assert abs(info[key] - gn) <= 1e-5 * gn
+        (rp,), _, _ = O.adam_step([mb["before"][name].double().cpu().numpy()], [gc], [np.zeros(sz)], [np.zeros(sz)],
+                                  0, algo.opt[name].lr)
+        assert np.abs(net.ps.flat.double().cpu().numpy() - rp).max() <= 1e-6, name
