@@ -5,7 +5,8 @@ LidarSpread, n=8 agents, 3 obstacles, 32 rays, 4096 parallel envs per GPU.  One 
 one episode of the rollout hot path: env reset + T=128 fused env steps over all 4096 envs, with
 synthetic random actions already resident in HBM, writing the full (B, T+1) graph rollout buffer
 (the reference's `collect` minus the policy).  `value` = env transitions per second over all
-ranks.  Multi-GPU: envs are sharded (rank r owns envs [r*B, (r+1)*B)), no data-path collective —
+ranks.  The "ppo" object times full DGPPO training iterations at the same config (policy rollout
++ update, batch 16384, rnn_step 16): `ppo_updates_per_s` = update() calls per second.  Multi-GPU: envs are sharded (rank r owns envs [r*B, (r+1)*B)), no data-path collective —
 weak scaling.
 
 roofline: the dominant kernel is the env-step kernel (HBM-bound).  Algorithmic bytes per env
@@ -65,6 +66,55 @@ def read_pmc_traffic():
     return None
 
 
+PPO_BATCH, RNN_STEP = 16384, 16  # BASELINE.md synthetic-input plan (batch_size, rnn_step)
+
+
+def ppo_bench(env, dev, world, rank, iters):
+    """DGPPO training iterations at the bench config: collect (policy rollout, 4096 envs x T=128 in
+    one hipGraph) + update (det rollout, Vl/Vh prepass, GAE, advantages, 32 minibatches x
+    [Vl, Vh, policy fwd+bwd, one grad all-reduce, clip + Adam]).  Random-init nets, synthetic envs.
+    Max over ranks of the wall time between barriers."""
+    from dgppo_fov_amd.algo import make_algo
+    from dgppo_fov_amd.nn import kernels as K
+
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=N_AGENTS, batch_size=PPO_BATCH * world, rnn_step=RNN_STEP,
+                     seed=0, device=dev, train_steps=1000)
+    r = algo.collect(algo.params, 0, n_env=B_PER_GPU)
+    algo.update(r, 0)  # warm-up: captures the deterministic-rollout graph, grows workspaces
+    K.GEMM_LOG = []
+    algo.update(r, 0)
+    gemm_flops = sum(2.0 * M * N * Kd * b for (M, N, Kd, b, *_rest) in K.GEMM_LOG)
+    K.GEMM_LOG = None
+    t_col = t_upd = 0.0
+    for it in range(iters):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        r = algo.collect(algo.params, 100 + it, n_env=B_PER_GPU)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        algo.update(r, it)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t2 = time.perf_counter()
+        t_col += t1 - t0
+        t_upd += t2 - t1
+    t = torch.tensor([t_col, t_upd], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_col, t_upd = (float(x) / iters for x in t.tolist())
+    return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),
+            "collect_ms": round(t_col * 1e3, 2),
+            "collect_env_steps_per_s": round(B_PER_GPU * T * world / t_col, 1),
+            "iters": iters, "batch_size": PPO_BATCH * world, "rnn_step": RNN_STEP, "epoch_ppo": 1,
+            "minibatches": B_PER_GPU * T * world // (PPO_BATCH * world),
+            "gemm_tflop_per_update": round(gemm_flops / 1e12, 3),
+            "gemm_tflops_over_update": round(gemm_flops / t_upd / 1e12, 3), "fp32_mfma_peak_tflops": 157.3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,6 +122,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ppo-iters", type=int, default=3, help="timed DGPPO collect+update iterations (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,6 +199,8 @@ def main():
     bytes_per_launch = BYTES_PER_ENV_STEP * B_PER_GPU
     achieved = bytes_per_launch / (step_ms * 1e-3) / 1e9
     traffic = read_pmc_traffic()
+    del eng, outs, cur, g_step
+    ppo = ppo_bench(env, dev, world, rank, args.ppo_iters) if args.ppo_iters > 0 else None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -169,7 +222,8 @@ def main():
                 "hip_graph": use_graph, "parallelism": f"dp{world} (env-sharded, no collective)",
             },
             "env_step_kernel_us": round(step_ms * 1e3, 3),
-            "ppo_updates_per_s": None,
+            "ppo_updates_per_s": None if ppo is None else ppo["updates_per_s"],
+            "ppo": ppo,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),

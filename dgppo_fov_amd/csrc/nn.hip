@@ -296,12 +296,47 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* x, cons
 }
 
 // ---- column sums (deterministic two-level) ----------------------------------------------------
-// part[b][c] = sum of rows [b*rpb, (b+1)*rpb) of x (grouped row addressing as in the GEMM)
+// Row partition shared by every two-level reduction: at most kMaxParts partial rows, each block
+// owning a contiguous run of >= min_rows rows.
+constexpr int kMaxParts = 512;
+struct RowSplit {
+  int nb;
+  int64_t rpb;
+};
+__host__ __device__ inline RowSplit row_split(int64_t rows, int64_t min_rows) {
+  int64_t nb = (rows + min_rows - 1) / min_rows;
+  if (nb > kMaxParts) nb = kMaxParts;
+  if (nb < 1) nb = 1;
+  return {(int)nb, (rows + nb - 1) / nb};
+}
+
+// part[b][c] = sum of rows [b*rpb, (b+1)*rpb) of x (grouped row addressing as in the GEMM).
+// cols <= 256: 256/cols threads per column walk interleaved rows, combined in LDS in fixed order.
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int64_t rows, int cols, int64_t ld,
                                                              int grp, int64_t gstride, float* part,
                                                              int64_t rows_per_block) {
+  __shared__ float red[256];
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
+  if (cols <= 256) {
+    const int tpc = 256 / cols;
+    const int c = threadIdx.x % cols, j = threadIdx.x / cols;
+    float s = 0.0f;
+    if (j < tpc) {
+      for (int64_t r = r0 + j; r < r1; r += tpc) {
+        const int64_t off = grp > 0 ? (r / grp) * gstride + (r % grp) * ld : r * ld;
+        s += x[off + c];
+      }
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < cols) {
+      float t = 0.0f;
+      for (int k = 0; k < tpc; ++k) t += red[k * cols + threadIdx.x];
+      part[(int64_t)blockIdx.x * cols + threadIdx.x] = t;
+    }
+    return;
+  }
   for (int c = threadIdx.x; c < cols; c += 256) {
     float s = 0.0f;
     for (int64_t r = r0; r < r1; ++r) {
@@ -312,12 +347,19 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int
   }
 }
 
+// out[c] = alpha * sum_b part[b * pstride + c] + beta * out[c]; 64 columns x 4 phases per block
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nparts, int cols, int64_t pstride,
                                                            float* out, float alpha, float beta) {
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < cols; c += gridDim.x * 256) {
-    float s = 0.0f;
-    for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * pstride + c];
-    out[c] = alpha * s + (beta != 0.0f ? beta * out[c] : 0.0f);
+  __shared__ float red[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), j = threadIdx.x >> 6;
+  float s = 0.0f;
+  if (c < cols)
+    for (int b = j; b < nparts; b += 4) s += part[(int64_t)b * pstride + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < cols) {
+    const float t = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
+    out[c] = alpha * t + (beta != 0.0f ? beta * out[c] : 0.0f);
   }
 }
 
@@ -534,10 +576,11 @@ __global__ __launch_bounds__(256) void l2_loss_kernel(const float* pred, const f
 
 __global__ __launch_bounds__(64) void partial_reduce_kernel(const float* part, int nparts, int nv, float* out,
                                                             float scale) {
-  if (threadIdx.x < nv) {
+  for (int v = 0; v < nv; ++v) {  // lanes stride the partials, fixed-order butterfly -> deterministic
     float s = 0.0f;
-    for (int b = 0; b < nparts; ++b) s += part[b * 8 + threadIdx.x];
-    out[threadIdx.x] = s * scale;
+    for (int b = threadIdx.x; b < nparts; b += 64) s += part[b * 8 + v];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[v] = s * scale;
   }
 }
 
@@ -678,12 +721,14 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* g, int6
 
 // state[0] = global norm, state[1] = non-finite count, state[2] = adam step count (float)
 __global__ __launch_bounds__(64) void norm_final_kernel(const float* part, int nparts, float* state) {
+  float s = 0.0f, nf = 0.0f;
+  for (int b = threadIdx.x; b < nparts; b += 64) {
+    s += part[b * 8 + 0];
+    nf += part[b * 8 + 1];
+  }
+  s = wave_sum(s);
+  nf = wave_sum(nf);
   if (threadIdx.x == 0) {
-    float s = 0.0f, nf = 0.0f;
-    for (int b = 0; b < nparts; ++b) {
-      s += part[b * 8 + 0];
-      nf += part[b * 8 + 1];
-    }
     state[0] = sqrtf(s);
     state[1] = nf;
   }
@@ -799,8 +844,7 @@ extern "C" int dgppo_layernorm_fwd(const float* x, const float* scale, const flo
 }
 
 extern "C" int64_t dgppo_layernorm_bwd_workspace_floats(int64_t rows, int32_t F) {
-  const int64_t rpb = 64;
-  return ((rows + rpb - 1) / rpb) * 2 * F;
+  return (int64_t)row_split(rows, 64).nb * 2 * F;
 }
 
 // dscale / dbias are ACCUMULATED (+=) so one call serves a whole parameter-gradient buffer
@@ -810,32 +854,30 @@ extern "C" int dgppo_layernorm_bwd(const float* x, const float* y, const float* 
   if (rows < 0 || F < 1 || !x || !dy || !scale || !dx || !dscale || !dbias || !workspace || (relu && !y))
     return DGPPO_EINVAL;
   if (rows == 0) return 0;
-  const int rpb = 64;
-  const int nb = (int)((rows + rpb - 1) / rpb);
-  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nb), dim3(256), 8 * F * sizeof(float), DG_STREAM(stream), x, y, dy,
-                     scale, mean, rstd, dx, workspace, rows, F, relu, rpb);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(256), 0, DG_STREAM(stream), workspace, nb, F,
+  const RowSplit sp = row_split(rows, 64);
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(sp.nb), dim3(256), 8 * F * sizeof(float), DG_STREAM(stream), x, y,
+                     dy, scale, mean, rstd, dx, workspace, rows, F, relu, (int)sp.rpb);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((F + 63) / 64), dim3(256), 0, DG_STREAM(stream), workspace, sp.nb, F,
                      (int64_t)2 * F, dscale, 1.0f, 1.0f);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(256), 0, DG_STREAM(stream), workspace + F, nb, F,
-                     (int64_t)2 * F, dbias, 1.0f, 1.0f);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((F + 63) / 64), dim3(256), 0, DG_STREAM(stream), workspace + F, sp.nb,
+                     F, (int64_t)2 * F, dbias, 1.0f, 1.0f);
   return (int)hipGetLastError();
 }
 
 extern "C" int64_t dgppo_colsum_workspace_floats(int64_t rows, int32_t cols) {
-  const int64_t rpb = 256;
-  return ((rows + rpb - 1) / rpb) * cols;
+  return (int64_t)row_split(rows, 64).nb * cols;
 }
 
 // out = alpha * colsum(x) + beta * out, deterministic
 extern "C" int dgppo_colsum(const float* x, int64_t rows, int32_t cols, int64_t ld, int32_t grp, int64_t gstride,
                             float* out, float alpha, float beta, float* workspace, void* stream) {
   if (rows < 0 || cols < 1 || !x || !out || !workspace) return DGPPO_EINVAL;
-  const int64_t rpb = 256;
-  const int nb = (int)((rows + rpb - 1) / rpb);
+  const RowSplit sp = row_split(rows, 64);
+  const int nb = rows > 0 ? sp.nb : 0;
   if (nb > 0)
     hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, DG_STREAM(stream), x, rows, cols, ld, grp,
-                       gstride, workspace, rpb);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, DG_STREAM(stream), workspace, nb,
+                       gstride, workspace, sp.rpb);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64), dim3(256), 0, DG_STREAM(stream), workspace, nb,
                      cols, (int64_t)cols, out, alpha, beta);
   return (int)hipGetLastError();
 }

@@ -36,6 +36,9 @@ def _chk(rc, what):
     _lib.check(rc, what)
 
 
+GEMM_LOG = None  # set to a list to record (M, N, K, batch, ta, tb, split_k, has_bias) per launch
+
+
 def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
          a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
          bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
@@ -59,6 +62,8 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
         tiles = math.ceil(M / 64) * math.ceil(N / 64) * batch
         split_k = max(1, min(math.ceil(K / 512), 1024 // max(tiles, 1))) if K >= 2048 else 1
     g.split_k = int(split_k)
+    if GEMM_LOG is not None:
+        GEMM_LOG.append((int(M), int(N), int(K), int(batch), int(ta), int(tb), int(split_k), bias is not None))
     ws = None
     if g.split_k > 1:
         ws = workspace(lib.dgppo_gemm_workspace_floats(ctypes.byref(g)), C.device, "gemm")
