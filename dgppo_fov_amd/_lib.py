@@ -109,6 +109,15 @@ class GemmArgs(ctypes.Structure):
         ("relu", ctypes.c_int32),
         ("split_k", ctypes.c_int32),
         ("workspace", c_f32p),
+        ("bias_grad", c_f32p),
+    ]
+
+
+class GruSeqArgs(ctypes.Structure):
+    _fields_ = [
+        ("Q", ctypes.c_int32), ("L", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("H", ctypes.c_int32),
+        ("gi", c_f32p), ("Wh", c_f32p), ("bhn", c_f32p), ("h0", c_f32p), ("hs", c_f32p), ("hT", c_f32p),
+        ("dhs", c_f32p), ("dgi", c_f32p), ("dgh", c_f32p), ("dh0", c_f32p), ("dbhn_part", c_f32p),
     ]
 
 
@@ -178,6 +187,9 @@ SIGNATURES = {
     "dgppo_colsum": (ctypes.c_int, [_V, _I64, _I32, _I64, _I32, _I64, _V, _F32, _F32, _V, _V]),
     "dgppo_gru_fwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, _I32, _V]),
     "dgppo_gru_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _V]),
+    "dgppo_gru_seq_blocks": (ctypes.c_int64, [_I32]),
+    "dgppo_gru_seq_fwd": (ctypes.c_int, [_V, _V]),
+    "dgppo_gru_seq_bwd": (ctypes.c_int, [_V, _V]),
     "dgppo_agent_mean_fwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),
     "dgppo_agent_mean_bwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),
     "dgppo_tanh_normal": (ctypes.c_int, [ctypes.POINTER(TanhNormalArgs), ctypes.c_void_p]),

@@ -85,9 +85,7 @@ class ActorNet(_Net):
         1 = sample_action with standard-normal `noise` (G*n, A).  Returns (action, log_pi, h_new)."""
         rows = g.G * self.n
         y, _ = self._trunk(g)
-        h2 = h_out if h_out is not None else torch.empty_like(h)
-        hn, _ = self.gru.fwd(y, h)
-        h2.copy_(hn)
+        h2, _ = self.gru.fwd(y, h, h_out=h_out)
         _, mu, sr = self._outputs(h2)
         action = action_out if action_out is not None else torch.empty((rows, self.A), device=h.device)
         log_pi = log_pi_out if log_pi_out is not None else torch.empty(rows, device=h.device)
@@ -104,17 +102,8 @@ class ActorNet(_Net):
         """eval_action over S sequences of L steps (scan_eval_action, informarl.py:387-403), zero
         initial carries.  actions (S*L*n, A) rows (s, t, agent).  Returns log_pi, entropy (S*L*n,)."""
         n, dev = self.n, actions.device
-        y, tc = self._trunk(g)  # (S*L*n, 64)
-        y4 = y.view(S, L, n, 64)
-        h = torch.zeros((S * n, 64), device=dev)
-        Hs = torch.empty((S, L, n, 64), device=dev)
-        gcs = []
-        for t in range(L):
-            x_t = y4[:, t].contiguous().view(S * n, 64)
-            h, c = self.gru.fwd(x_t, h)
-            gcs.append(c)
-            Hs[:, t].copy_(h.view(S, n, 64))
-        H2 = Hs.view(S * L * n, 64)
+        y, tc = self._trunk(g)  # (S*L*n, 64) rows (s, t, agent)
+        H2, gcs = self.gru.seq_fwd(y, S * n, L, n)
         s, mu, sr = self._outputs(H2)
         rows = S * L * n
         log_pi = torch.empty(rows, device=dev)
@@ -147,15 +136,9 @@ class ActorNet(_Net):
         self._bptt(dH2.view(S, L, n, 64), gcs, S, L, tc, g)
 
     def _bptt(self, dHs, gcs, S, L, tc, g):
-        n, dev = self.n, dHs.device
-        dY = torch.empty((S, L, n, 64), device=dev)
-        dh = torch.zeros((S * n, 64), device=dev)
-        for t in range(L - 1, -1, -1):
-            dtot = dHs[:, t].contiguous().view(S * n, 64) + dh
-            dx, dh = self.gru.bwd(gcs[t], dtot)
-            dY[:, t].copy_(dx.view(S, n, 64))
+        dY, _ = self.gru.seq_bwd(gcs, dHs.reshape(S * L * self.n, 64))
         gc, hc = tc
-        dz = self.head.bwd(hc, dY.view(S * L * n, 64))
+        dz = self.head.bwd(hc, dY)
         self.gnn.bwd(gc, dz, g)
 
 
@@ -188,30 +171,19 @@ class VlNet(_Net):
         zm = torch.empty((G, 64), device=dev)
         K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
         y, hc = self.head.fwd(zm)
-        y3 = y.view(S, L, 64)
-        h = torch.zeros((S, 64), device=dev) if h0 is None else h0
-        Hs = torch.empty((S, L, 64), device=dev)
-        gcs = []
-        for t in range(L):
-            h, c = self.gru.fwd(y3[:, t].contiguous(), h)
-            if keep_cache:
-                gcs.append(c)
-            Hs[:, t].copy_(h)
-        v = self.out.fwd(Hs.view(G, 64), G)
+        hT = torch.empty((S, 64), device=dev)
+        Hs, gcs = self.gru.seq_fwd(y, S, L, 1, h0=h0, hT_out=hT)
+        v = self.out.fwd(Hs, G)
         cache = (g, S, L, gc, z, hc, gcs, Hs) if keep_cache else None
-        return v.view(S, L), h, cache
+        return v.view(S, L), hT, cache
 
     def seq_bwd(self, cache, dv):
         g, S, L, gc, z, hc, gcs, Hs = cache
         n, dev = self.n, dv.device
         G = S * L
-        dH = self.out.bwd(Hs.view(G, 64), dv.reshape(G, 1).contiguous(), G).view(S, L, 64)
-        dY = torch.empty((S, L, 64), device=dev)
-        dh = torch.zeros((S, 64), device=dev)
-        for t in range(L - 1, -1, -1):
-            dx, dh = self.gru.bwd(gcs[t], dH[:, t].contiguous() + dh)
-            dY[:, t].copy_(dx)
-        dzm = self.head.bwd(hc, dY.view(G, 64))
+        dH = self.out.bwd(Hs, dv.reshape(G, 1).contiguous(), G)
+        dY, _ = self.gru.seq_bwd(gcs, dH)
+        dzm = self.head.bwd(hc, dY)
         dz = torch.empty_like(z)
         K.agent_mean_bwd(dzm, dz, G, n, 64, n * 64)
         self.gnn.bwd(gc, dz, g)
@@ -250,6 +222,6 @@ class VhNet(_Net):
         g, gc, hc, rc, h2 = cache
         rows = g.G * self.n
         dh2 = self.out.bwd(h2, dout, rows)
-        dy, _ = self.gru.bwd(rc, dh2)
+        dy, _ = self.gru.seq_bwd(rc, dh2)
         dz = self.head.bwd(hc, dy)
         self.gnn.bwd(gc, dz, g)

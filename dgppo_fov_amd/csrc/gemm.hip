@@ -1,18 +1,26 @@
-// Batched fp32 GEMM on gfx950 matrix cores (v_mfma_f32_32x32x2_f32: exact f32 FMA chains in k
-// order, 157 TF/s peak = the fp32 VALU peak, with operands one VGPR per lane).
+// Batched fp32 GEMM on gfx950 matrix cores (v_mfma_f32_32x32x2_f32: exact f32 FMA chains, 157 TF/s
+// peak = the fp32 VALU peak, operands one VGPR per lane).
 //
 //   C[b] = alpha * op(A[b]) @ op(B[b]) + beta * C[b] + bias + addend[b]   (optional ReLU)
 //   op(A) is (M, K): A row-major (M, K) with lda, or trans_a: A stored (K, M) with lda.
 //   op(B) is (K, N): B row-major (K, N) with ldb, or trans_b: B stored (N, K) with ldb.
 //
 // Every dense layer of the DGPPO networks (flax Dense y = x W + b, its dX = dY W^T and
-// dW = X^T dY) is one call.  The weight-gradient shapes have a huge reduction dimension
-// (K = rows of the minibatch, ~10^5) and tiny M, N: those run split-K into a workspace slab and a
-// deterministic reduce kernel (no float atomics: bitwise-reproducible gradients).
+// dW = X^T dY, db = colsum dY) is one call.  The shapes are skinny (rows ~10^5..10^6, weights
+// <= 192 x 192) and HBM-bound, so three kernels split the work by shape:
 //
-// Tile: 64 x 64 per 256-thread workgroup, 4 waves in 2 x 2, each wave one 32 x 32 accumulator
-// (16 fp32 per lane).  K advances 32 per LDS tile (16 MFMAs per wave per tile).  LDS images are
-// k-major ([k][m] / [k][n], row pitch 65 floats) so the MFMA operand reads are lane-contiguous.
+//  rows   (!trans_a, N <= 192, K <= 256): panel kernel.  The small weight op(B) is staged ONCE per
+//         workgroup into LDS (k-major); each wave owns 32 rows x all N columns and streams its
+//         rows' A values straight from HBM into MFMA operands (16-byte loads: the K index is
+//         permuted so lane half h covers k in [h*Kh, (h+1)*Kh) contiguously).  Grid-stride over
+//         128-row panels.
+//  wgrad  (trans_a, !trans_b, M <= 128 per group, N <= 192): weight gradient X^T dY with the
+//         reduction over ~10^5 rows.  Each workgroup takes a contiguous row chunk, its 8 waves
+//         interleave row pairs and keep the WHOLE (M x N) partial in accumulators, so every
+//         input byte is read once; the bias gradient colsum(dY) rides along on the VALU.
+//         Wave partials combine in LDS in fixed order, chunk partials in a fixed-order reduce:
+//         bitwise-deterministic gradients without float atomics.
+//  tile   everything else: 64 x 64 LDS-tiled MFMA, optional split-K (the original kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -49,6 +57,12 @@ __device__ __forceinline__ float load_a(const GemmTileArgs& g, int m, int k) {
 __device__ __forceinline__ float load_b(const GemmTileArgs& g, int k, int n) {
   if (n >= g.N || k >= g.k_end) return 0.0f;
   return g.tb ? g.B[row_off(n, g.ldb, g.b_grp, g.b_gstride) + k] : g.B[row_off(k, g.ldb, g.b_grp, g.b_gstride) + n];
+}
+
+__device__ __forceinline__ int64_t row_off64(int64_t r, int64_t ld, int grp, int64_t gstride) {
+  if (grp <= 0) return r * ld;
+  const int64_t q = r / grp;
+  return q * gstride + (r - q * grp) * ld;
 }
 
 // accumulate the (m0, n0) 64x64 tile over [k_begin, k_end) into acc (this wave's 32x32 block)
@@ -162,11 +176,341 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(dgppo_gemm_args p) {
   }
 }
 
+
+// ================================================================================================
+// rows: C = alpha * A op(B) + ... for M large, N <= 32 * NT, K <= kRowsMaxK
+// ================================================================================================
+constexpr int kRowsMaxK = 256;
+constexpr int kRowsLdsFloats = 12800;  // 50 KB: K * (N + 1) must fit
+
+template <int NT, bool VEC>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
+  extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K][NP] k-major, NP = 32 NT + 1
+  constexpr int NP = 32 * NT + 1;
+  const int K = p.K, N = p.N, M = p.M;
+  const int Kh = (K + 1) >> 1;
+  const int b = blockIdx.z;
+  const float* A = p.A + (int64_t)b * p.stride_a;
+  const float* B = p.B + (int64_t)b * p.stride_b;
+  // stage op(B) (K x N) into LDS, zero-padded to 32 NT columns and 2 Kh rows
+  for (int e = threadIdx.x; e < 2 * Kh * 32 * NT; e += 256) {
+    int k, n;
+    if (p.trans_b) { k = e % (2 * Kh); n = e / (2 * Kh); }  // stored (N, K): k fastest
+    else { n = e % (32 * NT); k = e / (32 * NT); }         // stored (K, N): n fastest
+    float v = 0.0f;
+    if (k < K && n < N)
+      v = p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k] : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n];
+    Bs[k * NP + n] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int kofs = h * Kh;
+  float* C = p.C + (int64_t)b * p.stride_c;
+  const float* D = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  const int panels = (M + 127) / 128;
+  for (int panel = blockIdx.x; panel < panels; panel += gridDim.x) {
+    const int m0 = panel * 128 + wave * 32;
+    const int arow = m0 + i;
+    const bool rok = arow < M;
+    const float* Ar = A + (rok ? row_off(arow, p.lda, p.a_grp, p.a_gstride) : 0) + kofs;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    for (int kb = 0; kb < Kh; kb += 8) {
+      float a[8];
+      if (VEC) {  // Kh % 8 == 0, rows 16-byte aligned
+        const float4 v0 = rok ? *(const float4*)(Ar + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v1 = rok ? *(const float4*)(Ar + kb + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w;
+        a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int kk = kb + q;
+          a[q] = (rok && kk < Kh && kofs + kk < K) ? Ar[kk] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int kk = kb + q;
+        if (!VEC && kk >= Kh) break;
+        const float* brow = Bs + (kofs + kk) * NP + i;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], brow[32 * t], acc[t], 0, 0, 0);
+      }
+    }
+    // epilogue: lane holds column (t*32 + i), rows (r&3) + 8 (r>>2) + 4 h of this wave's 32
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = t * 32 + i;
+      if (col >= N) continue;
+      const float bv = p.bias ? p.bias[col] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < M) {
+          float* cp = C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
+          float v = p.alpha * acc[t][r];
+          if (p.beta != 0.0f) v += p.beta * *cp;
+          v += bv;
+          if (D) v += D[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
+          if (p.relu) v = v > 0.0f ? v : 0.0f;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
+// ================================================================================================
+// wgrad: C = alpha * A^T B + beta C over K rows (+ bias_grad = alpha * colsum(B) + beta bias_grad)
+// ================================================================================================
+constexpr int kWWaves = 8;
+constexpr int kWMaxChunks = 256;
+constexpr int kWMinRows = 512;
+
+__host__ __device__ inline int wgrad_chunks(int64_t K) {
+  int64_t c = (K + kWMinRows - 1) / kWMinRows;
+  if (c > kWMaxChunks) c = kWMaxChunks;
+  return c < 1 ? 1 : (int)c;
+}
+
+// workspace layout: [batch][chunk][M*N + N]
+template <int MT, int NT>
+__global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
+  constexpr int CP = NT * 32 + 1;
+  const int c = blockIdx.x;
+  const int gm = blockIdx.y / ngroups_n, gn = blockIdx.y % ngroups_n;
+  const int b = blockIdx.z;
+  const int m0 = gm * MT * 32, n0 = gn * NT * 32;
+  const int M = p.M, N = p.N;
+  const int64_t K = p.K;
+  const int64_t rpc = (K + chunks - 1) / chunks;
+  const int64_t r0 = (int64_t)c * rpc;
+  const int64_t r1 = r0 + rpc < K ? r0 + rpc : K;
+  const float* A = p.A + (int64_t)b * p.stride_a;
+  const float* B = p.B + (int64_t)b * p.stride_b;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const bool do_bias = p.bias_grad != nullptr && gm == 0;
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
+  float bs[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) bs[nt] = 0.0f;
+  bool mok[MT], nok[NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) mok[mt] = m0 + mt * 32 + i < M;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) nok[nt] = n0 + nt * 32 + i < N;
+  // row pairs (2q, 2q+1) of the chunk, interleaved over the waves; lane half h takes row 2q + h
+  constexpr int U = 2;  // row pairs in flight per wave
+  for (int64_t k0 = r0 + 2 * wave; k0 < r1; k0 += 2 * kWWaves * U) {
+    float a[U][MT], bb[U][NT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = k0 + 2 * kWWaves * u + h;
+      const bool kok = k < r1;
+      const float* Ar = A + (kok ? row_off64(k, p.lda, p.a_grp, p.a_gstride) : 0) + m0 + i;
+      const float* Br = B + (kok ? row_off64(k, p.ldb, p.b_grp, p.b_gstride) : 0) + n0 + i;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? Ar[mt * 32] : 0.0f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? Br[nt * 32] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][mt], bb[u][nt], acc[mt][nt], 0, 0, 0);
+      if (do_bias)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bs[nt] += bb[u][nt];
+    }
+  }
+  // combine the 8 wave partials in LDS, fixed order
+  float* bred = red + MT * 32 * CP;
+  for (int w = 0; w < kWWaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float* dst = red + row * CP + nt * 32 + i;
+            *dst = (w == 0 ? 0.0f : *dst) + acc[mt][nt][r];
+          }
+    }
+    __syncthreads();
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bred[(wave * 2 + h) * (NT * 32) + nt * 32 + i] = bs[nt];
+  }
+  __syncthreads();
+  const int64_t slab = (int64_t)M * N + N;
+  const bool direct = chunks == 1;
+  float* W = p.workspace + ((int64_t)b * chunks + c) * slab;
+  float* Cb = p.C + (int64_t)b * p.stride_c;
+  for (int e = threadIdx.x; e < MT * 32 * NT * 32; e += 512) {
+    const int row = e / (NT * 32), col = e % (NT * 32);
+    const int m = m0 + row, n = n0 + col;
+    if (m >= M || n >= N) continue;
+    const float v = red[row * CP + col];
+    if (direct) {
+      float* cp = Cb + row_off(m, p.ldc, p.c_grp, p.c_gstride) + n;
+      *cp = p.alpha * v + (p.beta != 0.0f ? p.beta * *cp : 0.0f);
+    } else {
+      W[(int64_t)m * N + n] = v;
+    }
+  }
+  if (do_bias) {
+    for (int col = threadIdx.x; col < NT * 32; col += 512) {
+      const int n = n0 + col;
+      if (n >= N) continue;
+      float s = 0.0f;
+      for (int q = 0; q < 2 * kWWaves; ++q) s += bred[q * (NT * 32) + col];
+      if (direct) {
+        float* bp = p.bias_grad + (int64_t)b * N + n;
+        *bp = p.alpha * s + (p.beta != 0.0f ? p.beta * *bp : 0.0f);
+      } else {
+        W[(int64_t)M * N + n] = s;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int chunks) {
+  const int64_t MN = (int64_t)p.M * p.N;
+  const int64_t slab = MN + p.N;
+  const int64_t total = slab * p.batch;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int b = (int)(t / slab);
+    const int64_t e = t - (int64_t)b * slab;
+    if (e >= MN && !p.bias_grad) continue;
+    const float* W = p.workspace + (int64_t)b * chunks * slab + e;
+    float s = 0.0f;
+    for (int q = 0; q < chunks; ++q) s += W[(int64_t)q * slab];
+    float* dst;
+    if (e < MN) {
+      const int row = (int)(e / p.N), col = (int)(e - (int64_t)row * p.N);
+      dst = p.C + (int64_t)b * p.stride_c + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
+    } else {
+      dst = p.bias_grad + (int64_t)b * p.N + (e - MN);
+    }
+    *dst = p.alpha * s + (p.beta != 0.0f ? p.beta * *dst : 0.0f);
+  }
+}
+
 }  // namespace dgppo
 
+namespace {
+enum GemmPath { kPathTile = 0, kPathRows = 1, kPathWgrad = 2 };
+
+GemmPath gemm_path(const dgppo_gemm_args* p) {
+  if (p->trans_a && !p->trans_b && p->N <= 192 && p->M <= 4096 && !p->bias && !p->addend && !p->relu)
+    return kPathWgrad;
+  if (!p->trans_a && p->N <= 192 && p->K <= dgppo::kRowsMaxK) {
+    int nt = (p->N + 31) / 32;
+    if (nt == 5) nt = 6;
+    if (2 * ((p->K + 1) / 2) * (32 * nt + 1) <= dgppo::kRowsLdsFloats) return kPathRows;
+  }
+  return kPathTile;
+}
+
+// (MT, NT) tile-group shape for the wgrad kernel: MT * NT <= 12 accumulators of 16 per lane
+void wgrad_shape(int M, int N, int* MT, int* NT) {
+  const int mt = (M + 31) / 32, nt = (N + 31) / 32;
+  *NT = nt >= 6 ? 6 : nt >= 3 ? 3 : nt;   // 1, 2, 3 or 6 (groups of 3/6 cover larger N)
+  if (nt == 4 || nt == 5) *NT = 3;
+  const int mmax = 12 / *NT;
+  *MT = mt < mmax ? mt : mmax;
+  if (*MT > 4) *MT = 4;
+  if (*MT == 3 && *NT == 6) *MT = 2;
+}
+
+template <int MT, int NT>
+void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
+  const int gm = (p->M + MT * 32 - 1) / (MT * 32), gn = (p->N + NT * 32 - 1) / (NT * 32);
+  const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
+  hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT>), dim3(chunks, gm * gn, p->batch), dim3(512), lds, s, *p,
+                     chunks, gn);
+}
+
+int launch_wgrad(const dgppo_gemm_args* p, hipStream_t s) {
+  int MT, NT;
+  wgrad_shape(p->M, p->N, &MT, &NT);
+  const int chunks = dgppo::wgrad_chunks(p->K);
+  if (chunks > 1 && !p->workspace) return DGPPO_EINVAL;
+#define DG_W(a, b) \
+  if (MT == a && NT == b) { launch_wgrad_t<a, b>(p, chunks, s); goto launched; }
+  DG_W(1, 1) DG_W(1, 2) DG_W(1, 3) DG_W(1, 6) DG_W(2, 1) DG_W(2, 2) DG_W(2, 3) DG_W(2, 6)
+  DG_W(3, 1) DG_W(3, 2) DG_W(3, 3) DG_W(4, 1) DG_W(4, 2) DG_W(4, 3)
+#undef DG_W
+  return DGPPO_EINVAL;
+launched:
+  if (chunks > 1) {
+    const int64_t total = ((int64_t)p->M * p->N + p->N) * p->batch;
+    int64_t nb = (total + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    hipLaunchKernelGGL(dgppo::gemm_wgrad_reduce, dim3((int)nb), dim3(256), 0, s, *p, chunks);
+  }
+  return 0;
+}
+
+template <int NT>
+void launch_rows_t(const dgppo_gemm_args* p, hipStream_t s) {
+  const int Kh = (p->K + 1) / 2;
+  const size_t lds = (size_t)2 * Kh * (32 * NT + 1) * sizeof(float);
+  const int panels = (p->M + 127) / 128;
+  const int grid = panels < 1024 ? panels : 1024;
+  const bool vec = (Kh % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
+                   (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
+  if (vec)
+    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NT, true>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p);
+  else
+    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NT, false>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p);
+}
+
+int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {
+  switch ((p->N + 31) / 32) {
+    case 1: launch_rows_t<1>(p, s); return 0;
+    case 2: launch_rows_t<2>(p, s); return 0;
+    case 3: launch_rows_t<3>(p, s); return 0;
+    case 4: launch_rows_t<4>(p, s); return 0;
+    case 5:
+    case 6: launch_rows_t<6>(p, s); return 0;
+  }
+  return DGPPO_EINVAL;
+}
+}  // namespace
+
 extern "C" int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* p) {
-  if (!p || p->split_k <= 1) return 0;
-  return (int64_t)p->split_k * p->batch * (int64_t)p->M * p->N;
+  if (!p) return 0;
+  switch (gemm_path(p)) {
+    case kPathWgrad: {
+      const int chunks = dgppo::wgrad_chunks(p->K);
+      return chunks > 1 ? (int64_t)chunks * p->batch * ((int64_t)p->M * p->N + p->N) : 0;
+    }
+    case kPathRows:
+      return 0;
+    default:
+      if (p->split_k <= 1) return 0;
+      return (int64_t)p->split_k * p->batch * (int64_t)p->M * p->N;
+  }
 }
 
 extern "C" int dgppo_gemm(const dgppo_gemm_args* p, void* stream) {
@@ -174,8 +518,18 @@ extern "C" int dgppo_gemm(const dgppo_gemm_args* p, void* stream) {
     return DGPPO_EINVAL;
   if (p->M == 0 || p->N == 0) return 0;
   if (!p->A || !p->B || !p->C) return DGPPO_EINVAL;
-  if (p->split_k > 1 && !p->workspace) return DGPPO_EINVAL;
+  if (p->bias_grad && gemm_path(p) != kPathWgrad) return DGPPO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  const GemmPath path = gemm_path(p);
+  if (path == kPathWgrad) {
+    if (launch_wgrad(p, s)) return DGPPO_EINVAL;
+    return (int)hipGetLastError();
+  }
+  if (path == kPathRows) {
+    if (launch_rows(p, s)) return DGPPO_EINVAL;
+    return (int)hipGetLastError();
+  }
+  if (p->split_k > 1 && !p->workspace) return DGPPO_EINVAL;
   const int tiles = ((p->M + dgppo::kBM - 1) / dgppo::kBM) * ((p->N + dgppo::kBN - 1) / dgppo::kBN);
   hipLaunchKernelGGL(dgppo::gemm_kernel, dim3(tiles, p->split_k, p->batch), dim3(256), 0, s, *p);
   if (p->split_k > 1) {

@@ -32,201 +32,6 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float softplusf_(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
-constexpr int kMaxCand = 128;
-constexpr int kMaxHD = 3 * 64;
-
-// ---- GraphTransformer attention core ---------------------------------------------------------
-// One wave per graph; agents processed in order (so the sender-gradient accumulation of the
-// backward is a deterministic, conflict-free per-lane column update in LDS).
-struct AttnLds {
-  float qt[kMaxHD];             // H*D
-  float beta[4];
-  float a[kMaxCand * 3];        // [c][h]
-  int s[kMaxCand];              // sender node (or -1)
-  int e[kMaxCand];              // edge id
-  float g[kMaxHD + 3 * 4 + 4];  // backward: dxbar (H*D) | debar (H*4) | dsig (H)
-  float dl[kMaxCand * 3];       // backward: scaled dlogit [c][h]
-};
-
-__device__ void attn_candidates(const dgppo_gnn_attn_args& p, int g, int i, AttnLds& L, int lane) {
-  const int32_t* recv = p.receivers + (int64_t)g * p.E;
-  const int32_t* send = p.senders + (int64_t)g * p.E;
-  for (int c = lane; c < p.C; c += 64) {
-    const int e = p.cand[i * p.C + c];
-    int s = -1;
-    if (e >= 0 && recv[e] == i) s = send[e];
-    L.s[c] = s;
-    L.e[c] = e;
-  }
-}
-
-__global__ __launch_bounds__(64) void gnn_attn_fwd_kernel(dgppo_gnn_attn_args p) {
-  __shared__ AttnLds L;
-  const int g = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int H = p.H, D = p.D, F = p.F, C = p.C;
-  const float* xg = p.x + (int64_t)g * p.x_gstride;
-  const float* efg = p.ef + (int64_t)g * p.ef_gstride;
-  const int W = H * (D + 5);
-  for (int i = 0; i < p.n_agents; ++i) {
-    const int64_t row = (int64_t)g * p.n_agents + i;
-    for (int t = lane; t < H * D; t += 64) L.qt[t] = p.qt[row * H * D + t];
-    for (int h = 0; h < H; ++h) {  // beta_h = q_h . bk_h
-      float acc = 0.0f;
-      for (int f = lane; f < F; f += 64) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
-      acc = wave_sum(acc);
-      if (lane == 0) L.beta[h] = acc;
-    }
-    attn_candidates(p, g, i, L, lane);
-    __syncthreads();
-    // logits (one candidate per lane), then softmax per head over valid candidates
-    float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int c = lane; c < C; c += 64) {
-      const int s = L.s[c];
-      for (int h = 0; h < H; ++h) {
-        float lg = -INFINITY;
-        if (s >= 0) {
-          const float* xs = xg + (int64_t)s * D;
-          float acc = 0.0f;
-          for (int d = 0; d < D; ++d) acc += L.qt[h * D + d] * xs[d];
-          lg = (acc + L.beta[h]) * p.scale;
-        }
-        L.a[c * 3 + h] = lg;
-        mx[h] = fmaxf(mx[h], lg);
-      }
-    }
-    float sm[3];
-    for (int h = 0; h < H; ++h) mx[h] = wave_max(mx[h]);
-    __syncthreads();
-    for (int h = 0; h < H; ++h) sm[h] = 0.0f;
-    for (int c = lane; c < C; c += 64) {
-      for (int h = 0; h < H; ++h) {
-        const float ex = L.s[c] >= 0 ? expf(L.a[c * 3 + h] - mx[h]) : 0.0f;
-        L.a[c * 3 + h] = ex;
-        sm[h] += ex;
-      }
-    }
-    for (int h = 0; h < H; ++h) sm[h] = wave_sum(sm[h]);
-    __syncthreads();
-    for (int c = lane; c < C; c += 64) {
-      for (int h = 0; h < H; ++h) {
-        const float a = L.a[c * 3 + h] / sm[h];
-        L.a[c * 3 + h] = a;
-        if (p.attn) p.attn[(row * H + h) * C + c] = a;
-      }
-    }
-    __syncthreads();
-    // xbar_h[d] (lane = d), ebar_h[j], sig_h
-    float* out = p.xcat + row * W;
-    for (int d = lane; d < D; d += 64) {
-      float acc[3] = {0.0f, 0.0f, 0.0f};
-      for (int c = 0; c < C; ++c) {
-        const int s = L.s[c];
-        if (s < 0) continue;
-        const float xv = xg[(int64_t)s * D + d];
-        for (int h = 0; h < H; ++h) acc[h] += L.a[c * 3 + h] * xv;
-      }
-      for (int h = 0; h < H; ++h) out[h * D + d] = acc[h];
-    }
-    if (lane < H * 4) {
-      const int h = lane >> 2, j = lane & 3;
-      float acc = 0.0f;
-      for (int c = 0; c < C; ++c)
-        if (L.s[c] >= 0) acc += L.a[c * 3 + h] * efg[(int64_t)L.e[c] * 4 + j];
-      out[H * D + lane] = acc;
-    }
-    if (lane < H) {
-      float acc = 0.0f;
-      for (int c = 0; c < C; ++c)
-        if (L.s[c] >= 0) acc += L.a[c * 3 + lane];
-      out[H * D + H * 4 + lane] = acc;
-    }
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(64) void gnn_attn_bwd_kernel(dgppo_gnn_attn_args p) {
-  __shared__ AttnLds L;
-  extern __shared__ __attribute__((aligned(16))) float dxs[];  // (N, D) sender gradients
-  const int g = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int H = p.H, D = p.D, F = p.F, C = p.C, N = p.N;
-  const float* xg = p.x + (int64_t)g * p.x_gstride;
-  const float* efg = p.ef + (int64_t)g * p.ef_gstride;
-  const int W = H * (D + 5);
-  const bool want_dx = p.dx != nullptr;
-  if (want_dx)
-    for (int t = lane; t < N * D; t += 64) dxs[t] = 0.0f;
-  for (int i = 0; i < p.n_agents; ++i) {
-    const int64_t row = (int64_t)g * p.n_agents + i;
-    for (int t = lane; t < H * D; t += 64) L.qt[t] = p.qt[row * H * D + t];
-    for (int t = lane; t < W; t += 64) L.g[t] = p.dxcat[row * W + t];
-    attn_candidates(p, g, i, L, lane);
-    for (int t = lane; t < C * H; t += 64) {
-      const int c = t / H, h = t - (t / H) * H;
-      L.a[c * 3 + h] = p.attn[(row * H + h) * C + c];
-    }
-    __syncthreads();
-    // da_c,h = dxbar_h . x_s + debar_h . ef_e + dsig_h ; softmax backward -> dlogit
-    float dot[3] = {0.0f, 0.0f, 0.0f};
-    float da_[2][3];
-    int k = 0;
-    for (int c = lane; c < C; c += 64, ++k) {
-      const int s = L.s[c];
-      for (int h = 0; h < H; ++h) {
-        float v = 0.0f;
-        if (s >= 0) {
-          const float* xs = xg + (int64_t)s * D;
-          for (int d = 0; d < D; ++d) v += L.g[h * D + d] * xs[d];
-          const float* ef = efg + (int64_t)L.e[c] * 4;
-          for (int j = 0; j < 4; ++j) v += L.g[H * D + h * 4 + j] * ef[j];
-          v += L.g[H * D + H * 4 + h];
-        }
-        da_[k][h] = v;
-        dot[h] += L.a[c * 3 + h] * v;
-      }
-    }
-    for (int h = 0; h < H; ++h) dot[h] = wave_sum(dot[h]);
-    k = 0;
-    float dbeta[3] = {0.0f, 0.0f, 0.0f};
-    for (int c = lane; c < C; c += 64, ++k) {
-      for (int h = 0; h < H; ++h) {
-        const float dlg = L.s[c] >= 0 ? L.a[c * 3 + h] * (da_[k][h] - dot[h]) * p.scale : 0.0f;
-        L.dl[c * 3 + h] = dlg;
-        dbeta[h] += dlg;
-      }
-    }
-    for (int h = 0; h < H; ++h) dbeta[h] = wave_sum(dbeta[h]);
-    if (lane < H) p.dbeta[row * H + lane] = lane == 0 ? dbeta[0] : (lane == 1 ? dbeta[1] : dbeta[2]);
-    for (int t = lane; t < H * F; t += 64) {
-      const int h = t / F;
-      p.dq[row * H * F + t] = (h == 0 ? dbeta[0] : (h == 1 ? dbeta[1] : dbeta[2])) * p.bk[t];
-    }
-    __syncthreads();
-    // dqt_h[d] = sum_c dl_c,h x_s[d];  sender grads  dx_s[d] += sum_h a_c,h dxbar_h[d] + dl_c,h qt_h[d]
-    for (int d = lane; d < D; d += 64) {
-      float acc[3] = {0.0f, 0.0f, 0.0f};
-      for (int c = 0; c < C; ++c) {
-        const int s = L.s[c];
-        if (s < 0) continue;
-        const float xv = xg[(int64_t)s * D + d];
-        float contrib = 0.0f;
-        for (int h = 0; h < H; ++h) {
-          acc[h] += L.dl[c * 3 + h] * xv;
-          contrib += L.a[c * 3 + h] * L.g[h * D + d] + L.dl[c * 3 + h] * L.qt[h * D + d];
-        }
-        if (want_dx) dxs[s * D + d] += contrib;
-      }
-      for (int h = 0; h < H; ++h) p.dqt[row * H * D + h * D + d] = acc[h];
-    }
-    __syncthreads();
-  }
-  if (want_dx) {
-    float* dxg = p.dx + (int64_t)g * p.dx_gstride;
-    for (int t = lane; t < N * D; t += 64) dxg[t] += dxs[t];
-  }
-}
-
 // ---- LayerNorm (+ReLU) over rows of width F (flax LayerNorm, eps 1e-6, fast variance) --------
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* x, const float* scale, const float* bias,
                                                             float* y, float* mean_out, float* rstd_out,
@@ -806,26 +611,6 @@ static int grid_for(int64_t n) {
 using namespace dgppo;
 
 #define DG_STREAM(s) ((hipStream_t)(s))
-
-extern "C" int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* p, void* stream) {
-  if (!p || p->H < 1 || p->H > 3 || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > kMaxCand ||
-      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->q || !p->bk || !p->xcat || !p->cand)
-    return DGPPO_EINVAL;
-  if (p->G == 0) return 0;
-  hipLaunchKernelGGL(gnn_attn_fwd_kernel, dim3(p->G), dim3(64), 0, DG_STREAM(stream), *p);
-  return (int)hipGetLastError();
-}
-
-extern "C" int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* p, void* stream) {
-  if (!p || p->H < 1 || p->H > 3 || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > kMaxCand ||
-      !p->attn || !p->dxcat || !p->dqt || !p->dq || !p->dbeta)
-    return DGPPO_EINVAL;
-  if (p->G == 0) return 0;
-  const size_t shmem = p->dx ? (size_t)p->N * p->D * sizeof(float) : 0;
-  if (shmem > 48 * 1024) return DGPPO_EINVAL;
-  hipLaunchKernelGGL(gnn_attn_bwd_kernel, dim3(p->G), dim3(64), shmem, DG_STREAM(stream), *p);
-  return (int)hipGetLastError();
-}
 
 extern "C" int dgppo_relu_bwd(float* dy, const float* y, int64_t n, void* stream) {
   if (n < 0 || !dy || !y) return DGPPO_EINVAL;

@@ -42,8 +42,9 @@ GEMM_LOG = None  # set to a list to record (M, N, K, batch, ta, tb, split_k, has
 def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
          a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
          bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
-         alpha=1.0, beta=0.0, relu=False, split_k=None):
-    """C = alpha op(A) op(B) + beta C + bias + addend (see dgppo_gemm).  Element offsets/strides."""
+         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None):
+    """C = alpha op(A) op(B) + beta C + bias + addend (see dgppo_gemm).  Element offsets/strides.
+    bias_grad (ta only): bias_grad = alpha colsum(B) + beta bias_grad, fused into the dW GEMM."""
     lib = _lib.load()
     _lib.require_gpu(C.device, "gemm")
     g = _lib.GemmArgs()
@@ -62,12 +63,11 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
         tiles = math.ceil(M / 64) * math.ceil(N / 64) * batch
         split_k = max(1, min(math.ceil(K / 512), 1024 // max(tiles, 1))) if K >= 2048 else 1
     g.split_k = int(split_k)
+    g.bias_grad = _p(bias_grad)
     if GEMM_LOG is not None:
         GEMM_LOG.append((int(M), int(N), int(K), int(batch), int(ta), int(tb), int(split_k), bias is not None))
-    ws = None
-    if g.split_k > 1:
-        ws = workspace(lib.dgppo_gemm_workspace_floats(ctypes.byref(g)), C.device, "gemm")
-    g.workspace = _p(ws)
+    nws = lib.dgppo_gemm_workspace_floats(ctypes.byref(g))
+    g.workspace = _p(workspace(nws, C.device, "gemm")) if nws > 0 else None
     _chk(lib.dgppo_gemm(ctypes.byref(g), _stream(C)), "dgppo_gemm")
 
 
@@ -106,6 +106,22 @@ def gru_bwd(gi, gh, bhn, h, dh_new, dgi, dgh, dh):
     rows, H = h.shape
     _chk(_lib.load().dgppo_gru_bwd(_p(gi), _p(gh), _p(bhn), _p(h), _p(dh_new), _p(dgi), _p(dgh), _p(dh), int(rows),
                                    int(H), _stream(h)), "dgppo_gru_bwd")
+
+
+def gru_seq(fwd, Q, L, n, gi, Wh, bhn, h0, hs, hT=None, dhs=None, dgi=None, dgh=None, dh0=None, dbhn_part=None):
+    a = _lib.GruSeqArgs()
+    a.Q, a.L, a.n_agents, a.H = int(Q), int(L), int(n), 64
+    a.gi, a.Wh, a.bhn, a.h0, a.hs, a.hT = _p(gi), _p(Wh), _p(bhn), _p(h0), _p(hs), _p(hT)
+    a.dhs, a.dgi, a.dgh, a.dh0, a.dbhn_part = _p(dhs), _p(dgi), _p(dgh), _p(dh0), _p(dbhn_part)
+    lib = _lib.load()
+    if fwd:
+        _chk(lib.dgppo_gru_seq_fwd(ctypes.byref(a), _stream(hs)), "dgppo_gru_seq_fwd")
+    else:
+        _chk(lib.dgppo_gru_seq_bwd(ctypes.byref(a), _stream(hs)), "dgppo_gru_seq_bwd")
+
+
+def gru_seq_blocks(Q):
+    return int(_lib.load().dgppo_gru_seq_blocks(int(Q)))
 
 
 def agent_mean_fwd(x, y, G, n, F, x_gstride):

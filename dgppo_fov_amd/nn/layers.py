@@ -143,9 +143,7 @@ class Dense:
         return y
 
     def bwd(self, x, dy, rows, need_dx=True, dx_out=None, accumulate=False):
-        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0)
-        if self.has_bias:
-            K.colsum(dy, rows, self.d_out, self.b(True), beta=1.0)
+        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0, bias_grad=self.b(True))
         if not need_dx:
             return None
         dx = dx_out if dx_out is not None else torch.empty((rows, self.d_in), device=dy.device)
@@ -260,34 +258,50 @@ class GRUCell:
         self.v("Wh").copy_(torch.from_numpy(wh))
         self.v("bhn").copy_(torch.as_tensor(np.asarray(d["hn"]["bias"], np.float32)))
 
-    def fwd(self, x, h):
-        rows, H = h.shape[0], self.H
+    def seq_fwd(self, x, Q, L, n, h0=None, hs_out=None, hT_out=None):
+        """Scan over L steps of Q sequence rows (x rows ordered ((q // n) * L + t) * n + q % n, see
+        dgppo_gru_seq_args): one input GEMM + one recurrent kernel.  Returns (hs (Q*L, 64), cache)."""
+        rows, H = Q * L, self.H
         gi = torch.empty((rows, 3 * H), device=x.device)
-        gh = torch.empty((rows, 3 * H), device=x.device)
         K.gemm(x, self.v("Wi"), gi, rows, 3 * H, self.d_in, bias=self.v("bi"))
-        K.gemm(h, self.v("Wh"), gh, rows, 3 * H, H)
-        hn = torch.empty_like(h)
-        K.gru_fwd(gi, gh, self.v("bhn"), h, hn)
-        return hn, (x, h, gi, gh)
+        hs = hs_out if hs_out is not None else torch.empty((rows, H), device=x.device)
+        K.gru_seq(True, Q, L, n, gi, self.v("Wh"), self.v("bhn"), h0, hs, hT=hT_out)
+        return hs, (x, gi, hs, h0, Q, L, n)
 
-    def bwd(self, cache, dhn, need_dx=True):
-        """returns (dx, dh)"""
-        x, h, gi, gh = cache
-        rows, H = h.shape[0], self.H
-        dgi = torch.empty_like(gi)
-        dgh = torch.empty_like(gh)
-        dh = torch.zeros_like(h)
-        K.gru_bwd(gi, gh, self.v("bhn"), h, dhn, dgi, dgh, dh)
-        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0)
-        K.colsum(dgi, rows, 3 * H, self.v("bi", True), beta=1.0)
-        K.gemm(h, dgh, self.v("Wh", True), H, 3 * H, rows, ta=True, beta=1.0)
-        K.colsum(dgh, rows, H, self.v("bhn", True), ld=3 * H, x_off=2 * H, beta=1.0)
-        K.gemm(dgh, self.v("Wh"), dh, rows, H, 3 * H, tb=True, ldb=3 * H, beta=1.0)
+    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False):
+        """Backward of seq_fwd: accumulates dWi, dbi, dWh, dbhn; returns (dx, dh0)."""
+        x, gi, hs, h0, Q, L, n = cache
+        rows, H, dev = Q * L, self.H, dhs.device
+        dgi = torch.empty((rows, 3 * H), device=dev)
+        dgh = torch.empty((rows, 3 * H), device=dev)
+        dh0 = torch.empty((Q, H), device=dev) if need_dh0 else None
+        nb = K.gru_seq_blocks(Q)
+        part = K.workspace(nb * H, dev, "gru_bhn")
+        K.gru_seq(False, Q, L, n, gi, self.v("Wh"), self.v("bhn"), h0, hs, dhs=dhs, dgi=dgi, dgh=dgh, dh0=dh0,
+                  dbhn_part=part)
+        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0, bias_grad=self.v("bi", True))
+        S = Q // n
+        if L > 1:  # h_{t-1} of step t >= 1 is hs of step t-1: row-grouped per sequence, B shifted by n rows
+            K.gemm(hs, dgh, self.v("Wh", True), H, 3 * H, S * (L - 1) * n, ta=True, lda=H, a_grp=(L - 1) * n,
+                   a_gs=L * n * H, ldb=3 * H, b_off=n * 3 * H, b_grp=(L - 1) * n, b_gs=L * n * 3 * H, beta=1.0)
+        if h0 is not None:  # step 0 uses the initial carries
+            K.gemm(h0, dgh, self.v("Wh", True), H, 3 * H, Q, ta=True, lda=H, ldb=3 * H, b_grp=n,
+                   b_gs=L * n * 3 * H, beta=1.0)
+        K.colsum(part, nb, H, self.v("bhn", True), beta=1.0)
         dx = None
         if need_dx:
             dx = torch.empty_like(x)
             K.gemm(dgi, self.v("Wi"), dx, rows, self.d_in, 3 * H, tb=True, ldb=3 * H)
-        return dx, dh
+        return dx, dh0
+
+    def fwd(self, x, h, h_out=None):
+        """One step for `rows` independent carries (act / get_Vh): (h_new, cache)."""
+        rows = h.shape[0]
+        return self.seq_fwd(x, rows, 1, 1, h0=h, hs_out=h_out)
+
+    def bwd(self, cache, dhn, need_dx=True):
+        """returns (dx, dh)"""
+        return self.seq_bwd(cache, dhn, need_dx=need_dx, need_dh0=True)
 
 
 class GraphTransformer:
@@ -412,14 +426,13 @@ class GraphTransformer:
                batch=H, beta=1.0)
         K.gemm(dQT, self.v("Wkt"), dQ, R, F, D, lda=H * D, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
                batch=H, beta=1.0)
-        K.gemm(X, dQ, self.v("Wq", True), D, H * F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0)
-        K.colsum(dQ, R, H * F, self.v("bq", True), beta=1.0)
+        K.gemm(X, dQ, self.v("Wq", True), D, H * F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0,
+               bias_grad=self.v("bq", True))
         if last:
-            K.gemm(X, dY, self.v("Wu", True), D, F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0)
-            K.colsum(dY, R, F, self.v("bu", True), beta=1.0)
+            K.gemm(X, dY, self.v("Wu", True), D, F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0,
+                   bias_grad=self.v("bu", True))
         else:
-            K.gemm(X, dY, self.v("Wu", True), D, F, G * N, ta=True, lda=D, beta=1.0)
-            K.colsum(dY, G * N, F, self.v("bu", True), beta=1.0)
+            K.gemm(X, dY, self.v("Wu", True), D, F, G * N, ta=True, lda=D, beta=1.0, bias_grad=self.v("bu", True))
         if need_dx:
             if last:
                 K.gemm(dY, self.v("Wu"), dX, R, D, F, tb=True, ldb=F, c_grp=n, c_gs=N * D, ldc=D, beta=1.0)

@@ -157,6 +157,8 @@ typedef struct dgppo_gemm_args {
   int32_t relu;
   int32_t split_k;
   float* workspace;
+  float* bias_grad;  /* trans_a && !trans_b only: bias_grad[n] = alpha * sum_k B[k][n] + beta * bias_grad[n]
+                        (the dense layer's db fused into its dW = X^T dY), or NULL */
 } dgppo_gemm_args;
 
 int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* args);
@@ -213,6 +215,34 @@ int dgppo_gru_fwd(const float* gi, const float* gh, const float* bhn, const floa
                   int32_t H, void* stream);
 int dgppo_gru_bwd(const float* gi, const float* gh, const float* bhn, const float* h, const float* dh_new,
                   float* dgi, float* dgh, float* dh, int64_t rows, int32_t H, void* stream);
+
+/* Whole-sequence GRU (the rnn_step scans of informarl.py:281-293 / 387-403 and the 1-step carries
+ * of act / get_Vh) in one launch per direction.  Q sequence rows (q = s * n_agents + a) over L steps;
+ * step-t row of sequence row q in the (rows = Q*L) tensors: ((q / n_agents) * L + t) * n_agents +
+ * q % n_agents.  gi = x Wi + bi for all rows is computed outside (one GEMM).  H must be 64.
+ *   fwd: hs[row] = h_t (carry after step t), hT (optional) = h_{L-1}; h0 NULL = zero carries.
+ *   bwd: from dhs (upstream grads on hs) writes dgi = [dr|dz|dn] and dgh = [dr|dz|dn*r] (pre-
+ *        activation grads; dWi = x^T dgi, dbi = colsum dgi, dWh = h_{t-1}^T dgh are GEMMs outside),
+ *        dh0 (optional), and dbhn_part[b][H] = per-workgroup column sums of dn*r over its rows
+ *        (dgppo_gru_seq_blocks(Q) workgroups; reduce with dgppo_colsum). */
+typedef struct dgppo_gru_seq_args {
+  int32_t Q, L, n_agents, H;
+  const float* gi;     /* (rows, 3H) */
+  const float* Wh;     /* (H, 3H) */
+  const float* bhn;    /* (H) */
+  const float* h0;     /* (Q, H) or NULL */
+  float* hs;           /* (rows, H): fwd output, bwd input */
+  float* hT;           /* (Q, H) or NULL */
+  const float* dhs;    /* (rows, H) */
+  float* dgi;          /* (rows, 3H) */
+  float* dgh;          /* (rows, 3H) */
+  float* dh0;          /* (Q, H) or NULL */
+  float* dbhn_part;    /* (blocks, H) or NULL */
+} dgppo_gru_seq_args;
+
+int64_t dgppo_gru_seq_blocks(int32_t Q);
+int dgppo_gru_seq_fwd(const dgppo_gru_seq_args* args, void* stream);
+int dgppo_gru_seq_bwd(const dgppo_gru_seq_args* args, void* stream);
 
 /* mean over the agents of each graph (RStateFn, dgppo/algo/module/value.py:29) */
 int dgppo_agent_mean_fwd(const float* x, float* y, int64_t G, int32_t n, int32_t F, int64_t x_gstride, void* stream);

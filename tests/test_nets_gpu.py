@@ -64,6 +64,39 @@ def test_gemm_matches_float64(cuda, M, N, Kd, ta, tb, batch):
     assert (Cd.double().cpu() - ref).abs().max().item() <= 2e-6 * scale + 1e-5
 
 
+@pytest.mark.parametrize("M,N,Kd,batch,grp", [(64, 192, 131072, 1, 0), (111, 64, 20000, 1, 0), (7, 32, 70001, 1, 0),
+                                               (64, 32, 5000, 3, 0), (200, 150, 3001, 1, 0), (64, 192, 4096, 1, 24),
+                                               (36, 64, 777, 2, 7)])
+def test_gemm_weight_grad_with_fused_bias_grad(cuda, M, N, Kd, batch, grp):
+    """dW = A^T B (+ beta) with db = colsum(B) fused (the wgrad path), incl. row-grouped operands."""
+    g = torch.Generator().manual_seed(M + N + Kd)
+    if grp:  # stored rows k live at (k // grp) * gstride + (k % grp) * ld: groups padded by 5 rows
+        ng = (Kd + grp - 1) // grp
+        Kd = ng * grp
+        Ab = torch.randn(batch, ng, grp + 5, M, generator=g, dtype=torch.float64)
+        Bb = torch.randn(batch, ng, grp + 5, N, generator=g, dtype=torch.float64)
+        A = Ab[:, :, :grp].reshape(batch, Kd, M)
+        B = Bb[:, :, :grp].reshape(batch, Kd, N)
+        kw = dict(a_grp=grp, a_gs=(grp + 5) * M, b_grp=grp, b_gs=(grp + 5) * N, sa=ng * (grp + 5) * M,
+                  sb=ng * (grp + 5) * N)
+        Ad, Bd = Ab.float().to(cuda), Bb.float().to(cuda)
+    else:
+        A = torch.randn(batch, Kd, M, generator=g, dtype=torch.float64)
+        B = torch.randn(batch, Kd, N, generator=g, dtype=torch.float64)
+        kw = dict(sa=Kd * M, sb=Kd * N)
+        Ad, Bd = A.float().to(cuda), B.float().to(cuda)
+    C0 = torch.randn(batch, M, N, generator=g, dtype=torch.float64)
+    b0 = torch.randn(batch, N, generator=g, dtype=torch.float64)
+    Cd, bd = C0.float().to(cuda), b0.float().to(cuda)
+    K.gemm(Ad, Bd, Cd, M, N, Kd, ta=True, batch=batch, sc=M * N, alpha=0.5, beta=1.0, bias_grad=bd, **kw)
+    torch.cuda.synchronize()
+    ref = 0.5 * A.transpose(1, 2) @ B + C0
+    refb = 0.5 * B.sum(1) + b0
+    scale = (A.abs().transpose(1, 2) @ B.abs()).max().item()
+    assert (Cd.double().cpu() - ref).abs().max().item() <= 2e-6 * scale + 1e-5
+    assert (bd.double().cpu() - refb).abs().max().item() <= 2e-6 * B.abs().sum(1).max().item() + 1e-5
+
+
 def test_gemm_row_grouping(cuda):
     """agent rows (first n of N per graph) as GEMM rows, in and out."""
     G, N, n, D, F = 5, 9, 3, 6, 4
