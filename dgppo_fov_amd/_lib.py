@@ -132,7 +132,9 @@ class GnnAttnArgs(ctypes.Structure):
         ("attn", c_f32p), ("xcat", c_f32p),
         ("dxcat", c_f32p), ("dqt", c_f32p), ("dq", c_f32p), ("dbeta", c_f32p),
         ("dx", c_f32p), ("dx_gstride", ctypes.c_int64),
-        ("scale", ctypes.c_float),
+        ("scale", ctypes.c_float), ("D0", ctypes.c_int32),
+        ("xa", c_f32p), ("xa_gstride", ctypes.c_int64), ("pre_W", c_f32p), ("pre_b", c_f32p),
+        ("dxa", c_f32p), ("dxa_gstride", ctypes.c_int64), ("dpre_part", c_f32p), ("sidx", c_f32p),
     ]
 
 
@@ -188,6 +190,8 @@ SIGNATURES = {
     "dgppo_gru_fwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, _I32, _V]),
     "dgppo_gru_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _V]),
     "dgppo_gru_seq_blocks": (ctypes.c_int64, [_I32]),
+    "dgppo_gnn_attn_partial_blocks": (ctypes.c_int64, [_V]),
+    "dgppo_gnn_sender_table": (ctypes.c_int, [_I32, _I32, _I32, _I32, _V, _V, _V, _V, _V]),
     "dgppo_gru_seq_fwd": (ctypes.c_int, [_V, _V]),
     "dgppo_gru_seq_bwd": (ctypes.c_int, [_V, _V]),
     "dgppo_agent_mean_fwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),

@@ -3,12 +3,21 @@
 //
 // Thread mapping: a receiver (graph g, agent i) owns a group of CP = pow2 >= C lanes, one lane per
 // candidate edge; a 256-thread workgroup processes R = 256 / CP receivers per round and `gpb` whole
-// graphs (rounds loop over their receivers).  Each lane gathers its sender's feature row ONCE into
-// registers (D <= DM floats) plus the edge's 4 features, so the softmax logits, the softmax
-// backward and the sender gradients are per-lane register math; the weighted sums over candidates
-// (xbar, ebar, dqt) go through an LDS transpose so every output column is one lane's dot product.
-// Sender gradients of the backward accumulate in an LDS image of the block's graphs in fixed
-// receiver order (bitwise-deterministic, no atomics) and are added to dx once per node.
+// graphs per block (rounds loop over their receivers); blocks are persistent (grid-stride).  Each
+// lane gathers its sender's feature row ONCE into registers (D <= DM floats) plus the edge's 4
+// features -- issued before the round's staging barrier so the gathers overlap it -- and the
+// softmax logits, the softmax backward and the sender gradients are per-lane register math; the
+// weighted sums over candidates (xbar, ebar, dqt) go through an LDS transpose so every output
+// column is one lane's dot product.
+//
+// Agent mode (xa != NULL): nodes that never receive (goals, LiDAR hits, obstacles) are only ever
+// SENDERS, so their features at a layer are the previous layer's Dense_4 + ReLU of their raw row
+// (empty aggregation); the kernel recomputes them per candidate (D0 x D FMAs) instead of
+// materialising (G, N, D) hidden features, and folds their gradient straight into the previous
+// layer's Dense_4 weight/bias gradient (per-block partials, fixed order).
+//
+// Sender gradients accumulate in an LDS image of the block's graphs in fixed receiver order, and
+// every reduction has a fixed order: bitwise-deterministic, no atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -17,7 +26,9 @@
 namespace dgppo {
 namespace {
 
-constexpr int kH = 3;  // heads (GraphTransformer num_heads of the reference GNN)
+constexpr int kH = 3;         // heads (GraphTransformer num_heads of the reference GNN)
+constexpr int kD0 = 8;        // max raw feature width in agent mode
+constexpr int kMaxBlocks = 2048;
 
 template <int CP>
 __device__ __forceinline__ float group_sum(float v, float* scratch) {
@@ -66,9 +77,24 @@ __device__ __forceinline__ Cand candidate(const dgppo_gnn_attn_args& p, int64_t 
   if (c < p.C) {
     const int e = p.cand[i * p.C + c];
     k.e = e;
-    if (e >= 0 && p.receivers[g * p.E + e] == i) k.s = p.senders[g * p.E + e];
+    if (p.sidx) k.s = p.sidx[(g * p.n_agents + i) * p.C + c];
+    else if (e >= 0 && p.receivers[g * p.E + e] == i) k.s = p.senders[g * p.E + e];
   }
   return k;
+}
+
+__global__ __launch_bounds__(256) void sender_table_kernel(int32_t G, int32_t n, int32_t C, int32_t E,
+                                                           const int32_t* cand, const int32_t* recv,
+                                                           const int32_t* send, int32_t* sidx) {
+  const int64_t total = (int64_t)G * n * C;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int c = (int)(t % C);
+    const int64_t gi = t / C;
+    const int i = (int)(gi % n);
+    const int64_t g = gi / n;
+    const int e = cand[i * C + c];
+    sidx[t] = (e >= 0 && recv[g * E + e] == i) ? send[g * E + e] : -1;
+  }
 }
 
 template <int DM>
@@ -85,222 +111,407 @@ __device__ __forceinline__ void load_row(const float* xr, int D, bool ok, float 
   }
 }
 
-// LDS carve (floats): qt [R][kH*DM] | beta/dbeta [R][4] | xs [256][DM+1] | a [256][kH] | ef [256][4]
-//                     | g (bwd: dxcat) [R][kH*(DM+5)] | scratch[8] | dxs (bwd) [gpb][N][D]
+// LDS carve (floats), CR = candidate rows kept per receiver (C rounded up to 8, <= CP):
+//   preW [kD0][DM] | preb [DM] | scratch [8] | qt [R][kH*DM] | xs [R*CR][DM+1] | a [R*CR][kH]
+//   | ef [R*CR][4] | (bwd) g [R][kH*(DM+5)] | x0s [R*CR][kD0+1] | dxs [gpb][Nacc][D]
 template <int CP, int DM>
 struct Carve {
   static constexpr int R = 256 / CP;
   static constexpr int XP = DM + 1;
-  float *qt, *beta, *xs, *a, *ef, *g, *scr, *dxs;
-  __device__ Carve(float* base) {
-    qt = base;
-    beta = qt + R * kH * DM;
-    xs = beta + R * 4;
-    a = xs + 256 * XP;
-    ef = a + 256 * kH;
-    g = ef + 256 * 4;
-    scr = g + R * kH * (DM + 5);
-    dxs = scr + 8;
+  float *preW, *preb, *scr, *qt, *xs, *a, *ef, *g, *x0s, *dxs;
+  __device__ Carve(float* base, int CR, bool bwd) {
+    preW = base;
+    preb = preW + kD0 * DM;
+    scr = preb + DM;
+    qt = scr + 8;
+    xs = qt + R * kH * DM;
+    a = xs + R * CR * XP;
+    ef = a + R * CR * kH;
+    g = ef + R * CR * 4;
+    x0s = g + (bwd ? R * kH * (DM + 5) : 0);
+    dxs = x0s + (bwd ? R * CR * (kD0 + 1) : 0);
   }
-  static constexpr size_t floats_fixed() {
-    return (size_t)R * kH * DM + R * 4 + 256 * XP + 256 * kH + 256 * 4 + R * kH * (DM + 5) + 8;
+  static size_t floats_fixed(int CR, bool bwd) {
+    return (size_t)kD0 * DM + DM + 8 + R * kH * DM + (size_t)R * CR * (XP + kH + 4) +
+           (bwd ? (size_t)R * kH * (DM + 5) + (size_t)R * CR * (kD0 + 1) : 0);
   }
 };
 
-template <int CP, int DM>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(dgppo_gnn_attn_args p, int gpb) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  using CV = Carve<CP, DM>;
-  constexpr int R = CV::R, XP = CV::XP;
-  CV L(lds);
-  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = p.H;
-  const int W = H * (D + 5);
-  const int t = threadIdx.x, slot = t / CP, c = t % CP;
-  const int64_t g0 = (int64_t)blockIdx.x * gpb;
-  const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
-  const int nrec = ng * n;
-  for (int r0 = 0; r0 < nrec; r0 += R) {
-    // stage qt and beta_h = q_h . bk_h of the round's receivers
-    for (int e = t; e < R * H * D; e += 256) {
-      const int rr = e / (H * D), k = e - rr * (H * D);
-      if (r0 + rr < nrec) L.qt[rr * kH * DM + k] = p.qt[(g0 * n + r0 + rr) * H * D + k];
-    }
-    if (t < R * H) {
-      const int rr = t / H, h = t - rr * H;
-      float acc = 0.0f;
-      if (r0 + rr < nrec) {
-        const float* q = p.q + (g0 * n + r0 + rr) * H * F + h * F;
-        for (int f = 0; f < F; ++f) acc += q[f] * p.bk[h * F + f];
-      }
-      L.beta[rr * 4 + h] = acc;
-    }
-    __syncthreads();
-    const int rl = r0 + slot;
-    const bool active = rl < nrec;
-    const int64_t g = g0 + (active ? rl / n : 0);
-    const int i = active ? rl % n : 0;
-    const int64_t row = g0 * n + rl;
-    const Cand k = active ? candidate(p, g, i, c) : Cand{-1, -1};
-    const bool ok = k.s >= 0;
-    float x[DM];
-    load_row<DM>(p.x + g * p.x_gstride + (int64_t)(ok ? k.s : 0) * D, D, ok, x);
-    float ef[4];
+__host__ __device__ inline int cand_rows(int C, int CP) {
+  const int cr = (C + 7) & ~7;
+  return cr < CP ? cr : CP;
+}
+
+// sender row of candidate k into x (and its raw row into x0 when it goes through the transform)
+template <int DM>
+__device__ __forceinline__ void gather_sender(const dgppo_gnn_attn_args& p, int64_t g, int s, bool ok, int D,
+                                              const float* preW, const float* preb, float (&x)[DM],
+                                              float (&x0)[kD0], bool& via_pre) {
+  via_pre = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ef[j] = ok ? p.ef[g * p.ef_gstride + (int64_t)k.e * 4 + j] : 0.0f;
-    float lg[kH], mx[kH], a[kH];
+  for (int k = 0; k < kD0; ++k) x0[k] = 0.0f;
+  if (p.xa == nullptr) {
+    load_row<DM>(p.x + g * p.x_gstride + (int64_t)(ok ? s : 0) * D, D, ok, x);
+    return;
+  }
+  if (!ok || s < p.n_agents) {
+    load_row<DM>(p.xa + g * p.xa_gstride + (int64_t)(ok ? s : 0) * D, D, ok, x);
+    return;
+  }
+  const float* xr = p.x + g * p.x_gstride + (int64_t)s * p.D0;
 #pragma unroll
-    for (int h = 0; h < kH; ++h) {
-      float acc = 0.0f;
-      const float* qt = L.qt + slot * kH * DM + h * D;
+  for (int k = 0; k < kD0; ++k) x0[k] = k < p.D0 ? xr[k] : 0.0f;
+  if (p.pre_W == nullptr) {  // raw rows used directly (D0 == D <= kD0)
 #pragma unroll
-      for (int d = 0; d < DM; ++d)
-        if (d < D) acc += qt[d] * x[d];
-      lg[h] = (ok && h < H) ? (acc + L.beta[slot * 4 + h]) * p.scale : -INFINITY;
-      mx[h] = group_max<CP>(lg[h], L.scr);
-    }
+    for (int d = 0; d < DM; ++d) x[d] = d < kD0 ? x0[d < kD0 ? d : 0] : 0.0f;
+    return;
+  }
+  via_pre = true;
 #pragma unroll
-    for (int h = 0; h < kH; ++h) {
-      const float ex = ok && h < H ? expf(lg[h] - mx[h]) : 0.0f;
-      const float sm = group_sum<CP>(ex, L.scr);
-      a[h] = ok && h < H ? ex / sm : 0.0f;
-      if (active && c < C && h < H && p.attn) p.attn[(row * H + h) * C + c] = a[h];
-    }
-    // LDS transpose: candidates' rows and weights, then one output column per lane
+  for (int d = 0; d < DM; ++d) {
+    float v = preb[d];
 #pragma unroll
-    for (int d = 0; d < DM; ++d) L.xs[t * XP + d] = x[d];
-#pragma unroll
-    for (int h = 0; h < kH; ++h) L.a[t * kH + h] = a[h];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) L.ef[t * 4 + j] = ef[j];
-    __syncthreads();
-    if (active) {
-      const int base = slot * CP;
-      float* out = p.xcat + row * W;
-      for (int o = c; o < W; o += CP) {
-        float acc = 0.0f;
-        if (o < H * D) {
-          const int h = o / D, d = o - h * D;
-          for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
-        } else if (o < H * D + 4 * H) {
-          const int q = o - H * D, h = q >> 2, j = q & 3;
-          for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.ef[(base + cc) * 4 + j];
-        } else {
-          const int h = o - H * D - 4 * H;
-          for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h];
-        }
-        out[o] = acc;
-      }
-    }
-    __syncthreads();
+    for (int k = 0; k < kD0; ++k) v += x0[k] * preW[k * DM + d];
+    x[d] = v > 0.0f ? v : 0.0f;
   }
 }
 
+__device__ __forceinline__ void stage_pre(const dgppo_gnn_attn_args& p, float* preW, float* preb, int DM) {
+  if (p.xa == nullptr || p.pre_W == nullptr) return;
+  for (int e = threadIdx.x; e < kD0 * DM; e += 256) {
+    const int k = e / DM, d = e - k * DM;
+    preW[e] = (k < p.D0 && d < p.D) ? p.pre_W[k * p.D + d] : 0.0f;
+  }
+  for (int d = threadIdx.x; d < DM; d += 256) preb[d] = d < p.D ? p.pre_b[d] : 0.0f;
+}
+
 template <int CP, int DM>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, int gpb) {
+__global__ __launch_bounds__(256) void attn_fwd_kernel(dgppo_gnn_attn_args p, int gpb, int64_t nblk) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   using CV = Carve<CP, DM>;
   constexpr int R = CV::R, XP = CV::XP;
-  CV L(lds);
-  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = p.H, N = p.N;
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = p.H;
+  const int CR = cand_rows(C, CP);
+  CV L(lds, CR, false);
   const int W = H * (D + 5);
   const int t = threadIdx.x, slot = t / CP, c = t % CP;
-  const int64_t g0 = (int64_t)blockIdx.x * gpb;
-  const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
-  const int nrec = ng * n;
-  const bool want_dx = p.dx != nullptr;
-  if (want_dx)
-    for (int e = t; e < ng * N * D; e += 256) L.dxs[e] = 0.0f;
-  for (int r0 = 0; r0 < nrec; r0 += R) {
-    for (int e = t; e < R * H * D; e += 256) {
-      const int rr = e / (H * D), kk = e - rr * (H * D);
-      if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
-    }
-    for (int e = t; e < R * W; e += 256) {
-      const int rr = e / W, kk = e - rr * W;
-      if (r0 + rr < nrec) L.g[rr * kH * (DM + 5) + kk] = p.dxcat[(g0 * n + r0 + rr) * W + kk];
-    }
-    __syncthreads();
-    const int rl = r0 + slot;
-    const bool active = rl < nrec;
-    const int gl = active ? rl / n : 0;
-    const int64_t g = g0 + gl;
-    const int i = active ? rl % n : 0;
-    const int64_t row = g0 * n + rl;
-    const Cand k = active ? candidate(p, g, i, c) : Cand{-1, -1};
-    const bool ok = k.s >= 0;
-    float x[DM];
-    load_row<DM>(p.x + g * p.x_gstride + (int64_t)(ok ? k.s : 0) * D, D, ok, x);
-    float ef[4];
+  const int lr = slot * CR + c;  // this lane's LDS row (valid when c < CR)
+  stage_pre(p, L.preW, L.preb, DM);
+  __syncthreads();
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t g0 = blk * gpb;
+    const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
+    const int nrec = ng * n;
+    for (int r0 = 0; r0 < nrec; r0 += R) {
+      const int rl = r0 + slot;
+      const bool active = rl < nrec;
+      const int64_t g = g0 + (active ? rl / n : 0);
+      const int i = active ? rl % n : 0;
+      const int64_t row = g0 * n + rl;
+      // gathers first (they overlap the staging barrier below)
+      const Cand k = active ? candidate(p, g, i, c) : Cand{-1, -1};
+      const bool ok = k.s >= 0;
+      float x[DM], x0[kD0];
+      bool via_pre;
+      gather_sender<DM>(p, g, k.s, ok, D, L.preW, L.preb, x, x0, via_pre);
+      float ef[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ef[j] = ok ? p.ef[g * p.ef_gstride + (int64_t)k.e * 4 + j] : 0.0f;
-    const float* gv = L.g + slot * kH * (DM + 5);  // dxbar (H*D) | debar (H*4) | dsig (H)
-    float a[kH], dl[kH], dbeta[kH];
+      for (int j = 0; j < 4; ++j) ef[j] = ok ? p.ef[g * p.ef_gstride + (int64_t)k.e * 4 + j] : 0.0f;
+      // stage qt; beta_h = q_h . bk_h as a group dot product
+      for (int e = t; e < R * H * D; e += 256) {
+        const int rr = e / (H * D), kk = e - rr * (H * D);
+        if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
+      }
+      float beta[kH];
 #pragma unroll
-    for (int h = 0; h < kH; ++h) {
-      a[h] = (ok && h < H) ? p.attn[(row * H + h) * C + c] : 0.0f;
-      float da = 0.0f;
-      if (ok && h < H) {
+      for (int h = 0; h < kH; ++h) {
+        float acc = 0.0f;
+        if (active && h < H)
+          for (int f = c; f < F; f += CP) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
+        beta[h] = group_sum<CP>(acc, L.scr);
+      }
+      __syncthreads();
+      float lg[kH], mx[kH], a[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float acc = 0.0f;
+        const float* qt = L.qt + slot * kH * DM + h * D;
 #pragma unroll
         for (int d = 0; d < DM; ++d)
-          if (d < D) da += gv[h * D + d] * x[d];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) da += gv[H * D + h * 4 + j] * ef[j];
-        da += gv[H * D + H * 4 + h];
+          if (d < D) acc += qt[d] * x[d];
+        lg[h] = (ok && h < H) ? (acc + beta[h]) * p.scale : -INFINITY;
+        mx[h] = group_max<CP>(lg[h], L.scr);
       }
-      const float dot = group_sum<CP>(a[h] * da, L.scr);
-      dl[h] = (ok && h < H) ? a[h] * (da - dot) * p.scale : 0.0f;
-      dbeta[h] = group_sum<CP>(dl[h], L.scr);
-    }
-    if (active && c == 0)
-      for (int h = 0; h < H; ++h) p.dbeta[row * H + h] = dbeta[h];
-    if (active)
-      for (int kk = c; kk < H * F; kk += CP) {
-        const int h = kk / F;
-        p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        const float ex = ok && h < H ? expf(lg[h] - mx[h]) : 0.0f;
+        const float sm = group_sum<CP>(ex, L.scr);
+        a[h] = ok && h < H ? ex / sm : 0.0f;
+        if (active && c < C && h < H && p.attn) p.attn[(row * H + h) * C + c] = a[h];
       }
-    // dqt_h[d] = sum_c dl_c,h x_s[d]: LDS transpose as in the forward
+      // LDS transpose: candidates' rows and weights, then one output column per lane
+      if (c < CR) {
 #pragma unroll
-    for (int d = 0; d < DM; ++d) L.xs[t * XP + d] = x[d];
+        for (int d = 0; d < DM; ++d) L.xs[lr * XP + d] = x[d];
 #pragma unroll
-    for (int h = 0; h < kH; ++h) L.a[t * kH + h] = dl[h];
-    __syncthreads();
-    if (active) {
-      const int base = slot * CP;
-      for (int o = c; o < H * D; o += CP) {
-        const int h = o / D, d = o - h * D;
-        float acc = 0.0f;
-        for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
-        p.dqt[row * H * D + o] = acc;
+        for (int h = 0; h < kH; ++h) L.a[lr * kH + h] = a[h];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L.ef[lr * 4 + j] = ef[j];
       }
-    }
-    // sender gradients dx_s[d] += sum_h a_h dxbar_h[d] + dl_h qt_h[d], receivers in fixed order
-    if (want_dx) {
-      float contrib[DM];
-      const float* qt = L.qt + slot * kH * DM;
-#pragma unroll
-      for (int d = 0; d < DM; ++d) {
-        float v = 0.0f;
-#pragma unroll
-        for (int h = 0; h < kH; ++h)
-          if (h < H && d < D) v += a[h] * gv[h * D + d] + dl[h] * qt[h * D + d];
-        contrib[d] = v;
-      }
-      for (int rr = 0; rr < R; ++rr) {
-        __syncthreads();
-        if (slot == rr && ok) {
-          float* dst = L.dxs + ((int64_t)gl * N + k.s) * D;
-#pragma unroll
-          for (int d = 0; d < DM; ++d)
-            if (d < D) dst[d] += contrib[d];
+      __syncthreads();
+      if (active) {
+        const int base = slot * CR;
+        float* out = p.xcat + row * W;
+        for (int o = c; o < W; o += CP) {
+          float acc = 0.0f;
+          if (o < H * D) {
+            const int h = o / D, d = o - h * D;
+            for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
+          } else if (o < H * D + 4 * H) {
+            const int q = o - H * D, h = q >> 2, j = q & 3;
+            for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.ef[(base + cc) * 4 + j];
+          } else {
+            const int h = o - H * D - 4 * H;
+            for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h];
+          }
+          out[o] = acc;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
   }
-  if (want_dx) {
-    for (int e = t; e < ng * N * D; e += 256) {
-      const int gg = e / (N * D), kk = e - gg * (N * D);
-      p.dx[(g0 + gg) * p.dx_gstride + kk] += L.dxs[e];
+}
+
+// backward LDS carve (floats):
+//   preW [kD0][DM] | preb [DM] | scratch [8] | qt [R][kH*DM] | g [R][kH*(DM+5)] | xs [R*CR][DM+1]
+//   | a [R*CR][kH] | ps [R*CR][DM+1] | x0s [R*CR][kD0+1] | cb [R][n][DM] | dxs [gpb][N][D] (full mode)
+template <int CP, int DM>
+struct BwdCarve {
+  static constexpr int R = 256 / CP;
+  static constexpr int XP = DM + 1;
+  float *preW, *preb, *scr, *qt, *g, *xs, *a, *ps, *x0s, *cb, *dxs;
+  __device__ BwdCarve(float* base, int CR, int n) {
+    preW = base;
+    preb = preW + kD0 * DM;
+    scr = preb + DM;
+    qt = scr + 8;
+    g = qt + R * kH * DM;
+    xs = g + R * kH * (DM + 5);
+    a = xs + R * CR * XP;
+    ps = a + R * CR * kH;
+    x0s = ps + R * CR * XP;
+    cb = x0s + R * CR * (kD0 + 1);
+    dxs = cb + R * n * DM;
+  }
+  static size_t floats_fixed(int CR, int n) {
+    return (size_t)kD0 * DM + DM + 8 + R * kH * DM + R * kH * (DM + 5) + (size_t)R * CR * (2 * XP + kH + kD0 + 1) +
+           (size_t)R * n * DM;
+  }
+};
+
+// Backward.  Agent mode relies on the env layout of the candidate table (env/base.py
+// agent_candidates): an agent sender j only ever appears at candidate slot c == j (the agent-agent
+// block edge i*n + j), so the sender gradient of agent j is the fixed-order sum over the graph's
+// receivers of their slot-j contributions -- one barrier, no serialised accumulation.
+template <int CP, int DM>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, int gpb, int64_t nblk) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  using CV = BwdCarve<CP, DM>;
+  constexpr int R = CV::R, XP = CV::XP;
+  constexpr int NTD = (DM + 31) / 32;  // 32-column tiles of the pre-gradient accumulator
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = p.H;
+  const int CR = cand_rows(C, CP);
+  CV L(lds, CR, n);
+  const int W = H * (D + 5);
+  const int t = threadIdx.x, slot = t / CP, c = t % CP;
+  const int lane = t & 63, wave = t >> 6;
+  const int lr = slot * CR + c;
+  const bool agent_mode = p.xa != nullptr;
+  const bool want_dxa = agent_mode && p.dxa != nullptr;
+  const bool want_dx = !agent_mode && p.dx != nullptr;
+  const bool want_pre = agent_mode && p.pre_W != nullptr && p.dpre_part != nullptr;
+  const int N = p.N;
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  f32x16 pacc[NTD];
+#pragma unroll
+  for (int q = 0; q < NTD; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pacc[q][r] = 0.0f;
+  stage_pre(p, L.preW, L.preb, DM);
+  __syncthreads();
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t g0 = blk * gpb;
+    const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
+    const int nrec = ng * n;
+    if (want_dx) {
+      for (int e = t; e < ng * N * D; e += 256) L.dxs[e] = 0.0f;
+      __syncthreads();
+    }
+    for (int r0 = 0; r0 < nrec; r0 += R) {
+      const int rl = r0 + slot;
+      const bool active = rl < nrec;
+      const int gl = active ? rl / n : 0;
+      const int64_t g = g0 + gl;
+      const int i = active ? rl % n : 0;
+      const int64_t row = g0 * n + rl;
+      const Cand k = active ? candidate(p, g, i, c) : Cand{-1, -1};
+      const bool ok = k.s >= 0;
+      float x[DM], x0[kD0];
+      bool via_pre;
+      gather_sender<DM>(p, g, k.s, ok, D, L.preW, L.preb, x, x0, via_pre);
+      float ef[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ef[j] = ok ? p.ef[g * p.ef_gstride + (int64_t)k.e * 4 + j] : 0.0f;
+      float a[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) a[h] = (ok && h < H) ? p.attn[(row * H + h) * C + c] : 0.0f;
+      for (int e = t; e < R * H * D; e += 256) {
+        const int rr = e / (H * D), kk = e - rr * (H * D);
+        if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
+      }
+      for (int e = t; e < R * W; e += 256) {
+        const int rr = e / W, kk = e - rr * W;
+        if (r0 + rr < nrec) L.g[rr * kH * (DM + 5) + kk] = p.dxcat[(g0 * n + r0 + rr) * W + kk];
+      }
+      __syncthreads();  // (1) qt / dxcat staged
+      const float* gv = L.g + slot * kH * (DM + 5);  // dxbar (H*D) | debar (H*4) | dsig (H)
+      float dl[kH], dbeta[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float da = 0.0f;
+        if (ok && h < H) {
+#pragma unroll
+          for (int d = 0; d < DM; ++d)
+            if (d < D) da += gv[h * D + d] * x[d];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) da += gv[H * D + h * 4 + j] * ef[j];
+          da += gv[H * D + H * 4 + h];
+        }
+        const float dot = group_sum<CP>(a[h] * da, L.scr);
+        dl[h] = (ok && h < H) ? a[h] * (da - dot) * p.scale : 0.0f;
+        dbeta[h] = group_sum<CP>(dl[h], L.scr);
+      }
+      if (active && c == 0)
+        for (int h = 0; h < H; ++h) p.dbeta[row * H + h] = dbeta[h];
+      if (active)
+        for (int kk = c; kk < H * F; kk += CP) {
+          const int h = kk / F;
+          p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+        }
+      // sender contribution dx_s[d] = sum_h a_h dxbar_h[d] + dl_h qt_h[d]
+      float contrib[DM];
+      {
+        const float* qt = L.qt + slot * kH * DM;
+#pragma unroll
+        for (int d = 0; d < DM; ++d) {
+          float v = 0.0f;
+#pragma unroll
+          for (int h = 0; h < kH; ++h)
+            if (h < H && d < D) v += a[h] * gv[h * D + d] + dl[h] * qt[h * D + d];
+          contrib[d] = v;
+        }
+      }
+      // LDS images for the column reductions
+      if (c < CR) {
+#pragma unroll
+        for (int d = 0; d < DM; ++d) L.xs[lr * XP + d] = x[d];
+#pragma unroll
+        for (int h = 0; h < kH; ++h) L.a[lr * kH + h] = dl[h];
+        if (want_pre) {
+#pragma unroll
+          for (int d = 0; d < DM; ++d) L.ps[lr * XP + d] = via_pre && x[d] > 0.0f ? contrib[d] : 0.0f;
+#pragma unroll
+          for (int kk = 0; kk < kD0; ++kk) L.x0s[lr * (kD0 + 1) + kk] = via_pre ? x0[kk] : 0.0f;
+          L.x0s[lr * (kD0 + 1) + kD0] = via_pre ? 1.0f : 0.0f;
+        }
+      }
+      if (want_dxa && c < n) {
+#pragma unroll
+        for (int d = 0; d < DM; ++d) L.cb[(slot * n + c) * DM + d] = (ok && k.s < n) ? contrib[d] : 0.0f;
+      }
+      __syncthreads();  // (2) images written
+      if (active) {
+        const int base = slot * CR;
+        for (int o = c; o < H * D; o += CP) {
+          const int h = o / D, d = o - h * D;
+          float acc = 0.0f;
+          for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
+          p.dqt[row * H * D + o] = acc;
+        }
+      }
+      if (want_dxa) {  // agent j of each graph in this round: sum of its receivers' slot-j rows, in order
+        const int rounds_graphs = (R + n - 1) / n + 1;
+        for (int e = t; e < rounds_graphs * n * D; e += 256) {
+          const int q = e / (n * D), jd = e - q * (n * D), j = jd / D, d = jd - j * D;
+          const int gg = (r0 / n) + q;  // local graph index
+          if (gg >= ng) continue;
+          const int s0 = gg * n - r0, s1 = s0 + n;  // this graph's receivers' slots in the round
+          float acc = 0.0f;
+          bool any = false;
+          for (int s = s0 < 0 ? 0 : s0; s < (s1 < R ? s1 : R); ++s) {
+            if (r0 + s >= nrec) break;
+            acc += L.cb[(s * n + j) * DM + d];
+            any = true;
+          }
+          if (any) p.dxa[(g0 + gg) * p.dxa_gstride + j * D + d] += acc;
+        }
+      }
+      if (want_pre) {  // pre-gradient += x0s^T ps over this round's rows (MFMA, per-wave accumulators)
+        const int rows = R * CR;
+        for (int t0 = 2 * wave; t0 < rows; t0 += 8) {
+          const int tr = t0 + (lane >> 5);
+          const int m = lane & 31;
+          const float av = (tr < rows && m <= kD0) ? L.x0s[tr * (kD0 + 1) + m] : 0.0f;
+#pragma unroll
+          for (int q = 0; q < NTD; ++q) {
+            const int d = q * 32 + m;
+            const float bv = (tr < rows && d < DM) ? L.ps[tr * XP + d] : 0.0f;
+            pacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, pacc[q], 0, 0, 0);
+          }
+        }
+      }
+      if (want_dx) {  // full mode: serialised fixed-order accumulation into the graph image
+        for (int rr = 0; rr < R; ++rr) {
+          __syncthreads();
+          if (slot == rr && ok) {
+            float* dst = L.dxs + ((int64_t)gl * N + k.s) * D;
+#pragma unroll
+            for (int d = 0; d < DM; ++d)
+              if (d < D) dst[d] += contrib[d];
+          }
+        }
+      }
+      __syncthreads();  // (3) round done
+    }
+    if (want_dx) {
+      for (int e = t; e < ng * N * D; e += 256) {
+        const int gg = e / (N * D), kk = e - gg * (N * D);
+        p.dx[(g0 + gg) * p.dx_gstride + kk] += L.dxs[e];
+      }
+      __syncthreads();
+    }
+  }
+  if (want_pre) {  // combine the 4 waves' accumulators in fixed order, write this block's partial
+    float* red = L.xs;  // >= 4 * 32 * (32*NTD + 1) floats are available from xs onwards
+    constexpr int RP = 32 * NTD + 1;
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int q = 0; q < NTD; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            float* dst = red + m * RP + q * 32 + (lane & 31);
+            *dst = (w == 0 ? 0.0f : *dst) + pacc[q][r];
+          }
+      }
+      __syncthreads();
+    }
+    const int PK = p.D0 * D + D;
+    for (int o = t; o < PK; o += 256) {
+      const int m = o < p.D0 * D ? o / D : kD0;
+      const int d = o < p.D0 * D ? o - m * D : o - p.D0 * D;
+      p.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * RP + d];
     }
   }
 }
@@ -311,16 +522,49 @@ int pick_cp(int C) {
   return cp;
 }
 
+struct Plan {
+  int cp, dm, gpb;
+  int64_t nblk, grid;
+  size_t bytes;
+};
+
 template <int CP, int DM>
-int launch(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
+Plan plan_t(const dgppo_gnn_attn_args* p, bool bwd) {
   constexpr int R = 256 / CP;
-  size_t fixed = Carve<CP, DM>::floats_fixed();
-  int gpb = R >= p->n_agents ? R / p->n_agents : 1;
-  size_t per_graph = bwd && p->dx ? (size_t)p->N * p->D : 0;
-  while (gpb > 1 && (fixed + gpb * per_graph) * sizeof(float) > 64 * 1024) --gpb;
-  const size_t bytes = (fixed + gpb * per_graph) * sizeof(float);
-  if (bytes > 160 * 1024) return DGPPO_EINVAL;
-  if (bytes > 64 * 1024) {  // once per instantiation: allow up to the CU's 160 KB
+  Plan pl{CP, DM, 1, 0, 0, 0};
+  const size_t fixed = bwd ? BwdCarve<CP, DM>::floats_fixed(cand_rows(p->C, CP), p->n_agents)
+                           : Carve<CP, DM>::floats_fixed(cand_rows(p->C, CP), false);
+  pl.gpb = R >= p->n_agents ? R / p->n_agents : 1;
+  const bool agent_mode = p->xa != nullptr;
+  const bool dx = bwd && (agent_mode ? p->dxa != nullptr : p->dx != nullptr);
+  const size_t per_graph = dx && !agent_mode ? (size_t)p->N * p->D : 0;
+  while (pl.gpb > 1 && (fixed + pl.gpb * per_graph) * sizeof(float) > 64 * 1024) --pl.gpb;
+  pl.bytes = (fixed + pl.gpb * per_graph) * sizeof(float);
+  pl.nblk = (p->G + pl.gpb - 1) / pl.gpb;
+  pl.grid = pl.nblk < kMaxBlocks ? pl.nblk : kMaxBlocks;
+  return pl;
+}
+
+template <int DM>
+Plan plan_cp(const dgppo_gnn_attn_args* p, bool bwd) {
+  switch (pick_cp(p->C)) {
+    case 8: return plan_t<8, DM>(p, bwd);
+    case 16: return plan_t<16, DM>(p, bwd);
+    case 32: return plan_t<32, DM>(p, bwd);
+    case 64: return plan_t<64, DM>(p, bwd);
+    default: return plan_t<128, DM>(p, bwd);
+  }
+}
+
+Plan make_plan(const dgppo_gnn_attn_args* p, bool bwd) {
+  if (p->D <= 8) return plan_cp<8>(p, bwd);
+  if (p->D <= 32) return plan_cp<32>(p, bwd);
+  return plan_cp<64>(p, bwd);
+}
+
+template <int CP, int DM>
+void launch_t(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream_t s) {
+  if (pl.bytes > 64 * 1024) {  // once per instantiation: allow up to the CU's 160 KB
     static bool raised[2] = {false, false};
     if (!raised[bwd]) {
       (void)hipFuncSetAttribute(bwd ? (const void*)attn_bwd_kernel<CP, DM> : (const void*)attn_fwd_kernel<CP, DM>,
@@ -328,50 +572,74 @@ int launch(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
       raised[bwd] = true;
     }
   }
-  const int blocks = (int)((p->G + gpb - 1) / gpb);
   if (bwd)
-    hipLaunchKernelGGL((attn_bwd_kernel<CP, DM>), dim3(blocks), dim3(256), bytes, s, *p, gpb);
+    hipLaunchKernelGGL((attn_bwd_kernel<CP, DM>), dim3((unsigned)pl.grid), dim3(256), pl.bytes, s, *p, pl.gpb,
+                       pl.nblk);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<CP, DM>), dim3(blocks), dim3(256), bytes, s, *p, gpb);
-  return 0;
+    hipLaunchKernelGGL((attn_fwd_kernel<CP, DM>), dim3((unsigned)pl.grid), dim3(256), pl.bytes, s, *p, pl.gpb,
+                       pl.nblk);
 }
 
 template <int DM>
-int launch_cp(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
-  switch (pick_cp(p->C)) {
-    case 8: return launch<8, DM>(p, bwd, s);
-    case 16: return launch<16, DM>(p, bwd, s);
-    case 32: return launch<32, DM>(p, bwd, s);
-    case 64: return launch<64, DM>(p, bwd, s);
-    case 128: return launch<128, DM>(p, bwd, s);
+void launch_cp(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream_t s) {
+  switch (pl.cp) {
+    case 8: launch_t<8, DM>(p, pl, bwd, s); break;
+    case 16: launch_t<16, DM>(p, pl, bwd, s); break;
+    case 32: launch_t<32, DM>(p, pl, bwd, s); break;
+    case 64: launch_t<64, DM>(p, pl, bwd, s); break;
+    default: launch_t<128, DM>(p, pl, bwd, s); break;
   }
-  return DGPPO_EINVAL;
 }
 
-int dispatch(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
-  if (p->D <= 8) return launch_cp<8>(p, bwd, s);
-  if (p->D <= 32) return launch_cp<32>(p, bwd, s);
-  return launch_cp<64>(p, bwd, s);
+int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
+  const Plan pl = make_plan(p, bwd);
+  if (pl.bytes > 160 * 1024) return DGPPO_EINVAL;
+  if (pl.dm == 8) launch_cp<8>(p, pl, bwd, s);
+  else if (pl.dm == 32) launch_cp<32>(p, pl, bwd, s);
+  else launch_cp<64>(p, pl, bwd, s);
+  return 0;
+}
+
+bool valid(const dgppo_gnn_attn_args* p) {
+  if (!p || p->H < 1 || p->H > kH || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > 128 ||
+      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->q || !p->bk || !p->cand || !p->receivers || !p->senders)
+    return false;
+  if (p->xa && (p->D0 < 1 || p->D0 > kD0 || (!p->pre_W && p->D0 != p->D) || (p->pre_W && !p->pre_b)))
+    return false;
+  return true;
 }
 
 }  // namespace
 }  // namespace dgppo
 
+extern "C" int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, int32_t E, const int32_t* cand,
+                                      const int32_t* receivers, const int32_t* senders, int32_t* sidx,
+                                      void* stream) {
+  if (G < 0 || n_agents < 1 || C < 1 || E < 1 || !cand || !receivers || !senders || !sidx) return DGPPO_EINVAL;
+  const int64_t total = (int64_t)G * n_agents * C;
+  if (total == 0) return 0;
+  int64_t nb = (total + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(dgppo::sender_table_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, G, n_agents,
+                     C, E, cand, receivers, senders, sidx);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* p) {
+  if (!dgppo::valid(p)) return 0;
+  return dgppo::make_plan(p, true).grid;
+}
+
 extern "C" int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* p, void* stream) {
-  if (!p || p->H < 1 || p->H > 3 || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > 128 ||
-      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->q || !p->bk || !p->xcat || !p->cand)
-    return DGPPO_EINVAL;
+  if (!dgppo::valid(p) || !p->xcat) return DGPPO_EINVAL;
   if (p->G == 0) return 0;
-  if (dgppo::dispatch(p, false, (hipStream_t)stream)) return DGPPO_EINVAL;
+  if (dgppo::run(p, false, (hipStream_t)stream)) return DGPPO_EINVAL;
   return (int)hipGetLastError();
 }
 
 extern "C" int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* p, void* stream) {
-  if (!p || p->H < 1 || p->H > 3 || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > 128 ||
-      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->attn || !p->dxcat || !p->dqt || !p->dq || !p->dbeta ||
-      !p->cand)
-    return DGPPO_EINVAL;
+  if (!dgppo::valid(p) || !p->attn || !p->dxcat || !p->dqt || !p->dq || !p->dbeta) return DGPPO_EINVAL;
   if (p->G == 0) return 0;
-  if (dgppo::dispatch(p, true, (hipStream_t)stream)) return DGPPO_EINVAL;
+  if (dgppo::run(p, true, (hipStream_t)stream)) return DGPPO_EINVAL;
   return (int)hipGetLastError();
 }

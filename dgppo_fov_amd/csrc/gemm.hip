@@ -192,15 +192,34 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
   const int b = blockIdx.z;
   const float* A = p.A + (int64_t)b * p.stride_a;
   const float* B = p.B + (int64_t)b * p.stride_b;
-  // stage op(B) (K x N) into LDS, zero-padded to 32 NT columns and 2 Kh rows
-  for (int e = threadIdx.x; e < 2 * Kh * 32 * NT; e += 256) {
-    int k, n;
-    if (p.trans_b) { k = e % (2 * Kh); n = e / (2 * Kh); }  // stored (N, K): k fastest
-    else { n = e % (32 * NT); k = e / (32 * NT); }         // stored (K, N): n fastest
-    float v = 0.0f;
-    if (k < K && n < N)
-      v = p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k] : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n];
-    Bs[k * NP + n] = v;
+  // stage op(B) (K x N) into LDS, zero-padded to 32 NT columns and 2 Kh rows; 16 independent loads
+  // in flight per thread before their stores (one L2 round trip per 4096 elements, not per 256)
+  {
+    const int total = 2 * Kh * 32 * NT;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = e0 + u * 256;
+        int k, n;
+        if (p.trans_b) { k = e % (2 * Kh); n = e / (2 * Kh); }  // stored (N, K): k fastest
+        else { n = e % (32 * NT); k = e / (32 * NT); }         // stored (K, N): n fastest
+        v[u] = (e < total && k < K && n < N)
+                   ? (p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k]
+                                : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n])
+                   : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = e0 + u * 256;
+        if (e < total) {
+          int k, n;
+          if (p.trans_b) { k = e % (2 * Kh); n = e / (2 * Kh); }
+          else { n = e % (32 * NT); k = e / (32 * NT); }
+          Bs[k * NP + n] = v[u];
+        }
+      }
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -393,17 +412,29 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
   }
 }
 
+// chunk partials -> C / bias_grad: 32 output elements per block, 8 chunk subsets each (coalesced
+// over elements), combined in LDS in fixed order
 __global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int chunks) {
+  __shared__ float red[8][33];
   const int64_t MN = (int64_t)p.M * p.N;
   const int64_t slab = MN + p.N;
   const int64_t total = slab * p.batch;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
-    const int b = (int)(t / slab);
-    const int64_t e = t - (int64_t)b * slab;
-    if (e >= MN && !p.bias_grad) continue;
+  const int j = threadIdx.x >> 5;
+  const int64_t t = (int64_t)blockIdx.x * 32 + (threadIdx.x & 31);
+  const int b = (int)(t / slab);
+  const int64_t e = t - (int64_t)b * slab;
+  const bool ok = t < total && (e < MN || p.bias_grad);
+  float s = 0.0f;
+  if (ok) {
     const float* W = p.workspace + (int64_t)b * chunks * slab + e;
-    float s = 0.0f;
-    for (int q = 0; q < chunks; ++q) s += W[(int64_t)q * slab];
+#pragma unroll 8
+    for (int q = j; q < chunks; q += 8) s += W[(int64_t)q * slab];
+  }
+  red[j][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (j == 0 && ok) {
+    const int l = threadIdx.x;
+    const float v = ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l])) + ((red[4][l] + red[5][l]) + (red[6][l] + red[7][l]));
     float* dst;
     if (e < MN) {
       const int row = (int)(e / p.N), col = (int)(e - (int64_t)row * p.N);
@@ -411,7 +442,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int 
     } else {
       dst = p.bias_grad + (int64_t)b * p.N + (e - MN);
     }
-    *dst = p.alpha * s + (p.beta != 0.0f ? p.beta * *dst : 0.0f);
+    *dst = p.alpha * v + (p.beta != 0.0f ? p.beta * *dst : 0.0f);
   }
 }
 
@@ -464,9 +495,7 @@ int launch_wgrad(const dgppo_gemm_args* p, hipStream_t s) {
 launched:
   if (chunks > 1) {
     const int64_t total = ((int64_t)p->M * p->N + p->N) * p->batch;
-    int64_t nb = (total + 255) / 256;
-    if (nb > 2048) nb = 2048;
-    hipLaunchKernelGGL(dgppo::gemm_wgrad_reduce, dim3((int)nb), dim3(256), 0, s, *p, chunks);
+    hipLaunchKernelGGL(dgppo::gemm_wgrad_reduce, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s, *p, chunks);
   }
   return 0;
 }

@@ -47,21 +47,59 @@ __device__ __forceinline__ void gh_tiles(const float* A, const float* Whs, int c
 
 __device__ __forceinline__ int tile_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// Wh (64 x 192 row-major) -> LDS [k][kWP]: float4 loads, 8 in flight per thread
+__device__ __forceinline__ void stage_wh(const float* Wh, float* Whs) {
+  constexpr int n4 = kHid * kG3 / 4;
+  if (((uintptr_t)Wh & 15) != 0) {  // unaligned view: scalar loads, 8 in flight
+    for (int e0 = threadIdx.x; e0 < kHid * kG3; e0 += 128 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = e0 + u * 128 < kHid * kG3 ? Wh[e0 + u * 128] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 128;
+        if (e < kHid * kG3) Whs[(e / kG3) * kWP + (e % kG3)] = v[u];
+      }
+    }
+    return;
+  }
+  for (int e0 = threadIdx.x; e0 < n4; e0 += 128 * 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * 128;
+      v[u] = e < n4 ? ((const float4*)Wh)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * 128;
+      if (e < n4) {
+        const int k = (4 * e) / kG3, c = (4 * e) % kG3;
+        float* d = Whs + k * kWP + c;
+        d[0] = v[u].x, d[1] = v[u].y, d[2] = v[u].z, d[3] = v[u].w;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(128) void gru_seq_fwd_kernel(dgppo_gru_seq_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* Whs = lds;                   // [64][kWP]
   float* hb = Whs + kHid * kWP;       // [2][32][kHP]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int q0 = blockIdx.x * kRows;
   const int Q = p.Q, L = p.L, n = p.n_agents;
-  for (int e = tid; e < kHid * kG3; e += 128) Whs[(e / kG3) * kWP + (e % kG3)] = p.Wh[e];
+  const int nblk = (Q + kRows - 1) / kRows;
+  stage_wh(p.Wh, Whs);
+  const int col = w * 32 + (lane & 31);
+  const float bn = p.bhn[col];
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // persistent: Wh staged once
+  const int q0 = blk * kRows;
+  __syncthreads();
   for (int e = tid; e < kRows * kHid; e += 128) {
     const int r = e / kHid, k = e % kHid, q = q0 + r;
     hb[r * kHP + k] = (q < Q && p.h0) ? p.h0[(int64_t)q * kHid + k] : 0.0f;
   }
   __syncthreads();
-  const int col = w * 32 + (lane & 31);
-  const float bn = p.bhn[col];
   for (int t = 0; t < L; ++t) {
     const float* hcur = hb + (t & 1) * kRows * kHP;
     float* hnext = hb + ((t + 1) & 1) * kRows * kHP;
@@ -85,6 +123,7 @@ __global__ __launch_bounds__(128) void gru_seq_fwd_kernel(dgppo_gru_seq_args p) 
     }
     __syncthreads();
   }
+  }
 }
 
 __global__ __launch_bounds__(128) void gru_seq_bwd_kernel(dgppo_gru_seq_args p) {
@@ -95,15 +134,17 @@ __global__ __launch_bounds__(128) void gru_seq_bwd_kernel(dgppo_gru_seq_args p) 
   float* red = dg + kRows * kWP;    // [2][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, hh = lane >> 5;
-  const int q0 = blockIdx.x * kRows;
   const int Q = p.Q, L = p.L, n = p.n_agents;
-  for (int e = tid; e < kHid * kG3; e += 128) Whs[(e / kG3) * kWP + (e % kG3)] = p.Wh[e];
+  const int nblk = (Q + kRows - 1) / kRows;
+  stage_wh(p.Wh, Whs);
   const int col = w * 32 + i;
   const float bn = p.bhn[col];
+  float dbn = 0.0f;
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // persistent: Wh staged once
+  const int q0 = blk * kRows;
   float dh[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) dh[r] = 0.0f;
-  float dbn = 0.0f;
   for (int t = L - 1; t >= 0; --t) {
     __syncthreads();  // previous step's readers of hp / dg are done
     for (int e = tid; e < kRows * kHid; e += 128) {
@@ -174,6 +215,7 @@ __global__ __launch_bounds__(128) void gru_seq_bwd_kernel(dgppo_gru_seq_args p) 
       if (q < Q) p.dh0[(int64_t)q * kHid + col] = dh[r];
     }
   }
+  }
   if (p.dbhn_part) {
     red[hh * kHid + col] = dbn;
     __syncthreads();
@@ -187,7 +229,11 @@ size_t bwd_lds() { return (size_t)(kHid * kWP + kRows * kHP + kRows * kWP + 2 * 
 }  // namespace
 }  // namespace dgppo
 
-extern "C" int64_t dgppo_gru_seq_blocks(int32_t Q) { return (Q + dgppo::kRows - 1) / dgppo::kRows; }
+// persistent grid: at most 512 workgroups (2 per CU), each looping over 32-row blocks
+extern "C" int64_t dgppo_gru_seq_blocks(int32_t Q) {
+  const int64_t nb = (Q + dgppo::kRows - 1) / dgppo::kRows;
+  return nb < 512 ? nb : 512;
+}
 
 extern "C" int dgppo_gru_seq_fwd(const dgppo_gru_seq_args* p, void* stream) {
   if (!p || p->Q < 0 || p->L < 1 || p->n_agents < 1 || p->H != dgppo::kHid || !p->gi || !p->Wh || !p->bhn || !p->hs ||

@@ -140,6 +140,15 @@ def gnn_attn(args: _lib.GnnAttnArgs, backward: bool, device):
     _chk(fn(ctypes.byref(args), _lib.stream_handle(device)), "dgppo_gnn_attn")
 
 
+def sender_table(G, n, C, E, cand, receivers, senders, out):
+    _chk(_lib.load().dgppo_gnn_sender_table(int(G), int(n), int(C), int(E), _p(cand), _p(receivers), _p(senders),
+                                            _p(out), _stream(out)), "dgppo_gnn_sender_table")
+
+
+def gnn_attn_partial_blocks(args: _lib.GnnAttnArgs) -> int:
+    return int(_lib.load().dgppo_gnn_attn_partial_blocks(ctypes.byref(args)))
+
+
 def tanh_normal(args: _lib.TanhNormalArgs, device):
     _chk(_lib.load().dgppo_tanh_normal(ctypes.byref(args), _lib.stream_handle(device)), "dgppo_tanh_normal")
 

@@ -31,7 +31,9 @@ from . import kernels as K
 
 # ---- parameter space ------------------------------------------------------------------------
 class ParamSpace:
-    """Flat parameter + gradient buffers with named views."""
+    """Flat parameter + gradient buffers with named views.  Every entry starts on a 16-byte boundary
+    (the kernels stage weights with 16-byte loads); the padding floats stay zero (zero gradient,
+    zero Adam update)."""
 
     def __init__(self):
         self.entries: List[Tuple[str, Tuple[int, ...], str]] = []
@@ -45,7 +47,7 @@ class ParamSpace:
         assert name not in self.offsets, name
         self.offsets[name] = self.size
         self.entries.append((name, shape, init))
-        self.size += int(np.prod(shape))
+        self.size = (self.size + int(np.prod(shape)) + 3) & ~3
         return name
 
     def build(self, device):
@@ -358,88 +360,102 @@ class GraphTransformer:
              "Dense_4": {"kernel": orthogonal(rng, (D, F)), "bias": np.zeros(F, np.float32)}}
         self.load_flax(d)
 
-    def _attn_args(self, X, g: "GraphBatch"):
+    def _attn_args(self, g: "GraphBatch", xa=None, pre=None):
         a = K._lib.GnnAttnArgs()
-        G, N, D = X.shape
+        G, N, D0 = g.nodes.shape
         a.G, a.N, a.E, a.n_agents = G, N, g.E, g.n
-        a.D, a.F, a.H, a.C = D, self.F, self.H, g.C
+        a.D, a.F, a.H, a.C = self.D, self.F, self.H, g.C
         a.cand, a.receivers, a.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
-        a.x, a.x_gstride = K._p(X), N * D
+        a.sidx = K._p(g.sidx)
+        a.x, a.x_gstride = K._p(g.nodes), N * D0
         a.ef, a.ef_gstride = K._p(g.edges), g.E * 4
         a.bk = K._p(self.v("bk"))
         a.scale = 1.0 / math.sqrt(self.F)
+        if xa is not None:  # agent mode: agents from xa, other senders = pre's Dense_4 + ReLU of raw rows
+            a.D0 = D0
+            a.xa, a.xa_gstride = K._p(xa), g.n * self.D
+            if pre is not None:
+                a.pre_W, a.pre_b = K._p(pre.v("Wu")), K._p(pre.v("bu"))
         return a
 
-    def fwd(self, X, g: "GraphBatch", last: bool):
-        """X (G, N, D) contiguous -> Y: (G*n, F) agent rows if last else (G, N, F)."""
-        G, N, D = X.shape
-        n, F, H, C = g.n, self.F, self.H, g.C
-        dev = X.device
+    def fwd(self, g: "GraphBatch", xa=None, pre=None):
+        """One layer on the graph batch.  xa None: senders read the raw nodes (G, N, D) (first layer);
+        else xa (G*n, D) holds the agents' rows and the never-receiving nodes are `pre`'s
+        Dense_4 + ReLU of their raw rows (agent mode).  Returns Y (G*n, F) = the agents' outputs
+        (only agents receive, so only their rows feed the next layer's queries) and the cache."""
+        G, N, n = g.G, g.N, g.n
+        D, F, H, C = self.D, self.F, self.H, g.C
+        dev = g.nodes.device
         R = G * n
+        A, akw = (g.nodes, dict(lda=D, a_grp=n, a_gs=N * D)) if xa is None else (xa, dict(lda=D))
         Q = torch.empty((R, H * F), device=dev)
-        K.gemm(X, self.v("Wq"), Q, R, H * F, D, lda=D, a_grp=n, a_gs=N * D, bias=self.v("bq"))
+        K.gemm(A, self.v("Wq"), Q, R, H * F, D, bias=self.v("bq"), **akw)
         QT = torch.empty((R, H * D), device=dev)
         K.gemm(Q, self.v("Wkt"), QT, R, D, F, lda=H * F, sa=F, ldb=D, sb=F * D, ldc=H * D, sc=D, batch=H)
         attn = torch.empty((R, H, C), device=dev)
         xcat = torch.empty((R, H * (D + 5)), device=dev)
-        a = self._attn_args(X, g)
+        a = self._attn_args(g, xa, pre)
         a.q, a.qt, a.attn, a.xcat = K._p(Q), K._p(QT), K._p(attn), K._p(xcat)
         K.gnn_attn(a, False, dev)
         M = torch.empty((R, F), device=dev)
         K.gemm(xcat, self.v("Wcat"), M, R, F, H * (D + 5), alpha=1.0 / H)
-        if last:
-            Y = torch.empty((R, F), device=dev)
-            K.gemm(X, self.v("Wu"), Y, R, F, D, lda=D, a_grp=n, a_gs=N * D, bias=self.v("bu"), addend=M, relu=True)
-        else:
-            Y = torch.empty((G, N, F), device=dev)
-            K.gemm(X, self.v("Wu"), Y, R, F, D, lda=D, a_grp=n, a_gs=N * D, c_grp=n, c_gs=N * F,
-                   bias=self.v("bu"), addend=M, relu=True)
-            K.gemm(X, self.v("Wu"), Y, G * (N - n), F, D, lda=D, a_off=n * D, a_grp=N - n, a_gs=N * D,
-                   c_off=n * F, c_grp=N - n, c_gs=N * F, bias=self.v("bu"), relu=True)
-        return Y, (X, Q, QT, attn, xcat, Y, last)
+        Y = torch.empty((R, F), device=dev)
+        K.gemm(A, self.v("Wu"), Y, R, F, D, bias=self.v("bu"), addend=M, relu=True, **akw)
+        return Y, (xa, pre, Q, QT, attn, xcat, Y)
 
-    def bwd(self, cache, dY, g: "GraphBatch", need_dx: bool):
-        X, Q, QT, attn, xcat, Y, last = cache
-        G, N, D = X.shape
-        n, F, H = g.n, self.F, self.H
+    def bwd(self, cache, dY, g: "GraphBatch"):
+        """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, else None;
+        accumulates this layer's grads and, in agent mode with `pre`, pre's Dense_4 grads from the
+        transformed senders."""
+        xa, pre, Q, QT, attn, xcat, Y = cache
+        G, N, n = g.G, g.N, g.n
+        D, F, H = self.D, self.F, self.H
         R = G * n
         W = H * (D + 5)
-        dev = X.device
+        dev = dY.device
+        A, akw = (g.nodes, dict(lda=D, a_grp=n, a_gs=N * D)) if xa is None else (xa, dict(lda=D))
         K.relu_bwd_(dY, Y)  # dY := dZ
-        za = dict(lda=F) if last else dict(lda=F, a_grp=n, a_gs=N * F)
-        zb = dict(ldb=F) if last else dict(ldb=F, b_grp=n, b_gs=N * F)
         dxcat = torch.empty((R, W), device=dev)
-        K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H, **za)
-        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0, **zb)
+        K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
+        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)
         dQT = torch.empty((R, H * D), device=dev)
         dQ = torch.empty((R, H * F), device=dev)
         dbeta = torch.empty((R, H), device=dev)
-        dX = torch.zeros((G, N, D), device=dev) if need_dx else None
-        a = self._attn_args(X, g)
+        dXa = torch.zeros((R, D), device=dev) if xa is not None else None
+        a = self._attn_args(g, xa, pre)
         a.q, a.qt, a.attn = K._p(Q), K._p(QT), K._p(attn)
         a.dxcat, a.dqt, a.dq, a.dbeta = K._p(dxcat), K._p(dQT), K._p(dQ), K._p(dbeta)
-        a.dx, a.dx_gstride = K._p(dX), N * D
+        part = None
+        if xa is not None:
+            a.dxa, a.dxa_gstride = K._p(dXa), n * D
+            if pre is not None:
+                nb = K.gnn_attn_partial_blocks(a)
+                PK = a.D0 * D + D
+                part = K.workspace(nb * PK, dev, "attn_pre")
+                a.dpre_part = K._p(part)
         K.gnn_attn(a, True, dev)
+        if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre
+            ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
+            nw = a.D0 * D
+            if ob == ow + nw:
+                K.colsum(part, nb, PK, pre.ps.grad[ow:ow + PK], beta=1.0)
+            else:
+                tmp = torch.empty(PK, device=dev)
+                K.colsum(part, nb, PK, tmp)
+                pre.ps.grad[ow:ow + nw].add_(tmp[:nw])
+                pre.ps.grad[ob:ob + D].add_(tmp[nw:])
         K.gemm(dbeta, Q, self.v("bk", True), 1, F, R, ta=True, lda=H, sa=1, ldb=H * F, sb=F, ldc=F, sc=F,
                batch=H, beta=1.0)
         K.gemm(Q, dQT, self.v("Wkt", True), F, D, R, ta=True, lda=H * F, sa=F, ldb=H * D, sb=D, ldc=D, sc=F * D,
                batch=H, beta=1.0)
         K.gemm(dQT, self.v("Wkt"), dQ, R, F, D, lda=H * D, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
                batch=H, beta=1.0)
-        K.gemm(X, dQ, self.v("Wq", True), D, H * F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0,
-               bias_grad=self.v("bq", True))
-        if last:
-            K.gemm(X, dY, self.v("Wu", True), D, F, R, ta=True, lda=D, a_grp=n, a_gs=N * D, beta=1.0,
-                   bias_grad=self.v("bu", True))
-        else:
-            K.gemm(X, dY, self.v("Wu", True), D, F, G * N, ta=True, lda=D, beta=1.0, bias_grad=self.v("bu", True))
-        if need_dx:
-            if last:
-                K.gemm(dY, self.v("Wu"), dX, R, D, F, tb=True, ldb=F, c_grp=n, c_gs=N * D, ldc=D, beta=1.0)
-            else:
-                K.gemm(dY, self.v("Wu"), dX, G * N, D, F, tb=True, ldb=F, ldc=D, beta=1.0)
-            K.gemm(dQ, self.v("Wq"), dX, R, D, H * F, tb=True, ldb=H * F, c_grp=n, c_gs=N * D, ldc=D, beta=1.0)
-        return dX
+        K.gemm(A, dQ, self.v("Wq", True), D, H * F, R, ta=True, beta=1.0, bias_grad=self.v("bq", True), **akw)
+        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
+        if dXa is not None:
+            K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
+            K.gemm(dQ, self.v("Wq"), dXa, R, D, H * F, tb=True, ldb=H * F, beta=1.0)
+        return dXa
 
 
 class GraphBatch:
@@ -465,6 +481,16 @@ class GraphBatch:
         self.n = int(n_agents)
         self.cand = cand
         self.C = int(cand.shape[1])
+        self._sidx = None
+
+    @property
+    def sidx(self) -> torch.Tensor:
+        """(G*n, C) resolved sender of every candidate edge (-1 if masked), built once per batch and
+        shared by every attention launch on it."""
+        if self._sidx is None:
+            self._sidx = torch.empty((self.G * self.n, self.C), dtype=torch.int32, device=self.nodes.device)
+            K.sender_table(self.G, self.n, self.C, self.E, self.cand, self.receivers, self.senders, self._sidx)
+        return self._sidx
 
 
 class GNN:
@@ -472,6 +498,9 @@ class GNN:
     type_nodes(agent): returns the agent rows of the last layer, (G*n, out_dim)."""
 
     def __init__(self, ps, name, node_dim, n_layers, msg_dim=32, out_dim=64, n_heads=3):
+        if not 1 <= n_layers <= 2:
+            raise NotImplementedError("GNN depth 1 or 2 (the reference's actor/Vl/Vh configs): deeper stacks need "
+                                      "the never-receiving nodes' hidden features materialised")
         self.layers = []
         d = node_dim
         for i in range(n_layers):
@@ -491,14 +520,14 @@ class GNN:
             L.load_flax(d)
 
     def fwd(self, g: GraphBatch):
-        X = g.nodes
         caches = []
+        Y = None
         for i, L in enumerate(self.layers):
-            X, c = L.fwd(X, g, i == len(self.layers) - 1)
+            Y, c = L.fwd(g) if i == 0 else L.fwd(g, xa=Y, pre=self.layers[0])
             caches.append(c)
-        return X, caches
+        return Y, caches
 
     def bwd(self, caches, dZ, g: GraphBatch):
         d = dZ
         for i in range(len(self.layers) - 1, -1, -1):
-            d = self.layers[i].bwd(caches[i], d, g, need_dx=i > 0)
+            d = self.layers[i].bwd(caches[i], d, g)

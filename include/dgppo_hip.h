@@ -167,16 +167,24 @@ int dgppo_gemm(const dgppo_gemm_args* args, void* stream);
 /* GraphTransformer attention core (dgppo/nn/gnn.py:78-117 + jraph.segment_softmax/segment_sum),
  * per RECEIVING AGENT: only agents receive messages in the DGPPO env graphs, so with
  * qt_h = Wk_h q_h the logits are (qt_h . x_s + q_h . bk_h) / sqrt(F) and the aggregated message is
- * xbar_h Wv_h + sig_h bv_h + ebar_h We_h (see csrc/nn.hip).  fwd writes attn (G*n, H, C) and
+ * xbar_h Wv_h + sig_h bv_h + ebar_h We_h (see csrc/attn.hip).  fwd writes attn (G*n, H, C) and
  * xcat (G*n, H*(D+5)) = [xbar (H*D) | ebar (H*4) | sig (H)]; bwd consumes dxcat and writes dqt,
- * dq (= dbeta_h * bk_h), dbeta and ACCUMULATES sender-node gradients into dx (optional).
- * cand (n, C): edge ids that may target agent i (checked against receivers at run time). */
+ * dq (= dbeta_h * bk_h), dbeta and the sender gradients.
+ * cand (n, C): edge ids that may target agent i (checked against receivers at run time).
+ * Sender features, two modes:
+ *   full  (xa == NULL): x (G, N, D) holds every node's features; bwd ACCUMULATES dx (G, N, D).
+ *   agent (xa != NULL): agent senders (node < n) read xa (G, n, D); other senders are nodes that
+ *         never receive, so their features are a function of their raw row x (G, N, D0):
+ *         relu(x pre_W + pre_b) (the previous layer's Dense_4 with an empty aggregation), or x
+ *         itself when pre_W == NULL (D0 == D).  bwd ACCUMULATES dxa (G, n, D) and writes per-block
+ *         partial gradients of [pre_W (D0*D) | pre_b (D)] into dpre_part
+ *         (dgppo_gnn_attn_partial_blocks rows; reduce with dgppo_colsum). */
 typedef struct dgppo_gnn_attn_args {
   int32_t G, N, E, n_agents, D, F, H, C;
   const int32_t* cand;
   const int32_t* receivers;
   const int32_t* senders;     /* (G, E) */
-  const float* x; int64_t x_gstride;   /* node features (G, N, D) */
+  const float* x; int64_t x_gstride;   /* node features (G, N, D) [full] / raw (G, N, D0) [agent mode] */
   const float* ef; int64_t ef_gstride; /* edge features (G, E, 4) */
   const float* q;   /* (G*n, H*F) */
   const float* qt;  /* (G*n, H*D) */
@@ -189,8 +197,19 @@ typedef struct dgppo_gnn_attn_args {
   float* dbeta;     /* (G*n, H) */
   float* dx; int64_t dx_gstride;
   float scale;      /* 1/sqrt(F) */
+  int32_t D0;       /* raw feature width (agent mode) */
+  const float* xa; int64_t xa_gstride;  /* agent-mode agent rows (G, n, D) */
+  const float* pre_W; const float* pre_b;
+  float* dxa; int64_t dxa_gstride;
+  float* dpre_part;
+  const int32_t* sidx;  /* optional (G*n, C) sender table from dgppo_gnn_sender_table (else resolved per use) */
 } dgppo_gnn_attn_args;
 
+int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
+/* sidx[(g*n + i)*C + c] = senders[g][cand[i][c]] if that edge's receiver is i, else -1: the
+ * candidate resolution shared by every attention launch on one graph batch */
+int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, int32_t E, const int32_t* cand,
+                           const int32_t* receivers, const int32_t* senders, int32_t* sidx, void* stream);
 int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* args, void* stream);
 int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* args, void* stream);
 
