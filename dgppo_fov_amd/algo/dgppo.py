@@ -31,6 +31,32 @@ from ..trainer.rollout import RolloutEngine
 from .module.nets import ActorNet, VhNet, VlNet
 
 
+class _Phases:
+    """Host wall-clock per update phase (synchronising) when DGPPO_PROFILE=1; no-op otherwise."""
+
+    def __init__(self, device):
+        self.on = os.environ.get("DGPPO_PROFILE", "0") == "1"
+        self.device = device
+        self.acc = {}
+        self.t = None
+
+    def mark(self, name=None):
+        if not self.on:
+            return
+        import time
+        torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        if name is not None and self.t is not None:
+            self.acc[name] = self.acc.get(name, 0.0) + now - self.t
+        self.t = now
+
+    def report(self):
+        if self.on and self.acc:
+            tot = sum(self.acc.values())
+            print("DGPPO update phases (ms): " + ", ".join(f"{k} {1e3 * v:.1f}" for k, v in self.acc.items()) +
+                  f" | total {1e3 * tot:.1f}", flush=True)
+
+
 class _Opt:
     """optax.apply_if_finite(optax.adam(lr), 1e6) state + compute_norm_and_clip for one flat buffer."""
 
@@ -225,7 +251,10 @@ class DGPPO:
         env, dev = self._env, self.device
         B, T = rollout.rewards.shape
         n = self._n_agents
+        ph = _Phases(dev)
+        ph.mark()
         det = self.det_rollout(B, int(self.key.integers(0, 2 ** 62)))
+        ph.mark("det_rollout")
         assert B * T * self.world >= self.batch_size
         chunk = max(1, min(B, 65536 // T))
         info = {}
@@ -240,8 +269,10 @@ class DGPPO:
                 vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
                                            keep_cache=False)
                 Vl[e0:e1, T].copy_(vf[:, 0])
+            ph.mark("prepass_Vl")
             Vh = self._vh_all(rollout, chunk)
             Vh_det = self._vh_all(det, chunk)
+            ph.mark("prepass_Vh")
             # ---- GAE + advantages
             costs = rollout.costs.contiguous()
             l = (-rollout.rewards).contiguous()
@@ -255,6 +286,7 @@ class DGPPO:
             A = torch.empty((B, T, n), device=dev)
             safe_cnt = torch.empty(B, device=dev)
             K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, env.dt, self.alpha, self.cbf_eps, self.cbf_weight_at(step))
+            ph.mark("gae_adv")
             if self.trace is not None:
                 self.trace.update(det=det, Vl=Vl.clone(), Vh=Vh.clone(), Vh_det=Vh_det.clone(), Ql=Ql.clone(),
                                   Qh=Qh.clone(), Qh_det=Qh_det.clone(), A=A.clone(), safe_cnt=safe_cnt.clone(),
@@ -279,8 +311,10 @@ class DGPPO:
                 dv = torch.empty_like(v)
                 vl_loss = torch.empty(1, device=dev)
                 K.l2_loss(v, tgt, dv, vl_loss)
+                ph.mark("Vl_fwd")
                 self.Vl.seq_bwd(cache, dv)
                 del cache
+                ph.mark("Vl_bwd")
                 # update_Vh (dgppo.py:296-321) on the deterministic rollout
                 gd = self._graphs(det.graph, envs)
                 hd = det.rnn_states.index_select(0, envs).reshape(Bm * T * n, 64).contiguous()
@@ -288,8 +322,10 @@ class DGPPO:
                 dvh = torch.empty_like(vh)
                 vh_loss = torch.empty(1, device=dev)
                 K.l2_loss(vh, Qh_det.index_select(0, envs).reshape(-1, env.n_cost), dvh, vh_loss)
+                ph.mark("Vh_fwd")
                 self.Vh.bwd(cache, dvh)
                 del cache
+                ph.mark("Vh_bwd")
                 # update_policy (informarl.py:405-457)
                 acts = rollout.actions.index_select(0, envs).reshape(-1, self._action_dim).contiguous()
                 lp_old = rollout.log_pis.index_select(0, envs).reshape(-1).contiguous()
@@ -299,8 +335,10 @@ class DGPPO:
                 dent = torch.empty_like(ent)
                 stats = torch.empty(4, device=dev)
                 K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, stats)
+                ph.mark("pi_fwd")
                 self.actor.eval_seq_bwd(cache, dlp, dent)
                 del cache
+                ph.mark("pi_bwd")
                 # one all-reduce for the three nets, then clip + finite check + Adam per net
                 self._allreduce_grads()
                 if self.trace is not None:
@@ -312,12 +350,14 @@ class DGPPO:
                         state_before={k: o.state.clone() for k, o in self.opt.items()}))
                 for name in ("Vl", "Vh", "policy"):
                     self.opt[name].step()
+                ph.mark("allreduce_adam")
                 info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
                         "Vh/loss_Vh": vh_loss, "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
             safe = safe_cnt.sum()
             if self.world > 1:
                 dist.all_reduce(safe)
             info["eval/safe_data"] = safe / (B * self.world * T * n)
+        ph.report()
         return self._finish_info(info)
 
     def _finish_info(self, info) -> dict:

@@ -238,11 +238,12 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-    for (int kb = 0; kb < Kh; kb += 8) {
-      float a[8];
+    // A values in chunks of 8 per lane, double-buffered: chunk j+1's loads are in flight while
+    // chunk j's MFMAs run
+    auto load8 = [&](int kb, float (&a)[8]) {
       if (VEC) {  // Kh % 8 == 0, rows 16-byte aligned
-        const float4 v0 = rok ? *(const float4*)(Ar + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 v1 = rok ? *(const float4*)(Ar + kb + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v0 = (rok && kb < Kh) ? *(const float4*)(Ar + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v1 = (rok && kb < Kh) ? *(const float4*)(Ar + kb + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
         a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w;
         a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
       } else {
@@ -252,6 +253,8 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
           a[q] = (rok && kk < Kh && kofs + kk < K) ? Ar[kk] : 0.0f;
         }
       }
+    };
+    auto mma8 = [&](int kb, const float (&a)[8]) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int kk = kb + q;
@@ -260,6 +263,14 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], brow[32 * t], acc[t], 0, 0, 0);
       }
+    };
+    float a0[8], a1[8];
+    load8(0, a0);
+    for (int kb = 0; kb < Kh; kb += 8) {
+      load8(kb + 8, a1);  // zeros past Kh
+      mma8(kb, a0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a0[q] = a1[q];
     }
     // epilogue: lane holds column (t*32 + i), rows (r&3) + 8 (r>>2) + 4 h of this wave's 32
 #pragma unroll

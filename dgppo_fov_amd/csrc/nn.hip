@@ -33,6 +33,97 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 __device__ __forceinline__ float softplusf_(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
 
 // ---- LayerNorm (+ReLU) over rows of width F (flax LayerNorm, eps 1e-6, fast variance) --------
+// ---- F = 64 LayerNorm: 16 lanes x float4 per row, 16 rows per 256-thread block ----------------
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void layernorm64_fwd_kernel(const float* x, const float* scale, const float* bias,
+                                                              float* y, float* mean_out, float* rstd_out,
+                                                              int64_t rows, int relu, float eps) {
+  const int c4 = threadIdx.x & 15;
+  const float4 sc = ((const float4*)scale)[c4], bi = ((const float4*)bias)[c4];
+  for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += (int64_t)gridDim.x * 16) {
+    const float4 v = ((const float4*)(x + r * 64))[c4];
+    const float s = sum16((v.x + v.y) + (v.z + v.w));
+    const float s2 = sum16((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w));
+    const float mean = s / 64.0f;
+    float var = s2 / 64.0f - mean * mean;
+    var = var > 0.0f ? var : 0.0f;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    float4 o;
+    o.x = (v.x - mean) * rstd * sc.x + bi.x;
+    o.y = (v.y - mean) * rstd * sc.y + bi.y;
+    o.z = (v.z - mean) * rstd * sc.z + bi.z;
+    o.w = (v.w - mean) * rstd * sc.w + bi.w;
+    if (relu) {
+      o.x = o.x > 0.0f ? o.x : 0.0f, o.y = o.y > 0.0f ? o.y : 0.0f;
+      o.z = o.z > 0.0f ? o.z : 0.0f, o.w = o.w > 0.0f ? o.w : 0.0f;
+    }
+    ((float4*)(y + r * 64))[c4] = o;
+    if (c4 == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+  }
+}
+
+// dx (overwrite) and this block's partial [dscale (64) | dbias (64)] over rows [b*rpb, (b+1)*rpb)
+__global__ __launch_bounds__(256) void layernorm64_bwd_kernel(const float* x, const float* y, const float* dy,
+                                                              const float* scale, const float* mean_in,
+                                                              const float* rstd_in, float* dx, float* part,
+                                                              int64_t rows, int relu, int64_t rpb) {
+  __shared__ float red[16][2 * 64 + 4];
+  const int c4 = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const float4 sc = ((const float4*)scale)[c4];
+  float ds[4] = {0.0f, 0.0f, 0.0f, 0.0f}, db[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < rows ? r0 + rpb : rows;
+  for (int64_t r = r0 + rl; r < r1; r += 16) {
+    const float4 xv = ((const float4*)(x + r * 64))[c4];
+    float4 g = ((const float4*)(dy + r * 64))[c4];
+    if (relu) {
+      const float4 yv = ((const float4*)(y + r * 64))[c4];
+      g.x = yv.x > 0.0f ? g.x : 0.0f, g.y = yv.y > 0.0f ? g.y : 0.0f;
+      g.z = yv.z > 0.0f ? g.z : 0.0f, g.w = yv.w > 0.0f ? g.w : 0.0f;
+    }
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    const float xh[4] = {(xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd};
+    const float gg[4] = {g.x, g.y, g.z, g.w};
+    const float sv[4] = {sc.x, sc.y, sc.z, sc.w};
+    float s1 = 0.0f, s2 = 0.0f, gx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ds[j] += gg[j] * xh[j];
+      db[j] += gg[j];
+      gx[j] = gg[j] * sv[j];
+      s1 += gx[j];
+      s2 += gx[j] * xh[j];
+    }
+    s1 = sum16(s1) / 64.0f;
+    s2 = sum16(s2) / 64.0f;
+    float4 o;
+    o.x = rstd * (gx[0] - s1 - xh[0] * s2);
+    o.y = rstd * (gx[1] - s1 - xh[1] * s2);
+    o.z = rstd * (gx[2] - s1 - xh[2] * s2);
+    o.w = rstd * (gx[3] - s1 - xh[3] * s2);
+    ((float4*)(dx + r * 64))[c4] = o;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[rl][4 * c4 + j] = ds[j];
+    red[rl][64 + 4 * c4 + j] = db[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    float acc = 0.0f;
+    for (int q = 0; q < 16; ++q) acc += red[q][threadIdx.x];
+    part[(int64_t)blockIdx.x * 128 + threadIdx.x] = acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* x, const float* scale, const float* bias,
                                                             float* y, float* mean_out, float* rstd_out,
                                                             int64_t rows, int F, int relu, float eps) {
@@ -101,6 +192,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* x, cons
 }
 
 // ---- column sums (deterministic two-level) ----------------------------------------------------
+__host__ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 // Row partition shared by every two-level reduction: at most kMaxParts partial rows, each block
 // owning a contiguous run of >= min_rows rows.
 constexpr int kMaxParts = 512;
@@ -152,18 +245,22 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int
   }
 }
 
-// out[c] = alpha * sum_b part[b * pstride + c] + beta * out[c]; 64 columns x 4 phases per block
+// out[c] = alpha * sum_b part[b * pstride + c] + beta * out[c]; 16 columns x 16 phases per block
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nparts, int cols, int64_t pstride,
                                                            float* out, float alpha, float beta) {
-  __shared__ float red[256];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), j = threadIdx.x >> 6;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, j = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s = 0.0f;
-  if (c < cols)
-    for (int b = j; b < nparts; b += 4) s += part[(int64_t)b * pstride + c];
-  red[threadIdx.x] = s;
+  if (c < cols) {
+#pragma unroll 4
+    for (int b = j; b < nparts; b += 16) s += part[(int64_t)b * pstride + c];
+  }
+  red[j][cl] = s;
   __syncthreads();
-  if (threadIdx.x < 64 && c < cols) {
-    const float t = (red[threadIdx.x] + red[64 + threadIdx.x]) + (red[128 + threadIdx.x] + red[192 + threadIdx.x]);
+  if (threadIdx.x < 16 && c < cols) {
+    float t = 0.0f;
+    for (int q = 0; q < 16; ++q) t += red[q][cl];
     out[c] = alpha * t + (beta != 0.0f ? beta * out[c] : 0.0f);
   }
 }
@@ -623,6 +720,12 @@ extern "C" int dgppo_layernorm_fwd(const float* x, const float* scale, const flo
                                    float* rstd, int64_t rows, int32_t F, int32_t relu, float eps, void* stream) {
   if (rows < 0 || F < 1 || !x || !scale || !bias || !y || !mean || !rstd) return DGPPO_EINVAL;
   if (rows == 0) return 0;
+  if (F == 64 && aligned16(x) && aligned16(y) && aligned16(scale) && aligned16(bias)) {
+    const int64_t g = (rows + 15) / 16;
+    hipLaunchKernelGGL(layernorm64_fwd_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, DG_STREAM(stream),
+                       x, scale, bias, y, mean, rstd, rows, relu, eps);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, DG_STREAM(stream), x,
                      scale, bias, y, mean, rstd, rows, F, relu, eps);
   return (int)hipGetLastError();
@@ -640,11 +743,16 @@ extern "C" int dgppo_layernorm_bwd(const float* x, const float* y, const float* 
     return DGPPO_EINVAL;
   if (rows == 0) return 0;
   const RowSplit sp = row_split(rows, 64);
+  if (F == 64 && aligned16(x) && aligned16(dy) && aligned16(dx) && aligned16(scale) && (!relu || aligned16(y))) {
+    hipLaunchKernelGGL(layernorm64_bwd_kernel, dim3(sp.nb), dim3(256), 0, DG_STREAM(stream), x, y, dy, scale, mean,
+                       rstd, dx, workspace, rows, relu, sp.rpb);
+  } else {
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(sp.nb), dim3(256), 8 * F * sizeof(float), DG_STREAM(stream), x, y,
                      dy, scale, mean, rstd, dx, workspace, rows, F, relu, (int)sp.rpb);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((F + 63) / 64), dim3(256), 0, DG_STREAM(stream), workspace, sp.nb, F,
+  }
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((F + 15) / 16), dim3(256), 0, DG_STREAM(stream), workspace, sp.nb, F,
                      (int64_t)2 * F, dscale, 1.0f, 1.0f);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((F + 63) / 64), dim3(256), 0, DG_STREAM(stream), workspace + F, sp.nb,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((F + 15) / 16), dim3(256), 0, DG_STREAM(stream), workspace + F, sp.nb,
                      F, (int64_t)2 * F, dbias, 1.0f, 1.0f);
   return (int)hipGetLastError();
 }
@@ -662,7 +770,7 @@ extern "C" int dgppo_colsum(const float* x, int64_t rows, int32_t cols, int64_t 
   if (nb > 0)
     hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, DG_STREAM(stream), x, rows, cols, ld, grp,
                        gstride, workspace, sp.rpb);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64), dim3(256), 0, DG_STREAM(stream), workspace, nb,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 15) / 16), dim3(256), 0, DG_STREAM(stream), workspace, nb,
                      cols, (int64_t)cols, out, alpha, beta);
   return (int)hipGetLastError();
 }
