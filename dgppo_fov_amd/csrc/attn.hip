@@ -20,6 +20,7 @@
 // every reduction has a fixed order: bitwise-deterministic, no atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dgppo_hip.h"
 
@@ -266,13 +267,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(dgppo_gnn_attn_args p, in
           float acc = 0.0f;
           if (o < H * D) {
             const int h = o / D, d = o - h * D;
-            for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
+            #pragma unroll 8
+            for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
           } else if (o < H * D + 4 * H) {
             const int q = o - H * D, h = q >> 2, j = q & 3;
-            for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.ef[(base + cc) * 4 + j];
+            #pragma unroll 8
+            for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.ef[(base + cc) * 4 + j];
           } else {
             const int h = o - H * D - 4 * H;
-            for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h];
+            #pragma unroll 8
+            for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h];
           }
           out[o] = acc;
         }
@@ -435,7 +439,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
         for (int o = c; o < H * D; o += CP) {
           const int h = o / D, d = o - h * D;
           float acc = 0.0f;
-          for (int cc = 0; cc < C; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
+          #pragma unroll 8
+          for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
           p.dqt[row * H * D + o] = acc;
         }
       }
@@ -516,6 +521,428 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
   }
 }
 
+
+// ---- raw gather / transform split (wave kernels prefetch the next sub-round's raw rows) ----------
+typedef const __attribute__((address_space(4))) float* cfloat_p;  // uniform reads -> scalar loads
+
+template <int DM>
+struct Gath {
+  Cand k;
+  float x[DM];   // agent row / full-mode row (or transformed row after finish())
+  float x0[kD0]; // raw row of a transformed sender
+  float ef[4];
+  bool via_pre;
+};
+
+template <int DM>
+__device__ __forceinline__ void gath_load(const dgppo_gnn_attn_args& p, int64_t g, int i, int c, bool active, int D,
+                                          Gath<DM>& r) {
+  r.k = active ? candidate(p, g, i, c) : Cand{-1, -1};
+  const int s = r.k.s;
+  const bool ok = s >= 0;
+  r.via_pre = false;
+#pragma unroll
+  for (int k = 0; k < kD0; ++k) r.x0[k] = 0.0f;
+  if (p.xa == nullptr) {
+    load_row<DM>(p.x + g * p.x_gstride + (int64_t)(ok ? s : 0) * D, D, ok, r.x);
+  } else if (!ok || s < p.n_agents) {
+    load_row<DM>(p.xa + g * p.xa_gstride + (int64_t)(ok ? s : 0) * D, D, ok, r.x);
+  } else {
+    const float* xr = p.x + g * p.x_gstride + (int64_t)s * p.D0;
+#pragma unroll
+    for (int k = 0; k < kD0; ++k) r.x0[k] = k < p.D0 ? xr[k] : 0.0f;
+    r.via_pre = p.pre_W != nullptr;
+#pragma unroll
+    for (int d = 0; d < DM; ++d) r.x[d] = 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r.ef[j] = ok ? p.ef[g * p.ef_gstride + (int64_t)r.k.e * 4 + j] : 0.0f;
+}
+
+// non-agent senders of agent mode: relu(x0 pre_W + pre_b) (or the raw row itself without pre_W)
+template <int DM>
+__device__ __forceinline__ void gath_finish(const dgppo_gnn_attn_args& p, const float* preW, const float* preb,
+                                            Gath<DM>& r) {
+  if (p.xa == nullptr || r.k.s < p.n_agents) return;
+  if (!r.via_pre) {
+#pragma unroll
+    for (int d = 0; d < DM; ++d) r.x[d] = d < kD0 ? r.x0[d < kD0 ? d : 0] : 0.0f;
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < DM; ++d) {
+    float v = preb[d];
+#pragma unroll
+    for (int k = 0; k < kD0; ++k) v += r.x0[k] * preW[k * DM + d];
+    r.x[d] = v > 0.0f ? v : 0.0f;
+  }
+}
+
+// ================================================================================================
+// Wave-independent kernels (CP <= 64): each WAVE owns whole graphs and walks their receivers RW =
+// 64 / CP at a time, with all its LDS images private, so waves never wait on each other (no block
+// barriers inside the loops; the hardware interleaves the waves' gathers).  Block barriers only at
+// start (pre_W staging) and end (pre-gradient combine).
+// ================================================================================================
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// per-wave LDS (floats): qt [RW][QP] | g [RW][GP] (bwd) | xs [RW*CR][XP] | a [RW*CR][kH]
+//   | ef [RW*CR][4] | x0s [RW*CR][kD0+1] (bwd) | cb [gpw][n][DM] (bwd)
+template <int CP, int DM>
+struct WaveCarve {
+  static constexpr int RW = 64 / CP;
+  static constexpr int XP = DM + 1;
+  static constexpr int QP = kH * DM;
+  static constexpr int GP = kH * DM + 16;  // dxbar (H*DM) | debar (kH*4) | dsig (kH) | pad
+  float *qt, *g, *xs, *a, *ef, *x0s, *cb;
+  __device__ WaveCarve(float* base, int CR, int cbf, bool bwd) {
+    qt = base;
+    g = qt + RW * QP;
+    xs = g + (bwd ? RW * GP : 0);
+    a = xs + RW * CR * XP;
+    ef = a + RW * CR * kH;
+    x0s = ef + RW * CR * 4;
+    cb = x0s + (bwd ? RW * CR * (kD0 + 1) : 0);
+    (void)cbf;
+  }
+  static size_t floats(int CR, int cbf, bool bwd) {
+    size_t f = (size_t)RW * QP + (size_t)RW * CR * (XP + kH + 4);
+    if (bwd) f += (size_t)RW * GP + (size_t)RW * CR * (kD0 + 1) + cbf;
+    return (f + 3) & ~(size_t)3;
+  }
+};
+
+// shared block header: preW [kD0][DM] | preb [DM] | (then 4 wave regions)
+template <int DM>
+constexpr int wave_header_floats() {
+  return ((kD0 * DM + DM) + 3) & ~3;
+}
+
+template <int CP, int DM>
+__global__ __launch_bounds__(256) void attn_fwd_wave_kernel(dgppo_gnn_attn_args p, int gpw, int64_t nitems,
+                                                            int wfloats) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  using CV = WaveCarve<CP, DM>;
+  constexpr int RW = CV::RW, XP = CV::XP, QP = CV::QP;
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = p.H;
+  const int CR = cand_rows(C, CP);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  CV L(lds + wave_header_floats<DM>() + wave * wfloats, CR, 0, false);
+  const int W = H * (D + 5);
+  const int slot = lane / CP, c = lane % CP;
+  const int lr = slot * CR + c;
+  float* preW = lds;
+  float* preb = preW + kD0 * DM;
+  stage_pre(p, preW, preb, DM);
+  __syncthreads();
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+  // this wave's sub-rounds j = (its k-th item, r0): a flat sequence so the next one's gathers are
+  // issued while the current one computes
+  const int spi = (gpw * n + RW - 1) / RW;
+  const int64_t my_items = gw < nitems ? (nitems - gw + nw - 1) / nw : 0;
+  const int64_t J = my_items * spi;
+  auto sub = [&](int64_t j, int64_t& g0, int& nrec, int& r0) {
+    const int64_t item = gw + (j / spi) * nw;
+    g0 = item * gpw;
+    const int ng = (int)((int64_t)p.G - g0 < gpw ? (int64_t)p.G - g0 : gpw);
+    nrec = ng * n;
+    r0 = (int)(j % spi) * RW;
+  };
+  Gath<DM> cur, nxt;
+  if (J > 0) {
+    int64_t g0;
+    int nrec, r0;
+    sub(0, g0, nrec, r0);
+    const int rl = r0 + slot;
+    gath_load<DM>(p, g0 + (rl < nrec ? rl / n : 0), rl < nrec ? rl % n : 0, c, rl < nrec, D, cur);
+  }
+  for (int64_t j = 0; j < J; ++j) {
+    int64_t g0;
+    int nrec, r0;
+    sub(j, g0, nrec, r0);
+    const int rl = r0 + slot;
+    const bool active = rl < nrec;
+    const int64_t row = g0 * n + rl;
+    // this sub-round's small loads first (in-order completion), then the next sub-round's gathers
+    float qv[(RW * kH * DM + 63) / 64];
+#pragma unroll
+    for (int u = 0; u < (RW * kH * DM + 63) / 64; ++u) {
+      const int e = lane + 64 * u, rr = e / (H * D), kk = e - rr * (H * D);
+      qv[u] = (e < RW * H * D && r0 + rr < nrec) ? p.qt[(g0 * n + r0 + rr) * H * D + kk] : 0.0f;
+    }
+    float bacc[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float acc = 0.0f;
+      if (active && h < H)
+        for (int f = c; f < F; f += CP) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
+      bacc[h] = acc;
+    }
+    if (j + 1 < J) {
+      int64_t g0n;
+      int nrecn, r0n;
+      sub(j + 1, g0n, nrecn, r0n);
+      const int rln = r0n + slot;
+      gath_load<DM>(p, g0n + (rln < nrecn ? rln / n : 0), rln < nrecn ? rln % n : 0, c, rln < nrecn, D, nxt);
+    }
+#pragma unroll
+    for (int u = 0; u < (RW * kH * DM + 63) / 64; ++u) {
+      const int e = lane + 64 * u, rr = e / (H * D), kk = e - rr * (H * D);
+      if (e < RW * H * D) L.qt[rr * QP + kk] = qv[u];
+    }
+    float beta[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) beta[h] = group_sum<CP>(bacc[h], nullptr);
+    gath_finish<DM>(p, preW, preb, cur);
+    const bool ok = cur.k.s >= 0;
+    wave_sync();
+    float lg[kH], mx[kH], a[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float acc = 0.0f;
+      const float* qt = L.qt + slot * QP + h * D;
+#pragma unroll
+      for (int d = 0; d < DM; ++d)
+        if (d < D) acc += qt[d] * cur.x[d];
+      lg[h] = (ok && h < H) ? (acc + beta[h]) * p.scale : -INFINITY;
+      mx[h] = group_max<CP>(lg[h], nullptr);
+    }
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      const float ex = ok && h < H ? expf(lg[h] - mx[h]) : 0.0f;
+      const float sm = group_sum<CP>(ex, nullptr);
+      a[h] = ok && h < H ? ex / sm : 0.0f;
+      if (active && c < C && h < H && p.attn) p.attn[(row * H + h) * C + c] = a[h];
+    }
+    if (c < CR) {
+#pragma unroll
+      for (int d = 0; d < DM; ++d) L.xs[lr * XP + d] = cur.x[d];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) L.a[lr * kH + h] = a[h];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) L.ef[lr * 4 + jj] = cur.ef[jj];
+    }
+    wave_sync();
+    if (active) {
+      const int base = slot * CR;
+      float* out = p.xcat + row * W;
+      for (int o = c; o < W; o += CP) {
+        float acc = 0.0f;
+        if (o < H * D) {
+          const int h = o / D, d = o - h * D;
+          #pragma unroll 8
+          for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
+        } else if (o < H * D + 4 * H) {
+          const int q = o - H * D, h = q >> 2, jj = q & 3;
+          #pragma unroll 8
+          for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.ef[(base + cc) * 4 + jj];
+        } else {
+          const int h = o - H * D - 4 * H;
+          #pragma unroll 8
+          for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h];
+        }
+        out[o] = acc;
+      }
+    }
+    wave_sync();
+    cur = nxt;
+  }
+}
+
+template <int CP, int DM>
+__global__ __launch_bounds__(256) void attn_bwd_wave_kernel(dgppo_gnn_attn_args p, int gpw, int64_t nitems,
+                                                            int wfloats) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  using CV = WaveCarve<CP, DM>;
+  constexpr int RW = CV::RW, XP = CV::XP, QP = CV::QP, GP = CV::GP;
+  constexpr int NTD = (DM + 31) / 32;
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = p.H;
+  const int CR = cand_rows(C, CP);
+  float* preW = lds;
+  float* preb = preW + kD0 * DM;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  CV L(lds + wave_header_floats<DM>() + wave * wfloats, CR, gpw * n * DM, true);
+  const int W = H * (D + 5);
+  const int slot = lane / CP, c = lane % CP;
+  const int lr = slot * CR + c;
+  const bool agent_mode = p.xa != nullptr;
+  const bool want_dxa = agent_mode && p.dxa != nullptr;
+  const bool want_pre = agent_mode && p.pre_W != nullptr && p.dpre_part != nullptr;
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  f32x16 pacc[NTD];
+#pragma unroll
+  for (int q = 0; q < NTD; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pacc[q][r] = 0.0f;
+  stage_pre(p, preW, preb, DM);
+  __syncthreads();
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+  for (int64_t item = gw; item < nitems; item += nw) {
+    const int64_t g0 = item * gpw;
+    const int ng = (int)((int64_t)p.G - g0 < gpw ? (int64_t)p.G - g0 : gpw);
+    const int nrec = ng * n;
+    if (want_dxa) {
+      for (int e = lane; e < ng * n * D; e += 64) L.cb[e] = 0.0f;
+    }
+    for (int r0 = 0; r0 < nrec; r0 += RW) {
+      const int rl = r0 + slot;
+      const bool active = rl < nrec;
+      const int gl = active ? rl / n : 0;
+      const int64_t g = g0 + gl;
+      const int i = active ? rl % n : 0;
+      const int64_t row = g0 * n + rl;
+      const Cand k = active ? candidate(p, g, i, c) : Cand{-1, -1};
+      const bool ok = k.s >= 0;
+      float x[DM], x0[kD0];
+      bool via_pre;
+      gather_sender<DM>(p, g, k.s, ok, D, preW, preb, x, x0, via_pre);
+      float ef[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ef[j] = ok ? p.ef[g * p.ef_gstride + (int64_t)k.e * 4 + j] : 0.0f;
+      float a[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) a[h] = (ok && h < H) ? p.attn[(row * H + h) * C + c] : 0.0f;
+      for (int e = lane; e < RW * H * D; e += 64) {
+        const int rr = e / (H * D), kk = e - rr * (H * D);
+        if (r0 + rr < nrec) L.qt[rr * QP + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
+      }
+      for (int e = lane; e < RW * W; e += 64) {  // dxcat row -> [dxbar | debar | dsig] at aligned offsets
+        const int rr = e / W, kk = e - rr * W;
+        if (r0 + rr < nrec) {
+          const int dst = kk < H * D ? kk : (kk < H * D + 4 * H ? kH * DM + (kk - H * D) : kH * DM + 12 + (kk - H * D - 4 * H));
+          L.g[rr * GP + dst] = p.dxcat[(g0 * n + r0 + rr) * W + kk];
+        }
+      }
+      wave_sync();
+      const float* gv = L.g + slot * GP;
+      float dl[kH], dbeta[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float da = 0.0f;
+        if (ok && h < H) {
+#pragma unroll
+          for (int d = 0; d < DM; ++d)
+            if (d < D) da += gv[h * D + d] * x[d];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) da += gv[kH * DM + h * 4 + j] * ef[j];
+          da += gv[kH * DM + 12 + h];
+        }
+        const float dot = group_sum<CP>(a[h] * da, nullptr);
+        dl[h] = (ok && h < H) ? a[h] * (da - dot) * p.scale : 0.0f;
+        dbeta[h] = group_sum<CP>(dl[h], nullptr);
+      }
+      if (active && c == 0)
+        for (int h = 0; h < H; ++h) p.dbeta[row * H + h] = dbeta[h];
+      if (active)
+        for (int kk = c; kk < H * F; kk += CP) {
+          const int h = kk / F;
+          p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+        }
+      float contrib[DM];
+      {
+        const float* qt = L.qt + slot * QP;
+#pragma unroll
+        for (int d = 0; d < DM; ++d) {
+          float v = 0.0f;
+#pragma unroll
+          for (int h = 0; h < kH; ++h)
+            if (h < H && d < D) v += a[h] * gv[h * D + d] + dl[h] * qt[h * D + d];
+          contrib[d] = v;
+        }
+      }
+      if (c < CR) {
+#pragma unroll
+        for (int d = 0; d < DM; ++d) L.xs[lr * XP + d] = x[d];
+#pragma unroll
+        for (int h = 0; h < kH; ++h) L.a[lr * kH + h] = dl[h];
+      }
+      wave_sync();
+      if (active) {
+        const int base = slot * CR;
+        for (int o = c; o < H * D; o += CP) {
+          const int h = o / D, d = o - h * D;
+          float acc = 0.0f;
+          #pragma unroll 8
+          for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
+          p.dqt[row * H * D + o] = acc;
+        }
+      }
+      if (want_dxa) {  // agent senders: the wave's graph image, slots in fixed order
+        const bool mine = ok && k.s < n;
+        for (int ss = 0; ss < RW; ++ss) {
+          wave_sync();
+          if (slot == ss && mine) {
+            float* dst = L.cb + ((int64_t)gl * n + k.s) * D;
+#pragma unroll
+            for (int d = 0; d < DM; ++d)
+              if (d < D) dst[d] += contrib[d];
+          }
+        }
+      }
+      if (want_pre) {  // transformed senders: x0s^T (dz) into the wave's MFMA accumulators
+        wave_sync();   // dqt readers of xs are done: xs now holds dz
+        if (c < CR) {
+#pragma unroll
+          for (int d = 0; d < DM; ++d) L.xs[lr * XP + d] = via_pre && x[d] > 0.0f ? contrib[d] : 0.0f;
+#pragma unroll
+          for (int kk = 0; kk < kD0; ++kk) L.x0s[lr * (kD0 + 1) + kk] = via_pre ? x0[kk] : 0.0f;
+          L.x0s[lr * (kD0 + 1) + kD0] = via_pre ? 1.0f : 0.0f;
+        }
+        wave_sync();
+        const int rows = RW * CR;
+        for (int t0 = 0; t0 < rows; t0 += 2) {
+          const int tr = t0 + (lane >> 5);
+          const int m = lane & 31;
+          const float av = (tr < rows && m <= kD0) ? L.x0s[tr * (kD0 + 1) + m] : 0.0f;
+#pragma unroll
+          for (int q = 0; q < NTD; ++q) {
+            const int d = q * 32 + m;
+            const float bv = (tr < rows && d < DM) ? L.xs[tr * XP + d] : 0.0f;
+            pacc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, pacc[q], 0, 0, 0);
+          }
+        }
+      }
+      wave_sync();
+    }
+    if (want_dxa) {
+      wave_sync();
+      for (int e = lane; e < ng * n * D; e += 64) {
+        const int gg = e / (n * D), kk = e - gg * (n * D);
+        p.dxa[(g0 + gg) * p.dxa_gstride + kk] += L.cb[e];
+      }
+      wave_sync();
+    }
+  }
+  if (want_pre) {  // combine the 4 waves' accumulators in fixed order, write this block's partial
+    __syncthreads();
+    float* red = lds + wave_header_floats<DM>();  // wave regions are free now
+    constexpr int RP = 32 * NTD + 1;
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int q = 0; q < NTD; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            float* dst = red + m * RP + q * 32 + (lane & 31);
+            *dst = (w == 0 ? 0.0f : *dst) + pacc[q][r];
+          }
+      }
+      __syncthreads();
+    }
+    const int PK = p.D0 * D + D;
+    for (int o = threadIdx.x; o < PK; o += 256) {
+      const int m = o < p.D0 * D ? o / D : kD0;
+      const int d = o < p.D0 * D ? o - m * D : o - p.D0 * D;
+      p.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * RP + d];
+    }
+  }
+}
+
 int pick_cp(int C) {
   int cp = 8;
   while (cp < C) cp <<= 1;
@@ -526,12 +953,37 @@ struct Plan {
   int cp, dm, gpb;
   int64_t nblk, grid;
   size_t bytes;
+  bool wave;
+  int wfloats;
 };
 
 template <int CP, int DM>
 Plan plan_t(const dgppo_gnn_attn_args* p, bool bwd) {
   constexpr int R = 256 / CP;
-  Plan pl{CP, DM, 1, 0, 0, 0};
+  Plan pl{CP, DM, 1, 0, 0, 0, false, 0};
+  const bool full_dx = bwd && p->xa == nullptr && p->dx != nullptr;
+  // measured on MI355X (LidarSpread n8, 16384 graphs): the block-synchronous forward and the
+  // wave-independent backward are the faster pair; DGPPO_ATTN_WAVE=0/1 forces either family
+  static const int wave_env = [] {
+    const char* e = getenv("DGPPO_ATTN_WAVE");
+    return e ? atoi(e) : -1;
+  }();
+  const bool use_wave = wave_env < 0 ? bwd : wave_env != 0;
+  if (CP <= 64 && !full_dx && use_wave) {  // wave-independent kernels
+    constexpr int RW = 64 / CP;
+    pl.wave = true;
+    pl.gpb = RW >= p->n_agents ? RW / p->n_agents : 1;  // graphs per wave item
+    const int cbf = bwd ? pl.gpb * p->n_agents * DM : 0;
+    pl.wfloats = (int)WaveCarve<CP, DM>::floats(cand_rows(p->C, CP), cbf, bwd);
+    size_t tot = wave_header_floats<DM>() + 4 * (size_t)pl.wfloats;
+    if (bwd && tot < (size_t)wave_header_floats<DM>() + 32 * (32 * ((DM + 31) / 32) + 1))
+      tot = wave_header_floats<DM>() + 32 * (32 * ((DM + 31) / 32) + 1);
+    pl.bytes = tot * sizeof(float);
+    pl.nblk = (p->G + pl.gpb - 1) / pl.gpb;  // wave items
+    const int64_t blocks = (pl.nblk + 3) / 4;
+    pl.grid = blocks < kMaxBlocks ? blocks : kMaxBlocks;
+    return pl;
+  }
   const size_t fixed = bwd ? BwdCarve<CP, DM>::floats_fixed(cand_rows(p->C, CP), p->n_agents)
                            : Carve<CP, DM>::floats_fixed(cand_rows(p->C, CP), false);
   pl.gpb = R >= p->n_agents ? R / p->n_agents : 1;
@@ -571,6 +1023,26 @@ void launch_t(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream_
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       raised[bwd] = true;
     }
+  }
+  if (pl.wave) {
+    if constexpr (CP <= 64) {
+      if (pl.bytes > 64 * 1024) {
+        static bool raised_w[2] = {false, false};
+        if (!raised_w[bwd]) {
+          (void)hipFuncSetAttribute(
+              bwd ? (const void*)attn_bwd_wave_kernel<CP, DM> : (const void*)attn_fwd_wave_kernel<CP, DM>,
+              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          raised_w[bwd] = true;
+        }
+      }
+      if (bwd)
+        hipLaunchKernelGGL((attn_bwd_wave_kernel<CP, DM>), dim3((unsigned)pl.grid), dim3(256), pl.bytes, s, *p,
+                           pl.gpb, pl.nblk, pl.wfloats);
+      else
+        hipLaunchKernelGGL((attn_fwd_wave_kernel<CP, DM>), dim3((unsigned)pl.grid), dim3(256), pl.bytes, s, *p,
+                           pl.gpb, pl.nblk, pl.wfloats);
+    }
+    return;
   }
   if (bwd)
     hipLaunchKernelGGL((attn_bwd_kernel<CP, DM>), dim3((unsigned)pl.grid), dim3(256), pl.bytes, s, *p, pl.gpb,
