@@ -67,6 +67,11 @@ def read_pmc_traffic():
 
 
 PPO_BATCH, RNN_STEP = 16384, 16  # BASELINE.md synthetic-input plan (batch_size, rnn_step)
+# SURVEY.md §8(d) official algorithmic flops (minimal node-level projection formulation), LidarSpread n8
+# B4096: one PPO update (det rollout excluded: prepass + SGD, fwd+bwd = 3x fwd) and the two rollouts'
+# actor inference; MFMA% = flops / (t * 157.3 TF * n_gpu)
+UPDATE_TFLOP_PER_4096_ENVS, ROLLOUT_TFLOP_PER_4096_ENVS = 22.1, 5.3
+FP32_MFMA_PEAK_TFLOPS = 157.3
 
 
 def ppo_bench(env, dev, world, rank, iters):
@@ -106,7 +111,13 @@ def ppo_bench(env, dev, world, rank, iters):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_col, t_upd = (float(x) / iters for x in t.tolist())
+    upd_tf = UPDATE_TFLOP_PER_4096_ENVS * (B_PER_GPU / 4096) * world + ROLLOUT_TFLOP_PER_4096_ENVS / 2 * (
+        B_PER_GPU / 4096) * world  # the update runs the deterministic rollout too
     return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),
+            "update_roofline": {"bound": "mfma", "algorithmic_tflop": round(upd_tf, 2),
+                                "achieved": round(upd_tf / t_upd, 2), "peak": FP32_MFMA_PEAK_TFLOPS * world,
+                                "unit": "TFLOP/s", "frac": round(upd_tf / t_upd / (FP32_MFMA_PEAK_TFLOPS * world), 4),
+                                "flops_source": "SURVEY.md 8(d): 22.1 TF per update + 2.65 TF det-rollout inference"},
             "collect_ms": round(t_col * 1e3, 2),
             "collect_env_steps_per_s": round(B_PER_GPU * T * world / t_col, 1),
             "iters": iters, "batch_size": PPO_BATCH * world, "rnn_step": RNN_STEP, "epoch_ppo": 1,

@@ -13,7 +13,7 @@ rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
 if fatal $rc; then exit $rc; fi
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
+      python3 bench.py --steps 3 --warmup 1 --ppo-iters 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
 fi
 exit 0
