@@ -31,6 +31,29 @@ from ..trainer.rollout import RolloutEngine
 from .module.nets import ActorNet, VhNet, VlNet
 
 
+def minibatch_plan(n_env_local: int, T: int, world: int, batch_size: int, rng: np.random.Generator):
+    """Env-index minibatches of one PPO epoch for this rank (dgppo.py:155-159 sharded): the reference
+    permutes all B envs and splits them into B / (batch_size / T) minibatches; with p ranks each rank
+    permutes its own B/p envs and minibatch k is the k-th chunk of every rank's permutation (same
+    global minibatch size, rank-local shuffle).  Returns a list of index arrays."""
+    mb_envs_global = batch_size // T
+    n_mb = (n_env_local * world) // mb_envs_global if mb_envs_global >= 1 else 0
+    if n_mb < 1 or n_env_local % n_mb != 0:  # jnp.array(jnp.array_split(...)) needs equal chunks
+        raise ValueError(f"{n_mb} minibatches (batch_size {batch_size}, T {T}) do not split the "
+                         f"{n_env_local} envs of a rank evenly")
+    idx = np.arange(n_env_local)
+    rng.shuffle(idx)
+    return np.array_split(idx, n_mb)
+
+
+def allreduce_mean_(t: torch.Tensor, world: int):
+    """In-place mean over ranks (one collective: SUM then scale; RCCL on GPUs, gloo on CPU)."""
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.mul_(1.0 / world)
+    return t
+
+
 class _Phases:
     """Host wall-clock per update phase (synchronising) when DGPPO_PROFILE=1; no-op otherwise."""
 
@@ -243,9 +266,7 @@ class DGPPO:
         return out
 
     def _allreduce_grads(self):
-        if self.world > 1:
-            dist.all_reduce(self.grad_flat, op=dist.ReduceOp.SUM)
-            self.grad_flat.mul_(1.0 / self.world)
+        allreduce_mean_(self.grad_flat, self.world)
 
     def update(self, rollout: Rollout, step: int) -> dict:
         env, dev = self._env, self.device
@@ -292,11 +313,7 @@ class DGPPO:
                                   Qh=Qh.clone(), Qh_det=Qh_det.clone(), A=A.clone(), safe_cnt=safe_cnt.clone(),
                                   mb=[])
             # ---- minibatches (dgppo.py:155-159, 275-289)
-            idx = np.arange(B)
-            self.np_rng.shuffle(idx)
-            mb_envs_global = self.batch_size // T
-            n_mb = (B * self.world) // mb_envs_global
-            batches = np.array_split(idx, n_mb)
+            batches = minibatch_plan(B, T, self.world, self.batch_size, self.np_rng)
             L = self.rnn_step
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
             S_per_env = T // L

@@ -179,3 +179,18 @@ def test_golden_fixtures_on_gpu(cuda):
             np.testing.assert_array_equal(_np(getattr(res.graph, f)), z[f], err_msg=f"{fn}:{f}")
         np.testing.assert_array_equal(_np(res.reward), z["reward"], err_msg=fn)
         np.testing.assert_array_equal(_np(res.cost), z["cost"], err_msg=fn)
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("MPESpread", 3, 3)])
+def test_env_shards_equal_global_slices(cuda, eid, n, obs):
+    """Multi-GPU env sharding: rank r's reset with env_offset = r*B reproduces envs
+    [r*B, (r+1)*B) of a single-process reset, bit for bit, and so does every step."""
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    full = env.reset(key=9, n_env=8)
+    part = env.reset(key=9, n_env=4, env_offset=4)
+    for k in ("nodes", "edges", "states", "receivers", "senders"):
+        assert torch.equal(getattr(full, k)[4:], getattr(part, k)), k
+    a = torch.rand(8, n, 2, device=cuda) * 2 - 1
+    nf = env.step(full, a)
+    npart = env.step(part, a[4:].contiguous())
+    assert torch.equal(nf.graph.nodes[4:], npart.graph.nodes) and torch.equal(nf.reward[4:], npart.reward)
