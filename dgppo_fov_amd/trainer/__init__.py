@@ -1,0 +1,1 @@
+from .data import Rollout  # noqa: F401

@@ -1,0 +1,85 @@
+"""Trainer (dgppo/trainer/trainer.py:17-140): collect -> update loop with periodic deterministic
+evaluation and checkpoints.  Same constructor and `params` contract as the reference; logging goes
+to `<log_dir>/log.jsonl` (+ stdout) instead of wandb (not installed, no network).  Multi-GPU: every
+rank trains on its own env shard (`DGPPO` all-reduces the gradients); rank 0 evaluates, logs and
+saves."""
+from __future__ import annotations
+
+import json
+import os
+from time import time
+
+import numpy as np
+import torch.distributed as dist
+
+from ..algo.dgppo import DGPPO
+from ..env.base import MultiAgentEnv
+from ..trainer.rollout import RolloutEngine
+from .utils import eval_info
+
+
+class Trainer:
+    def __init__(self, env: MultiAgentEnv, env_test: MultiAgentEnv, algo: DGPPO, gamma: float, n_env_train: int,
+                 n_env_test: int, log_dir: str, seed: int, params: dict, save_log: bool = True):
+        self.env, self.env_test, self.algo = env, env_test, algo
+        self.gamma, self.n_env_train, self.n_env_test = gamma, n_env_train, n_env_test
+        self.log_dir, self.seed = log_dir, seed
+        if Trainer._check_params(params):
+            self.params = params
+        self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.save_log = save_log and self.rank == 0
+        if self.save_log:
+            os.makedirs(log_dir, exist_ok=True)
+            self.model_dir = os.path.join(log_dir, "models")
+            os.makedirs(self.model_dir, exist_ok=True)
+        self.steps = params["training_steps"]
+        self.eval_interval = params["eval_interval"]
+        self.eval_epi = params["eval_epi"]
+        self.save_interval = params["save_interval"]
+        self.update_steps = 0
+        self.rng = np.random.default_rng(seed)
+        self._test_engine = None
+
+    @staticmethod
+    def _check_params(params: dict) -> bool:
+        assert "run_name" in params, "run_name not found in params"
+        assert "training_steps" in params, "training_steps not found in params"
+        assert "eval_interval" in params, "eval_interval not found in params"
+        assert params["eval_interval"] > 0, "eval_interval must be positive"
+        assert "eval_epi" in params, "eval_epi not found in params"
+        assert params["eval_epi"] >= 1, "eval_epi must be greater than or equal to 1"
+        assert "save_interval" in params, "save_interval not found in params"
+        assert params["save_interval"] > 0, "save_interval must be positive"
+        return True
+
+    def _log(self, record: dict):
+        if self.save_log:
+            with open(os.path.join(self.log_dir, "log.jsonl"), "a") as f:
+                f.write(json.dumps(record) + "\n")
+
+    def evaluate(self, key: int) -> dict:
+        """test_rollout with the deterministic policy on n_env_test envs (trainer.py:85-116)."""
+        assert self.n_env_test <= 1_000, "n_env_test must be less than or equal to 1_000"
+        if self._test_engine is None:
+            self._test_engine = RolloutEngine(self.env_test, self.n_env_test, self.env_test.max_episode_steps,
+                                              self.algo.device, actor=self.algo.actor, mode=RolloutEngine.MODE_DET)
+        r = self._test_engine.run(key)
+        return eval_info(r.rewards, r.costs)
+
+    def train(self):
+        start_time = time()
+        test_key = int(self.seed)
+        for step in range(0, self.steps + 1):
+            if step % self.eval_interval == 0 and self.rank == 0:
+                info = self.evaluate(test_key)
+                print(f"step: {step:3}, time: {time() - start_time:5.0f}s, reward: {info['eval/reward']:9.4f}, "
+                      f"min/max reward: {info['eval/reward_min']:7.2f}/{info['eval/reward_max']:7.2f}, "
+                      f"cost: {info['eval/cost']:8.4f}, unsafe_frac: {info['eval/unsafe_frac']:6.2f}", flush=True)
+                self._log({"step": self.update_steps, **info})
+            if self.save_log and step % self.save_interval == 0:
+                self.algo.save(self.model_dir, step)
+            key = int(self.rng.integers(0, 2 ** 62))
+            rollouts = self.algo.collect(self.algo.params, key, n_env=self.n_env_train)
+            update_info = self.algo.update(rollouts, step)
+            self._log({"step": self.update_steps, **update_info})
+            self.update_steps += 1

@@ -213,3 +213,20 @@ def test_dgppo_update_matches_oracle(cuda, eid, n, obs):
         (rp,), _, _ = O.adam_step([mb["before"][name].double().cpu().numpy()], [gc], [np.zeros(sz)], [np.zeros(sz)],
                                   0, algo.opt[name].lr)
         assert np.abs(net.ps.flat.double().cpu().numpy() - rp).max() <= 1e-6, name
+
+
+def test_checkpoint_round_trip(cuda, tmp_path):
+    env = make_env("MPETarget", 3, num_obs=0, max_step=16, device=cuda)
+    kw = dict(env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+              action_dim=env.action_dim, n_agents=3, batch_size=64, rnn_step=16, device=cuda)
+    a = make_algo("dgppo", seed=3, **kw)
+    a.update(a.collect(a.params, 1, n_env=8), 0)
+    a.save(str(tmp_path), 7)
+    b = make_algo("dgppo", seed=4, **kw)
+    b.load(str(tmp_path), 7)
+    for k in ("policy", "Vl", "Vh"):
+        assert torch.equal(a.params[k], b.params[k])
+    for k in a.opt:
+        assert torch.equal(a.opt[k].m, b.opt[k].m) and torch.equal(a.opt[k].state, b.opt[k].state)
+    ra, rb = a.collect(a.params, 5, n_env=8), b.collect(b.params, 5, n_env=8)
+    assert torch.equal(ra.actions, rb.actions)
