@@ -121,6 +121,31 @@ class GruSeqArgs(ctypes.Structure):
     ]
 
 
+class GtLayer(ctypes.Structure):
+    _fields_ = [("Wq", c_f32p), ("bq", c_f32p), ("Wkt", c_f32p), ("bk", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p),
+                ("bu", c_f32p), ("D", ctypes.c_int32), ("F", ctypes.c_int32)]
+
+
+class PolicyStepArgs(ctypes.Structure):
+    _fields_ = [
+        ("G", ctypes.c_int32), ("N", ctypes.c_int32), ("E", ctypes.c_int32), ("n_agents", ctypes.c_int32),
+        ("C", ctypes.c_int32), ("D0", ctypes.c_int32), ("A", ctypes.c_int32), ("n_layers", ctypes.c_int32),
+        ("H", ctypes.c_int32), ("mode", ctypes.c_int32),
+        ("cand", c_f32p),
+        ("nodes", c_f32p), ("nodes_gstride", ctypes.c_int64),
+        ("edges", c_f32p), ("edges_gstride", ctypes.c_int64),
+        ("receivers", c_f32p), ("senders", c_f32p), ("idx_gstride", ctypes.c_int64),
+        ("layer", GtLayer * 2),
+        ("head_W0", c_f32p), ("head_b0", c_f32p), ("ln0_s", c_f32p), ("ln0_b", c_f32p),
+        ("head_W1", c_f32p), ("head_b1", c_f32p), ("ln1_s", c_f32p), ("ln1_b", c_f32p),
+        ("gru_Wi", c_f32p), ("gru_bi", c_f32p), ("gru_Wh", c_f32p), ("gru_bhn", c_f32p),
+        ("Ws", c_f32p), ("bs", c_f32p), ("Wm", c_f32p), ("bm", c_f32p), ("Wsd", c_f32p), ("bsd", c_f32p),
+        ("std_shift", ctypes.c_float), ("std_min", ctypes.c_float),
+        ("h_in", c_f32p), ("h_out", c_f32p), ("noise", c_f32p), ("action", c_f32p), ("log_pi", c_f32p),
+        ("work", c_f32p),
+    ]
+
+
 class GnnAttnArgs(ctypes.Structure):
     _fields_ = [
         ("G", ctypes.c_int32), ("N", ctypes.c_int32), ("E", ctypes.c_int32), ("n_agents", ctypes.c_int32),
@@ -191,6 +216,10 @@ SIGNATURES = {
     "dgppo_gru_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _V]),
     "dgppo_gru_seq_blocks": (ctypes.c_int64, [_I32]),
     "dgppo_gnn_attn_partial_blocks": (ctypes.c_int64, [_V]),
+    "dgppo_policy_step_supported": (ctypes.c_int, [_V]),
+    "dgppo_policy_work_floats": (ctypes.c_int64, []),
+    "dgppo_policy_prepare": (ctypes.c_int, [_V, _V]),
+    "dgppo_policy_step": (ctypes.c_int, [_V, _V]),
     "dgppo_gnn_sender_table": (ctypes.c_int, [_I32, _I32, _I32, _I32, _V, _V, _V, _V, _V]),
     "dgppo_gru_seq_fwd": (ctypes.c_int, [_V, _V]),
     "dgppo_gru_seq_bwd": (ctypes.c_int, [_V, _V]),

@@ -15,7 +15,9 @@ informarl.py:365-367 / 409-413) are (sequence s, step t) graph-major, carries st
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -79,11 +81,59 @@ class ActorNet(_Net):
         sr = self.std.fwd(s, rows)
         return s, mu, sr
 
+    def _fused_args(self, g: GraphBatch):
+        """dgppo_policy_step_args with this net's parameter pointers (None if the fused kernel does not
+        cover the configuration)."""
+        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1":
+            return None
+        a = _lib.PolicyStepArgs()
+        a.N, a.E, a.n_agents, a.C, a.D0, a.A = g.N, g.E, self.n, g.C, g.nodes.shape[2], self.A
+        a.n_layers, a.H = len(self.gnn.layers), 3
+        for i, L in enumerate(self.gnn.layers):
+            ly = a.layer[i]
+            ly.Wq, ly.bq, ly.Wkt, ly.bk = K._p(L.v("Wq")), K._p(L.v("bq")), K._p(L.v("Wkt")), K._p(L.v("bk"))
+            ly.Wcat, ly.Wu, ly.bu = K._p(L.v("Wcat")), K._p(L.v("Wu")), K._p(L.v("bu"))
+            ly.D, ly.F = L.D, L.F
+        hd = self.head
+        a.head_W0, a.head_b0, a.head_W1, a.head_b1 = K._p(hd.d0.W()), K._p(hd.d0.b()), K._p(hd.d1.W()), K._p(hd.d1.b())
+        a.ln0_s, a.ln0_b = K._p(self.ps.view(hd.ln0.name + ".scale")), K._p(self.ps.view(hd.ln0.name + ".bias"))
+        a.ln1_s, a.ln1_b = K._p(self.ps.view(hd.ln1.name + ".scale")), K._p(self.ps.view(hd.ln1.name + ".bias"))
+        a.gru_Wi, a.gru_bi = K._p(self.gru.v("Wi")), K._p(self.gru.v("bi"))
+        a.gru_Wh, a.gru_bhn = K._p(self.gru.v("Wh")), K._p(self.gru.v("bhn"))
+        a.Ws, a.bs = K._p(self.scale_hid.W()), K._p(self.scale_hid.b())
+        a.Wm, a.bm, a.Wsd, a.bsd = K._p(self.mean.W()), K._p(self.mean.b()), K._p(self.std.W()), K._p(self.std.b())
+        a.std_shift, a.std_min = STD_DEV_INIT_INV, STD_DEV_MIN
+        if not _lib.load().dgppo_policy_step_supported(ctypes.byref(a)):
+            return None
+        if getattr(self, "_policy_work", None) is None:
+            self._policy_work = torch.zeros(_lib.load().dgppo_policy_work_floats(), device=self.ps.flat.device)
+        a.work = K._p(self._policy_work)
+        return a
+
     def act(self, g: GraphBatch, h: torch.Tensor, mode: int, noise=None, action_out=None, log_pi_out=None,
-            h_out=None):
+            h_out=None, prepare=True):
         """One policy step for G graphs: mode 0 = deterministic (get_action: tanh(mean)),
-        1 = sample_action with standard-normal `noise` (G*n, A).  Returns (action, log_pi, h_new)."""
+        1 = sample_action with standard-normal `noise` (G*n, A).  Returns (action, log_pi, h_new).
+        Runs the fused dgppo_policy_step kernel when it covers the configuration; `prepare` refreshes
+        its query-key products from the current weights (needed once after every weight change)."""
         rows = g.G * self.n
+        fa = self._fused_args(g)
+        if fa is not None:
+            if prepare:
+                K._chk(_lib.load().dgppo_policy_prepare(ctypes.byref(fa), _lib.stream_handle(h.device)),
+                       "dgppo_policy_prepare")
+            dev = h.device
+            h2 = h_out if h_out is not None else torch.empty_like(h)
+            action = action_out if action_out is not None else torch.empty((rows, self.A), device=dev)
+            log_pi = log_pi_out if log_pi_out is not None else torch.empty(rows, device=dev)
+            fa.G, fa.mode = g.G, int(mode)
+            fa.cand, fa.receivers, fa.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
+            fa.nodes, fa.nodes_gstride = K._p(g.nodes), g.N * g.nodes.shape[2]
+            fa.edges, fa.edges_gstride, fa.idx_gstride = K._p(g.edges), g.E * 4, g.E
+            fa.h_in, fa.h_out, fa.noise = K._p(h), K._p(h2), K._p(noise)
+            fa.action, fa.log_pi = K._p(action), K._p(log_pi)
+            K._chk(_lib.load().dgppo_policy_step(ctypes.byref(fa), _lib.stream_handle(dev)), "dgppo_policy_step")
+            return action, log_pi, h2
         y, _ = self._trunk(g)
         h2, _ = self.gru.fwd(y, h, h_out=h_out)
         _, mu, sr = self._outputs(h2)

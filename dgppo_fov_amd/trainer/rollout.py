@@ -67,10 +67,11 @@ class RolloutEngine:
             # per-step, per-shard Philox stream: (env_offset, t) -> disjoint noise across ranks
             K.normal_(self.noise, stream_id=(self.env_offset << 32) | t, seed_tensor=self.key)
             self.actor.act(g, h, 1, noise=self.noise, action_out=self.actions[t].view(-1, env.action_dim),
-                           log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, 64))
+                           log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, 64),
+                           prepare=t == 0)
         else:
             self.actor.act(g, h, 0, action_out=self.actions[t].view(-1, env.action_dim),
-                           h_out=self.rnn[t + 1].view(self.B * n, 64))
+                           h_out=self.rnn[t + 1].view(self.B * n, 64), prepare=t == 0)
 
     def _run(self):
         env = self.env

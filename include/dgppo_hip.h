@@ -263,6 +263,46 @@ int64_t dgppo_gru_seq_blocks(int32_t Q);
 int dgppo_gru_seq_fwd(const dgppo_gru_seq_args* args, void* stream);
 int dgppo_gru_seq_bwd(const dgppo_gru_seq_args* args, void* stream);
 
+/* Fused policy step (one launch per env step of the rollouts): GNN -> MLP head -> GRUCell ->
+ * ScaleHid -> mean/std -> TanhNormal sample (mode 1, standard-normal noise) or mode (mode 0), i.e.
+ * PPOPolicy.sample_action / get_action (dgppo/algo/module/policy.py:191-203) for G graphs at once.
+ * Parameter pointers are the layouts of dgppo_fov_amd/nn/layers.py (GraphTransformer: Wq (D, H F),
+ * bq, Wkt (H, F, D), bk, Wcat (H (D+5), F) = [Wv; We; bv], Wu (D, F), bu; GRU Wi (64, 192) [r|z|n],
+ * bi, Wh (64, 192), bhn).  dgppo_policy_step_supported() tells whether a configuration fits the
+ * fused kernel (n <= 32, C <= 32, D0 <= 8, H = 3, actor GNN D0->32->64 or D0->64, A in {1, 2, 4}).
+ * `work` (dgppo_policy_work_floats() floats) holds the per-layer query-key products
+ * [Wq_h Wkt_h | Wq_h bk_h] and their biases; dgppo_policy_prepare() fills it from the current weights
+ * and must run after every weight change (the rollouts call it once per rollout, inside the graph). */
+typedef struct dgppo_gt_layer {
+  const float *Wq, *bq, *Wkt, *bk, *Wcat, *Wu, *bu;
+  int32_t D, F;
+} dgppo_gt_layer;
+
+typedef struct dgppo_policy_step_args {
+  int32_t G, N, E, n_agents, C, D0, A, n_layers, H, mode;
+  const int32_t* cand;
+  const float* nodes; int64_t nodes_gstride;   /* (G, N, D0) */
+  const float* edges; int64_t edges_gstride;   /* (G, E, 4) */
+  const int32_t* receivers;
+  const int32_t* senders; int64_t idx_gstride; /* (G, E) */
+  dgppo_gt_layer layer[2];
+  const float *head_W0, *head_b0, *ln0_s, *ln0_b, *head_W1, *head_b1, *ln1_s, *ln1_b;
+  const float *gru_Wi, *gru_bi, *gru_Wh, *gru_bhn;
+  const float *Ws, *bs, *Wm, *bm, *Wsd, *bsd;
+  float std_shift, std_min;
+  const float* h_in;   /* (G n, 64) */
+  float* h_out;        /* (G n, 64) */
+  const float* noise;  /* (G n, A), mode 1 */
+  float* action;       /* (G n, A) */
+  float* log_pi;       /* (G n) or NULL */
+  float* work;         /* dgppo_policy_work_floats() floats */
+} dgppo_policy_step_args;
+
+int dgppo_policy_step_supported(const dgppo_policy_step_args* args);
+int64_t dgppo_policy_work_floats(void);
+int dgppo_policy_prepare(const dgppo_policy_step_args* args, void* stream);
+int dgppo_policy_step(const dgppo_policy_step_args* args, void* stream);
+
 /* mean over the agents of each graph (RStateFn, dgppo/algo/module/value.py:29) */
 int dgppo_agent_mean_fwd(const float* x, float* y, int64_t G, int32_t n, int32_t F, int64_t x_gstride, void* stream);
 int dgppo_agent_mean_bwd(const float* dy, float* dx, int64_t G, int32_t n, int32_t F, int64_t dx_gstride,

@@ -57,7 +57,9 @@ def _c_layout(struct, fields):
                                             (_lib.TanhNormalArgs, "dgppo_tanh_normal_args"),
                                             (_lib.GaeArgs, "dgppo_gae_args"),
                                             (_lib.AdvArgs, "dgppo_adv_args"),
-                                            (_lib.GruSeqArgs, "dgppo_gru_seq_args")])
+                                            (_lib.GruSeqArgs, "dgppo_gru_seq_args"),
+                                            (_lib.GtLayer, "dgppo_gt_layer"),
+                                            (_lib.PolicyStepArgs, "dgppo_policy_step_args")])
 def test_ctypes_mirror_matches_c_layout(pystruct, cname):
     names = [f[0] for f in pystruct._fields_]
     got = _c_layout(cname, names)

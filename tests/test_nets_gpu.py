@@ -205,3 +205,32 @@ def test_vh_fwd_bwd(cuda, eid, n, obs):
     net.ps.swap_views()
     for path, a, b in _walk(g, R.grads(p)):
         _grad_close(a, b, "Vh grad " + path)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("layers", [2, 1])
+@pytest.mark.parametrize("eid,n,obs", CASES)
+def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
+    """ActorNet.act (PPOPolicy.get_action / sample_action, policy.py:191-212) for one graph batch with
+    non-zero carries, through the fused dgppo_policy_step kernel ("1") and the unfused layer chain
+    ("0"): carry, action (tanh of mean, or of mean + std * noise) and log_pi against float64."""
+    monkeypatch.setenv("DGPPO_FUSED_POLICY", fused)
+    S, L = 5, 3  # 15 graphs: partial last row group in the fused kernel for every n
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=2)
+    net = ActorNet(env.node_dim, n, cuda, seed=5, gnn_layers=layers)
+    rows = S * L * n
+    rng = np.random.default_rng(4)
+    h = torch.from_numpy(rng.standard_normal((rows, 64)).astype(np.float32) * 0.5).to(cuda)
+    noise = torch.from_numpy(rng.standard_normal((rows, 2)).astype(np.float32)).to(cuda)
+    p = R.to_t(net.flax())
+    h2_ref = R.actor_carry(p, host, h.cpu().double().reshape(S * L, n, 64), n)
+    mu, sd = R.policy_dist(p, h2_ref)
+    for mode in (0, 1):
+        a, lp, h2 = net.act(gb, h, mode, noise=noise if mode else None)
+        torch.cuda.synchronize()
+        _close(h2.cpu().numpy(), h2_ref.numpy().reshape(rows, 64), what=f"carry mode {mode}")
+        pre = mu + sd * noise.cpu().double().reshape(S * L, n, 2) if mode else mu
+        a_ref = torch.tanh(pre)
+        _close(a.cpu().numpy(), a_ref.numpy().reshape(rows, 2), what=f"action mode {mode}")
+        lp_ref = R.tanh_normal_log_prob(a.cpu().double().reshape(S * L, n, 2), mu, sd)
+        _close(lp.cpu().numpy(), lp_ref.numpy().reshape(rows), rtol=3e-5, atol=3e-5, what=f"log_pi mode {mode}")
