@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include "../../include/dgppo_hip.h"
+#include "lanes.h"
 
 namespace dgppo {
 namespace {
@@ -949,6 +950,238 @@ int pick_cp(int C) {
   return cp;
 }
 
+// ================================================================================================
+// Forward, row-block form (C <= 32, H = 3, D <= 32, sender table given): a 256-thread workgroup
+// takes 16 consecutive receiver rows, each wave two rows per sub-round (32 lanes = candidates) for
+// two sub-rounds.  The rows' qt and beta sit in LDS; every lane's sender row and edge features for
+// both sub-rounds are gathered up front (one exposed gather latency per block); in agent mode the
+// never-receiving senders' relu(x_raw pre_W + pre_b) is one MFMA tile product per wave and
+// sub-round; the softmax reductions are DPP lane shuffles; the weighted sums read float4 rows.
+// ================================================================================================
+namespace fwd2 {
+constexpr int kRows = 16, kSR = 2, kQP = 100;
+// xs row pitch: x (DM floats; the pre-transform writes 32) then the edge features at column EC
+template <int DM>
+struct Pitch {
+  static constexpr int EC = DM <= 8 ? 8 : 32, XSP = EC + (DM <= 8 ? 4 : 8), AW = 64 * (XSP + 4);
+};
+template <int DM>
+constexpr size_t lds_floats() {
+  return (size_t)kRows * kQP + kD0 * 32 + 32 + 4 * Pitch<DM>::AW;
+}
+}  // namespace fwd2
+
+template <int DM>
+__global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
+  using lanes::f32x4;
+  using lanes::wave_sync;
+  constexpr int kRows = fwd2::kRows, kSR = fwd2::kSR, kQP = fwd2::kQP;
+  constexpr int kXSP = fwd2::Pitch<DM>::XSP, EC = fwd2::Pitch<DM>::EC;
+  static_assert(DM == 8 || DM == 32, "fwd2 instantiations");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* qts = lds;                 // [16][100]: qt_h (32-float stride per head) | beta_h at 96 + h
+  float* preW = qts + kRows * kQP;  // [8][32]
+  float* preb = preW + kD0 * 32;    // [32]
+  float* att = preb + 32;           // per wave: xs [64][kXSP] | aa [64][4]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int slot = lane >> 5, c = lane & 31;
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = kH;
+  const int nrows = p.G * n;
+  const int row0 = blockIdx.x * kRows;
+  const bool agent = p.xa != nullptr;
+  const bool pre = DM > 8 && agent && p.pre_W != nullptr;  // the launcher sends pre mode to DM = 32
+  // ---- gathers of both sub-rounds
+  float xv[kSR][DM];
+  f32x4 efv[kSR];
+  int sv[kSR];
+#pragma unroll
+  for (int sr = 0; sr < kSR; ++sr) {
+    const int row = row0 + 2 * wave + 8 * sr + slot;
+    const bool active = row < nrows;
+    const int g = active ? row / n : 0;
+    const int i = active ? row - g * n : 0;
+    int s = -1, e = 0;
+    if (active && c < C) {
+      e = p.cand[i * C + c];
+      s = p.sidx[(int64_t)row * C + c];
+    }
+    const bool ok = s >= 0;
+    sv[sr] = s;
+    const float* er = p.ef + (int64_t)g * p.ef_gstride + (int64_t)(ok ? e : 0) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) efv[sr][j] = ok ? er[j] : 0.0f;
+    if (!agent) {
+      load_row<DM>(p.x + (int64_t)g * p.x_gstride + (int64_t)(ok ? s : 0) * D, D, ok, xv[sr]);
+    } else if (!ok || s < n) {
+      load_row<DM>(p.xa + (int64_t)g * p.xa_gstride + (int64_t)(ok ? s : 0) * D, D, ok, xv[sr]);
+    } else {
+      const float* xr = p.x + (int64_t)g * p.x_gstride + (int64_t)s * p.D0;
+#pragma unroll
+      for (int k = 0; k < DM; ++k) xv[sr][k] = (k < kD0 && k < p.D0) ? xr[k < kD0 ? k : 0] : 0.0f;
+    }
+  }
+  // ---- stage qt (zero padded per head), beta_h = q_h . bk_h, pre weights
+  for (int e = threadIdx.x; e < kRows * 96; e += 256) {
+    const int r = e / 96, k = e - r * 96, h = k >> 5, d = k & 31;
+    qts[r * kQP + k] = (row0 + r < nrows && d < D) ? p.qt[(int64_t)(row0 + r) * H * D + h * D + d] : 0.0f;
+  }
+  {
+    const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const bool act = row0 + r < nrows;
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float acc = 0.0f;
+      if (act)
+        for (int f = j; f < F; f += 16) acc += p.q[(int64_t)(row0 + r) * H * F + h * F + f] * p.bk[h * F + f];
+      acc = lanes::sum16(acc);
+      if (j == 0) qts[r * kQP + 96 + h] = acc;
+    }
+  }
+  if (pre) {
+    const int k = threadIdx.x >> 5, d = threadIdx.x & 31;
+    preW[threadIdx.x] = (k < p.D0 && d < D) ? p.pre_W[k * D + d] : 0.0f;
+    if (threadIdx.x < 32) preb[threadIdx.x] = threadIdx.x < D ? p.pre_b[threadIdx.x] : 0.0f;
+  }
+  __syncthreads();
+  float pw[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}}, pb[2] = {0.0f, 0.0f};
+  if (pre) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) pw[ks][ct] = preW[(4 * ks + kq) * 32 + 16 * ct + i16];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) pb[ct] = preb[16 * ct + i16];
+  }
+  float* xs = att + wave * fwd2::Pitch<DM>::AW;
+  float* aa = xs + 64 * kXSP;
+  const int pr = slot * 32 + c;
+  float* xp = xs + pr * kXSP;
+  const int TQ = (D + 3) >> 2, Th = TQ + 2, W = H * (D + 5);
+  int th = 0, tq = c;  // this lane's weighted-sum task: head th, column block tq
+  while (tq >= Th && th < kH) {
+    tq -= Th;
+    ++th;
+  }
+#pragma unroll
+  for (int sr = 0; sr < kSR; ++sr) {
+    const int rl = 2 * wave + 8 * sr + slot;
+    const int row = row0 + rl;
+    const bool active = row < nrows;
+    const int s = sv[sr];
+    const bool ok = s >= 0;
+    if (pre) {
+      const bool viapre = ok && s >= n;
+#pragma unroll
+      for (int k = 0; k < kD0; ++k) xp[k] = viapre ? xv[sr][k < DM ? k : 0] : 0.0f;
+      wave_sync();
+      float a[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a[t][ks] = xs[(16 * t + i16) * kXSP + 4 * ks + kq];
+      f32x4 pacc[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          pacc[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            pacc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][ks], pw[ks][ct], pacc[t][ct], 0, 0, 0);
+        }
+      wave_sync();
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = pacc[t][ct][i] + pb[ct];
+            xs[(16 * t + 4 * kq + i) * kXSP + 16 * ct + i16] = v > 0.0f ? v : 0.0f;
+          }
+      wave_sync();
+      if (!viapre) {
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q)
+          ((f32x4*)xp)[q] = f32x4{xv[sr][4 * q], xv[sr][4 * q + 1], xv[sr][4 * q + 2], xv[sr][4 * q + 3]};
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < DM / 4; ++q)
+        ((f32x4*)xp)[q] = f32x4{xv[sr][4 * q], xv[sr][4 * q + 1], xv[sr][4 * q + 2], xv[sr][4 * q + 3]};
+    }
+    *(f32x4*)(xp + EC) = efv[sr];
+    wave_sync();
+    // logits, softmax over the row's candidates, attention weights out
+    const float* qt = qts + rl * kQP;
+    float aw[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int q = 0; q < DM / 4; ++q)
+        if (q < TQ) {
+          const f32x4 xq = ((const f32x4*)xp)[q], qq = ((const f32x4*)(qt + 32 * h))[q];
+          acc += xq[0] * qq[0] + xq[1] * qq[1] + xq[2] * qq[2] + xq[3] * qq[3];
+        }
+      const float lg = ok ? (acc + qt[96 + h]) * p.scale : -INFINITY;
+      const float mx = lanes::max32(lg);
+      const float ex = ok ? expf(lg - mx) : 0.0f;
+      const float sm = lanes::sum32(ex);
+      aw[h] = ok ? ex / sm : 0.0f;
+      if (active && c < C && p.attn) p.attn[((int64_t)row * H + h) * C + c] = aw[h];
+    }
+#pragma unroll
+    for (int h = 0; h < kH; ++h) aa[pr * 4 + h] = aw[h];
+    wave_sync();
+    // xcat row = [xbar_h | ebar_h | sig_h]
+    if (active && th < kH) {
+      const float* xb = xs + slot * 32 * kXSP;
+      const float* ab = aa + slot * 32 * 4 + th;
+      float* o = p.xcat + (int64_t)row * W;
+      if (tq <= TQ) {
+        const int col = tq < TQ ? 4 * tq : EC;
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 8
+        for (int cc = 0; cc < 32; ++cc) acc += ab[cc * 4] * *(const f32x4*)(xb + cc * kXSP + col);
+        if (tq < TQ) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * tq + j < D) o[th * D + 4 * tq + j] = acc[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[H * D + 4 * th + j] = acc[j];
+        }
+      } else {
+        float acc = 0.0f;
+#pragma unroll 8
+        for (int cc = 0; cc < 32; ++cc) acc += ab[cc * 4];
+        o[H * D + 4 * H + th] = acc;
+      }
+    }
+    wave_sync();
+  }
+}
+
+bool fwd2_ok(const dgppo_gnn_attn_args* p) {
+  static const bool off = [] {
+    const char* e = getenv("DGPPO_ATTN_FWD1");
+    return e && atoi(e) != 0;
+  }();
+  return !off && p->H == kH && p->C <= 32 && p->D <= 32 && p->F <= 64 && p->sidx != nullptr &&
+         (int64_t)p->G * p->n_agents < (int64_t)1 << 30 && (p->xa == nullptr || p->D0 <= kD0);
+}
+
+void fwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
+  const int64_t rows = (int64_t)p->G * p->n_agents;
+  const unsigned grid = (unsigned)((rows + fwd2::kRows - 1) / fwd2::kRows);
+  if (p->D <= 8 && !(p->xa && p->pre_W))
+    hipLaunchKernelGGL(attn_fwd2_kernel<8>, dim3(grid), dim3(256), fwd2::lds_floats<8>() * sizeof(float), s, *p);
+  else
+    hipLaunchKernelGGL(attn_fwd2_kernel<32>, dim3(grid), dim3(256), fwd2::lds_floats<32>() * sizeof(float), s, *p);
+}
+
 struct Plan {
   int cp, dm, gpb;
   int64_t nblk, grid;
@@ -1064,6 +1297,10 @@ void launch_cp(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream
 }
 
 int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
+  if (!bwd && fwd2_ok(p)) {
+    if (p->G > 0) fwd2_launch(p, s);
+    return 0;
+  }
   const Plan pl = make_plan(p, bwd);
   if (pl.bytes > 160 * 1024) return DGPPO_EINVAL;
   if (pl.dm == 8) launch_cp<8>(p, pl, bwd, s);

@@ -27,11 +27,17 @@
 #include <stdint.h>
 
 #include "../../include/dgppo_hip.h"
+#include "lanes.h"
 
 namespace dgppo {
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+using lanes::f32x4;
+using lanes::wave_sync;
+__device__ __forceinline__ float gsum32(float v) { return lanes::sum32(v); }
+__device__ __forceinline__ float gmax32(float v) { return lanes::max32(v); }
+__device__ __forceinline__ float gsum8(float v) { return lanes::sum8(v); }
+
 constexpr int kRowsG = 16, kThreads = 256, kHeads = 3, kHid = 64;
 // row tiles of 16, attention sub-rounds (a wave takes two rows per sub-round), pairs per thread
 constexpr int kRT = kRowsG / 16, kSR = kRowsG / 8;
@@ -65,43 +71,6 @@ __device__ __forceinline__ float log_ndtr(float z) {
   return -0.5f * z2 - logf(-z) - 0.91893853320467274f + logf(s);
 }
 __device__ __forceinline__ float tanh_fldj(float x) { return 2.0f * (0.69314718055994531f - x - softplusf(-2.0f * x)); }
-
-// all-reduce over each 32-lane half of the wave without LDS round trips: DPP quad/row rotations
-// reduce each 16-lane row, then the four row totals are combined through readlane
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float rlane(float v, int l) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
-__device__ __forceinline__ float gsum32(float v) {
-  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dppf<0x124>(v);  // row_ror:4
-  v += dppf<0x128>(v);  // row_ror:8
-  const float lo = rlane(v, 0) + rlane(v, 16), hi = rlane(v, 32) + rlane(v, 48);
-  return (threadIdx.x & 32) ? hi : lo;
-}
-// all-reduce over 8-lane groups: quad xor 1, 2 then row_half_mirror (lane i <-> 7 - i)
-__device__ __forceinline__ float gsum8(float v) {
-  v += dppf<0xB1>(v);
-  v += dppf<0x4E>(v);
-  return v + dppf<0x141>(v);
-}
-__device__ __forceinline__ float gmax32(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));
-  v = fmaxf(v, dppf<0x4E>(v));
-  v = fmaxf(v, dppf<0x124>(v));
-  v = fmaxf(v, dppf<0x128>(v));
-  const float lo = fmaxf(rlane(v, 0), rlane(v, 16)), hi = fmaxf(rlane(v, 32), rlane(v, 48));
-  return (threadIdx.x & 32) ? hi : lo;
-}
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // ---- register-resident weight operands -------------------------------------------------------
 // Frag<KS, CT>: the B operand of v_mfma_f32_16x16x4_f32 for KS k-steps of this wave's column tiles
