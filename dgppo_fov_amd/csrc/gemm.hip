@@ -178,104 +178,123 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(dgppo_gemm_args p) {
 
 
 // ================================================================================================
-// rows: C = alpha * A op(B) + ... for M large, N <= 32 * NT, K <= kRowsMaxK
+// rows: C = alpha * A op(B) + beta C + bias + addend (relu) for M large, N <= 192, K <= kRowsMaxK.
+// op(B) (K x N, rows zero-padded to a multiple of 16) is staged once per workgroup in LDS.  The work
+// unit is one WAVE's (32-row panel, group of NTW 32-column tiles); waves walk the units round-robin
+// (u = 4 block + wave + k * 4 grid, column group fastest, so the waves of a workgroup share their A
+// panel through L2) -- fine-grained units keep every SIMD busy to the end instead of leaving a
+// partially filled last round of whole-panel workgroups.  A is read 32 contiguous bytes per lane:
+// in k-chunk c (16 values) lane half h holds k = 16 c + 8 h .. +7, i.e. MFMA k-step q of the chunk
+// is k = 16 c + 8 h + q in half h (B rows follow the same map), so both halves of a row read one
+// 64-byte run.  Chunk c + 1 (or the next unit's chunk 0) is in flight while chunk c's MFMAs issue;
+// the first chunk is requested before B is staged.
 // ================================================================================================
 constexpr int kRowsMaxK = 256;
-constexpr int kRowsLdsFloats = 12800;  // 50 KB: K * (N + 1) must fit
+constexpr int kRowsLdsFloats = 12800;  // 50 KB: K16 * (N + 1) must fit
 
-template <int NT, bool VEC>
-__global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
-  extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K][NP] k-major, NP = 32 NT + 1
-  constexpr int NP = 32 * NT + 1;
+template <int NTW, bool VEC>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int ncg) {
+  extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
+  const int NC = 32 * NTW * ncg, NP = NC + 1;
   const int K = p.K, N = p.N, M = p.M;
-  const int Kh = (K + 1) >> 1;
+  const int K16 = (K + 15) & ~15;
   const int b = blockIdx.z;
   const float* A = p.A + (int64_t)b * p.stride_a;
   const float* B = p.B + (int64_t)b * p.stride_b;
-  // stage op(B) (K x N) into LDS, zero-padded to 32 NT columns and 2 Kh rows; 16 independent loads
-  // in flight per thread before their stores (one L2 round trip per 4096 elements, not per 256)
-  {
-    const int total = 2 * Kh * 32 * NT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int panels = (M + 31) / 32;
+  const int64_t nunits = (int64_t)panels * ncg;
+  const int64_t ustep = (int64_t)gridDim.x * 4;
+  const int nch = K16 / 16;
+  auto row_ptr = [&](int64_t uu, bool& rok) -> const float* {
+    const int row = (int)(uu / ncg) * 32 + i;
+    rok = uu < nunits && row < M;
+    return A + (rok ? row_off(row, p.lda, p.a_grp, p.a_gstride) : 0) + 8 * h;
+  };
+  auto load8 = [&](const float* Ar, bool rok, int c, float (&a)[8]) {
+    const int k0 = 16 * c + 8 * h;
+    if (VEC) {  // K % 8 == 0 and 16-byte aligned rows: a lane's 8 values are all in or all out
+      const bool ok = rok && k0 < K;
+      const float4 v0 = ok ? *(const float4*)(Ar + 16 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v1 = ok ? *(const float4*)(Ar + 16 * c + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w;
+      a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = (rok && k0 + q < K) ? Ar[16 * c + q] : 0.0f;
+    }
+  };
+  int64_t u = (int64_t)blockIdx.x * 4 + wave;
+  bool rok;
+  const float* Ar = row_ptr(u, rok);
+  float a0[8], a1[8];
+  load8(Ar, rok, 0, a0);  // the first unit's first chunk is requested before B is staged
+  {  // stage op(B): 16 independent loads in flight per thread before their stores.  Index split
+     // e -> (major, minor) by a float reciprocal (exact: e < 2^16, divisor <= 256) -- an integer
+     // division per element would cost more VALU time than the whole GEMM's MFMAs
+    const int total = K16 * NC;
+    const int dv = p.trans_b ? K16 : NC;  // minor extent
+    const float inv = 1.0f / (float)dv;
     for (int e0 = threadIdx.x; e0 < total; e0 += 256 * 16) {
       float v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int e = e0 + u * 256;
-        int k, n;
-        if (p.trans_b) { k = e % (2 * Kh); n = e / (2 * Kh); }  // stored (N, K): k fastest
-        else { n = e % (32 * NT); k = e / (32 * NT); }         // stored (K, N): n fastest
-        v[u] = (e < total && k < K && n < N)
-                   ? (p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k]
-                                : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n])
-                   : 0.0f;
+      for (int uu = 0; uu < 16; ++uu) {
+        const int e = e0 + uu * 256;
+        const int mj = (int)(((float)e + 0.5f) * inv), mn = e - mj * dv;
+        const int k = p.trans_b ? mn : mj, n = p.trans_b ? mj : mn;
+        v[uu] = (e < total && k < K && n < N)
+                    ? (p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k]
+                                 : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n])
+                    : 0.0f;
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int e = e0 + u * 256;
+      for (int uu = 0; uu < 16; ++uu) {
+        const int e = e0 + uu * 256;
         if (e < total) {
-          int k, n;
-          if (p.trans_b) { k = e % (2 * Kh); n = e / (2 * Kh); }
-          else { n = e % (32 * NT); k = e / (32 * NT); }
-          Bs[k * NP + n] = v[u];
+          const int mj = (int)(((float)e + 0.5f) * inv), mn = e - mj * dv;
+          const int k = p.trans_b ? mn : mj, n = p.trans_b ? mj : mn;
+          Bs[k * NP + n] = v[uu];
         }
       }
     }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 31, h = lane >> 5;
-  const int kofs = h * Kh;
   float* C = p.C + (int64_t)b * p.stride_c;
-  const float* D = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
-  const int panels = (M + 127) / 128;
-  for (int panel = blockIdx.x; panel < panels; panel += gridDim.x) {
-    const int m0 = panel * 128 + wave * 32;
-    const int arow = m0 + i;
-    const bool rok = arow < M;
-    const float* Ar = A + (rok ? row_off(arow, p.lda, p.a_grp, p.a_gstride) : 0) + kofs;
-    f32x16 acc[NT];
+  const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  for (; u < nunits; u += ustep) {
+    const int panel = (int)(u / ncg), cg = (int)(u - (int64_t)panel * ncg);
+    const int m0 = panel * 32;
+    f32x16 acc[NTW];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NTW; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-    // A values in chunks of 8 per lane, double-buffered: chunk j+1's loads are in flight while
-    // chunk j's MFMAs run
-    auto load8 = [&](int kb, float (&a)[8]) {
-      if (VEC) {  // Kh % 8 == 0, rows 16-byte aligned
-        const float4 v0 = (rok && kb < Kh) ? *(const float4*)(Ar + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 v1 = (rok && kb < Kh) ? *(const float4*)(Ar + kb + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w;
-        a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
+    const float* bcol = Bs + 8 * h * NP + cg * 32 * NTW + i;
+    bool rokn = false;
+    const float* Arn = Ar;
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) {
+        load8(Ar, rok, c + 1, a1);
       } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int kk = kb + q;
-          a[q] = (rok && kk < Kh && kofs + kk < K) ? Ar[kk] : 0.0f;
-        }
+        Arn = row_ptr(u + ustep, rokn);
+        load8(Arn, rokn, 0, a1);
       }
-    };
-    auto mma8 = [&](int kb, const float (&a)[8]) {
+      const float* brow = bcol + 16 * c * NP;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int kk = kb + q;
-        if (!VEC && kk >= Kh) break;
-        const float* brow = Bs + (kofs + kk) * NP + i;
+      for (int q = 0; q < 8; ++q)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], brow[32 * t], acc[t], 0, 0, 0);
-      }
-    };
-    float a0[8], a1[8];
-    load8(0, a0);
-    for (int kb = 0; kb < Kh; kb += 8) {
-      load8(kb + 8, a1);  // zeros past Kh
-      mma8(kb, a0);
+        for (int t = 0; t < NTW; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[q], brow[q * NP + 32 * t], acc[t], 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < 8; ++q) a0[q] = a1[q];
     }
-    // epilogue: lane holds column (t*32 + i), rows (r&3) + 8 (r>>2) + 4 h of this wave's 32
+    Ar = Arn;
+    rok = rokn;
+    // epilogue: lane holds column (cg NTW + t) 32 + i, rows (r&3) + 8 (r>>2) + 4 h of the panel
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = t * 32 + i;
+    for (int t = 0; t < NTW; ++t) {
+      const int col = (cg * NTW + t) * 32 + i;
       if (col >= N) continue;
       const float bv = p.bias ? p.bias[col] : 0.0f;
 #pragma unroll
@@ -286,7 +305,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p) {
           float v = p.alpha * acc[t][r];
           if (p.beta != 0.0f) v += p.beta * *cp;
           v += bv;
-          if (D) v += D[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
+          if (Dd) v += Dd[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
           if (p.relu) v = v > 0.0f ? v : 0.0f;
           *cp = v;
         }
@@ -468,7 +487,7 @@ GemmPath gemm_path(const dgppo_gemm_args* p) {
   if (!p->trans_a && p->N <= 192 && p->K <= dgppo::kRowsMaxK) {
     int nt = (p->N + 31) / 32;
     if (nt == 5) nt = 6;
-    if (2 * ((p->K + 1) / 2) * (32 * nt + 1) <= dgppo::kRowsLdsFloats) return kPathRows;
+    if (((p->K + 15) & ~15) * (32 * nt + 1) <= dgppo::kRowsLdsFloats) return kPathRows;
   }
   return kPathTile;
 }
@@ -511,28 +530,37 @@ launched:
   return 0;
 }
 
-template <int NT>
-void launch_rows_t(const dgppo_gemm_args* p, hipStream_t s) {
-  const int Kh = (p->K + 1) / 2;
-  const size_t lds = (size_t)2 * Kh * (32 * NT + 1) * sizeof(float);
-  const int panels = (p->M + 127) / 128;
-  const int grid = panels < 1024 ? panels : 1024;
-  const bool vec = (Kh % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
+// column-tile groups: NTW tiles per wave unit, ncg groups across N
+void rows_split(int N, int* ntw, int* ncg) {
+  const int nt = (N + 31) / 32;  // two tiles per unit keep the operands within 168 registers
+  if (nt <= 2) { *ntw = nt; *ncg = 1; }
+  else if (nt == 3) { *ntw = 1; *ncg = 3; }
+  else { *ntw = 2; *ncg = (nt + 1) / 2; }
+}
+
+template <int NTW>
+void launch_rows_t(const dgppo_gemm_args* p, int ncg, hipStream_t s) {
+  const int K16 = (p->K + 15) & ~15;
+  const size_t lds = (size_t)K16 * (32 * NTW * ncg + 1) * sizeof(float);
+  const int64_t units = (int64_t)((p->M + 31) / 32) * ncg;
+  int per_cu = (int)((160 * 1024) / (lds > 0 ? lds : 1));
+  per_cu = per_cu < 1 ? 1 : per_cu > 5 ? 5 : per_cu;
+  const int64_t want = (units + 3) / 4, cap = 256LL * per_cu;
+  const int grid = (int)(want < cap ? want : cap);
+  const bool vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
                    (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
   if (vec)
-    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NT, true>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p);
+    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, true>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
   else
-    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NT, false>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p);
+    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, false>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
 }
 
 int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {
-  switch ((p->N + 31) / 32) {
-    case 1: launch_rows_t<1>(p, s); return 0;
-    case 2: launch_rows_t<2>(p, s); return 0;
-    case 3: launch_rows_t<3>(p, s); return 0;
-    case 4: launch_rows_t<4>(p, s); return 0;
-    case 5:
-    case 6: launch_rows_t<6>(p, s); return 0;
+  int ntw, ncg;
+  rows_split(p->N, &ntw, &ncg);
+  switch (ntw) {
+    case 1: launch_rows_t<1>(p, ncg, s); return 0;
+    case 2: launch_rows_t<2>(p, ncg, s); return 0;
   }
   return DGPPO_EINVAL;
 }
