@@ -59,6 +59,8 @@ class EnvCfg(ctypes.Structure):
         ("c_mpe_obs_goal", ctypes.c_float),
         ("c_mpe_obs_lo", ctypes.c_float),
         ("c_mpe_obs_hi", ctypes.c_float),
+        ("t2_comm", ctypes.c_float),
+        ("t2_lidar", ctypes.c_float),
     ]
 
 
@@ -201,6 +203,7 @@ SIGNATURES = {
     "dgppo_env_cfg_finalize": (ctypes.c_int, [ctypes.POINTER(EnvCfg)]),
     "dgppo_ray_table": (ctypes.c_int, [ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]),
     "dgppo_env_step": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvStepIO), ctypes.c_void_p]),
+    "dgppo_env_set_step_kernel": (ctypes.c_int, [ctypes.c_int]),
     "dgppo_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvResetIO), ctypes.c_void_p]),
     "dgppo_gemm_workspace_floats": (ctypes.c_int64, [ctypes.POINTER(GemmArgs)]),
     "dgppo_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), ctypes.c_void_p]),

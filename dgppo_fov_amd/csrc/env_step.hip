@@ -20,6 +20,9 @@
 //                env/utils.py:139-244
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
 
 #include "../../include/dgppo_hip.h"
 #include "math32.h"
@@ -530,6 +533,556 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
   write_graph<ENGINE, GOAL, SD>(cfg, d, lds + cv.nxt, goal, third, out, vec4, tid, BLOCK);
 }
 
+// Rectangle.inside with r = 0 (raytracing's is_in): the rounded-corner term sqrt(.) < 0 never holds
+__device__ __forceinline__ bool rect_inside0(const float* rec, float px, float py) {
+  const float rel_x = px - rec[0];
+  const float rel_y = py - rec[1];
+  const float c = rec[5], s = rec[6];
+  const float rel_xx = fabsf(rel_x * c + rel_y * s) - rec[2] / 2.0f;
+  const float rel_yy = fabsf(rel_x * s - rel_y * c) - rec[3] / 2.0f;
+  return (rel_xx < 0.0f) & (rel_yy < 0.0f);
+}
+
+// ---- wave-per-env Lidar step (n = 8 agents, R = 32 rays, top-k = 8) ----------------------------
+// The BASELINE Lidar configs (LidarSpread / LidarTarget / LidarBicycleTarget, n = 8): one 64-lane
+// wave owns one environment end to end, so no phase needs a workgroup barrier (LDS hand-offs
+// between the lanes of one wave only need wave_sync) and 4096 envs are resident at once (16 waves
+// per CU).  Lane l maps to the pair (i = l / 8, j = l % 8): the 64 agent-agent, 64 goal-agent and
+// 64 agent-hit distances are one value per lane, row minima are 3 DPP steps, and each lane owns
+// 4 of its agent's 32 rays (r = 4 (l % 8) + q) for the sort.
+//
+// Exact ray culling.  Rectangle.raytracing of a (ray, obstacle) pair is exactly 1e6 in the
+// reference whenever no edge can be valid and no alpha is NaN.  A triple (agent, obstacle, ray) is
+// skipped (left at 1e6) only when all of the following hold, evaluated with NaN-false comparisons:
+//   * the obstacle is "eligible": its 4 corners lie in [-2, 2]^2 and its circumradius rho <= 0.5;
+//     the agent position lies in [-2, 2]^2 and the ray vector |d| <= 1;
+//   * for all 4 edges the IDEAL determinant |d_y e_x - d_x e_y| >= kDetMin = 1e-3 (the computed
+//     det then differs by < 5e-7, so no clipping, no det == 0, no NaN);
+//   * the segment S -> S + d misses the disc (c, rho + kCullMargin), kCullMargin = 0.01 (capsule test).
+// With every coordinate in [-2, 2] the numerators carry < 1.4e-6 (na) / 2.4e-6 (nb) absolute error,
+// so computed alpha / beta differ from the exact line parameters by < 2e-3 / 3e-3 near [0, 1]:
+// alpha, beta in [0, 1] would put the two segments within 2e-3 |d| + 3e-3 |e| <= 5e-3 < kCullMargin
+// of each other.  Every skipped triple is therefore provably the reference's 1e6.  All other triples
+// (~65 of 768 per env at the bench distribution) go to a compacted work list, pooled over the 4 envs
+// of a workgroup, and run the exact per-edge arithmetic (raytrace_nodiv / rect_raytrace), combined
+// per ray with an LDS atomic min on an order-preserving encoding (NaN wins, as jnp.min).
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"  // branch-free predicates on purpose
+namespace wv {
+constexpr int NA = 8, NR = 32, NK = 8;
+constexpr float kCullMargin = 0.01f;
+constexpr float kDetMin = 1e-3f;
+constexpr uint32_t kEncMiss = 0x49742400u + 1u;  // enc(1e6f)
+
+// order-preserving encoding of a ray's alpha (>= +0, 1e6 or NaN) for an LDS atomic min; NaN wins
+__device__ __forceinline__ uint32_t enc_alpha(float a) { return a != a ? 0u : __float_as_uint(a) + 1u; }
+__device__ __forceinline__ float dec_alpha(uint32_t e) {
+  return e == 0u ? __builtin_nanf("") : __uint_as_float(e - 1u);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float rlf(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// min_nan over each 8-lane group: quad xor 1, xor 2, row_half_mirror
+__device__ __forceinline__ float min8(float v) {
+  v = min_nan(v, dpp<0xB1>(v));
+  v = min_nan(v, dpp<0x4E>(v));
+  return min_nan(v, dpp<0x141>(v));
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Rectangle.raytracing (env/obstacle.py:74-105) of one ray against one obstacle WITHOUT the two
+// per-edge divisions, bit-identical to the reference.  With detc = sign(det) clip(|det|, 1e-7, 1e7)
+// = +-cl and na' = sign(det) na, nb' = sign(det) nb (exact sign flips):
+//   fl(na / detc) >= 0  <=>  na' >= 0     (unless 0 < |na'| < 1e-30: a tiny negative could round to -0)
+//   fl(na / detc) <= 1  <=>  na' <= cl    (round-to-nearest: fl(x) <= 1 <=> x <= 1 + 2^-24, and the
+//                                          float after cl exceeds cl (1 + 2^-24))
+// so validity needs no quotient.  The smallest valid alpha is picked by exact-order cross products
+// (fl(a c) < fl(b d) implies a/d <= b/c, and fl of the quotient is monotone), and divided once.
+// NaN: the reference's alpha is NaN iff det == 0 / NaN or na is NaN (0 * inf, NaN propagation).
+// Returns false for the cases this does not decide (denormal or > 1e30 numerators, tied cross
+// products); the caller then runs the literal per-edge code (rect_raytrace).
+__device__ __forceinline__ bool raytrace_nodiv(const float4 pA, const float4 pB, const float4 eA, const float4 eB,
+                                               float x1, float y1, float ax, float ay, float* out) {
+  const float px3[4] = {pA.x, pA.z, pB.x, pB.z}, py3[4] = {pA.y, pA.w, pB.y, pB.w};
+  const float ex[4] = {eA.x, eA.z, eB.x, eB.z}, ey[4] = {eA.y, eA.w, eB.y, eB.w};
+  float bn = 0.0f, bc = 1.0f;
+  bool has = false, nan = false, weird = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float px = x1 - px3[e], py = y1 - py3[e];
+    const float det = ax * ey[e] - ay * ex[e];
+    const float na = ey[e] * px - ex[e] * py;
+    const float nb = (-ay) * px + ax * py;
+    const float adet = fabsf(det);
+    nan = nan | !(adet > 0.0f) | (na != na);
+    const float cl = fminf(fmaxf(adet, 1e-7f), 1e7f);
+    const bool neg = det < 0.0f;
+    const float nap = neg ? -na : na, nbp = neg ? -nb : nb;
+    const float ana = fabsf(na), anb = fabsf(nb);
+    weird = weird | (ana > 1e30f) | ((ana < 1e-30f) & (ana != 0.0f)) | ((anb < 1e-30f) & (anb != 0.0f));
+    const bool valid = (nap >= 0.0f) & (nap <= cl) & (nbp >= 0.0f) & (nbp <= cl);
+    const float p1 = nap * bc, p2 = bn * cl;
+    weird = weird | (valid & has & (p1 == p2));
+    const bool better = valid & (!has | (p1 < p2));
+    bn = better ? nap : bn;
+    bc = better ? cl : bc;
+    has = has | valid;
+  }
+  *out = nan ? __builtin_nanf("") : (has ? bn / bc + 0.0f : 1e6f);
+  return !weird;
+}
+
+// per-wave LDS carve (floats); every region 16-byte aligned
+template <int SD, int O>
+struct Carve {
+  static constexpr int N = 2 * NA + NA * NK + 1;
+  static constexpr int ND = SD + 3;
+  static constexpr int cur = 0;  // agents (8 SD) then goals (8 SD)
+  static constexpr int nxt = cur + 16 * SD;
+  static constexpr int obst = nxt + ((NA * SD + 3) & ~3);
+  static constexpr int evec = obst + O * DGPPO_OBST_FIELDS;
+  static constexpr int rays = evec + O * 8;
+  static constexpr int alpha = rays + 2 * NR;  // (8, 32) encoded alphas (uint32)
+  static constexpr int hits = alpha + NA * NR;  // (8, 8, 2)
+  static constexpr int olist = hits + NA * NK * 2;  // compacted non-miss rays
+  static constexpr int uni = olist + NA * NR;  // union: items | keys
+  static constexpr int key_stride = 2 * NR + 4;  // dwords per agent row of 64-bit keys (bank-padded)
+  static constexpr int n_items = NA * O * NR;
+  static constexpr int uni_size = n_items + 64 > NA * key_stride ? n_items + 64 : NA * key_stride;
+  static_assert(rays - obst >= 64, "the 64-lane obstacle staging store stays below the ray table");
+  static constexpr int total = (uni + uni_size + 3) & ~3;
+};
+
+template <int ENGINE, int GOAL, int SD, int O>
+__global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+  static_assert(O >= 1 && O <= 4, "obstacle records are staged by one load per lane");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int wg_items[4];
+  using C = Carve<SD, O>;
+  constexpr int N = C::N, ND = C::ND, pad = N - 1;
+  constexpr int n_ag = GOAL == DGPPO_GOAL_SPREAD ? NA * NA : NA;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int64_t env_raw = (int64_t)blockIdx.x * 4 + wid;
+  // a wave past the last env replays the last env without storing anything: it must still join
+  // the two workgroup barriers around the pooled ray cast
+  const bool live = env_raw < io.n_env;
+  const int64_t env = live ? env_raw : io.n_env - 1;
+  float* lds = smem + wid * C::total;
+  const int gi = lane >> 3, gj = lane & 7;
+
+  // ---- A: every global load first (unconditional, clamped addresses), then stage in LDS -------
+  const float* st = io.states + env * io.states_stride;
+  const float* ob = io.obstacles + env * io.obstacles_stride;
+  const float* ac = io.action + env * io.action_stride;
+  const float cv0 = st[lane];
+  const float cv1 = SD == 5 ? st[64 + (lane & 15)] : 0.0f;
+  const float hcx = st[(16 + lane) * SD + 0], hcy = st[(16 + lane) * SD + 1];
+  const float obv = ob[lane < O * DGPPO_OBST_FIELDS ? lane : 0];
+  const float rdv = io.ray_dirs[lane];
+  const float a0 = clampf_nan(ac[2 * gj + 0], -1.0f, 1.0f), a1 = clampf_nan(ac[2 * gj + 1], -1.0f, 1.0f);
+  // unconditional LDS stores: a store under a lane predicate lets the compiler sink its global load
+  // into the predicated block, serialising a second HBM round trip
+  lds[C::cur + lane] = cv0;
+  if (SD == 5) lds[C::cur + 64 + (lane & 15)] = cv1;
+  lds[C::obst + lane] = obv;  // lanes >= 16 O land in evec / rays, both written after this
+  lds[C::rays + lane] = rdv;
+  wave_sync();
+  const float* cur = lds + C::cur;
+  const float* goal = cur + NA * SD;
+  float* nxt = lds + C::nxt;
+  float* hits = lds + C::hits;
+  const float* obst = lds + C::obst;
+  const float* evec = lds + C::evec;
+  const float* rays = lds + C::rays;
+
+  // ---- B: dynamics of agent j (every lane; lanes 0..7 store it), distances, edge vectors -------
+  float x[SD];
+#pragma unroll
+  for (int c = 0; c < SD; ++c) x[c] = cur[gj * SD + c];
+  const float cix = cur[gi * SD], ciy = cur[gi * SD + 1];
+  const float gix = goal[gi * SD], giy = goal[gi * SD + 1];
+  float ev;
+  {
+    const int o = (lane >> 3) < O ? (lane >> 3) : 0, e = (lane >> 1) & 3, c = lane & 1;
+    const float* rec = obst + o * DGPPO_OBST_FIELDS;
+    ev = rec[8 + 2 * ((e + 3) & 3) + c] - rec[8 + 2 * e + c];  // (x4 - x3, y4 - y3)
+  }
+  float y[SD];
+  if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+    const float theta = atan2_32(x[3], x[2]);
+    const float theta_next = theta + ((x[4] * a0) * cfg.dt) * 10.0f;
+    float st_, ct_, sn_, cn_;
+    sincos32(theta, &st_, &ct_);
+    sincos32(theta_next, &sn_, &cn_);
+    y[0] = x[0] + (x[4] * ct_) * cfg.dt;
+    y[1] = x[1] + (x[4] * st_) * cfg.dt;
+    y[2] = cn_;
+    y[3] = sn_;
+    y[4] = x[4] + (a1 * cfg.dt) * 10.0f;
+  } else {
+    y[0] = x[2] * cfg.dt + x[0];
+    y[1] = x[3] * cfg.dt + x[1];
+    y[2] = (a0 * 10.0f) * cfg.dt + x[2];
+    y[3] = (a1 * 10.0f) * cfg.dt + x[3];
+  }
+#pragma unroll
+  for (int c = 0; c < SD; ++c) y[c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+  if (lane < NA) {
+#pragma unroll
+    for (int c = 0; c < SD; ++c) nxt[lane * SD + c] = y[c];
+  }
+  if (lane < O * 8) lds[C::evec + lane] = ev;
+  const float an = norm2(a0, a1);
+  const float a2 = an * an;
+  float daa = norm2(cix - x[0], ciy - x[1]);
+  if (gi == gj) daa = daa + 1e6f;
+  const float dga = GOAL == DGPPO_GOAL_SPREAD ? norm2(gix - x[0], giy - x[1]) : norm2(gix - cix, giy - ciy);
+  const float dh = norm2(hcx - cix, hcy - ciy);
+  const float md = min8(daa), dg = min8(dga), mo = min8(dh);
+
+  // ---- C: cost (lanes j < 2 of group i), reward (lane 0) -----------------------------------
+  {
+    float c0 = cfg.c_agent_cost - md;
+    float c1 = cfg.c_obs_cost - mo;
+    c0 = c0 <= 0.0f ? c0 - 0.5f : c0 + 0.5f;
+    c1 = c1 <= 0.0f ? c1 - 0.5f : c1 + 0.5f;
+    c0 = clampf_nan(c0, -1.0f, 1.0f);
+    c1 = clampf_nan(c1, -1.0f, 1.0f);
+    if (live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = gj == 0 ? c0 : c1;
+    const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
+    float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      sd_ = sd_ + rlf(dg, 8 * i);
+      sf = sf + rlf(far, 8 * i);
+      sa = sa + rlf(a2, i);  // lane i holds agent j = i
+    }
+    if (live & (lane == 0)) {
+      const float nn = (float)NA;
+      float r = 0.0f - (sd_ / nn) * 0.01f;
+      r = r - (sf / nn) * 0.001f;
+      r = r - (sa / nn) * 0.0001f;
+      io.reward[env * io.reward_stride] = r;
+    }
+  }
+  wave_sync();  // nxt, evec visible
+
+  // ---- F1: the graph parts that do not depend on the lidar, issued as store packets spread over
+  // the compute phases below so the HBM drains them while the ray cast runs (one burst would stall
+  // every wave on a full store queue at once)
+  float* no = io.nodes + env * io.nodes_stride;
+  float* so = io.out_states + env * io.out_states_stride;
+  float* eo = io.edges + env * io.edges_stride;
+  int32_t* ro = io.receivers + env * io.edge_index_stride;
+  int32_t* sno = io.senders + env * io.edge_index_stride;
+  const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
+  auto put = [&](int e, float f0, float f1, float f2, float f3, int rv, int sv) {
+    if (vec4) {
+      reinterpret_cast<float4*>(eo)[e] = make_float4(f0, f1, f2, f3);
+    } else {
+      eo[4 * e + 0] = f0;
+      eo[4 * e + 1] = f1;
+      eo[4 * e + 2] = f2;
+      eo[4 * e + 3] = f3;
+    }
+    ro[e] = rv;
+    sno[e] = sv;
+  };
+  float si[SD];
+#pragma unroll
+  for (int c = 0; c < SD; ++c) si[c] = nxt[gi * SD + c];
+  if (live) {  // store packet 1: agent-agent edges
+    float sj[SD];
+#pragma unroll
+    for (int c = 0; c < SD; ++c) sj[c] = y[c];  // this lane's dynamics result is agent j's next state
+    {  // agent-agent row l: mask norm + (comm_radius + 1 on the diagonal) < comm_radius, on |d|^2
+      float f2, f3;
+      if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+        f2 = si[4] * si[2] - sj[4] * sj[2];
+        f3 = si[4] * si[3] - sj[4] * sj[3];
+      } else {
+        f2 = si[2] - sj[2];
+        f3 = si[3] - sj[3];
+      }
+      const float dx = si[0] - sj[0], dy = si[1] - sj[1];
+      const float d2 = dx * dx + dy * dy;
+      const bool m = gi == gj ? ((d2 == 0.0f) & (cfg.c_self_dist < cfg.comm_radius)) : (d2 < cfg.t2_comm);
+      put(lane, dx, dy, f2, f3, m ? gi : pad, m ? gj : pad);
+    }
+  }
+
+  // ---- D: is-inside at the next state; culling masks; capsule tests -> item list -------------
+  const float sxi = si[0], syi = si[1];
+  const int oi = gj < O ? gj : 0;
+  const bool in_o = (gj < O) & rect_inside0(obst + oi * DGPPO_OBST_FIELDS, sxi, syi);
+  const uint64_t in_mask = __ballot(in_o);
+  const int rr = lane & 31;
+  const float rdx = rays[2 * rr], rdy = rays[2 * rr + 1];
+  const float rlen2 = rdx * rdx + rdy * rdy;
+  // obstacle o = lane (< O): circumradius (raw v_sqrt: the culling bounds carry margins) and eligibility
+  float rho_l;
+  uint64_t elig_mask;
+  {
+    const int o = lane < O ? lane : 0;
+    const float4* rec4 = reinterpret_cast<const float4*>(obst + o * DGPPO_OBST_FIELDS);
+    const float4 c4 = rec4[0], pA = rec4[2], pB = rec4[3];
+    const float pxs[4] = {pA.x, pA.z, pB.x, pB.z}, pys[4] = {pA.y, pA.w, pB.y, pB.w};
+    float r2 = 0.0f;
+    bool elig = (fabsf(c4.x) <= 2.0f) & (fabsf(c4.y) <= 2.0f);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      elig = elig & (fabsf(pxs[p]) <= 2.0f) & (fabsf(pys[p]) <= 2.0f);
+      const float dx = pxs[p] - c4.x, dy = pys[p] - c4.y;
+      r2 = fmaxf(r2, dx * dx + dy * dy);
+    }
+    rho_l = __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-6f;
+    elig = elig & (rho_l <= 0.5f);
+    elig_mask = __ballot(elig & (lane < O));
+  }
+  const float rlen = __builtin_amdgcn_sqrtf(rlen2) * 1.0001f;
+  uint32_t unsafe[O];
+#pragma unroll
+  for (int pass = 0; pass < (O + 1) / 2; ++pass) {  // (obstacle 2 pass + half, ray lane & 31)
+    const int o = 2 * pass + (lane >> 5) < O ? 2 * pass + (lane >> 5) : 0;
+    const float4* e4 = reinterpret_cast<const float4*>(evec + o * 8);
+    const float4 eA = e4[0], eB = e4[1];
+    const float exs[4] = {eA.x, eA.z, eB.x, eB.z}, eys[4] = {eA.y, eA.w, eB.y, eB.w};
+    bool safe = (((elig_mask >> o) & 1ull) != 0ull) & (rlen <= 1.0f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) safe = safe & (fabsf(rdy * exs[e] - rdx * eys[e]) >= kDetMin);
+    const uint64_t b = __ballot(!safe);
+    unsafe[2 * pass] = (uint32_t)b;
+    if (2 * pass + 1 < O) unsafe[2 * pass + 1] = (uint32_t)(b >> 32);
+  }
+  if (live) {  // store packet 2: agent-goal edges
+    float sj[SD], sg[SD];
+#pragma unroll
+    for (int c = 0; c < SD; ++c) {
+      sj[c] = y[c];
+      sg[c] = goal[gj * SD + c];
+    }
+    if (GOAL == DGPPO_GOAL_SPREAD) {  // agent i -> goal j
+      float f2, f3;
+      if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+        f2 = si[4] * si[2] - sg[4] * sg[2];
+        f3 = si[4] * si[3] - sg[4] * sg[3];
+      } else {
+        f2 = si[2] - sg[2];
+        f3 = si[3] - sg[3];
+      }
+      put(NA * NA + lane, si[0] - sg[0], si[1] - sg[1], f2, f3, gi, NA + gj);
+    } else if (lane < NA) {  // agent j -> own goal j
+      float f2, f3;
+      if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+        f2 = sj[4] * sj[2] - sg[4] * sg[2];
+        f3 = sj[4] * sj[3] - sg[4] * sg[3];
+      } else {
+        f2 = sj[2] - sg[2];
+        f3 = sj[3] - sg[3];
+      }
+      put(NA * NA + lane, sj[0] - sg[0], sj[1] - sg[1], f2, f3, lane, NA + lane);
+    }
+  }
+  // capsule test of every (agent, obstacle, ray) triple: pair p = o * 8 + i, 2 pairs per step (lane
+  // halves), o and i = 2 m + half known per step; survivors -> compacted item list
+  int n_items = 0;
+  {
+    int* items = reinterpret_cast<int*>(lds + C::uni);
+    const int h = lane >> 5;
+    float qx[4], qy[4];
+    bool qok[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      qx[m] = nxt[(2 * m + h) * SD];
+      qy[m] = nxt[(2 * m + h) * SD + 1];
+      qok[m] = (fabsf(qx[m]) <= 2.0f) & (fabsf(qy[m]) <= 2.0f);
+    }
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      const float cx = obst[o * DGPPO_OBST_FIELDS], cy = obst[o * DGPPO_OBST_FIELDS + 1];
+      const float Rl = (rlf(rho_l, o) + kCullMargin) * rlen;
+      const bool forced = (unsafe[o] >> rr) & 1u;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float vx = cx - qx[m], vy = cy - qy[m];
+        const float perp = vx * rdy - vy * rdx;
+        const float proj = vx * rdx + vy * rdy;
+        const bool miss = qok[m] & ((fabsf(perp) > Rl) | (proj < -Rl) | (proj > rlen2 + Rl));
+        const bool keep = (!miss | forced) & live;
+        const uint64_t kb = __ballot(keep);
+        if (keep) items[n_items + mbcnt(kb)] = ((o * 8 + 2 * m + h) << 5) | rr;
+        n_items += __popcll(kb);
+      }
+    }
+  }
+  if (live) {  // store packet 3: node / state rows of agents and goals, pad rows
+    // node rows 0..15 (agents, goals) and the pad row; state rows 0..15 and the pad row
+#pragma unroll
+    for (int k = 0; k < (16 * ND + 63) / 64; ++k) {
+      const int idx = lane + 64 * k;
+      const int r = idx / ND, c = idx - (idx / ND) * ND;
+      const int rs = r < 16 ? r : 15;
+      const float* src = rs < NA ? nxt + rs * SD : goal + (rs - NA) * SD;
+      const float sv = src[c < SD ? c : 0];
+      const float v = c < SD ? sv : (c == SD + 2 ? (r < NA ? 1.0f : 0.0f) : (c == SD + 1 ? (r < NA ? 0.0f : 1.0f) : 0.0f));
+      if (idx < 16 * ND) no[idx] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < (16 * SD + 63) / 64; ++k) {
+      const int idx = lane + 64 * k;
+      const int r = idx / SD, c = idx - (idx / SD) * SD;
+      const int rs = r < 16 ? r : 15;
+      const float v = (rs < NA ? nxt + rs * SD : goal + (rs - NA) * SD)[c];
+      if (idx < 16 * SD) so[idx] = v;
+    }
+    if (lane < ND) no[pad * ND + lane] = 0.0f;
+    if (lane < SD) so[pad * SD + lane] = -1.0f;
+  }
+  uint32_t* alpha = reinterpret_cast<uint32_t*>(lds + C::alpha);
+  reinterpret_cast<uint4*>(alpha)[lane] = make_uint4(kEncMiss, kEncMiss, kEncMiss, kEncMiss);
+  if (lane == 0) wg_items[wid] = n_items;
+  __syncthreads();  // item lists of the 4 envs of this workgroup are complete
+
+  // exact ray cast of the surviving triples, pooled over the workgroup's 4 envs (balances the
+  // per-env item counts; each item atomically min-combines into its own env's alpha row)
+  {
+    const int c0 = wg_items[0], c1 = wg_items[1], c2 = wg_items[2], c3 = wg_items[3];
+    const int s1 = c0, s2 = c0 + c1, s3 = c0 + c1 + c2, tot = s3 + c3;
+    for (int base = wid * 64; base < tot; base += 256) {
+      const int g = base + lane;
+      const bool act = g < tot;
+      const int gg = act ? g : 0;
+      const int w2 = gg < s1 ? 0 : (gg < s2 ? 1 : (gg < s3 ? 2 : 3));
+      const int k = gg - (w2 == 0 ? 0 : (w2 == 1 ? s1 : (w2 == 2 ? s2 : s3)));
+      float* L = smem + w2 * C::total;
+      const int it = reinterpret_cast<const int*>(L + C::uni)[k];
+      const int r = it & 31, p = (it >> 5) & 31, o = (p >> 3) < O ? (p >> 3) : 0, i = p & 7;
+      const float sx = L[C::nxt + i * SD + 0], sy = L[C::nxt + i * SD + 1];
+      const float2 rd = reinterpret_cast<const float2*>(L + C::rays)[r];
+      const float* rec = L + C::obst + o * DGPPO_OBST_FIELDS;
+      const float* evo = L + C::evec + o * 8;
+      const float4* rec4 = reinterpret_cast<const float4*>(rec);
+      const float4* e4 = reinterpret_cast<const float4*>(evo);
+      const float ex = sx + rd.x, ey = sy + rd.y;
+      float a;
+      const bool ok = raytrace_nodiv(rec4[2], rec4[3], e4[0], e4[1], sx, sy, sx - ex, sy - ey, &a);
+      if (act & !ok) a = rect_raytrace(rec, evo, sx, sy, sx - ex, sy - ey);
+      if (act) atomicMin(reinterpret_cast<uint32_t*>(L + C::alpha) + i * NR + r, enc_alpha(a));
+    }
+  }
+  if (live) {  // store packet 4: constant columns of the hit rows and lidar edges
+    // hit row 16 + lane and agent-lidar edge row n*n + n_ag + lane: every column except the hit
+    // coordinates / edge offsets is a constant ([., ., 0.. | obs 1, goal 0, agent 0], [., ., 0, 0])
+#pragma unroll
+    for (int c = 2; c < ND; ++c) no[(16 + lane) * ND + c] = c == SD ? 1.0f : 0.0f;
+#pragma unroll
+    for (int c = 2; c < SD; ++c) so[(16 + lane) * SD + c] = 0.0f;
+    eo[4 * (NA * NA + n_ag + lane) + 2] = 0.0f;
+    eo[4 * (NA * NA + n_ag + lane) + 3] = 0.0f;
+  }
+  __syncthreads();  // every alpha row is final
+
+  // ---- E: sort keys; misses ranked by popcount, the rest by comparison; top-k hit points ------
+  uint64_t* keys = reinterpret_cast<uint64_t*>(lds + C::uni);  // items are dead now
+  int* olist = reinterpret_cast<int*>(lds + C::olist);
+  const float isin = ((in_mask >> (8 * gi)) & 0xFFull) ? 1.0f : 0.0f;
+  int n_other = 0;
+  {
+    const uint4 e4 = reinterpret_cast<const uint4*>(alpha + gi * NR)[gj];
+    const float4 rA = reinterpret_cast<const float4*>(rays)[2 * gj], rB = reinterpret_cast<const float4*>(rays)[2 * gj + 1];
+    const uint32_t ev4[4] = {e4.x, e4.y, e4.z, e4.w};
+    const float rx[4] = {rA.x, rA.z, rB.x, rB.z}, ry[4] = {rA.y, rA.w, rB.y, rB.w};
+    float av[4], hx[4], hy[4];
+    bool miss[4];
+    uint32_t sm[4];
+    int hf = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      av[q] = dec_alpha(ev4[q]) * (1.0f - isin);
+      miss[q] = av[q] == 1e6f;
+      const float ex = sxi + rx[q], ey = syi + ry[q];
+      hx[q] = sxi + (ex - sxi) * av[q];
+      hy[q] = syi + (ey - syi) * av[q];
+      sm[q] = (uint32_t)(__ballot(miss[q]) >> (8 * gi)) & 0xFFu;
+      hf += __builtin_popcount((uint32_t)(__ballot(!miss[q] & (av[q] == av[q])) >> (8 * gi)) & 0xFFu);
+    }
+    uint64_t* krow = keys + gi * (C::key_stride / 2);
+    reinterpret_cast<ulonglong2*>(krow)[2 * gj] = make_ulonglong2(sort_key(av[0], 4 * gj), sort_key(av[1], 4 * gj + 1));
+    reinterpret_cast<ulonglong2*>(krow)[2 * gj + 1] = make_ulonglong2(sort_key(av[2], 4 * gj + 2), sort_key(av[3], 4 * gj + 3));
+    const uint32_t below = (1u << gj) - 1u;
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cnt += __builtin_popcount(sm[q] & below);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rank = hf + cnt;
+      if (miss[q] & (rank < NK)) {
+        hits[(gi * NK + rank) * 2 + 0] = hx[q];
+        hits[(gi * NK + rank) * 2 + 1] = hy[q];
+      }
+      cnt += (sm[q] >> gj) & 1u;
+      const uint64_t obq = __ballot(!miss[q]);
+      if (!miss[q]) olist[n_other + mbcnt(obq)] = gi * NR + 4 * gj + q;
+      n_other += __popcll(obq);
+    }
+  }
+  wave_sync();
+  for (int base = 0; base < n_other; base += 64) {
+    const int t = base + lane;
+    const int v = olist[t];  // past n_other: stale words (olist is followed by the key region)
+    const int i = (v >> 5) & 7, r = v & 31;
+    const uint64_t* krow = keys + i * (C::key_stride / 2);
+    const uint64_t key = krow[r];
+    const float a = dec_alpha(alpha[i * NR + r]) * (((in_mask >> (8 * i)) & 0xFFull) ? 0.0f : 1.0f);
+    const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
+    const float2 rd = reinterpret_cast<const float2*>(rays)[r];
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < NR; j += 2) {
+      const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(krow + j);
+      rank += kk.x < key ? 1 : 0;
+      rank += kk.y < key ? 1 : 0;
+    }
+    if ((t < n_other) & (rank < NK)) {
+      const float ex = sx + rd.x, ey = sy + rd.y;
+      hits[(i * NK + rank) * 2 + 0] = sx + (ex - sx) * a;
+      hits[(i * NK + rank) * 2 + 1] = sy + (ey - sy) * a;
+    }
+  }
+  wave_sync();
+  if (!live) return;
+
+  // ---- F2: the lidar-dependent columns: hit coordinates, agent-lidar edge offsets and masks -------
+  {
+    const float2 hl = reinterpret_cast<const float2*>(hits)[lane];
+    const float f0 = si[0] - hl.x;
+    const float f1 = si[1] - hl.y;
+    const bool m = f0 * f0 + f1 * f1 < cfg.t2_lidar;  // norm < comm_radius - 0.1, on |d|^2
+    const int e = NA * NA + n_ag + lane;
+    eo[4 * e + 0] = f0;
+    eo[4 * e + 1] = f1;
+    ro[e] = m ? gi : pad;
+    sno[e] = m ? 2 * NA + lane : pad;
+    no[(16 + lane) * ND + 0] = hl.x;
+    no[(16 + lane) * ND + 1] = hl.y;
+    so[(16 + lane) * SD + 0] = hl.x;
+    so[(16 + lane) * SD + 1] = hl.y;
+  }
+}
+
+}  // namespace wv
+
 // ---- reset ------------------------------------------------------------------------------------
 // Thread 0 runs the reference's sequential rejection sampler for its env (reset is once per
 // episode, amortised over T = 128 steps); then the whole workgroup ray-casts and writes the graph.
@@ -719,6 +1272,18 @@ static int validate(const dgppo_env_cfg* c) {
   return 0;
 }
 
+// Step-kernel selection: 0 = auto (wave-per-env kernel where the config allows), 1 = the
+// workgroup-per-env kernel everywhere.  Initialised from DGPPO_ENV_STEP_KERNEL=block|auto, changed
+// by dgppo_env_set_step_kernel (A/B timing and kernel-vs-kernel parity tests).
+static int g_step_kernel = -1;
+static bool wave_step_enabled() {
+  if (g_step_kernel < 0) {
+    const char* v = getenv("DGPPO_ENV_STEP_KERNEL");
+    g_step_kernel = (v && strcmp(v, "block") == 0) ? 1 : 0;
+  }
+  return g_step_kernel == 0;
+}
+
 // ---- launch helpers ---------------------------------------------------------------------------
 template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
 static void launch_step(const dgppo_env_cfg& c, const dgppo_env_step_io& io, size_t shmem, hipStream_t s) {
@@ -793,6 +1358,17 @@ extern "C" const char* dgppo_build_info(void) {
   return "libdgppo_hip gfx950 abi=" "1" " env_step+env_reset (fp-contract=off)";
 }
 
+// smallest fp32 x with sqrtf(x) >= r (IEEE sqrt is correctly rounded and monotone, so for every
+// x >= 0: sqrtf(x) < r  <=>  x < t; NaN compares false on both sides)
+static float sq_threshold(float r) {
+  if (!(r > 0.0f)) return 0.0f;
+  if (!(r < INFINITY)) return INFINITY;
+  float x = r * r;
+  while (x > 0.0f && sqrtf(x) >= r) x = nextafterf(x, 0.0f);
+  while (!(sqrtf(x) >= r)) x = nextafterf(x, INFINITY);
+  return x;
+}
+
 extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
   if (!c) return DGPPO_EINVAL;
   const bool mpe = c->engine == DGPPO_ENGINE_MPE;
@@ -829,6 +1405,8 @@ extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
   if (c->c_mpe_obs_goal == 0.f) c->c_mpe_obs_goal = (float)(r * 2 + orr);
   if (c->c_mpe_obs_lo == 0.f) c->c_mpe_obs_lo = (float)(r * 3);
   if (c->c_mpe_obs_hi == 0.f) c->c_mpe_obs_hi = (float)(c->area_size - r * 3);
+  c->t2_comm = sq_threshold(c->comm_radius);
+  c->t2_lidar = sq_threshold(c->c_lidar_active);
   return validate(c);
 }
 
@@ -853,6 +1431,14 @@ extern "C" int dgppo_ray_table(int32_t n_rays, float sense_range, float* out) {
   return 0;
 }
 
+extern "C" int dgppo_env_set_step_kernel(int mode) {
+  if (mode < 0 || mode > 1) return DGPPO_EINVAL;
+  wave_step_enabled();
+  const int prev = g_step_kernel;
+  g_step_kernel = mode;
+  return prev;
+}
+
 extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
   if (io->n_env == 0) return 0;
@@ -861,6 +1447,22 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
     return DGPPO_EINVAL;
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  if (lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
+      wave_step_enabled()) {
+    const dim3 grid((unsigned)((io->n_env + 3) / 4)), block(256);
+    const hipStream_t s = (hipStream_t)stream;
+    const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
+    if (cfg->engine == DGPPO_ENGINE_BICYCLE) {
+      const size_t sh = 4 * sizeof(float) * wv::Carve<5, 3>::total;
+      if (spread) hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5, 3>), grid, block, sh, s, *cfg, *io);
+      else hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5, 3>), grid, block, sh, s, *cfg, *io);
+    } else {
+      const size_t sh = 4 * sizeof(float) * wv::Carve<4, 3>::total;
+      if (spread) hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4, 3>), grid, block, sh, s, *cfg, *io);
+      else hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4, 3>), grid, block, sh, s, *cfg, *io);
+    }
+    return (int)hipGetLastError();
+  }
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                  cfg->engine != DGPPO_ENGINE_MPE);
   const size_t shmem = (size_t)cv.total * sizeof(float);

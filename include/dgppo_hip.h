@@ -70,6 +70,10 @@ typedef struct dgppo_env_cfg {
   float c_inside_r;     /* min_dist / 2                         (env/utils.py:173, 195) */
   float c_mpe_obs_agent, c_mpe_obs_goal; /* car+obs radius, 2*car+obs radius (mpe/base.py:104-105) */
   float c_mpe_obs_lo, c_mpe_obs_hi;     /* 3*car radius, area - 3*car radius (mpe/base.py:97-98) */
+  /* Squared-distance thresholds (filled by finalize): the smallest fp32 x with sqrt(x) >= r, so the
+   * reference's `norm(d) < r` masks are decided exactly as `|d|^2 < t2` (sqrt is correctly rounded
+   * and monotone).  t2_comm: r = comm_radius (agent-agent edges); t2_lidar: r = c_lidar_active. */
+  float t2_comm, t2_lidar;
 } dgppo_env_cfg;
 
 /* Fills n_nodes / n_edges / node_dim / state_lo/hi and zero derived constants from the other
@@ -108,6 +112,12 @@ typedef struct dgppo_env_step_io {
 } dgppo_env_step_io;
 
 int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io* io, void* stream);
+
+/* Step-kernel selection (no reference counterpart; both kernels are bit-identical): 0 = auto (the
+ * wave-per-env kernel for Lidar n=8 / 32 rays / top-8 / 3 obstacles, the workgroup-per-env kernel
+ * otherwise), 1 = workgroup-per-env everywhere.  Returns the previous mode or DGPPO_EINVAL.
+ * Initial mode: DGPPO_ENV_STEP_KERNEL=block|auto (default auto). */
+int dgppo_env_set_step_kernel(int mode);
 
 /* Batched reset: replaces `vmap(env.reset)(keys)` —
  *   LidarEnv.reset dgppo/env/lidar_env/base.py:89-124, LidarBicycleTarget.reset

@@ -194,3 +194,87 @@ def test_env_shards_equal_global_slices(cuda, eid, n, obs):
     nf = env.step(full, a)
     npart = env.step(part, a[4:].contiguous())
     assert torch.equal(nf.graph.nodes[4:], npart.graph.nodes) and torch.equal(nf.reward[4:], npart.reward)
+
+
+def _adversarial_lidar_inputs(env, spec, B, seed, cuda):
+    """Inputs aimed at the wave kernel's exact ray culling: tiny / huge / ineligible
+    obstacles, edges exactly parallel to a ray, NaN and far-away corners, agents at corners and
+    centres (inside -> alpha 0), agents crowded around one obstacle (> k hits), NaN actions."""
+    rng = np.random.default_rng(seed)
+    g = env.reset(key=seed, n_env=B)
+    states = _np(g.states).copy()
+    ob = _np(g.env_states.obstacle.packed).copy()
+    n = spec.n
+    rays = O.ray_table(spec.n_rays, 0.5)
+    kind = np.arange(B) % 8
+    for b in range(B):
+        k = kind[b]
+        if k == 0:  # random sizes spanning eligibility (rho <= 0.5) and tiny boxes, exact axis angles
+            wh = rng.choice([1e-4, 0.05, 0.3, 0.69, 0.9], size=(3, 2))
+            th = rng.choice([0.0, np.pi / 2, np.pi, rng.uniform(0, 2 * np.pi)], size=3)
+            ob[b] = O.make_rectangles(rng.uniform(0, 1.5, (3, 2)), wh[:, 0], wh[:, 1], th)
+        elif k == 1:  # agents exactly on corners / centres of obstacles
+            for i in range(n):
+                o = i % 3
+                p = ob[b, o, 8 + 2 * (i % 4):10 + 2 * (i % 4)] if i < 4 else ob[b, o, :2]
+                states[b, i, :2] = np.clip(p, 0, 1.5)
+                states[b, i, 2:4] = 0.0
+        elif k == 2:  # obstacle 0 = parallelogram whose first edge is exactly 2 x ray r
+            r = rng.integers(0, spec.n_rays)
+            c = states[b, 0, :2] + rays[(r + 8) % spec.n_rays] * 0.6
+            e1 = rays[r] * np.float32(2.0)
+            e2 = rays[(r + 8) % spec.n_rays] * np.float32(0.5)
+            p0 = c.astype(np.float32)
+            pts = np.stack([p0, p0 - e1, p0 - e1 - e2, p0 - e2]).astype(np.float32)
+            ob[b, 0, 8:] = pts.reshape(-1)
+            ob[b, 0, :2] = pts.mean(0)
+        elif k == 3:  # NaN corner and far / huge obstacles
+            ob[b, 0, 8] = np.nan
+            ob[b, 1, 8:] = ob[b, 1, 8:] + np.float32(1e3)
+            ob[b, 2, 8:] = ob[b, 2, 8:] * np.float32(3.0)
+        elif k == 4:  # everyone crowded around obstacle 0
+            states[b, :n, :2] = ob[b, 0, :2] + rng.uniform(-0.25, 0.25, (n, 2)).astype(np.float32)
+            states[b, :n, :2] = np.clip(states[b, :n, :2], 0, 1.5)
+        elif k == 5:  # agent on the ray line through a corner
+            r = rng.integers(0, spec.n_rays)
+            states[b, 0, :2] = np.clip(ob[b, 1, 8:10] - rays[r] * np.float32(0.5), 0, 1.5)
+            states[b, 0, 2:4] = 0.0
+    a = rng.uniform(-1, 1, (B, n, 2)).astype(np.float32)
+    a[kind == 1] = 0.0
+    a[kind == 5, 0] = 0.0
+    a[6, 0, 0] = np.nan
+    gin = env._assemble(g.nodes, g.edges, torch.from_numpy(states).to(cuda), g.receivers, g.senders,
+                        torch.from_numpy(ob).to(cuda))
+    return gin, states, ob, a
+
+
+@pytest.mark.parametrize("eid", ["LidarSpread", "LidarTarget", "LidarBicycleTarget"])
+def test_wave_step_kernel_adversarial(cuda, eid):
+    """The wave-per-env step kernel (exact ray culling + compacted ray cast) against the oracle and
+    against the workgroup-per-env kernel, bit for bit, on adversarial inputs."""
+    from dgppo_fov_amd import _lib
+
+    n, obs, B = 8, 3, 256
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    spec = O.Spec(eid, n, obs)
+    gin, states, ob, a = _adversarial_lidar_inputs(env, spec, B, 77, cuda)
+    at = torch.from_numpy(a).to(cuda)
+    lib = _lib.load()
+    prev = lib.dgppo_env_set_step_kernel(0)
+    try:
+        res = env.step(gin, at)
+        lib.dgppo_env_set_step_kernel(1)
+        res_blk = env.step(gin, at)
+    finally:
+        lib.dgppo_env_set_step_kernel(max(prev, 0))
+    torch.cuda.synchronize()
+    ref = O.env_step(spec, states, ob, a)
+    for f in ("nodes", "edges", "states", "receivers", "senders"):
+        x, y = getattr(res.graph, f), getattr(res_blk.graph, f)
+        same = (x == y) | (torch.isnan(x) & torch.isnan(y)) if x.is_floating_point() else (x == y)
+        assert bool(same.all()), f"wave vs block kernel: {f}"
+    assert_graph_equal(res.graph, ref, f"{eid} adversarial")
+    c, rc = _np(res.cost), ref["cost"]
+    assert np.array_equal(np.isnan(c), np.isnan(rc)) and np.array_equal(c[~np.isnan(c)], rc[~np.isnan(rc)])
+    r, rr = _np(res.reward), ref["reward"]
+    assert np.array_equal(np.isnan(r), np.isnan(rr)) and np.array_equal(r[~np.isnan(r)], rr[~np.isnan(rr)])
