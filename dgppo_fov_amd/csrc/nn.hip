@@ -486,77 +486,88 @@ __global__ __launch_bounds__(64) void partial_reduce_kernel(const float* part, i
   }
 }
 
-// ---- Dec-OCP GAE (algo/utils.py:11-79), literal reverse scan; one workgroup per env ------------
-// lanes over the (T+1)-long rows; the carry rows live in LDS.
-__global__ __launch_bounds__(256) void gae_kernel(dgppo_gae_args p) {
+// ---- Dec-OCP GAE (dgppo/algo/utils.py:11-79), one 256-thread workgroup per env ----------------
+// The reference scans the data from time T-1 down to 0 (lax.scan(reverse=True) over
+// ts = arange(T)[::-1]) and its loop variable ii = T-1-k COUNTS the steps: at step ii the rows
+// 0..ii of the (T+1)-row table are live, row t holds an n-step backup (n = ii - t + 1 for t >= 1,
+// ii + 1 for t = 0) and the output is Q[k] = sum_t c_ii[t] row[t] with c_ii[0] = lambda^ii and
+// c_ii[t] = lambda^(ii-t) (1 - lambda) (the rolled coefficient vector, closed form).  Every row
+// entry evolves independently, so thread (column q, chunk c) keeps the entries t = c + C e of
+// column q in registers (columns: the n*nh Vh heads, then the Vl column); the weighted sum is a
+// reduction over the C lanes of the column.  The env's inputs are staged in LDS once, so the T
+// sequential steps never wait on HBM.  Work is O(T^2) per column like the reference's row update
+// (its max(.) is not reducible to an O(T) recursion).
+template <int EPL>
+__global__ __launch_bounds__(256) void gae_kernel(dgppo_gae_args p, int C) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
-  const int T = p.T, n = p.n_agents, nh = p.n_h, Tp1 = T + 1;
-  const int K = n * nh;
-  float* vh_row = sh;                    // (T+1, K)
-  float* vl_row = vh_row + Tp1 * K;      // (T+1)
-  float* coef = vl_row + Tp1;            // (T+1)
-  float* red = coef + Tp1;               // (4 waves, K + 1)
+  const int T = p.T, n = p.n_agents, nh = p.n_h, K = n * nh, Tp1 = T + 1;
+  float* s_hs = sh;                 // (T, K)
+  float* s_Vh = s_hs + T * K;       // (T+1, K)
+  float* s_l = s_Vh + Tp1 * K;      // (T)
+  float* s_Vl = s_l + T;            // (T+1)
+  float* s_pw = s_Vl + Tp1;         // lambda^j, j = 0..T
+  float* s_pw1 = s_pw + Tp1;        // lambda^j (1 - lambda)
   const int64_t b = blockIdx.x;
-  const float* hs = p.hs + b * (int64_t)T * K;        // (T, n, nh)
-  const float* l = p.l + b * (int64_t)T;              // (T)
-  const float* Vh = p.Vh + b * (int64_t)Tp1 * K;      // (T+1, n, nh)
-  const float* Vl = p.Vl + b * (int64_t)Tp1;          // (T+1)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int t = tid; t < Tp1 * K; t += 256) vh_row[t] = t < K ? Vh[T * K + t] : 0.0f;
-  for (int t = tid; t < Tp1; t += 256) {
-    vl_row[t] = t == 0 ? Vl[T] : 0.0f;
-    coef[t] = t == 0 ? 1.0f : 0.0f;
+  const int tid = threadIdx.x;
+  {
+    const float* hs = p.hs + b * (int64_t)T * K;
+    const float* Vh = p.Vh + b * (int64_t)Tp1 * K;
+    for (int i = tid; i < T * K; i += 256) s_hs[i] = hs[i];
+    for (int i = tid; i < Tp1 * K; i += 256) s_Vh[i] = Vh[i];
+    for (int i = tid; i < T; i += 256) s_l[i] = p.l[b * T + i];
+    for (int i = tid; i < Tp1; i += 256) {
+      s_Vl[i] = p.Vl[b * Tp1 + i];
+      const float pw = powf(p.lambda, (float)i);
+      s_pw[i] = pw;
+      s_pw1[i] = pw * (1.0f - p.lambda);
+    }
   }
   __syncthreads();
-  const float gamma = p.gamma, lam = p.lambda;
-  for (int ii = T - 1; ii >= 0; --ii) {
-    // new rows (masked), weighted sums with the current coefficients
-    float acc[33];
-    for (int q = 0; q <= K; ++q) acc[q] = 0.0f;
-    const float lv = l[ii];
-    for (int t = tid; t < Tp1; t += 256) {
-      const bool m = t < ii + 1;
-      const float c = coef[t];
-      for (int a = 0; a < n; ++a) {
-        float hmax = hs[(int64_t)ii * K + a * nh];
-        for (int h = 1; h < nh; ++h) hmax = fmaxf(hmax, hs[(int64_t)ii * K + a * nh + h]);
-        for (int h = 0; h < nh; ++h) {
-          const int q = a * nh + h;
-          const float hv = hs[(int64_t)ii * K + q];
-          const float disc = (1.0f - gamma) * hmax + gamma * vh_row[t * K + q];
-          const float nv = m ? fmaxf(hv, disc) : 0.0f;
-          vh_row[t * K + q] = nv;
-          acc[q] += nv * c;
-        }
+  const int q = tid / C, c = tid - (tid / C) * C;
+  if (q > K) return;  // padding columns (no barrier below)
+  const bool is_l = q == K;
+  const int a = is_l ? 0 : q / nh;
+  const float gamma = p.gamma, omg = 1.0f - p.gamma;
+  float row[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) row[e] = 0.0f;
+  if (c == 0) row[0] = is_l ? s_Vl[T] : s_Vh[T * K + q];  // row 0 = V(x_T)
+  for (int ii = 0; ii < T; ++ii) {
+    const int k = T - 1 - ii;
+    float hv = 0.0f, hmax = 0.0f, lv = 0.0f;
+    if (is_l) {
+      lv = s_l[k];
+    } else {
+      hv = s_hs[k * K + q];
+      hmax = s_hs[k * K + a * nh];
+      for (int h = 1; h < nh; ++h) hmax = fmaxf(hmax, s_hs[k * K + a * nh + h]);
+    }
+    const float base = omg * hmax;
+    float acc = 0.0f;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      if (e * C > ii) break;  // uniform: no live entry left in this or later slots
+      const int t = c + C * e;
+      if (t <= ii) {
+        const float r = is_l ? lv + gamma * row[e] : fmaxf(hv, base + gamma * row[e]);
+        row[e] = r;
+        acc += (t == 0 ? s_pw[ii] : s_pw1[ii - t]) * r;
       }
-      const float nl = m ? lv + gamma * vl_row[t] : 0.0f;
-      vl_row[t] = nl;
-      acc[K] += nl * c;
     }
-    for (int q = 0; q <= K; ++q) {
-      const float s = wave_sum(acc[q]);
-      if (lane == 0) red[wave * (K + 1) + q] = s;
+    for (int o = 1; o < C; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (c == 0) {
+      if (is_l) p.Ql[b * T + k] = acc;
+      else p.Qh[(b * T + k) * K + q] = acc;
     }
-    __syncthreads();
-    if (tid <= K) {
-      const float s = red[tid] + red[(K + 1) + tid] + red[2 * (K + 1) + tid] + red[3 * (K + 1) + tid];
-      if (tid < K) p.Qh[(b * T + ii) * K + tid] = s;
-      else p.Ql[b * T + ii] = s;
+    // row ii + 1 <- V(x_k) for the next step
+    const int t1 = ii + 1;
+    if (c == t1 % C) {
+      const float v = is_l ? s_Vl[k] : s_Vh[k * K + q];
+      const int e1 = t1 / C;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e)
+        if (e == e1) row[e] = v;
     }
-    // row ii+1 <- current values; roll the coefficients
-    for (int q = tid; q < K; q += 256) vh_row[(ii + 1) * K + q] = Vh[(int64_t)ii * K + q];
-    if (tid == 0) vl_row[ii + 1] = Vl[ii];
-    __syncthreads();
-    float cprev = 0.0f;
-    for (int t = tid; t < Tp1; t += 256) cprev = t == 0 ? coef[T] : coef[t - 1];
-    __syncthreads();
-    for (int t = tid; t < Tp1; t += 256) {
-      float c = cprev;
-      if (t == 0) c = powf(lam, (float)(ii + 1));
-      if (t == 1) c = powf(lam, (float)ii) * (1.0f - lam);
-      coef[t] = c;
-    }
-    __syncthreads();
   }
 }
 
@@ -850,13 +861,35 @@ extern "C" int dgppo_l2_loss(const float* pred, const float* target, int64_t n, 
 }
 
 extern "C" int dgppo_gae(const dgppo_gae_args* p, void* stream) {
-  if (!p || p->B < 0 || p->T < 1 || p->T > 255 || p->n_agents < 1 || p->n_h < 1 || p->n_agents * p->n_h > 32 ||
-      !p->hs || !p->l || !p->Vh || !p->Vl || !p->Qh || !p->Ql)
+  if (!p || p->B < 0 || p->T < 1 || p->T > 1024 || p->n_agents < 1 || p->n_h < 1 || !p->hs || !p->l || !p->Vh ||
+      !p->Vl || !p->Qh || !p->Ql)
     return DGPPO_EINVAL;
+  const int K = p->n_agents * p->n_h, T = p->T;
+  if (K > 255) return DGPPO_EINVAL;
+  // LDS staging of one env: hs, Vh, l, Vl and the two coefficient tables
+  const size_t shmem = ((size_t)T * K + (size_t)(T + 1) * K + T + 3 * (size_t)(T + 1)) * sizeof(float);
+  if (shmem > 160 * 1024) return DGPPO_EINVAL;
   if (p->B == 0) return 0;
-  const int K = p->n_agents * p->n_h;
-  const size_t shmem = ((size_t)(p->T + 1) * (K + 2) + 4 * (K + 1)) * sizeof(float);
-  hipLaunchKernelGGL(gae_kernel, dim3((unsigned)p->B), dim3(256), shmem, DG_STREAM(stream), *p);
+  int Kp = 1;
+  while (Kp < K + 1) Kp <<= 1;
+  const int C = 256 / Kp < 64 ? 256 / Kp : 64;  // lanes per column (one wave holds a whole column)
+  const int epl = (T + 1 + C - 1) / C;
+  const dim3 grid((unsigned)p->B), block(256);
+  const hipStream_t s = DG_STREAM(stream);
+  if (shmem > 64 * 1024) {
+    static bool raised = false;
+    if (!raised) {
+      const void* fns[4] = {(const void*)gae_kernel<16>, (const void*)gae_kernel<32>, (const void*)gae_kernel<64>,
+                            (const void*)gae_kernel<128>};
+      for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised = true;
+    }
+  }
+  if (epl <= 16) hipLaunchKernelGGL(gae_kernel<16>, grid, block, shmem, s, *p, C);
+  else if (epl <= 32) hipLaunchKernelGGL(gae_kernel<32>, grid, block, shmem, s, *p, C);
+  else if (epl <= 64) hipLaunchKernelGGL(gae_kernel<64>, grid, block, shmem, s, *p, C);
+  else if (epl <= 128) hipLaunchKernelGGL(gae_kernel<128>, grid, block, shmem, s, *p, C);
+  else return DGPPO_EINVAL;
   return (int)hipGetLastError();
 }
 

@@ -352,7 +352,9 @@ int dgppo_ppo_loss(const float* log_pi, const float* log_pi_old, const float* ad
 int dgppo_l2_loss(const float* pred, const float* target, int64_t n, float* dpred, float* loss, float* workspace,
                   void* stream);
 
-/* compute_dec_ocp_gae (dgppo/algo/utils.py:11-79), one workgroup per env */
+/* compute_dec_ocp_gae (dgppo/algo/utils.py:11-79), one workgroup per env; the reference's
+ * lax.scan(reverse=True) step counter drives the mask and coefficients.  Limits: n*nh <= 255,
+ * T <= 1024 and one env's inputs (T*K + (T+1)*K + 4T + 3 floats) within 160 KiB of LDS. */
 typedef struct dgppo_gae_args {
   int32_t B, T, n_agents, n_h;
   const float* hs;  /* (B, T, n, nh) costs */

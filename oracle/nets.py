@@ -186,6 +186,11 @@ def tanh_normal_entropy(mu, sd, eps_fixed):
 
 # ---- GAE (dgppo/algo/utils.py:11-79), literal restatement -----------------------------------
 def compute_dec_ocp_gae(Tah_hs, T_l, Tp1ah_Vh, Tp1_Vl, disc_gamma, gae_lambda):
+    """The reference scans `inps = (ts = arange(T)[::-1], hs, l, Vh, Vl)` with
+    `lax.scan(..., reverse=True)` (utils.py:73-76): the data are visited from time T-1 down to 0 while
+    the loop variable `ii` = ts[k] = T-1-k COUNTS the steps taken (0, 1, ..., T-1).  `ii` drives the
+    mask (rows 0..ii live) and the coefficient updates; `k` indexes the data and the output.  With this
+    reading Ql is exactly the textbook TD(lambda) return of l (tests/test_oracle_kat.py)."""
     T, n_agent, nh = Tah_hs.shape
     Tah_Vh, T_Vl = Tp1ah_Vh[:-1], np.repeat(Tp1_Vl[:-1][:, None], n_agent, axis=1)
     Vh_final, Vl_final = Tp1ah_Vh[-1], Tp1_Vl[-1]
@@ -196,15 +201,16 @@ def compute_dec_ocp_gae(Tah_hs, T_l, Tp1ah_Vh, Tp1_Vl, disc_gamma, gae_lambda):
     gae_coeffs = np.zeros(T + 1)
     gae_coeffs[0] = 1.0
     Qs = np.zeros((T, n_agent, nh + 1))
-    for ii in range(T - 1, -1, -1):
-        hs, l, Vhs, Vl = Tah_hs[ii], T_l[ii], Tah_Vh[ii], T_Vl[ii]
+    for k in range(T - 1, -1, -1):  # scan(reverse=True) order over the data
+        ii = T - 1 - k  # ts[k]
+        hs, l, Vhs, Vl = Tah_hs[k], T_l[k], Tah_Vh[k], T_Vl[k]
         mask = np.arange(T + 1) < ii + 1
         h_disc = hs.max(-1)
         disc_to_h = (1 - disc_gamma) * h_disc[None, :, None] + disc_gamma * next_Vhs_row
         Vhs_row = mask[:, None, None] * np.maximum(hs, disc_to_h)
         Vl_row = mask[:, None] * (l + disc_gamma * next_Vl_row)
         cat = np.concatenate([Vhs_row, Vl_row[:, :, None]], axis=-1)
-        Qs[ii] = np.einsum("tah,t->ah", cat, gae_coeffs)
+        Qs[k] = np.einsum("tah,t->ah", cat, gae_coeffs)
         Vhs_row = Vhs_row.copy()
         Vl_row = Vl_row.copy()
         Vhs_row[ii + 1] = Vhs

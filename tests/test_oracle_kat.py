@@ -196,3 +196,58 @@ def test_reset_invariants():
         assert np.all((p >= 0) & (p <= 1.5))
         assert np.all(ag[b, :, 2:] == 0)
         assert np.all((ob[b, :, 2:4] >= 0.1) & (ob[b, :, 2:4] <= 0.3))
+
+
+# ---- Dec-OCP GAE (dgppo/algo/utils.py:11-79, lax.scan(reverse=True) over ts = arange(T)[::-1]) ------
+def _gae_inputs(T=12, n=3, nh=2, seed=0):
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal((T, n, nh)), rng.standard_normal(T), rng.standard_normal((T + 1, n, nh)),
+            rng.standard_normal(T + 1))
+
+
+def test_gae_ql_is_textbook_td_lambda():
+    from oracle.nets import compute_dec_ocp_gae
+
+    hs, l, Vh, Vl = _gae_inputs()
+    g, lam = 0.99, 0.95
+    T = len(l)
+    G = np.zeros(T)
+    for t in range(T - 1, -1, -1):
+        G[t] = l[t] + g * (Vl[T] if t == T - 1 else (1 - lam) * Vl[t + 1] + lam * G[t + 1])
+    _, Ql = compute_dec_ocp_gae(hs, l, Vh, Vl, g, lam)
+    np.testing.assert_allclose(Ql, G, rtol=0, atol=1e-12)
+
+
+def test_gae_lambda_zero_and_one():
+    """lambda = 0: every target is the one-step backup; lambda = 1: the full-horizon backup."""
+    from oracle.nets import compute_dec_ocp_gae
+
+    hs, l, Vh, Vl = _gae_inputs(T=7, n=2, nh=2, seed=3)
+    g = 0.9
+    T = len(l)
+    Qh, Ql = compute_dec_ocp_gae(hs, l, Vh, Vl, g, 0.0)
+    hmax = hs.max(-1, keepdims=True)
+    np.testing.assert_allclose(Ql, l + g * Vl[1:], atol=1e-12)
+    np.testing.assert_allclose(Qh, np.maximum(hs, (1 - g) * hmax + g * Vh[1:]), atol=1e-12)
+    Qh1, Ql1 = compute_dec_ocp_gae(hs, l, Vh, Vl, g, 1.0)
+    full_h = Vh[T]
+    full_l = Vl[T]
+    for t in range(T - 1, -1, -1):
+        full_h = np.maximum(hs[t], (1 - g) * hmax[t] + g * full_h)
+        full_l = l[t] + g * full_l
+        np.testing.assert_allclose(Qh1[t], full_h, atol=1e-12)
+        np.testing.assert_allclose(Ql1[t], full_l, atol=1e-12)
+
+
+def test_gae_two_steps_by_hand():
+    from oracle.nets import compute_dec_ocp_gae
+
+    hs, l, Vh, Vl = _gae_inputs(T=2, n=1, nh=2, seed=5)
+    g, lam = 0.99, 0.95
+    Qh, _ = compute_dec_ocp_gae(hs, l, Vh, Vl, g, lam)
+    hm = hs.max(-1, keepdims=True)
+    one1 = np.maximum(hs[1], (1 - g) * hm[1] + g * Vh[2])  # time 1: one-step
+    one0 = np.maximum(hs[0], (1 - g) * hm[0] + g * Vh[1])
+    two0 = np.maximum(hs[0], (1 - g) * hm[0] + g * one1)
+    np.testing.assert_allclose(Qh[1], one1, atol=1e-12)
+    np.testing.assert_allclose(Qh[0], lam * two0 + (1 - lam) * one0, atol=1e-12)

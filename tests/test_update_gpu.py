@@ -39,7 +39,7 @@ def _walk(a, b, path=""):
 
 
 # ---- GAE -------------------------------------------------------------------------------------
-@pytest.mark.parametrize("B,T,n,nh", [(3, 1, 1, 1), (2, 32, 3, 2), (2, 128, 8, 2), (1, 255, 16, 2)])
+@pytest.mark.parametrize("B,T,n,nh", [(3, 1, 1, 1), (2, 32, 3, 2), (2, 128, 8, 2), (1, 255, 16, 2), (1, 128, 32, 2), (2, 40, 1, 1)])
 def test_gae_matches_oracle(cuda, B, T, n, nh):
     rng = np.random.default_rng(T + n)
     hs = rng.standard_normal((B, T, n, nh)).astype(np.float32)
