@@ -14,7 +14,7 @@ PKG_DIR = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("DGPPO_HIP_LIB", PKG_DIR / "lib" / "libdgppo_hip.so"))
 
 DGPPO_EINVAL = -22
-DGPPO_ENGINE_LIDAR, DGPPO_ENGINE_BICYCLE, DGPPO_ENGINE_MPE = 0, 1, 2
+DGPPO_ENGINE_LIDAR, DGPPO_ENGINE_BICYCLE, DGPPO_ENGINE_MPE, DGPPO_ENGINE_OMNI = 0, 1, 2, 3
 DGPPO_GOAL_SPREAD, DGPPO_GOAL_TARGET = 0, 1
 DGPPO_OBST_FIELDS = 16
 
@@ -47,8 +47,8 @@ class EnvCfg(ctypes.Structure):
         ("obs_len_hi", ctypes.c_float),
         ("obs_theta_lo", ctypes.c_float),
         ("obs_theta_hi", ctypes.c_float),
-        ("state_lo", ctypes.c_float * 5),
-        ("state_hi", ctypes.c_float * 5),
+        ("state_lo", ctypes.c_float * 8),
+        ("state_hi", ctypes.c_float * 8),
         ("c_agent_cost", ctypes.c_float),
         ("c_obs_cost", ctypes.c_float),
         ("c_self_dist", ctypes.c_float),
@@ -61,6 +61,15 @@ class EnvCfg(ctypes.Structure):
         ("c_mpe_obs_hi", ctypes.c_float),
         ("t2_comm", ctypes.c_float),
         ("t2_lidar", ctypes.c_float),
+        ("edge_dim", ctypes.c_int32),
+        ("action_dim", ctypes.c_int32),
+        ("n_cost", ctypes.c_int32),
+        ("omni_max_w", ctypes.c_float),
+        ("fov_angle_deg", ctypes.c_float),
+        ("fov_rmax", ctypes.c_float),
+        ("fov_dmin", ctypes.c_float),
+        ("rot_pen", ctypes.c_float),
+        ("c_cos_fov", ctypes.c_float),
     ]
 
 

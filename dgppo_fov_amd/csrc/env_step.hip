@@ -1083,6 +1083,239 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
 
 }  // namespace wv
 
+// ---- LidarOmniTarget (dgppo/env/lidar_env/lidar_omni_target.py) --------------------------------
+// Omni-wheel agents [x, y, cos th, sin th, vx, vy, omega], actions [ax, ay, alpha], 5 costs
+// (agent collision, obstacle collision, FoV angle / max range / min distance on the chain i -> i+1),
+// 10-wide edge features [s_i - s_j (7) | critical i -> i+1 | ||p_j^i|| | i_x_j] with
+// p_j^i = R_i^T (p_j - p_i).  One workgroup per env (any n, O, R, k); the LiDAR is the Lidar
+// engines' lidar_scan.  Same graph layout as LidarTarget (own-goal edges), edge rows 10 wide.
+constexpr int kOmniSD = 7, kOmniED = 10, kOmniNC = 5;
+
+// nodes (N, 10), states (N, 7), edges (E, 10), receivers / senders (E) of the graph on `nxt`
+__device__ void write_graph_omni(const dgppo_env_cfg& cfg, int n, int k, bool lidar, const float* nxt,
+                                 const float* goal, const float* hits, GraphOut out, int tid, int nthr) {
+  constexpr int SD = kOmniSD, ND = SD + 3, ED = kOmniED;
+  const int nh = lidar ? n * k : 0;
+  const int N = 2 * n + nh + 1, E = n * n + n + nh, pad = N - 1;
+#pragma unroll 1
+  for (int idx = tid; idx < N * ND; idx += nthr) {
+    const int r = idx / ND, c = idx - (idx / ND) * ND;
+    float v = 0.0f;
+    if (r < n) v = c < SD ? nxt[r * SD + c] : (c == SD + 2 ? 1.0f : 0.0f);
+    else if (r < 2 * n) v = c < SD ? goal[(r - n) * SD + c] : (c == SD + 1 ? 1.0f : 0.0f);
+    else if (r < 2 * n + nh) v = c < 2 ? hits[(r - 2 * n) * 2 + c] : (c == SD ? 1.0f : 0.0f);
+    out.nodes[idx] = v;
+  }
+#pragma unroll 1
+  for (int idx = tid; idx < N * SD; idx += nthr) {
+    const int r = idx / SD, c = idx - (idx / SD) * SD;
+    float v;
+    if (r < n) v = nxt[r * SD + c];
+    else if (r < 2 * n) v = goal[(r - n) * SD + c];
+    else if (r < 2 * n + nh) v = c < 2 ? hits[(r - 2 * n) * 2 + c] : 0.0f;
+    else v = -1.0f;
+    out.states[idx] = v;
+  }
+#pragma unroll 1
+  for (int e = tid; e < E; e += nthr) {
+    float f[ED];
+#pragma unroll
+    for (int c = 0; c < ED; ++c) f[c] = 0.0f;
+    int rv, sv;
+    if (e < n * n) {  // agent-agent (lidar_omni_target.py:352-422)
+      const int i = e / n, j = e - (e / n) * n;
+      const float* si = nxt + i * SD;
+      const float* sj = nxt + j * SD;
+#pragma unroll
+      for (int c = 0; c < SD; ++c) f[c] = si[c] - sj[c];
+      f[7] = j == i + 1 ? 1.0f : 0.0f;
+      const float gx = -(si[0] - sj[0]), gy = -(si[1] - sj[1]);  // p_j - p_i
+      const float lx = si[2] * gx + si[3] * gy;                 // R_i^T (p_j - p_i)
+      const float ly = (-si[3]) * gx + si[2] * gy;
+      f[8] = norm2(lx, ly);
+      f[9] = lx;
+      const float dx = si[0] - sj[0], dy = si[1] - sj[1];
+      const float d2 = dx * dx + dy * dy;
+      const bool m = i == j ? ((d2 == 0.0f) & (cfg.c_self_dist < cfg.comm_radius)) : (d2 < cfg.t2_comm);
+      rv = m ? i : pad;
+      sv = m ? j : pad;
+    } else if (e < n * n + n) {  // own goal (lidar_omni_target.py:424-443), zero-padded
+      const int i = e - n * n;
+#pragma unroll
+      for (int c = 0; c < SD; ++c) f[c] = nxt[i * SD + c] - goal[i * SD + c];
+      rv = i;
+      sv = n + i;
+    } else {  // hits, masked at comm_radius (lidar_omni_target.py:446-489)
+      const int q = e - n * n - n, i = q / k;
+      f[0] = nxt[i * SD + 0] - hits[2 * q + 0];
+      f[1] = nxt[i * SD + 1] - hits[2 * q + 1];
+      const bool m = f[0] * f[0] + f[1] * f[1] < cfg.t2_comm;
+      rv = m ? i : pad;
+      sv = m ? 2 * n + q : pad;
+    }
+#pragma unroll
+    for (int c = 0; c < ED; ++c) out.edges[(int64_t)e * ED + c] = f[c];
+    out.recv[e] = rv;
+    out.send[e] = sv;
+  }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void omni_step_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int SD = kOmniSD, NC = kOmniNC;
+  const Dims<0, -1, 0, 0> d(cfg);
+  const int n = d.n, O = d.O, k = d.k;
+  const bool lidar = O > 0;
+  const Carve cv(n, SD, O, d.R, k, true);
+  const int nh = lidar ? n * k : 0;
+  const int n_ob = nh + 1;                                  // hit rows + the origin row (quirk, see oracle)
+  const int o_act = cv.total;                               // (n, 3) clipped actions
+  const int o_dd = o_act + ((3 * n + 3) & ~3);              // agent-agent distances (n, n)
+  const int o_do = o_dd + ((n * n + 3) & ~3);               // agent-obstacle-row distances (n, nh + 1)
+  const int o_red = o_do + ((n * n_ob + 3) & ~3);           // reward terms (5, n)
+  const int o_fov = o_red + 5 * n;                          // FoV costs (3, n)
+  const int tid = threadIdx.x;
+  const int64_t env = blockIdx.x;
+
+  // ---- A: stage agent / goal rows, every current hit, obstacles, clipped actions ------------------
+  const float* st = io.states + env * io.states_stride;
+  for (int idx = tid; idx < 2 * n * SD; idx += BLOCK) lds[cv.cur + idx] = st[idx];
+  for (int idx = tid; idx < nh * 2; idx += BLOCK) lds[cv.curhit + idx] = st[(2 * n + (idx >> 1)) * SD + (idx & 1)];
+  if (lidar) {
+    const float* ob = io.obstacles + env * io.obstacles_stride;
+    for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) lds[cv.obst + idx] = ob[idx];
+  }
+  const float* ac = io.action + env * io.action_stride;
+  for (int idx = tid; idx < 3 * n; idx += BLOCK) {  // action_lim (lidar_omni_target.py:511-521)
+    const float lim = (idx % 3) == 2 ? 1000.0f : 1.0f;
+    lds[o_act + idx] = clampf_nan(ac[idx], -lim, lim);
+  }
+  __syncthreads();
+
+  // ---- B: dynamics + per-agent reward terms + FoV costs; pairwise distance tasks ------------------
+  const float* cur = lds + cv.cur;
+  const float* goal = cur + n * SD;
+  const int n_task = n + n * n + n * n_ob;
+#pragma unroll 1
+  for (int q = tid; q < n_task; q += BLOCK) {
+    if (q < n) {
+      const int i = q;
+      const float* x = cur + i * SD;
+      const float* a = lds + o_act + 3 * i;
+      const float dt = cfg.dt;
+      // agent_step_euler (lidar_omni_target.py:146-197)
+      const float acc_x = a[0] * 10.0f, acc_y = a[1] * 10.0f, alpha = a[2] * 5.0f;
+      const float theta = atan2_32(x[3], x[2]);
+      const float new_theta = theta + x[6] * dt;
+      float sn, cn;
+      sincos32(new_theta, &sn, &cn);
+      const float y[SD] = {x[0] + x[4] * dt, x[1] + x[5] * dt, cn, sn, x[4] + acc_x * dt, x[5] + acc_y * dt,
+                           x[6] + alpha * dt};
+#pragma unroll
+      for (int c = 0; c < SD; ++c) lds[cv.nxt + i * SD + c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+      // get_reward terms (lidar_omni_target.py:295-336) on the pre-step graph
+      const float dg = norm2(goal[i * SD] - x[0], goal[i * SD + 1] - x[1]);
+      const float an = norm2(a[0], a[1]);
+      lds[o_red + i] = dg;
+      lds[o_red + n + i] = dg > cfg.dist2goal ? 1.0f : 0.0f;
+      lds[o_red + 2 * n + i] = an * an;
+      lds[o_red + 3 * n + i] = a[2] * a[2];
+      lds[o_red + 4 * n + i] = x[6] * x[6];
+      // FoV costs on the chain i -> i+1 (lidar_omni_target.py:577-631); the last agent is safe (-1)
+      float ha = -1.0f, hr = -1.0f, hc = -1.0f;
+      if (i + 1 < n) {
+        const float* xj = cur + (i + 1) * SD;
+        const float dx = xj[0] - x[0], dy = xj[1] - x[1];
+        const float lx = x[2] * dx + x[3] * dy;
+        const float ly = (-x[3]) * dx + x[2] * dy;
+        const float nrm = norm2(lx, ly);
+        ha = cfg.c_cos_fov * (nrm + 1e-8f) - lx;
+        hr = nrm - cfg.fov_rmax;
+        hc = cfg.fov_dmin - nrm;
+      }
+      lds[o_fov + i] = ha;
+      lds[o_fov + n + i] = hr;
+      lds[o_fov + 2 * n + i] = hc;
+      continue;
+    }
+    int t = q - n;
+    if (t < n * n) {  // agent-agent, eye * 1e6 on the diagonal
+      const int i = t / n, j = t - (t / n) * n;
+      float dj = norm2(cur[i * SD] - cur[j * SD], cur[i * SD + 1] - cur[j * SD + 1]);
+      if (i == j) dj = dj + 1e6f;
+      lds[o_dd + t] = dj;
+      continue;
+    }
+    t -= n * n;  // agent i vs obstacle row h: ||row_h - p_i||, row nh = the origin
+    const int i = t / n_ob, h = t - (t / n_ob) * n_ob;
+    const float ox = h < nh ? lds[cv.curhit + 2 * h] : 0.0f;
+    const float oy = h < nh ? lds[cv.curhit + 2 * h + 1] : 0.0f;
+    lds[o_do + t] = norm2(ox - cur[i * SD], oy - cur[i * SD + 1]);
+  }
+  if (lidar) stage_edge_vectors(O, lds, cv, tid, BLOCK);
+  __syncthreads();
+
+  // ---- C: costs (5 per agent, margin 0.1, clip [-1, 1]); is-inside at the next state -------------
+  for (int i = tid; i < n; i += BLOCK) {
+    float md = lds[o_dd + i * n];
+    for (int j = 1; j < n; ++j) md = min_nan(md, lds[o_dd + i * n + j]);
+    float c[NC];
+    c[0] = cfg.c_agent_cost - md;
+    c[1] = 0.0f;
+    if (lidar) {
+      float mo = lds[o_do + i * n_ob];
+      for (int h = 1; h < n_ob; ++h) mo = min_nan(mo, lds[o_do + i * n_ob + h]);
+      c[1] = cfg.c_obs_cost - mo;
+    }
+    c[2] = lds[o_fov + i];
+    c[3] = lds[o_fov + n + i];
+    c[4] = lds[o_fov + 2 * n + i];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const float v = c[q] <= 0.0f ? c[q] - 0.1f : c[q] + 0.1f;
+      io.cost[env * io.cost_stride + i * NC + q] = clampf_nan(v, -1.0f, 1.0f);
+    }
+    if (lidar) agent_is_inside(O, lds, cv, SD, i);
+  }
+  __syncthreads();
+
+  // ---- D: reward (sequential means), LiDAR of the next state -----------------------------------
+  if (tid == 0) {
+    float s[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) s[q] = s[q] + lds[o_red + q * n + i];
+    const float nn = (float)n;
+    float r = 0.0f - (s[0] / nn) * 0.01f;
+    r = r - (s[1] / nn) * 0.001f;
+    r = r - (s[2] / nn) * 0.0001f;
+    r = r - (s[3] / nn) * cfg.rot_pen;
+    r = r - ((s[4] / nn) * cfg.rot_pen) * 0.5f;
+    io.reward[env * io.reward_stride] = r;
+  }
+  if (lidar) {
+    lidar_scan<SD>(d, io.ray_dirs, lds, cv, tid, BLOCK);
+    __syncthreads();
+  }
+
+  // ---- E: the next graph ------------------------------------------------------------------------
+  GraphOut out;
+  out.nodes = io.nodes + env * io.nodes_stride;
+  out.edges = io.edges + env * io.edges_stride;
+  out.states = io.out_states + env * io.out_states_stride;
+  out.recv = io.receivers + env * io.edge_index_stride;
+  out.send = io.senders + env * io.edge_index_stride;
+  write_graph_omni(cfg, n, k, lidar, lds + cv.nxt, goal, lds + cv.hits, out, tid, BLOCK);
+}
+
+static size_t omni_step_lds_bytes(const dgppo_env_cfg& c) {
+  const Carve cv(c.n_agents, kOmniSD, c.n_obs, c.n_rays, c.top_k, true);
+  const int n = c.n_agents, nh = c.n_obs > 0 ? n * c.top_k : 0;
+  const size_t fl = cv.total + ((3 * n + 3) & ~3) + ((n * n + 3) & ~3) + ((n * (nh + 1) + 3) & ~3) + 8 * n;
+  return fl * sizeof(float);
+}
+
 // ---- reset ------------------------------------------------------------------------------------
 // Thread 0 runs the reference's sequential rejection sampler for its env (reset is once per
 // episode, amortised over T = 128 steps); then the whole workgroup ray-casts and writes the graph.
@@ -1218,6 +1451,18 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
         nxt[i * SD + 3] = s;
       }
     }
+    if (ENGINE == DGPPO_ENGINE_OMNI) {  // chain headings toward the next agent (lidar_omni_target.py:246-272)
+      for (int i = 0; i + 1 < n; ++i) {
+        const float dx = pos[2 * (i + 1)] - pos[2 * i], dy = pos[2 * (i + 1) + 1] - pos[2 * i + 1];
+        const float nrm = norm2(dx, dy) + 1e-8f;
+        nxt[i * SD + 2] = dx / nrm;
+        nxt[i * SD + 3] = dy / nrm;
+      }
+      float s, c;  // the last agent (or the only one) draws its heading
+      sincos32(rng.uniform(0.0f, 6.28318548202514648438f), &s, &c);
+      nxt[(n - 1) * SD + 2] = c;
+      nxt[(n - 1) * SD + 3] = s;
+    }
     if (mpe) {  // obstacles (mpe/base.py:92-118); the reference loop is unbounded, we cap it
       for (int o = 0; o < O; ++o) {
         float cx = rng.uniform(0.0f, area), cy = rng.uniform(0.0f, area);
@@ -1255,16 +1500,21 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
   out.states = io.out_states + env * io.out_states_stride;
   out.recv = io.receivers + env * io.edge_index_stride;
   out.send = io.senders + env * io.edge_index_stride;
-  const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
-  write_graph<ENGINE, GOAL, SD>(cfg, d, nxt, goal, mpe ? third : lds + cv.hits, out, vec4, tid, BLOCK);
+  if constexpr (ENGINE == DGPPO_ENGINE_OMNI) {
+    write_graph_omni(cfg, n, k, lidar, nxt, goal, lds + cv.hits, out, tid, BLOCK);
+  } else {
+    const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
+    write_graph<ENGINE, GOAL, SD>(cfg, d, nxt, goal, mpe ? third : lds + cv.hits, out, vec4, tid, BLOCK);
+  }
 }
 
 // ---- host dispatch --------------------------------------------------------------------------
 static int validate(const dgppo_env_cfg* c) {
   if (!c) return DGPPO_EINVAL;
-  if (c->engine < 0 || c->engine > 2 || c->goal_mode < 0 || c->goal_mode > 1) return DGPPO_EINVAL;
+  if (c->engine < 0 || c->engine > 3 || c->goal_mode < 0 || c->goal_mode > 1) return DGPPO_EINVAL;
   if (c->n_agents < 1 || c->n_agents > kMaxAgents || c->n_obs < 0 || c->n_obs > kMaxObs) return DGPPO_EINVAL;
-  const int sd = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : 4;
+  if (c->engine == DGPPO_ENGINE_OMNI && c->goal_mode != DGPPO_GOAL_TARGET) return DGPPO_EINVAL;
+  const int sd = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : (c->engine == DGPPO_ENGINE_OMNI ? 7 : 4);
   if (c->state_dim != sd || c->node_dim != sd + 3) return DGPPO_EINVAL;
   if (c->engine != DGPPO_ENGINE_MPE && c->n_obs > 0) {
     if (c->n_rays < 1 || c->n_rays > kMaxRays || c->top_k < 1 || c->top_k > c->n_rays) return DGPPO_EINVAL;
@@ -1342,6 +1592,8 @@ static void dispatch_reset(const dgppo_env_cfg& c, const dgppo_env_reset_io& io,
     case DGPPO_ENGINE_BICYCLE:
       return spread ? dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, io, shmem, s)
                     : dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, io, shmem, s);
+    case DGPPO_ENGINE_OMNI:
+      return dispatch_reset_sized<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD>(c, io, shmem, s);
     default:
       return spread ? dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
                     : dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
@@ -1373,8 +1625,12 @@ extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
   if (!c) return DGPPO_EINVAL;
   const bool mpe = c->engine == DGPPO_ENGINE_MPE;
   const int n = c->n_agents;
-  c->state_dim = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : 4;
+  const bool omni = c->engine == DGPPO_ENGINE_OMNI;
+  c->state_dim = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : (omni ? kOmniSD : 4);
   c->node_dim = c->state_dim + 3;
+  c->edge_dim = omni ? kOmniED : 4;
+  c->action_dim = omni ? 3 : 2;
+  c->n_cost = omni ? kOmniNC : 2;
   const int n_ag = c->goal_mode == DGPPO_GOAL_SPREAD ? n * n : n;
   if (mpe) {
     c->n_nodes = 2 * n + c->n_obs + 1;
@@ -1385,7 +1641,15 @@ extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
     c->n_edges = n * n + n_ag + hits;
   }
   const float a = c->area_size;
-  if (c->engine == DGPPO_ENGINE_BICYCLE) {
+  if (omni) {  // lidar_omni_target.py:502-509
+    const float w = c->omni_max_w;
+    const float lo[7] = {0.f, 0.f, -1.f, -1.f, -2.f, -2.f, -w}, hi[7] = {a, a, 1.f, 1.f, 2.f, 2.f, w};
+    for (int i = 0; i < 7; ++i) { c->state_lo[i] = lo[i]; c->state_hi[i] = hi[i]; }
+    // jnp.cos(jnp.deg2rad(fov_angle_deg)): fp32 product with fp32(pi / 180), cos by the shared fp32 routine
+    float sb, cb;
+    sincos32(c->fov_angle_deg * (float)(M_PI / 180.0), &sb, &cb);
+    c->c_cos_fov = cb;
+  } else if (c->engine == DGPPO_ENGINE_BICYCLE) {
     const float lo[5] = {0.f, 0.f, -1.f, -1.f, -0.5f}, hi[5] = {a, a, 1.f, 1.f, 0.5f};
     for (int i = 0; i < 5; ++i) { c->state_lo[i] = lo[i]; c->state_hi[i] = hi[i]; }
   } else {
@@ -1447,6 +1711,13 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
     return DGPPO_EINVAL;
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  if (cfg->engine == DGPPO_ENGINE_OMNI) {
+    const size_t sh = omni_step_lds_bytes(*cfg);
+    if (sh > 64 * 1024) return DGPPO_EINVAL;
+    hipLaunchKernelGGL(omni_step_kernel<256>, dim3((unsigned)io->n_env), dim3(256), sh, (hipStream_t)stream, *cfg,
+                       *io);
+    return (int)hipGetLastError();
+  }
   if (lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
       wave_step_enabled()) {
     const dim3 grid((unsigned)((io->n_env + 3) / 4)), block(256);

@@ -1,12 +1,12 @@
 """Env registry + make_env (dgppo/env/__init__.py:10-55).
 
-Only the engines BASELINE.json's configs use are built; the other reference
-variants (MPEFormation/Line/Corridor/ConnectSpread, LidarLine, LidarOmniTarget, VMAS) are listed
-in DESIGN.md as next rows and raise here."""
+The engines BASELINE.json's configs use plus LidarOmniTarget (the FoV env)
+are built; the other reference variants (MPEFormation/Line/Corridor/ConnectSpread, LidarLine, VMAS)
+are listed in DESIGN.md as next rows and raise here."""
 from typing import Optional
 
 from .base import MultiAgentEnv, StepResult, RolloutResult
-from .lidar_env import LidarSpread, LidarTarget, LidarBicycleTarget, LidarEnv, LidarEnvState
+from .lidar_env import LidarSpread, LidarTarget, LidarBicycleTarget, LidarOmniTarget, LidarEnv, LidarEnvState
 from .mpe import MPESpread, MPETarget, MPE, MPEEnvState
 
 ENV = {
@@ -15,10 +15,11 @@ ENV = {
     "LidarSpread": LidarSpread,
     "LidarTarget": LidarTarget,
     "LidarBicycleTarget": LidarBicycleTarget,
+    "LidarOmniTarget": LidarOmniTarget,
 }
 
 NOT_YET_BUILT = ("MPELine", "MPEFormation", "MPECorridor", "MPEConnectSpread", "LidarLine",
-                 "LidarOmniTarget", "VMASReverseTransport", "VMASWheel")
+                 "VMASReverseTransport", "VMASWheel")
 
 DEFAULT_MAX_STEP = 128
 

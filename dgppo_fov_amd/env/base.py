@@ -112,7 +112,7 @@ class MultiAgentEnv(ABC):
         raise NotImplementedError
 
     def action_lim(self):
-        return -torch.ones(2), torch.ones(2)
+        return -torch.ones(self.action_dim), torch.ones(self.action_dim)
 
     def clip_state(self, state: torch.Tensor) -> torch.Tensor:
         lo, hi = self.state_lim(state)
@@ -177,8 +177,12 @@ class MultiAgentEnv(ABC):
         c.c_mpe_obs_goal = r * 2 + orr
         c.c_mpe_obs_lo = r * 3
         c.c_mpe_obs_hi = self._area_size - r * 3
+        self._engine_cfg(c)
         _lib.check(_lib.load().dgppo_env_cfg_finalize(ctypes.byref(c)), "dgppo_env_cfg_finalize")
         return c
+
+    def _engine_cfg(self, c: _lib.EnvCfg) -> None:
+        """Engine-specific cfg fields (hook for subclasses), set before dgppo_env_cfg_finalize."""
 
     def _obs_theta_range(self):
         return 0.0, 2 * np.pi
@@ -318,7 +322,8 @@ class MultiAgentEnv(ABC):
             raise ValueError("graph does not match this env's layout")
         if action.dtype != torch.float32:
             action = action.float()
-        action = action if action.stride(-1) == 1 and action.stride(-2) == 2 else action.contiguous()
+        A = self.action_dim
+        action = action if action.stride(-1) == 1 and action.stride(-2) == A else action.contiguous()
         ob = self._obstacles_of(graph)
         io = _lib.EnvStepIO()
         io.states, io.states_stride = _lib.ptr(graph.states), self._env_stride(graph.states, 2)
@@ -353,7 +358,7 @@ class MultiAgentEnv(ABC):
 
     def get_cost(self, graph: GraphsTuple) -> torch.Tensor:
         """Cost of a graph (lidar_env/base.py:180-207): the step kernel evaluates it on its input."""
-        zero = torch.zeros(graph.states.shape[:-2] + (self._num_agents, 2), device=graph.states.device)
+        zero = torch.zeros(graph.states.shape[:-2] + (self._num_agents, self.action_dim), device=graph.states.device)
         return self.step(graph, zero).cost
 
 

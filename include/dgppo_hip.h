@@ -29,6 +29,7 @@ extern "C" {
 #define DGPPO_ENGINE_LIDAR 0   /* LidarEnv double integrator: dgppo/env/lidar_env/base.py */
 #define DGPPO_ENGINE_BICYCLE 1 /* LidarBicycleTarget: dgppo/env/lidar_env/lidar_bicycle_target.py */
 #define DGPPO_ENGINE_MPE 2     /* MPE double integrator: dgppo/env/mpe/base.py */
+#define DGPPO_ENGINE_OMNI 3    /* LidarOmniTarget omni-wheel + FoV costs: dgppo/env/lidar_env/lidar_omni_target.py */
 /* goal wiring */
 #define DGPPO_GOAL_SPREAD 0 /* every agent sees every goal: lidar_spread.py:86-91, mpe_spread.py:64-69 */
 #define DGPPO_GOAL_TARGET 1 /* agent i sees goal i only: lidar_target.py:77-84, mpe_target.py:63-70 */
@@ -59,7 +60,7 @@ typedef struct dgppo_env_cfg {
   float dist2goal;    /* 0.01 */
   float obs_len_lo, obs_len_hi; /* Lidar obstacle side range [0.1, 0.3] */
   float obs_theta_lo, obs_theta_hi; /* obstacle angle range: [0, 2pi) Lidar, [-pi, pi) bicycle */
-  float state_lo[5], state_hi[5]; /* state_lim() */
+  float state_lo[8], state_hi[8]; /* state_lim() */
   /* Derived constants.  The reference forms them in Python float64 and rounds once to fp32 when they
    * meet an fp32 array, so the host computes them the same way; finalize fills any left at 0. */
   float c_agent_cost;   /* car_radius * 2                      (lidar_env/base.py:188, mpe/base.py:173) */
@@ -74,6 +75,12 @@ typedef struct dgppo_env_cfg {
    * reference's `norm(d) < r` masks are decided exactly as `|d|^2 < t2` (sqrt is correctly rounded
    * and monotone).  t2_comm: r = comm_radius (agent-agent edges); t2_lidar: r = c_lidar_active. */
   float t2_comm, t2_lidar;
+  /* filled by finalize from the engine: edge feature / action / cost widths (4, 2, 2; Omni 10, 3, 5) */
+  int32_t edge_dim, action_dim, n_cost;
+  /* LidarOmniTarget PARAMS (lidar_omni_target.py:49-68): max_angular_vel (state limit of omega),
+   * fov_angle_deg (FoV half-angle beta), max_sensor_range (r_max), min_safe_distance (D),
+   * rotation_penalty; c_cos_fov = cos(deg2rad(fov_angle_deg)) in fp32 (filled by finalize). */
+  float omni_max_w, fov_angle_deg, fov_rmax, fov_dmin, rot_pen, c_cos_fov;
 } dgppo_env_cfg;
 
 /* Fills n_nodes / n_edges / node_dim / state_lo/hi and zero derived constants from the other

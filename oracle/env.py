@@ -28,7 +28,12 @@ MPE_PARAMS = {  # mpe_spread.py:12-19, mpe_target.py:12-19
     "dist2goal": 0.01,
 }
 
-ENGINE_LIDAR, ENGINE_BICYCLE, ENGINE_MPE = 0, 1, 2
+OMNI_PARAMS = dict(LIDAR_PARAMS, **{  # lidar_omni_target.py:49-68
+    "max_angular_vel": 100.0, "rotation_penalty": 0.001, "fov_angle_deg": 60.0, "max_sensor_range": 0.5,
+    "min_safe_distance": 0.2,
+})
+
+ENGINE_LIDAR, ENGINE_BICYCLE, ENGINE_MPE, ENGINE_OMNI = 0, 1, 2, 3
 GOAL_SPREAD, GOAL_TARGET = 0, 1
 
 ENVS = {
@@ -37,6 +42,7 @@ ENVS = {
     "LidarBicycleTarget": (ENGINE_BICYCLE, GOAL_TARGET),
     "MPESpread": (ENGINE_MPE, GOAL_SPREAD),
     "MPETarget": (ENGINE_MPE, GOAL_TARGET),
+    "LidarOmniTarget": (ENGINE_OMNI, GOAL_TARGET),
 }
 
 
@@ -52,7 +58,8 @@ class Spec:
 
     def __post_init__(self):
         self.engine, self.goal_mode = ENVS[self.env_id]
-        p = dict(MPE_PARAMS if self.engine == ENGINE_MPE else LIDAR_PARAMS)
+        p = dict(MPE_PARAMS if self.engine == ENGINE_MPE else (OMNI_PARAMS if self.engine == ENGINE_OMNI else LIDAR_PARAMS))
+        self.params = p
         self.car_r = p["car_radius"]
         self.comm_r = p["comm_radius"]
         self.area = p["default_area_size"]
@@ -61,8 +68,12 @@ class Spec:
         self.obs_r = p.get("obs_radius", 0.0)
         self.dist2goal = p["dist2goal"]
         self.obs_len_range = p.get("obs_len_range", [0.1, 0.3])
-        self.sd = 5 if self.engine == ENGINE_BICYCLE else 4
+        self.sd = {ENGINE_BICYCLE: 5, ENGINE_OMNI: 7}.get(self.engine, 4)
         self.nd = self.sd + 3
+        omni = self.engine == ENGINE_OMNI
+        self.ed = 10 if omni else 4  # edge_dim (lidar_omni_target.py:136-143)
+        self.ad = 3 if omni else 2  # action_dim (ax, ay, alpha)
+        self.n_cost = 5 if omni else 2
 
     @property
     def has_lidar(self):
@@ -89,6 +100,9 @@ class Spec:
         return self.n * self.n + self.n_ag + self.n_hits
 
     def state_lim(self):
+        if self.engine == ENGINE_OMNI:  # lidar_omni_target.py:502-509
+            w = self.params["max_angular_vel"]
+            return (np.array([0, 0, -1, -1, -2, -2, -w], F), np.array([self.area, self.area, 1, 1, 2, 2, w], F))
         if self.engine == ENGINE_BICYCLE:  # lidar_bicycle_target.py:120-123
             return (np.array([0, 0, -1, -1, -0.5], F), np.array([self.area, self.area, 1, 1, 0.5], F))
         if self.engine == ENGINE_MPE:  # mpe/base.py:243-246
@@ -250,6 +264,36 @@ def step_bicycle(spec, agent, action):
     return clip(new, lo, hi)
 
 
+def step_omni(spec, agent, action):
+    """LidarOmniTarget.agent_step_euler (lidar_omni_target.py:146-197): omni-wheel agent
+    [x, y, cos th, sin th, vx, vy, omega], action [ax, ay, alpha] -> acc = 10 a, alpha = 5 a."""
+    dt = F(spec.dt)
+    x = agent
+    acc_x, acc_y = action[..., 0] * F(10.0), action[..., 1] * F(10.0)
+    alpha = action[..., 2] * F(5.0)
+    theta = math32.atan2(x[..., 3], x[..., 2])
+    new_theta = theta + x[..., 6] * dt
+    sn, cn = math32.sincos(new_theta)
+    new = np.stack([
+        x[..., 0] + x[..., 4] * dt,
+        x[..., 1] + x[..., 5] * dt,
+        cn,
+        sn,
+        x[..., 4] + acc_x * dt,
+        x[..., 5] + acc_y * dt,
+        x[..., 6] + alpha * dt,
+    ], axis=-1).astype(F)
+    lo, hi = spec.state_lim()
+    return clip(new, lo, hi)
+
+
+def omni_cos_fov(spec):
+    """jnp.cos(jnp.deg2rad(fov_angle_deg)) in float32 (lidar_omni_target.py:93-94); cos by the
+    shared deterministic fp32 routine (math32), as every other trig term here."""
+    beta = F(F(spec.params["fov_angle_deg"]) * F(np.pi / 180))
+    return F(math32.sincos(np.array([beta], F))[1][0])
+
+
 def state2feat(spec, s):
     """LidarBicycleTarget.state2feat (lidar_bicycle_target.py:113-118); identity otherwise."""
     if spec.engine == ENGINE_BICYCLE:
@@ -323,6 +367,64 @@ def get_cost_mpe(spec, agent, obs):
     return _margin(np.stack([agent_cost, obs_cost], -1).astype(F), upper=False)
 
 
+def get_reward_omni(spec, agent, goal, action):
+    """LidarOmniTarget.get_reward (lidar_omni_target.py:295-336), means summed sequentially."""
+    n = spec.n
+    d = norm2d(goal[..., 0] - agent[..., 0], goal[..., 1] - agent[..., 1])
+    far = (d > F(spec.dist2goal)).astype(F)
+    an = norm2d(action[..., 0], action[..., 1])
+    terms = [d, far, an * an, action[..., 2] * action[..., 2], agent[..., 6] * agent[..., 6]]
+    sums = [np.zeros(d.shape[0], F) for _ in terms]
+    for i in range(n):
+        for q, t in enumerate(terms):
+            sums[q] = sums[q] + t[:, i]
+    nn = F(n)
+    rp = F(spec.params["rotation_penalty"])
+    r = F(0) - (sums[0] / nn) * F(0.01)
+    r = r - (sums[1] / nn) * F(0.001)
+    r = r - (sums[2] / nn) * F(0.0001)
+    r = r - (sums[3] / nn) * rp
+    r = r - ((sums[4] / nn) * rp) * F(0.5)  # `.mean() * rotation_penalty * 0.5`, left to right
+    return r.astype(F)
+
+
+def get_cost_omni(spec, agent, hits_all):
+    """LidarOmniTarget.get_cost (lidar_omni_target.py:517-649): 5 costs, margin 0.1, clip [-1, 1].
+
+    hits_all (B, n*k, 2): the pre-step graph's hit rows.  Reference quirk kept: the obstacle term
+    asks type_states for N - 2n = n*k + 1 rows (the pad node counted), so the extra row is the
+    origin and min_dist_obs also covers ||p_i - 0||; and it is the minimum over EVERY agent's hits."""
+    n = spec.n
+    agent_cost = F(spec.car_r * 2) - agent_min_dist(agent)
+    ap = agent[..., :2]
+    if spec.has_lidar:
+        B = agent.shape[0]
+        op = np.concatenate([hits_all, np.zeros((B, 1, 2), F)], axis=1)  # (B, nk+1, 2)
+        d = norm2d(op[:, None, :, 0] - ap[:, :, None, 0], op[:, None, :, 1] - ap[:, :, None, 1])
+        obs_cost = F(spec.car_r) - d.min(axis=2)
+    else:
+        obs_cost = np.zeros_like(agent_cost)
+    safe = F(-1.0)
+    h_a = np.full_like(agent_cost, safe)
+    h_r = np.full_like(agent_cost, safe)
+    h_c = np.full_like(agent_cost, safe)
+    if n > 1:
+        pi, pj = agent[:, :-1], agent[:, 1:]
+        dx = pj[..., 0] - pi[..., 0]
+        dy = pj[..., 1] - pi[..., 1]
+        c, s_ = pi[..., 2], pi[..., 3]
+        lx = c * dx + s_ * dy  # R_i^T (p_j - p_i), row 0
+        ly = (-s_) * dx + c * dy
+        nrm = norm2d(lx, ly)
+        h_a[:, :-1] = omni_cos_fov(spec) * (nrm + F(1e-8)) - lx
+        h_r[:, :-1] = nrm - F(spec.params["max_sensor_range"])
+        h_c[:, :-1] = F(spec.params["min_safe_distance"]) - nrm
+    cost = np.stack([agent_cost, obs_cost, h_a, h_r, h_c], -1).astype(F)
+    eps = F(0.1)
+    cost = np.where(cost <= 0, cost - eps, cost + eps).astype(F)
+    return clip(cost, F(-1), F(1))
+
+
 # ---- graph build -----------------------------------------------------------------------------
 def build_graph(spec, agent, goal, third):
     """get_graph + edge_blocks + GetGraph.to_padded.
@@ -367,14 +469,27 @@ def build_graph(spec, agent, goal, third):
         nr, ns = len(ids_recv), len(ids_send)
         r = np.broadcast_to(np.asarray(ids_recv, np.int32)[:, None], (nr, ns))
         s = np.broadcast_to(np.asarray(ids_send, np.int32)[None, :], (nr, ns))
-        edges.append(feats.reshape(B, nr * ns, 4))
+        edges.append(feats.reshape(B, nr * ns, spec.ed))
         recvs.append(np.where(mask, r[None], pad).reshape(B, nr * ns).astype(np.int32))
         sends.append(np.where(mask, s[None], pad).reshape(B, nr * ns).astype(np.int32))
 
     ids_a = np.arange(n)
+    omni = spec.engine == ENGINE_OMNI
     # agent-agent
     feats = fa[:, :, None, :] - fa[:, None, :, :]
-    dist = norm2d(ap[:, :, None, 0] - ap[:, None, :, 0], ap[:, :, None, 1] - ap[:, None, :, 1])
+    pdx = ap[:, :, None, 0] - ap[:, None, :, 0]
+    pdy = ap[:, :, None, 1] - ap[:, None, :, 1]
+    if omni:  # lidar_omni_target.py:352-419: [s_i - s_j (7) | critical i -> i+1 | ||p_j^i|| | i_x_j]
+        gx, gy = -pdx, -pdy  # p_j - p_i
+        c, s_ = agent[:, :, None, 2], agent[:, :, None, 3]
+        lx = c * gx + s_ * gy  # R_i^T (p_j - p_i)
+        ly = (-s_) * gx + c * gy
+        crit = np.zeros((n, n), F)
+        if n > 1:
+            crit[np.arange(n - 1), np.arange(1, n)] = 1
+        feats = np.concatenate([feats[..., :7], np.broadcast_to(crit[None, :, :, None], (B, n, n, 1)),
+                                norm2d(lx, ly)[..., None], lx[..., None]], -1).astype(F)
+    dist = norm2d(pdx, pdy)
     dist = dist + (np.eye(n, dtype=F) * F(spec.comm_r + 1))[None]
     block(feats, dist < F(spec.comm_r), ids_a, ids_a)
     # agent-goal
@@ -382,7 +497,10 @@ def build_graph(spec, agent, goal, third):
         block(fa[:, :, None, :] - fg[:, None, :, :], np.ones((B, n, n), bool), ids_a, n + ids_a)
     else:
         for i in range(n):
-            block((fa[:, i] - fg[:, i])[:, None, None, :], np.ones((B, 1, 1), bool), [i], [n + i])
+            gf = fa[:, i] - fg[:, i]
+            if omni:  # first 7 features, zero-padded to edge_dim (lidar_omni_target.py:424-443)
+                gf = np.concatenate([gf[:, :7], np.zeros((B, 3), F)], -1)
+            block(gf[:, None, None, :], np.ones((B, 1, 1), bool), [i], [n + i])
     # agent-obstacle / agent-lidar
     if spec.engine == ENGINE_MPE:
         O = spec.n_obs
@@ -395,8 +513,10 @@ def build_graph(spec, agent, goal, third):
         for i in range(n):
             lf = ap[:, i, None, :] - third[:, i]  # (B, k, 2)
             ld = norm2d(lf[..., 0], lf[..., 1])
-            active = ld < F(spec.comm_r - 1e-1)
-            feats = np.concatenate([lf, np.zeros((B, k, 2), F)], -1)
+            # LidarOmniTarget masks hits at comm_radius (lidar_omni_target.py:480), the others at
+            # comm_radius - 0.1 (lidar_spread.py:95)
+            active = ld < F(spec.comm_r if omni else spec.comm_r - 1e-1)
+            feats = np.concatenate([lf, np.zeros((B, k, spec.ed - 2), F)], -1)
             block(feats[:, None], active[:, None], [i], 2 * n + i * k + np.arange(k))
     out = dict(
         nodes=nodes,
@@ -405,7 +525,7 @@ def build_graph(spec, agent, goal, third):
         receivers=np.concatenate(recvs, 1),
         senders=np.concatenate(sends, 1),
     )
-    assert out["edges"].shape == (B, E, 4), (out["edges"].shape, E)
+    assert out["edges"].shape == (B, E, spec.ed), (out["edges"].shape, E)
     return out
 
 
@@ -423,25 +543,33 @@ def env_step(spec, states, obst, action):
     """LidarEnv.step (lidar_env/base.py:151-174) / MPE.step (mpe/base.py:137-158), batched.
 
     states: (B, N, sd) states of the current (pre-step) graph; obst: (B, O, 16) rectangles (Lidar)
-    or None (MPE reads obstacles from graph states); action (B, n, 2).
-    Returns dict(graph fields of the next graph, reward (B,), cost (B, n, 2), next_agent)."""
+    or None (MPE reads obstacles from graph states); action (B, n, action_dim).
+    Returns dict(graph fields of the next graph, reward (B,), cost (B, n, n_cost), next_agent)."""
     n = spec.n
     states = np.asarray(states, F)
     agent = states[:, :n]
     goal = states[:, n:2 * n]
-    a = clip(np.asarray(action, F), F(-1), F(1))
-    if spec.engine == ENGINE_BICYCLE:
-        nxt = step_bicycle(spec, agent, a)
+    if spec.engine == ENGINE_OMNI:  # action_lim: [-1, -1, -1000] .. [1, 1, 1000] (lidar_omni_target.py:511-521)
+        a = clip(np.asarray(action, F), np.array([-1, -1, -1000], F), np.array([1, 1, 1000], F))
+        nxt = step_omni(spec, agent, a)
+        reward = get_reward_omni(spec, agent, goal, a)
     else:
-        nxt = step_double_integrator(spec, agent, a)
-    reward = get_reward(spec, agent, goal, a)
+        a = clip(np.asarray(action, F), F(-1), F(1))
+        if spec.engine == ENGINE_BICYCLE:
+            nxt = step_bicycle(spec, agent, a)
+        else:
+            nxt = step_double_integrator(spec, agent, a)
+        reward = get_reward(spec, agent, goal, a)
     if spec.engine == ENGINE_MPE:
         obs = states[:, 2 * n:2 * n + spec.n_obs]
         cost = get_cost_mpe(spec, agent, obs)
         g = build_graph(spec, nxt, goal, obs)
     else:
         hits_cur = states[:, 2 * n:2 * n + spec.n_hits, :2].reshape(-1, n, spec.top_k, 2) if spec.has_lidar else None
-        cost = get_cost_lidar(spec, agent, hits_cur)
+        if spec.engine == ENGINE_OMNI:
+            cost = get_cost_omni(spec, agent, states[:, 2 * n:2 * n + spec.n_hits, :2] if spec.has_lidar else None)
+        else:
+            cost = get_cost_lidar(spec, agent, hits_cur)
         if spec.has_lidar:
             hits, _ = lidar(nxt[..., :2], obst, ray_table(spec.n_rays, spec.comm_r), spec.top_k)
         else:
@@ -518,6 +646,8 @@ def node_goal_rng(rng, side, n, min_dist, obst):
 
 
 def min_dist_for(spec):
+    if spec.engine == ENGINE_OMNI:  # jnp.maximum(2.2 r, D) (lidar_omni_target.py:237-240), float32
+        return float(max(F(2.2 * spec.car_r), F(spec.params["min_safe_distance"])))
     return 2.2 * spec.car_r if spec.engine != ENGINE_MPE else 2 * spec.car_r
 
 
@@ -570,6 +700,16 @@ def env_reset(spec, seed, n_env, env_offset=0):
             s, c = math32.sincos(hd)
             agents[b, :, 2] = c
             agents[b, :, 3] = s
+        if spec.engine == ENGINE_OMNI:  # chain headings (lidar_omni_target.py:246-272)
+            for i in range(n - 1):
+                dx, dy = F(st[i + 1, 0] - st[i, 0]), F(st[i + 1, 1] - st[i, 1])
+                nrm = F(norm2d(np.array([dx], F), np.array([dy], F))[0] + F(1e-8))
+                agents[b, i, 2] = F(dx / nrm)
+                agents[b, i, 3] = F(dy / nrm)
+            th = np.array([rng.uniform(0, 2 * np.pi)], F)  # last agent (or the only one): random heading
+            s, c = math32.sincos(th)
+            agents[b, n - 1, 2] = c[0]
+            agents[b, n - 1, 3] = s[0]
     return agents, goals, third
 
 

@@ -22,6 +22,10 @@ CONFIGS = [
     ("LidarSpread", 1, 3, 16),
     ("LidarSpread", 8, 0, 16),
     ("LidarTarget", 5, 1, 16),
+    ("LidarOmniTarget", 8, 3, 64),
+    ("LidarOmniTarget", 3, 2, 32),
+    ("LidarOmniTarget", 1, 3, 8),
+    ("LidarOmniTarget", 4, 0, 8),
 ]
 IDS = [f"{c[0]}-n{c[1]}-o{c[2]}" for c in CONFIGS]
 
@@ -72,7 +76,9 @@ def test_step_chain_matches_oracle(cuda, cfg):
     states = _np(g.states)
     third = oracle_third(spec, g)
     for t in range(6):
-        a = rng.uniform(-1.5, 1.5, (B, n, 2)).astype(np.float32)  # includes out-of-range actions (clipped)
+        a = rng.uniform(-1.5, 1.5, (B, n, spec.ad)).astype(np.float32)  # includes out-of-range actions (clipped)
+        if spec.ad == 3:
+            a[..., 2] *= 1000.0  # Omni angular acceleration, clipped at +-1000
         res = env.step(g, torch.from_numpy(a).to(cuda))
         ref = O.env_step(spec, states, third, a)
         torch.cuda.synchronize()
@@ -278,3 +284,48 @@ def test_wave_step_kernel_adversarial(cuda, eid):
     assert np.array_equal(np.isnan(c), np.isnan(rc)) and np.array_equal(c[~np.isnan(c)], rc[~np.isnan(rc)])
     r, rr = _np(res.reward), ref["reward"]
     assert np.array_equal(np.isnan(r), np.isnan(rr)) and np.array_equal(r[~np.isnan(r)], rr[~np.isnan(rr)])
+
+
+def test_omni_step_edge_cases(cuda):
+    """LidarOmniTarget: agent inside an obstacle, coincident agents (FoV norm 0), headings that are not
+    unit vectors, NaN / huge actions, angular rates at the limit."""
+    eid, n, obs, B = "LidarOmniTarget", 4, 2, 8
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    spec = O.Spec(eid, n, obs)
+    g = env.reset(key=11, n_env=B)
+    states = _np(g.states).copy()
+    ob = _np(g.env_states.obstacle.packed).copy()
+    states[0, 0, :2] = ob[0, 0, :2]
+    states[1, 1, :2] = states[1, 0, :2]
+    states[2, :n, 2:4] = [0.3, 0.4]
+    states[3, :n, 6] = 99.0
+    states[4, :n, 4:6] = -1.9
+    a = np.random.default_rng(2).uniform(-1, 1, (B, n, 3)).astype(np.float32)
+    a[5, 0, 0] = np.nan
+    a[6, 1, 2] = 1e30
+    a[7, 2, 2] = -np.inf
+    gin = env._assemble(g.nodes, g.edges, torch.from_numpy(states).to(cuda), g.receivers, g.senders,
+                        torch.from_numpy(ob).to(cuda))
+    res = env.step(gin, torch.from_numpy(a).to(cuda))
+    ref = O.env_step(spec, states, ob, a)
+    torch.cuda.synchronize()
+    assert_graph_equal(res.graph, ref, "omni edge cases")
+    c, rc = _np(res.cost), ref["cost"]
+    assert np.array_equal(np.isnan(c), np.isnan(rc)) and np.array_equal(c[~np.isnan(c)], rc[~np.isnan(rc)])
+    r, rr = _np(res.reward), ref["reward"]
+    assert np.array_equal(np.isnan(r), np.isnan(rr)) and np.array_equal(r[~np.isnan(r)], rr[~np.isnan(rr)])
+
+
+def test_omni_reset_chain_headings(cuda):
+    """Reset points agent i at agent i+1 (unit heading) and keeps agents >= D = 0.2 apart."""
+    env = make_env("LidarOmniTarget", 6, num_obs=3, device=cuda)
+    g = env.reset(key=5, n_env=64)
+    st = _np(g.states)
+    ag = st[:, :6]
+    d = ag[:, 1:, :2] - ag[:, :-1, :2]
+    u = d / (np.linalg.norm(d, axis=-1, keepdims=True) + 1e-8)
+    np.testing.assert_allclose(ag[:, :-1, 2:4], u, atol=1e-6)
+    np.testing.assert_allclose(np.linalg.norm(ag[:, -1, 2:4], axis=-1), 1.0, atol=1e-6)
+    pd = np.linalg.norm(ag[:, :, None, :2] - ag[:, None, :, :2], axis=-1) + np.eye(6) * 9
+    assert (pd > 0.2).all()
+    assert (ag[..., 4:] == 0).all()

@@ -251,3 +251,76 @@ def test_gae_two_steps_by_hand():
     two0 = np.maximum(hs[0], (1 - g) * hm[0] + g * one1)
     np.testing.assert_allclose(Qh[1], one1, atol=1e-12)
     np.testing.assert_allclose(Qh[0], lam * two0 + (1 - lam) * one0, atol=1e-12)
+
+
+# ---- LidarOmniTarget (lidar_omni_target.py) ------------------------------------------------------
+def _omni_states(spec, agent_rows, hits=None):
+    """(1, N, 7) pre-step states: agents, goals at the agents' positions, hits far away."""
+    n, N = spec.n, spec.n_nodes
+    st = np.zeros((1, N, 7), F)
+    st[0, :n] = np.asarray(agent_rows, F)
+    st[0, n:2 * n, :2] = st[0, :n, :2]
+    st[0, 2 * n:N - 1, :2] = 5.0 if hits is None else hits
+    st[0, N - 1] = -1
+    return st
+
+
+def test_omni_fov_costs_by_hand():
+    spec = O.Spec("LidarOmniTarget", 2, 1)
+    # agent 0 at (0.5, 0.5) facing +x, agent 1 straight ahead at distance 0.3 (in FoV, in range)
+    st = _omni_states(spec, [[0.5, 0.5, 1, 0, 0, 0, 0], [0.8, 0.5, 1, 0, 0, 0, 0]])
+    c = O.get_cost_omni(spec, st[:, :2], st[:, 4:4 + 16, :2])
+    cb = O.omni_cos_fov(spec)
+    np.testing.assert_allclose(c[0, 0, 2], cb * F(0.3 + 1e-8) - F(0.3) - F(0.1), atol=1e-6)  # h_angle
+    np.testing.assert_allclose(c[0, 0, 3], 0.3 - 0.5 - 0.1, atol=1e-6)  # h_range
+    np.testing.assert_allclose(c[0, 0, 4], 0.2 - 0.3 - 0.1, atol=1e-6)  # h_coll_fov
+    np.testing.assert_array_equal(c[0, 1, 2:], [-1.0, -1.0, -1.0])  # last agent: safe value -1 - 0.1, clipped
+    # agent 1 behind agent 0: angle violated (h_angle = cos_b * 0.3 + 0.3 > 0)
+    st = _omni_states(spec, [[0.5, 0.5, 1, 0, 0, 0, 0], [0.2, 0.5, 1, 0, 0, 0, 0]])
+    c = O.get_cost_omni(spec, st[:, :2], st[:, 4:4 + 16, :2])
+    np.testing.assert_allclose(c[0, 0, 2], min(1.0, cb * 0.3 + 0.3 + 0.1), atol=1e-6)
+
+
+def test_omni_obstacle_cost_includes_origin_row():
+    """type_states(2, N - 2n) asks for one row more than there are hits (the pad node is counted):
+    that zero row is the origin, so ||p_i|| enters min_dist_obs."""
+    spec = O.Spec("LidarOmniTarget", 2, 1)
+    st = _omni_states(spec, [[0.06, 0.08, 1, 0, 0, 0, 0], [1.0, 1.0, 1, 0, 0, 0, 0]])
+    c = O.get_cost_omni(spec, st[:, :2], st[:, 4:4 + 16, :2])
+    np.testing.assert_allclose(c[0, 0, 1], 0.05 - 0.1 - 0.1, atol=1e-6)  # r - ||p_0 - 0||, margin
+    # every agent's hits count, not only its own: put agent 1's first hit next to agent 0
+    hits = np.full((16, 2), 5.0, F)
+    hits[8] = [0.06 + 0.01, 0.08]
+    st = _omni_states(spec, [[0.06, 0.08, 1, 0, 0, 0, 0], [1.0, 1.0, 1, 0, 0, 0, 0]], hits)
+    c = O.get_cost_omni(spec, st[:, :2], st[:, 4:4 + 16, :2])
+    np.testing.assert_allclose(c[0, 0, 1], 0.05 - 0.01 + 0.1, atol=1e-6)
+
+
+def test_omni_dynamics_by_hand():
+    spec = O.Spec("LidarOmniTarget", 1, 0)
+    x = np.array([[[0.5, 0.5, 1.0, 0.0, 0.2, -0.1, 2.0]]], F)
+    a = np.array([[[0.5, -1.0, 3.0]]], F)
+    y = O.step_omni(spec, x, a)[0, 0]
+    dt = 0.03
+    np.testing.assert_allclose(y[:2], [0.5 + 0.2 * dt, 0.5 - 0.1 * dt], atol=1e-7)
+    np.testing.assert_allclose(y[2:4], [np.cos(2.0 * dt), np.sin(2.0 * dt)], atol=1e-6)
+    np.testing.assert_allclose(y[4:], [0.2 + 5 * dt, -0.1 - 10 * dt, 2.0 + 15 * dt], atol=1e-6)
+    # velocity and angular-rate limits
+    x = np.array([[[0.5, 0.5, 1.0, 0.0, 1.99, 0.0, 99.99]]], F)
+    y = O.step_omni(spec, x, np.array([[[1.0, 0.0, 1.0]]], F))[0, 0]
+    assert y[4] == F(2.0) and y[6] == F(100.0)
+
+
+def test_omni_edge_features_local_frame():
+    spec = O.Spec("LidarOmniTarget", 3, 0)
+    ag = np.array([[[0.5, 0.5, 0.0, 1.0, 0, 0, 0],   # faces +y
+                    [0.5, 0.7, 1.0, 0.0, 0, 0, 0],
+                    [0.9, 0.7, 1.0, 0.0, 0, 0, 0]]], F)
+    g = O.build_graph(spec, ag, np.zeros_like(ag), None)
+    e = g["edges"][0]
+    # edge (0 <- 1) is row 0*3 + 1: p_1 - p_0 = (0, 0.2); agent 0 faces +y -> local (0.2, 0)
+    np.testing.assert_allclose(e[1, 7:], [1.0, 0.2, 0.2], atol=1e-6)  # critical, ||p||, forward
+    np.testing.assert_allclose(e[3, 7], 0.0)  # (1 <- 0) is not critical
+    np.testing.assert_allclose(e[5, 7:], [1.0, 0.4, 0.4], atol=1e-6)  # (1 <- 2): ahead of agent 1 along +x
+    assert g["receivers"][0, 2] == 0  # (0, 2): |p| = 0.447 < comm_radius 0.5 -> kept
+    assert g["receivers"][0, 0] == spec.n_nodes - 1  # self edge -> pad
