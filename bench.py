@@ -139,10 +139,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev > 0 else local  # identity on a full node; wraps for one-GPU rehearsals
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL over xGMI; DGPPO_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+        # sharing one GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("DGPPO_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dgppo_fov_amd.env import make_env
     from dgppo_fov_amd.trainer.rollout import RolloutEngine
