@@ -171,6 +171,7 @@ class GnnAttnArgs(ctypes.Structure):
         ("scale", ctypes.c_float), ("D0", ctypes.c_int32),
         ("xa", c_f32p), ("xa_gstride", ctypes.c_int64), ("pre_W", c_f32p), ("pre_b", c_f32p),
         ("dxa", c_f32p), ("dxa_gstride", ctypes.c_int64), ("dpre_part", c_f32p), ("sidx", c_f32p),
+        ("da_add", c_f32p),
     ]
 
 
@@ -233,6 +234,8 @@ SIGNATURES = {
     "dgppo_policy_prepare": (ctypes.c_int, [_V, _V]),
     "dgppo_policy_step": (ctypes.c_int, [_V, _V]),
     "dgppo_gnn_sender_table": (ctypes.c_int, [_I32, _I32, _I32, _I32, _V, _V, _V, _V, _V]),
+    "dgppo_gnn_edge_wsum": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _V, _V, _V, _V, _V, _V]),
+    "dgppo_gnn_edge_da": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _V, _V, _V, _V, _V, _V]),
     "dgppo_gru_seq_fwd": (ctypes.c_int, [_V, _V]),
     "dgppo_gru_seq_bwd": (ctypes.c_int, [_V, _V]),
     "dgppo_agent_mean_fwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),

@@ -120,9 +120,10 @@ class DGPPO:
 
         dev = self.device
         self.actor = ActorNet(node_dim, n_agents, dev, seed=seed * 3 + 0, gnn_layers=actor_gnn_layers,
-                              action_dim=action_dim)
-        self.Vl = VlNet(node_dim, n_agents, dev, seed=seed * 3 + 1, gnn_layers=Vl_gnn_layers)
-        self.Vh = VhNet(node_dim, n_agents, env.n_cost, dev, seed=seed * 3 + 2, gnn_layers=Vh_gnn_layers)
+                              action_dim=action_dim, edge_dim=edge_dim)
+        self.Vl = VlNet(node_dim, n_agents, dev, seed=seed * 3 + 1, gnn_layers=Vl_gnn_layers, edge_dim=edge_dim)
+        self.Vh = VhNet(node_dim, n_agents, env.n_cost, dev, seed=seed * 3 + 2, gnn_layers=Vh_gnn_layers,
+                        edge_dim=edge_dim)
         # one flat gradient buffer for the three nets (one all-reduce per minibatch)
         sizes = [self.Vl.ps.size, self.Vh.ps.size, self.actor.ps.size]
         self.grad_flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
@@ -240,12 +241,13 @@ class DGPPO:
         Be, T = nodes.shape[:2]
         return GraphBatch(nodes.view(Be * T, *nodes.shape[2:]), edges.view(Be * T, *edges.shape[2:]),
                           recv.view(Be * T, -1), send.view(Be * T, -1), self._n_agents,
-                          self._env.agent_candidates(self.device))
+                          self._env.agent_candidates(self.device), raw_cols=self._env.nonagent_feature_cols)
 
     def _last_graph(self, next_graph, envs=slice(None)) -> GraphBatch:
         ng = next_graph
         return GraphBatch(ng.nodes[envs, -1], ng.edges[envs, -1], ng.receivers[envs, -1], ng.senders[envs, -1],
-                          self._n_agents, self._env.agent_candidates(self.device))
+                          self._n_agents, self._env.agent_candidates(self.device),
+                          raw_cols=self._env.nonagent_feature_cols)
 
     def _vh_all(self, rollout: Rollout, chunk: int):
         """Vh on every (env, t) graph with the stored actor carries, plus the final Vh (dgppo.py:218-228)."""

@@ -44,10 +44,12 @@ class _Net:
 
 
 class ActorNet(_Net):
-    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 0, gnn_layers: int = 2, action_dim: int = 2):
+    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 0, gnn_layers: int = 2, action_dim: int = 2,
+                 edge_dim: int = 4):
         self.n, self.A = n_agents, action_dim
+        self.node_dim, self.edge_dim = node_dim, edge_dim
         ps = self.ps = ParamSpace()
-        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers)
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head")
         self.gru = GRUCell(ps, "gru")
         self.scale_hid = Dense(ps, "ScaleHid", 64, 64, scale=0.01)
@@ -84,7 +86,7 @@ class ActorNet(_Net):
     def _fused_args(self, g: GraphBatch):
         """dgppo_policy_step_args with this net's parameter pointers (None if the fused kernel does not
         cover the configuration)."""
-        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1":
+        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1" or g.ED != 4 or g.nodes.shape[2] > GraphBatch.KD0:
             return None
         a = _lib.PolicyStepArgs()
         a.N, a.E, a.n_agents, a.C, a.D0, a.A = g.N, g.E, self.n, g.C, g.nodes.shape[2], self.A
@@ -193,10 +195,10 @@ class ActorNet(_Net):
 
 
 class VlNet(_Net):
-    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 1, gnn_layers: int = 2):
+    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 1, gnn_layers: int = 2, edge_dim: int = 4):
         self.n = n_agents
         ps = self.ps = ParamSpace()
-        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers)
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head")
         self.gru = GRUCell(ps, "gru")
         self.out = Dense(ps, "out", 64, 1)
@@ -240,10 +242,11 @@ class VlNet(_Net):
 
 
 class VhNet(_Net):
-    def __init__(self, node_dim: int, n_agents: int, n_cost: int, device, seed: int = 2, gnn_layers: int = 1):
+    def __init__(self, node_dim: int, n_agents: int, n_cost: int, device, seed: int = 2, gnn_layers: int = 1,
+                 edge_dim: int = 4):
         self.n, self.n_cost = n_agents, n_cost
         ps = self.ps = ParamSpace()
-        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers)
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head")
         self.gru = GRUCell(ps, "gru")
         self.out = Dense(ps, "out", 64, n_cost)

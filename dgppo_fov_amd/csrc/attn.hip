@@ -391,6 +391,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
 #pragma unroll
           for (int j = 0; j < 4; ++j) da += gv[H * D + h * 4 + j] * ef[j];
           da += gv[H * D + H * 4 + h];
+          if (p.da_add) da += p.da_add[(row * H + h) * C + c];
         }
         const float dot = group_sum<CP>(a[h] * da, L.scr);
         dl[h] = (ok && h < H) ? a[h] * (da - dot) * p.scale : 0.0f;
@@ -831,6 +832,7 @@ __global__ __launch_bounds__(256) void attn_bwd_wave_kernel(dgppo_gnn_attn_args 
 #pragma unroll
           for (int j = 0; j < 4; ++j) da += gv[kH * DM + h * 4 + j] * ef[j];
           da += gv[kH * DM + 12 + h];
+          if (p.da_add) da += p.da_add[(row * H + h) * C + c];
         }
         const float dot = group_sum<CP>(a[h] * da, nullptr);
         dl[h] = (ok && h < H) ? a[h] * (da - dot) * p.scale : 0.0f;
@@ -1376,6 +1378,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
 #pragma unroll
         for (int j = 0; j < 4; ++j) da += gv[3 * HS + 4 * h + j] * efv[sr][j];
         da += gv[3 * HS + 12 + h];
+        if (p.da_add && ok) da += p.da_add[(row * H + h) * C + c];
         da = ok ? da : 0.0f;
         const float dot = lanes::sum32(av[sr][h] * da);
         dl[h] = ok ? av[sr][h] * (da - dot) * p.scale : 0.0f;
@@ -1691,5 +1694,91 @@ extern "C" int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* p, void* stream) {
   if (!dgppo::valid(p) || !p->attn || !p->dxcat || !p->dqt || !p->dq || !p->dbeta) return DGPPO_EINVAL;
   if (p->G == 0) return 0;
   if (dgppo::run(p, true, (hipStream_t)stream)) return DGPPO_EINVAL;
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Edge columns past the first 4 (LidarOmniTarget's 10-wide edges).  The attention kernels keep their 4-wide edge
+// registers; the EX extra columns enter the value messages through xcat_x = sum_c attn * efx (edge_wsum, one
+// thread per output column) and the softmax backward through da_add (edge_da, one thread per (row, head, cand)).
+// Both are gather-bound over (G*n) x C x EX floats, a few % of the attention kernels' traffic.
+namespace dgppo {
+namespace {
+
+__global__ __launch_bounds__(256) void edge_wsum_kernel(int64_t R, int32_t n, int32_t C, int32_t H, int32_t EX,
+                                                        int32_t E, const float* __restrict__ attn,
+                                                        const int32_t* __restrict__ cand,
+                                                        const int32_t* __restrict__ sidx,
+                                                        const float* __restrict__ efx, float* __restrict__ out) {
+  const int W = H * EX;
+  const int64_t total = R * W;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / W;
+    const int k = (int)(t - r * W), h = k / EX, j = k - h * EX;
+    const int64_t g = r / n;
+    const int i = (int)(r - g * n);
+    const float* ar = attn + (r * H + h) * C;
+    const float* eg = efx + g * E * EX + j;
+    float acc = 0.0f;
+    for (int c = 0; c < C; ++c) {
+      const int e = cand[i * C + c];
+      if (sidx[r * C + c] >= 0) acc += ar[c] * eg[(int64_t)e * EX];
+    }
+    out[t] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void edge_da_kernel(int64_t R, int32_t n, int32_t C, int32_t H, int32_t EX,
+                                                      int32_t E, const float* __restrict__ dxx,
+                                                      const int32_t* __restrict__ cand,
+                                                      const int32_t* __restrict__ sidx,
+                                                      const float* __restrict__ efx, float* __restrict__ da) {
+  const int64_t total = R * H * C;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int c = (int)(t % C);
+    const int64_t rh = t / C;
+    const int h = (int)(rh % H);
+    const int64_t r = rh / H;
+    const int64_t g = r / n;
+    const int i = (int)(r - g * n);
+    float acc = 0.0f;
+    if (sidx[r * C + c] >= 0) {
+      const float* er = efx + (g * E + cand[i * C + c]) * EX;
+      const float* gr = dxx + r * H * EX + h * EX;
+      for (int j = 0; j < EX; ++j) acc += gr[j] * er[j];
+    }
+    da[t] = acc;
+  }
+}
+
+unsigned grid_for(int64_t total) {
+  int64_t nb = (total + 255) / 256;
+  return (unsigned)(nb < 8192 ? nb : 8192);
+}
+
+}  // namespace
+}  // namespace dgppo
+
+extern "C" int dgppo_gnn_edge_wsum(int32_t G, int32_t n_agents, int32_t C, int32_t H, int32_t EX, int32_t E,
+                                   const float* attn, const int32_t* cand, const int32_t* sidx, const float* efx,
+                                   float* out, void* stream) {
+  if (G < 0 || n_agents < 1 || C < 1 || H < 1 || EX < 1 || E < 1 || !attn || !cand || !sidx || !efx || !out)
+    return DGPPO_EINVAL;
+  const int64_t R = (int64_t)G * n_agents;
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(dgppo::edge_wsum_kernel, dim3(dgppo::grid_for(R * H * EX)), dim3(256), 0, (hipStream_t)stream,
+                     R, n_agents, C, H, EX, E, attn, cand, sidx, efx, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_gnn_edge_da(int32_t G, int32_t n_agents, int32_t C, int32_t H, int32_t EX, int32_t E,
+                                 const float* dxx, const int32_t* cand, const int32_t* sidx, const float* efx,
+                                 float* da_add, void* stream) {
+  if (G < 0 || n_agents < 1 || C < 1 || H < 1 || EX < 1 || E < 1 || !dxx || !cand || !sidx || !efx || !da_add)
+    return DGPPO_EINVAL;
+  const int64_t R = (int64_t)G * n_agents;
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(dgppo::edge_da_kernel, dim3(dgppo::grid_for(R * H * C)), dim3(256), 0, (hipStream_t)stream, R,
+                     n_agents, C, H, EX, E, dxx, cand, sidx, efx, da_add);
   return (int)hipGetLastError();
 }

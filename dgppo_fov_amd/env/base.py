@@ -49,6 +49,10 @@ class MultiAgentEnv(ABC):
     GOAL = 1
     OBS = 2
 
+    # node columns a never-receiving node can have nonzero (None: all); the GNN's agent-mode layers read only
+    # these when the nodes are wider than the attention kernels' raw-row limit (nn/layers.py GraphBatch)
+    nonagent_feature_cols = None
+
     def __init__(self, num_agents: int, area_size: float, max_step: int = 256, dt: float = 0.03,
                  params: Optional[dict] = None, device=None):
         self._num_agents = int(num_agents)

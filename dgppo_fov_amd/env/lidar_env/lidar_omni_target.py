@@ -41,6 +41,10 @@ class LidarOmniTarget(LidarTarget):
         assert p["min_safe_distance"] > 2 * p["car_radius"], "min_safe_distance must exceed 2 * car_radius"
         assert p["min_safe_distance"] < p["max_sensor_range"], "min_safe_distance must be below max_sensor_range"
 
+    # Node columns a goal / lidar-hit node can have nonzero: position (0, 1) and its type one-hot (7, 8);
+    # goals are [pos, 0 x 5] (lidar_omni_target.py:281-284), hits [pos, 0 x 5] (lidar_env/base.py get_graph).
+    nonagent_feature_cols = (0, 1, 7, 8)
+
     @property
     def n_cost(self) -> int:
         return 5

@@ -145,6 +145,16 @@ def sender_table(G, n, C, E, cand, receivers, senders, out):
                                             _p(out), _stream(out)), "dgppo_gnn_sender_table")
 
 
+def edge_wsum(G, n, C, H, EX, E, attn, cand, sidx, efx, out):
+    _chk(_lib.load().dgppo_gnn_edge_wsum(int(G), int(n), int(C), int(H), int(EX), int(E), _p(attn), _p(cand),
+                                         _p(sidx), _p(efx), _p(out), _stream(out)), "dgppo_gnn_edge_wsum")
+
+
+def edge_da(G, n, C, H, EX, E, dxx, cand, sidx, efx, out):
+    _chk(_lib.load().dgppo_gnn_edge_da(int(G), int(n), int(C), int(H), int(EX), int(E), _p(dxx), _p(cand),
+                                       _p(sidx), _p(efx), _p(out), _stream(out)), "dgppo_gnn_edge_da")
+
+
 def gnn_attn_partial_blocks(args: _lib.GnnAttnArgs) -> int:
     return int(_lib.load().dgppo_gnn_attn_partial_blocks(ctypes.byref(args)))
 

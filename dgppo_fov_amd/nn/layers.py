@@ -309,8 +309,11 @@ class GRUCell:
 class GraphTransformer:
     """GraphTransformer layer (dgppo/nn/gnn.py:78-117) in the per-receiving-agent form."""
 
-    def __init__(self, ps, name, D, F, H=3):
+    def __init__(self, ps, name, D, F, H=3, ED=4):
         self.ps, self.name, self.D, self.F, self.H = ps, name, D, F, H
+        self.ED, self.EX = ED, ED - 4  # edge width; columns past the first 4 go through Wex
+        if ED < 4:
+            raise ValueError(f"edge_dim {ED} < 4")
         ps.add(name + ".Wq", (D, H * F), "orthogonal")
         ps.add(name + ".bq", (H * F,), "zeros")
         ps.add(name + ".Wkt", (H, F, D), "orthogonal")
@@ -318,6 +321,8 @@ class GraphTransformer:
         ps.add(name + ".Wcat", (H * (D + 5), F), "orthogonal")
         ps.add(name + ".Wu", (D, F), "orthogonal")
         ps.add(name + ".bu", (F,), "zeros")
+        if self.EX:
+            ps.add(name + ".Wex", (H * self.EX, F), "orthogonal")  # Dense_3 rows 4.. as (head, column, F)
 
     def v(self, k, g=False):
         return self.ps.view(self.name + "." + k, g)
@@ -332,7 +337,10 @@ class GraphTransformer:
         self.v("Wkt").copy_(torch.from_numpy(np.ascontiguousarray(wk)))
         self.v("bk").copy_(torch.from_numpy(f32(d["Dense_1"]["bias"])))
         wv = f32(d["Dense_2"]["kernel"]).reshape(D, H, F).transpose(1, 0, 2).reshape(H * D, F)
-        we = f32(d["Dense_3"]["kernel"]).reshape(4, H, F).transpose(1, 0, 2).reshape(H * 4, F)
+        k3 = f32(d["Dense_3"]["kernel"]).reshape(self.ED, H, F)
+        we = k3[:4].transpose(1, 0, 2).reshape(H * 4, F)
+        if self.EX:
+            self.v("Wex").copy_(torch.from_numpy(np.ascontiguousarray(k3[4:].transpose(1, 0, 2).reshape(H * self.EX, F))))
         bv = f32(d["Dense_2"]["bias"]).reshape(H, F)
         self.v("Wcat").copy_(torch.from_numpy(np.concatenate([wv, we, bv], 0)))
         self.v("Wu").copy_(torch.from_numpy(f32(d["Dense_4"]["kernel"])))
@@ -342,12 +350,16 @@ class GraphTransformer:
         D, F, H = self.D, self.F, self.H
         wcat = self.v("Wcat").cpu().numpy()
         wv, we, bv = wcat[:H * D], wcat[H * D:H * D + 4 * H], wcat[H * D + 4 * H:]
+        k3 = we.reshape(H, 4, F).transpose(1, 0, 2).reshape(4, H * F)
+        if self.EX:
+            wex = self.v("Wex").cpu().numpy().reshape(H, self.EX, F).transpose(1, 0, 2).reshape(self.EX, H * F)
+            k3 = np.concatenate([k3, wex], 0)
         return {
             "Dense_0": {"kernel": self.v("Wq").cpu().numpy(), "bias": self.v("bq").cpu().numpy()},
             "Dense_1": {"kernel": self.v("Wkt").cpu().numpy().transpose(2, 0, 1).reshape(D, H * F),
                         "bias": self.v("bk").cpu().numpy()},
             "Dense_2": {"kernel": wv.reshape(H, D, F).transpose(1, 0, 2).reshape(D, H * F), "bias": bv.reshape(-1)},
-            "Dense_3": {"kernel": we.reshape(H, 4, F).transpose(1, 0, 2).reshape(4, H * F)},
+            "Dense_3": {"kernel": k3},
             "Dense_4": {"kernel": self.v("Wu").cpu().numpy(), "bias": self.v("bu").cpu().numpy()},
         }
 
@@ -356,33 +368,41 @@ class GraphTransformer:
         d = {"Dense_0": {"kernel": orthogonal(rng, (D, H * F)), "bias": np.zeros(H * F, np.float32)},
              "Dense_1": {"kernel": orthogonal(rng, (D, H * F)), "bias": np.zeros(H * F, np.float32)},
              "Dense_2": {"kernel": orthogonal(rng, (D, H * F)), "bias": np.zeros(H * F, np.float32)},
-             "Dense_3": {"kernel": orthogonal(rng, (4, H * F))},
+             "Dense_3": {"kernel": orthogonal(rng, (self.ED, H * F))},
              "Dense_4": {"kernel": orthogonal(rng, (D, F)), "bias": np.zeros(F, np.float32)}}
         self.load_flax(d)
 
     def _attn_args(self, g: "GraphBatch", xa=None, pre=None):
+        """Kernel arguments; returns (args, tensors the pointers refer to, kept alive over the launch)."""
         a = K._lib.GnnAttnArgs()
-        G, N, D0 = g.nodes.shape
+        G, N = g.G, g.N
         a.G, a.N, a.E, a.n_agents = G, N, g.E, g.n
         a.D, a.F, a.H, a.C = self.D, self.F, self.H, g.C
         a.cand, a.receivers, a.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
         a.sidx = K._p(g.sidx)
-        a.x, a.x_gstride = K._p(g.nodes), N * D0
-        a.ef, a.ef_gstride = K._p(g.edges), g.E * 4
+        a.ef, a.ef_gstride = K._p(g.edges_head), g.E * 4
         a.bk = K._p(self.v("bk"))
         a.scale = 1.0 / math.sqrt(self.F)
-        if xa is not None:  # agent mode: agents from xa, other senders = pre's Dense_4 + ReLU of raw rows
-            a.D0 = D0
+        keep = []
+        if xa is None:
+            a.x, a.x_gstride = K._p(g.nodes), N * g.nodes.shape[2]
+        else:  # agent mode: agents from xa, other senders = pre's Dense_4 + ReLU of raw rows
+            raw, cols = g.sender_raw
+            D0 = raw.shape[2]
+            a.x, a.x_gstride, a.D0 = K._p(raw), N * D0, D0
             a.xa, a.xa_gstride = K._p(xa), g.n * self.D
             if pre is not None:
-                a.pre_W, a.pre_b = K._p(pre.v("Wu")), K._p(pre.v("bu"))
-        return a
+                W = pre.v("Wu") if cols is None else pre.v("Wu").index_select(0, cols)
+                keep.append(W)
+                a.pre_W, a.pre_b = K._p(W), K._p(pre.v("bu"))
+        return a, keep
 
     def fwd(self, g: "GraphBatch", xa=None, pre=None):
         """One layer on the graph batch.  xa None: senders read the raw nodes (G, N, D) (first layer);
         else xa (G*n, D) holds the agents' rows and the never-receiving nodes are `pre`'s
         Dense_4 + ReLU of their raw rows (agent mode).  Returns Y (G*n, F) = the agents' outputs
-        (only agents receive, so only their rows feed the next layer's queries) and the cache."""
+        (only agents receive, so only their rows feed the next layer's queries) and the cache.
+        Edge columns past the first 4 add (sum_c attn * efx) @ Wex to the messages (edge_wsum)."""
         G, N, n = g.G, g.N, g.n
         D, F, H, C = self.D, self.F, self.H, g.C
         dev = g.nodes.device
@@ -394,22 +414,28 @@ class GraphTransformer:
         K.gemm(Q, self.v("Wkt"), QT, R, D, F, lda=H * F, sa=F, ldb=D, sb=F * D, ldc=H * D, sc=D, batch=H)
         attn = torch.empty((R, H, C), device=dev)
         xcat = torch.empty((R, H * (D + 5)), device=dev)
-        a = self._attn_args(g, xa, pre)
+        a, keep = self._attn_args(g, xa, pre)
         a.q, a.qt, a.attn, a.xcat = K._p(Q), K._p(QT), K._p(attn), K._p(xcat)
         K.gnn_attn(a, False, dev)
+        del keep
         M = torch.empty((R, F), device=dev)
         K.gemm(xcat, self.v("Wcat"), M, R, F, H * (D + 5), alpha=1.0 / H)
+        xcx = None
+        if self.EX:
+            xcx = torch.empty((R, H * self.EX), device=dev)
+            K.edge_wsum(G, n, C, H, self.EX, g.E, attn, g.cand, g.sidx, g.edges_x, xcx)
+            K.gemm(xcx, self.v("Wex"), M, R, F, H * self.EX, alpha=1.0 / H, beta=1.0)
         Y = torch.empty((R, F), device=dev)
         K.gemm(A, self.v("Wu"), Y, R, F, D, bias=self.v("bu"), addend=M, relu=True, **akw)
-        return Y, (xa, pre, Q, QT, attn, xcat, Y)
+        return Y, (xa, pre, Q, QT, attn, xcat, xcx, Y)
 
     def bwd(self, cache, dY, g: "GraphBatch"):
         """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, else None;
         accumulates this layer's grads and, in agent mode with `pre`, pre's Dense_4 grads from the
         transformed senders."""
-        xa, pre, Q, QT, attn, xcat, Y = cache
+        xa, pre, Q, QT, attn, xcat, xcx, Y = cache
         G, N, n = g.G, g.N, g.n
-        D, F, H = self.D, self.F, self.H
+        D, F, H, C = self.D, self.F, self.H, g.C
         R = G * n
         W = H * (D + 5)
         dev = dY.device
@@ -418,13 +444,22 @@ class GraphTransformer:
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
         K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)
+        da_add = None
+        if self.EX:
+            WX = H * self.EX
+            dxx = torch.empty((R, WX), device=dev)
+            K.gemm(dY, self.v("Wex"), dxx, R, WX, F, tb=True, ldb=F, alpha=1.0 / H)
+            K.gemm(xcx, dY, self.v("Wex", True), WX, F, R, ta=True, lda=WX, alpha=1.0 / H, beta=1.0)
+            da_add = torch.empty((R, H, C), device=dev)
+            K.edge_da(G, n, C, H, self.EX, g.E, dxx, g.cand, g.sidx, g.edges_x, da_add)
         dQT = torch.empty((R, H * D), device=dev)
         dQ = torch.empty((R, H * F), device=dev)
         dbeta = torch.empty((R, H), device=dev)
         dXa = torch.zeros((R, D), device=dev) if xa is not None else None
-        a = self._attn_args(g, xa, pre)
+        a, keep = self._attn_args(g, xa, pre)
         a.q, a.qt, a.attn = K._p(Q), K._p(QT), K._p(attn)
         a.dxcat, a.dqt, a.dq, a.dbeta = K._p(dxcat), K._p(dQT), K._p(dQ), K._p(dbeta)
+        a.da_add = K._p(da_add)
         part = None
         if xa is not None:
             a.dxa, a.dxa_gstride = K._p(dXa), n * D
@@ -434,15 +469,20 @@ class GraphTransformer:
                 part = K.workspace(nb * PK, dev, "attn_pre")
                 a.dpre_part = K._p(part)
         K.gnn_attn(a, True, dev)
-        if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre
+        del keep
+        if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre (Wu rows = the raw columns used)
+            cols = g.sender_raw[1]
             ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
             nw = a.D0 * D
-            if ob == ow + nw:
+            if ob == ow + nw and cols is None:
                 K.colsum(part, nb, PK, pre.ps.grad[ow:ow + PK], beta=1.0)
             else:
                 tmp = torch.empty(PK, device=dev)
                 K.colsum(part, nb, PK, tmp)
-                pre.ps.grad[ow:ow + nw].add_(tmp[:nw])
+                if cols is None:
+                    pre.ps.grad[ow:ow + nw].add_(tmp[:nw])
+                else:
+                    pre.v("Wu", True).index_add_(0, cols, tmp[:nw].view(a.D0, D))
                 pre.ps.grad[ob:ob + D].add_(tmp[nw:])
         K.gemm(dbeta, Q, self.v("bk", True), 1, F, R, ta=True, lda=H, sa=1, ldb=H * F, sb=F, ldc=F, sc=F,
                batch=H, beta=1.0)
@@ -458,9 +498,18 @@ class GraphTransformer:
         return dXa
 
 
+_COLS = {}
+
+
 class GraphBatch:
     """A batch of env graphs as the GNN kernels consume them (nodes/edges/receivers/senders contiguous
-    (G, ...)), plus the per-agent candidate-edge table of the env layout."""
+    (G, ...)), plus the per-agent candidate-edge table of the env layout.
+
+    raw_cols: the node-feature columns a never-receiving node (goal, obstacle, lidar hit) can have nonzero
+    (env.nonagent_feature_cols); needed when the node width exceeds the attention kernels' raw-row limit
+    (8), e.g. LidarOmniTarget's 10-wide nodes: agent-mode layers then read those columns only."""
+
+    KD0 = 8  # attn.hip kD0
 
     @staticmethod
     def from_graph(graph, env, flatten_dims=None):
@@ -469,19 +518,22 @@ class GraphBatch:
         G = int(np.prod(graph.nodes.shape[:nd]))
         return GraphBatch(graph.nodes.reshape(G, *graph.nodes.shape[nd:]), graph.edges.reshape(G, *graph.edges.shape[nd:]),
                           graph.receivers.reshape(G, -1), graph.senders.reshape(G, -1), env.num_agents,
-                          env.agent_candidates(graph.nodes.device))
+                          env.agent_candidates(graph.nodes.device), raw_cols=getattr(env, "nonagent_feature_cols", None))
 
-    def __init__(self, nodes, edges, receivers, senders, n_agents: int, cand: torch.Tensor):
+    def __init__(self, nodes, edges, receivers, senders, n_agents: int, cand: torch.Tensor, raw_cols=None):
         self.nodes = nodes.contiguous()
         self.edges = edges.contiguous()
         self.receivers = receivers.contiguous()
         self.senders = senders.contiguous()
         self.G, self.N = self.nodes.shape[0], self.nodes.shape[1]
         self.E = self.edges.shape[1]
+        self.ED = self.edges.shape[2]
         self.n = int(n_agents)
         self.cand = cand
         self.C = int(cand.shape[1])
+        self.raw_cols = tuple(int(c) for c in raw_cols) if raw_cols is not None else None
         self._sidx = None
+        self._edges_head = self._edges_x = self._sender_raw = None
 
     @property
     def sidx(self) -> torch.Tensor:
@@ -492,12 +544,48 @@ class GraphBatch:
             K.sender_table(self.G, self.n, self.C, self.E, self.cand, self.receivers, self.senders, self._sidx)
         return self._sidx
 
+    @property
+    def edges_head(self) -> torch.Tensor:
+        """(G, E, 4): the edge columns the attention kernels read."""
+        if self.ED == 4:
+            return self.edges
+        if self._edges_head is None:
+            self._edges_head = self.edges[..., :4].contiguous()
+        return self._edges_head
+
+    @property
+    def edges_x(self):
+        """(G, E, ED-4) the remaining edge columns (None for 4-wide edges)."""
+        if self.ED == 4:
+            return None
+        if self._edges_x is None:
+            self._edges_x = self.edges[..., 4:].contiguous()
+        return self._edges_x
+
+    @property
+    def sender_raw(self):
+        """(raw rows the agent-mode layers read for never-receiving senders, column index tensor or None)."""
+        if self._sender_raw is None:
+            D0 = self.nodes.shape[2]
+            if D0 <= self.KD0:
+                self._sender_raw = (self.nodes, None)
+            else:
+                if self.raw_cols is None or len(self.raw_cols) > self.KD0:
+                    raise NotImplementedError(
+                        f"node width {D0} > {self.KD0} needs raw_cols (<= {self.KD0} columns) for agent-mode layers")
+                key = (self.raw_cols, str(self.nodes.device))
+                if key not in _COLS:  # created once per device, so hipGraph capture never sees the H2D copy
+                    _COLS[key] = torch.tensor(self.raw_cols, dtype=torch.int64, device=self.nodes.device)
+                cols = _COLS[key]
+                self._sender_raw = (self.nodes.index_select(2, cols).contiguous(), cols)
+        return self._sender_raw
+
 
 class GNN:
     """GraphTransformerGNN (dgppo/nn/gnn.py:127-142), msg_dim 32, out_dim 64, 3 heads, followed by
     type_nodes(agent): returns the agent rows of the last layer, (G*n, out_dim)."""
 
-    def __init__(self, ps, name, node_dim, n_layers, msg_dim=32, out_dim=64, n_heads=3):
+    def __init__(self, ps, name, node_dim, n_layers, msg_dim=32, out_dim=64, n_heads=3, edge_dim=4):
         if not 1 <= n_layers <= 2:
             raise NotImplementedError("GNN depth 1 or 2 (the reference's actor/Vl/Vh configs): deeper stacks need "
                                       "the never-receiving nodes' hidden features materialised")
@@ -505,7 +593,7 @@ class GNN:
         d = node_dim
         for i in range(n_layers):
             od = out_dim if i == n_layers - 1 else msg_dim
-            self.layers.append(GraphTransformer(ps, f"{name}.GraphTransformer_{i}", d, od, n_heads))
+            self.layers.append(GraphTransformer(ps, f"{name}.GraphTransformer_{i}", d, od, n_heads, edge_dim))
             d = od
 
     def init_host(self, rng):

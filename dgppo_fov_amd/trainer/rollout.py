@@ -60,7 +60,7 @@ class RolloutEngine:
     def _act(self, t: int):
         env, b = self.env, self.buf
         g = GraphBatch(b.nodes[t], b.edges[t], b.receivers[t], b.senders[t], env.num_agents,
-                       env.agent_candidates(self.device))
+                       env.agent_candidates(self.device), raw_cols=env.nonagent_feature_cols)
         n = env.num_agents
         h = self.rnn[t].view(self.B * n, 64)
         if self.mode == self.MODE_SAMPLE:

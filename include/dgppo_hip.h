@@ -220,6 +220,8 @@ typedef struct dgppo_gnn_attn_args {
   float* dxa; int64_t dxa_gstride;
   float* dpre_part;
   const int32_t* sidx;  /* optional (G*n, C) sender table from dgppo_gnn_sender_table (else resolved per use) */
+  const float* da_add;  /* optional (G*n, H, C) extra dL/d attn added in the softmax backward: the edge columns
+                           past the first 4 (dgppo_gnn_edge_da) */
 } dgppo_gnn_attn_args;
 
 int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
@@ -229,6 +231,16 @@ int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, int32_t E, co
                            const int32_t* receivers, const int32_t* senders, int32_t* sidx, void* stream);
 int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* args, void* stream);
 int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* args, void* stream);
+/* Edge features wider than 4 (LidarOmniTarget's 10-wide edges, lidar_omni_target.py edge_dim): the attention
+ * kernels see columns 0..3, the remaining EX columns efx (G, E, EX) go through these two.
+ *   edge_wsum: out[r, h*EX + j] = sum_c attn[r, h, c] * efx[g, cand[i][c], j] over sidx[r][c] >= 0
+ *              (the attention-weighted edge term of the value messages, dgppo/nn/gnn.py:99-104)
+ *   edge_da:   da_add[r, h, c] = sum_j dxx[r, h*EX + j] * efx[g, cand[i][c], j] if sidx[r][c] >= 0 else 0
+ * with r = g*n + i. */
+int dgppo_gnn_edge_wsum(int32_t G, int32_t n_agents, int32_t C, int32_t H, int32_t EX, int32_t E, const float* attn,
+                        const int32_t* cand, const int32_t* sidx, const float* efx, float* out, void* stream);
+int dgppo_gnn_edge_da(int32_t G, int32_t n_agents, int32_t C, int32_t H, int32_t EX, int32_t E, const float* dxx,
+                      const int32_t* cand, const int32_t* sidx, const float* efx, float* da_add, void* stream);
 
 /* flax LayerNorm (+ReLU) over rows of width F (dgppo/nn/mlp.py:27-29); bwd accumulates dscale/dbias */
 int dgppo_layernorm_fwd(const float* x, const float* scale, const float* bias, float* y, float* mean, float* rstd,

@@ -118,29 +118,37 @@ def _graphs(cuda, eid, n, obs, S, L, seed=0):
     rng = np.random.default_rng(seed)
     for t in range(L):
         gs.append(g)
-        a = torch.from_numpy(rng.uniform(-1, 1, (S, n, 2)).astype(np.float32)).to(cuda)
+        a = torch.from_numpy(rng.uniform(-1, 1, (S, n, env.action_dim)).astype(np.float32)).to(cuda)
         g = env.step(g, a).graph
     stack = lambda f: torch.stack([getattr(x, f) for x in gs], 1).contiguous()  # noqa: E731
     nodes, edges, recv, send = stack("nodes"), stack("edges"), stack("receivers"), stack("senders")
     gb = GraphBatch(nodes.view(S * L, *nodes.shape[2:]), edges.view(S * L, *edges.shape[2:]),
-                    recv.view(S * L, -1), send.view(S * L, -1), n, env.agent_candidates(cuda))
+                    recv.view(S * L, -1), send.view(S * L, -1), n, env.agent_candidates(cuda),
+                    raw_cols=env.nonagent_feature_cols)
     host = dict(nodes=gb.nodes.cpu().numpy(), edges=gb.edges.cpu().numpy(), receivers=gb.receivers.cpu().numpy(),
                 senders=gb.senders.cpu().numpy())
     return env, gb, host
 
 
 CASES = [("LidarSpread", 8, 3), ("MPETarget", 3, 0), ("MPESpread", 3, 3), ("LidarBicycleTarget", 4, 2)]
+# 10-wide nodes and edges, 3-d actions: edge columns 4.. through edge_wsum / edge_da, agent-mode raw columns
+OMNI = [("LidarOmniTarget", 3, 2), ("LidarOmniTarget", 8, 3)]
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES)
+def _nets_kw(env):
+    return dict(edge_dim=env.edge_dim)
+
+
+@pytest.mark.parametrize("eid,n,obs", CASES + OMNI)
 def test_actor_eval_seq_fwd_bwd(cuda, eid, n, obs):
     S, L = 3, 4
     env, gb, host = _graphs(cuda, eid, n, obs, S, L)
-    net = ActorNet(env.node_dim, n, cuda, seed=3)
+    A = env.action_dim
+    net = ActorNet(env.node_dim, n, cuda, seed=3, action_dim=A, **_nets_kw(env))
     rng = np.random.default_rng(1)
-    actions = rng.uniform(-0.99, 0.99, (S * L * n, 2)).astype(np.float32)
-    actions[0] = [0.9995, -0.9999]  # both boundary branches of the clipped log_prob
-    eps = rng.standard_normal((n, 2)).astype(np.float32)
+    actions = rng.uniform(-0.99, 0.99, (S * L * n, A)).astype(np.float32)
+    actions[0, :2] = [0.9995, -0.9999]  # both boundary branches of the clipped log_prob
+    eps = rng.standard_normal((n, A)).astype(np.float32)
     lp, ent, cache = net.eval_seq_fwd(gb, S, L, torch.from_numpy(actions).to(cuda), torch.from_numpy(eps).to(cuda))
     p = R.to_t(net.flax(), requires_grad=True)
     rlp, rent = R.actor_eval_seq(p, host, S, L, n, actions, eps)
@@ -162,11 +170,11 @@ def test_actor_eval_seq_fwd_bwd(cuda, eid, n, obs):
         _grad_close(a, b, "actor grad " + path)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES[:2])
+@pytest.mark.parametrize("eid,n,obs", CASES[:2] + OMNI[:1])
 def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
     S, L = 3, 5
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=4)
-    net = VlNet(env.node_dim, n, cuda, seed=5)
+    net = VlNet(env.node_dim, n, cuda, seed=5, **_nets_kw(env))
     v, _, cache = net.seq_fwd(gb, S, L)
     p = R.to_t(net.flax(), requires_grad=True)
     rv = R.vl_seq(p, host, S, L, n)
@@ -184,11 +192,11 @@ def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
         _grad_close(a, b, "Vl grad " + path)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES[:3])
+@pytest.mark.parametrize("eid,n,obs", CASES[:3] + OMNI[:1])
 def test_vh_fwd_bwd(cuda, eid, n, obs):
     S, L = 2, 3
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=6)
-    net = VhNet(env.node_dim, n, 2, cuda, seed=7)
+    net = VhNet(env.node_dim, n, 2, cuda, seed=7, **_nets_kw(env))
     h = np.random.default_rng(3).standard_normal((S * L * n, 64)).astype(np.float32) * 0.5
     out, cache = net.fwd(gb, torch.from_numpy(h).to(cuda))
     p = R.to_t(net.flax(), requires_grad=True)
@@ -209,7 +217,7 @@ def test_vh_fwd_bwd(cuda, eid, n, obs):
 
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("layers", [2, 1])
-@pytest.mark.parametrize("eid,n,obs", CASES)
+@pytest.mark.parametrize("eid,n,obs", CASES + OMNI[:1])
 def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
     """ActorNet.act (PPOPolicy.get_action / sample_action, policy.py:191-212) for one graph batch with
     non-zero carries, through the fused dgppo_policy_step kernel ("1") and the unfused layer chain
@@ -217,11 +225,12 @@ def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
     monkeypatch.setenv("DGPPO_FUSED_POLICY", fused)
     S, L = 5, 3  # 15 graphs: partial last row group in the fused kernel for every n
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=2)
-    net = ActorNet(env.node_dim, n, cuda, seed=5, gnn_layers=layers)
+    A = env.action_dim
+    net = ActorNet(env.node_dim, n, cuda, seed=5, gnn_layers=layers, action_dim=A, **_nets_kw(env))
     rows = S * L * n
     rng = np.random.default_rng(4)
     h = torch.from_numpy(rng.standard_normal((rows, 64)).astype(np.float32) * 0.5).to(cuda)
-    noise = torch.from_numpy(rng.standard_normal((rows, 2)).astype(np.float32)).to(cuda)
+    noise = torch.from_numpy(rng.standard_normal((rows, A)).astype(np.float32)).to(cuda)
     p = R.to_t(net.flax())
     h2_ref = R.actor_carry(p, host, h.cpu().double().reshape(S * L, n, 64), n)
     mu, sd = R.policy_dist(p, h2_ref)
@@ -229,8 +238,8 @@ def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
         a, lp, h2 = net.act(gb, h, mode, noise=noise if mode else None)
         torch.cuda.synchronize()
         _close(h2.cpu().numpy(), h2_ref.numpy().reshape(rows, 64), what=f"carry mode {mode}")
-        pre = mu + sd * noise.cpu().double().reshape(S * L, n, 2) if mode else mu
+        pre = mu + sd * noise.cpu().double().reshape(S * L, n, A) if mode else mu
         a_ref = torch.tanh(pre)
-        _close(a.cpu().numpy(), a_ref.numpy().reshape(rows, 2), what=f"action mode {mode}")
-        lp_ref = R.tanh_normal_log_prob(a.cpu().double().reshape(S * L, n, 2), mu, sd)
+        _close(a.cpu().numpy(), a_ref.numpy().reshape(rows, A), what=f"action mode {mode}")
+        lp_ref = R.tanh_normal_log_prob(a.cpu().double().reshape(S * L, n, A), mu, sd)
         _close(lp.cpu().numpy(), lp_ref.numpy().reshape(rows), rtol=3e-5, atol=3e-5, what=f"log_pi mode {mode}")

@@ -46,7 +46,7 @@ def _host_graph(eng, t):
 
 
 @pytest.mark.parametrize("eid,n,obs,graph", [("LidarSpread", 3, 2, True), ("MPETarget", 3, 0, False),
-                                             ("LidarBicycleTarget", 2, 1, True)])
+                                             ("LidarBicycleTarget", 2, 1, True), ("LidarOmniTarget", 3, 2, True)])
 def test_policy_rollout_matches_oracle(cuda, eid, n, obs, graph):
     B, T = 3, 12
     env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
