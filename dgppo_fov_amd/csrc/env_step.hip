@@ -567,6 +567,7 @@ __device__ __forceinline__ bool rect_inside0(const float* rec, float px, float p
 // of a workgroup, and run the exact per-edge arithmetic (raytrace_nodiv / rect_raytrace), combined
 // per ray with an LDS atomic min on an order-preserving encoding (NaN wins, as jnp.min).
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"  // branch-free predicates on purpose
+constexpr int kOmniSD = 7, kOmniED = 10, kOmniNC = 5;  // LidarOmniTarget state / edge width, costs
 namespace wv {
 constexpr int NA = 8, NR = 32, NK = 8;
 constexpr float kCullMargin = 0.01f;
@@ -666,6 +667,12 @@ struct Carve {
 template <int ENGINE, int GOAL, int SD, int O>
 __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
   static_assert(O >= 1 && O <= 4, "obstacle records are staged by one load per lane");
+  // LidarOmniTarget (SD 7, own goals): omni dynamics, 5 costs, 10-wide edges; same LiDAR and graph rows
+  constexpr bool OMNI = ENGINE == DGPPO_ENGINE_OMNI;
+  static_assert(!OMNI || (SD == 7 && GOAL == DGPPO_GOAL_TARGET), "LidarOmniTarget layout");
+  constexpr int AD = OMNI ? 3 : 2;   // action width
+  constexpr int ED = OMNI ? 10 : 4;  // edge width
+  constexpr int XS = 16 * SD - 64;   // agent + goal state floats past the first 64
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int wg_items[4];
   using C = Carve<SD, O>;
@@ -686,15 +693,19 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
   const float* ob = io.obstacles + env * io.obstacles_stride;
   const float* ac = io.action + env * io.action_stride;
   const float cv0 = st[lane];
-  const float cv1 = SD == 5 ? st[64 + (lane & 15)] : 0.0f;
+  const int xsl = 64 + (lane < XS ? lane : XS - 1);
+  const float cv1 = XS > 0 ? st[xsl] : 0.0f;
   const float hcx = st[(16 + lane) * SD + 0], hcy = st[(16 + lane) * SD + 1];
   const float obv = ob[lane < O * DGPPO_OBST_FIELDS ? lane : 0];
   const float rdv = io.ray_dirs[lane];
-  const float a0 = clampf_nan(ac[2 * gj + 0], -1.0f, 1.0f), a1 = clampf_nan(ac[2 * gj + 1], -1.0f, 1.0f);
+  const float a0 = clampf_nan(ac[AD * gj + 0], -1.0f, 1.0f), a1 = clampf_nan(ac[AD * gj + 1], -1.0f, 1.0f);
+  const float aw = OMNI ? clampf_nan(ac[AD * gj + AD - 1], -1000.0f, 1000.0f) : 0.0f;  // omni alpha
   // unconditional LDS stores: a store under a lane predicate lets the compiler sink its global load
   // into the predicated block, serialising a second HBM round trip
   lds[C::cur + lane] = cv0;
-  if (SD == 5) lds[C::cur + 64 + (lane & 15)] = cv1;
+  if (XS > 0) lds[C::cur + xsl] = cv1;
+  // omni obstacle cost reads every current hit: staged in the next-hit rows (rewritten in E)
+  if (OMNI) reinterpret_cast<float2*>(lds + C::hits)[lane] = make_float2(hcx, hcy);
   lds[C::obst + lane] = obv;  // lanes >= 16 O land in evec / rays, both written after this
   lds[C::rays + lane] = rdv;
   wave_sync();
@@ -719,7 +730,20 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     ev = rec[8 + 2 * ((e + 3) & 3) + c] - rec[8 + 2 * e + c];  // (x4 - x3, y4 - y3)
   }
   float y[SD];
-  if (ENGINE == DGPPO_ENGINE_BICYCLE) {
+  if constexpr (OMNI) {  // agent_step_euler (lidar_omni_target.py:146-197)
+    const float acc_x = a0 * 10.0f, acc_y = a1 * 10.0f, alw = aw * 5.0f;
+    const float theta = atan2_32(x[3], x[2]);
+    const float new_theta = theta + x[6] * cfg.dt;
+    float sn_, cn_;
+    sincos32(new_theta, &sn_, &cn_);
+    y[0] = x[0] + x[4] * cfg.dt;
+    y[1] = x[1] + x[5] * cfg.dt;
+    y[2] = cn_;
+    y[3] = sn_;
+    y[4] = x[4] + acc_x * cfg.dt;
+    y[5] = x[5] + acc_y * cfg.dt;
+    y[6] = x[6] + alw * cfg.dt;
+  } else if constexpr (ENGINE == DGPPO_ENGINE_BICYCLE) {
     const float theta = atan2_32(x[3], x[2]);
     const float theta_next = theta + ((x[4] * a0) * cfg.dt) * 10.0f;
     float st_, ct_, sn_, cn_;
@@ -748,11 +772,62 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
   float daa = norm2(cix - x[0], ciy - x[1]);
   if (gi == gj) daa = daa + 1e6f;
   const float dga = GOAL == DGPPO_GOAL_SPREAD ? norm2(gix - x[0], giy - x[1]) : norm2(gix - cix, giy - ciy);
-  const float dh = norm2(hcx - cix, hcy - ciy);
+  float dh;
+  if constexpr (OMNI) {  // every agent's current hits and the origin row (see oracle get_cost_omni)
+    const float* ch = lds + C::hits;
+    dh = norm2(0.0f - cix, 0.0f - ciy);
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+      const float2 hv = reinterpret_cast<const float2*>(ch)[gj + 8 * t];
+      dh = min_nan(dh, norm2(hv.x - cix, hv.y - ciy));
+    }
+  } else {
+    dh = norm2(hcx - cix, hcy - ciy);
+  }
   const float md = min8(daa), dg = min8(dga), mo = min8(dh);
 
-  // ---- C: cost (lanes j < 2 of group i), reward (lane 0) -----------------------------------
-  {
+  // ---- C: cost (lanes j < 2 of group i, 5 for omni), reward (lane 0) -------------------------
+  if constexpr (OMNI) {
+    float cq[kOmniNC];
+    cq[0] = cfg.c_agent_cost - md;
+    cq[1] = cfg.c_obs_cost - mo;
+    cq[2] = -1.0f, cq[3] = -1.0f, cq[4] = -1.0f;  // FoV on the chain gi -> gi+1; the last agent is safe
+    if (gi + 1 < NA) {
+      const float xi0 = cix, xi1 = ciy, xi2 = cur[gi * SD + 2], xi3 = cur[gi * SD + 3];
+      const float dx = cur[(gi + 1) * SD] - xi0, dy = cur[(gi + 1) * SD + 1] - xi1;
+      const float lx = xi2 * dx + xi3 * dy;
+      const float ly = (-xi3) * dx + xi2 * dy;
+      const float nrm = norm2(lx, ly);
+      cq[2] = cfg.c_cos_fov * (nrm + 1e-8f) - lx;
+      cq[3] = nrm - cfg.fov_rmax;
+      cq[4] = cfg.fov_dmin - nrm;
+    }
+    const int q = gj < kOmniNC ? gj : 0;
+    float v = q == 0 ? cq[0] : (q == 1 ? cq[1] : (q == 2 ? cq[2] : (q == 3 ? cq[3] : cq[4])));
+    v = v <= 0.0f ? v - 0.1f : v + 0.1f;
+    v = clampf_nan(v, -1.0f, 1.0f);
+    if (live & (gj < kOmniNC)) io.cost[env * io.cost_stride + kOmniNC * gi + gj] = v;
+    const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
+    const float w2 = aw * aw, o2 = x[6] * x[6];
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f, s4 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      s0 = s0 + rlf(dg, 8 * i);
+      s1 = s1 + rlf(far, 8 * i);
+      s2 = s2 + rlf(a2, i);
+      s3 = s3 + rlf(w2, i);
+      s4 = s4 + rlf(o2, i);
+    }
+    if (live & (lane == 0)) {  // get_reward (lidar_omni_target.py:295-336)
+      const float nn = (float)NA;
+      float r = 0.0f - (s0 / nn) * 0.01f;
+      r = r - (s1 / nn) * 0.001f;
+      r = r - (s2 / nn) * 0.0001f;
+      r = r - (s3 / nn) * cfg.rot_pen;
+      r = r - ((s4 / nn) * cfg.rot_pen) * 0.5f;
+      io.reward[env * io.reward_stride] = r;
+    }
+  } else {
     float c0 = cfg.c_agent_cost - md;
     float c1 = cfg.c_obs_cost - mo;
     c0 = c0 <= 0.0f ? c0 - 0.5f : c0 + 0.5f;
@@ -799,6 +874,18 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     ro[e] = rv;
     sno[e] = sv;
   };
+  const bool vec2 = ((io.edges_stride & 1) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 7) == 0);
+  auto put_wide = [&](int e, const float (&f)[kOmniED], int rv, int sv) {
+    if (vec2) {
+#pragma unroll
+      for (int q = 0; q < kOmniED / 2; ++q) reinterpret_cast<float2*>(eo + kOmniED * e)[q] = make_float2(f[2 * q], f[2 * q + 1]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < kOmniED; ++c) eo[kOmniED * e + c] = f[c];
+    }
+    ro[e] = rv;
+    sno[e] = sv;
+  };
   float si[SD];
 #pragma unroll
   for (int c = 0; c < SD; ++c) si[c] = nxt[gi * SD + c];
@@ -818,7 +905,20 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
       const float dx = si[0] - sj[0], dy = si[1] - sj[1];
       const float d2 = dx * dx + dy * dy;
       const bool m = gi == gj ? ((d2 == 0.0f) & (cfg.c_self_dist < cfg.comm_radius)) : (d2 < cfg.t2_comm);
-      put(lane, dx, dy, f2, f3, m ? gi : pad, m ? gj : pad);
+      if constexpr (OMNI) {  // [s_i - s_j | critical i -> i+1 | ||p_j^i|| | i_x_j] (lidar_omni_target.py:352-422)
+        float f[kOmniED];
+#pragma unroll
+        for (int c = 0; c < SD; ++c) f[c] = si[c] - sj[c];
+        f[7] = gj == gi + 1 ? 1.0f : 0.0f;
+        const float gx = -(si[0] - sj[0]), gy = -(si[1] - sj[1]);
+        const float lx = si[2] * gx + si[3] * gy;
+        const float ly = (-si[3]) * gx + si[2] * gy;
+        f[8] = norm2(lx, ly);
+        f[9] = lx;
+        put_wide(lane, f, m ? gi : pad, m ? gj : pad);
+      } else {
+        put(lane, dx, dy, f2, f3, m ? gi : pad, m ? gj : pad);
+      }
     }
   }
 
@@ -882,6 +982,11 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
         f3 = si[3] - sg[3];
       }
       put(NA * NA + lane, si[0] - sg[0], si[1] - sg[1], f2, f3, gi, NA + gj);
+    } else if (OMNI & (lane < NA)) {  // agent j -> own goal j, zero-padded to 10 (lidar_omni_target.py:424-443)
+      float f[kOmniED];
+#pragma unroll
+      for (int c = 0; c < kOmniED; ++c) f[c] = c < SD ? sj[c < SD ? c : 0] - sg[c < SD ? c : 0] : 0.0f;
+      put_wide(NA * NA + lane, f, lane, NA + lane);
     } else if (lane < NA) {  // agent j -> own goal j
       float f2, f3;
       if (ENGINE == DGPPO_ENGINE_BICYCLE) {
@@ -988,8 +1093,8 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     for (int c = 2; c < ND; ++c) no[(16 + lane) * ND + c] = c == SD ? 1.0f : 0.0f;
 #pragma unroll
     for (int c = 2; c < SD; ++c) so[(16 + lane) * SD + c] = 0.0f;
-    eo[4 * (NA * NA + n_ag + lane) + 2] = 0.0f;
-    eo[4 * (NA * NA + n_ag + lane) + 3] = 0.0f;
+#pragma unroll
+    for (int c = 2; c < ED; ++c) eo[ED * (NA * NA + n_ag + lane) + c] = 0.0f;
   }
   __syncthreads();  // every alpha row is final
 
@@ -1068,10 +1173,11 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     const float2 hl = reinterpret_cast<const float2*>(hits)[lane];
     const float f0 = si[0] - hl.x;
     const float f1 = si[1] - hl.y;
-    const bool m = f0 * f0 + f1 * f1 < cfg.t2_lidar;  // norm < comm_radius - 0.1, on |d|^2
+    // Lidar: norm < comm_radius - 0.1; omni: norm < comm_radius (lidar_omni_target.py:446-489); on |d|^2
+    const bool m = f0 * f0 + f1 * f1 < (OMNI ? cfg.t2_comm : cfg.t2_lidar);
     const int e = NA * NA + n_ag + lane;
-    eo[4 * e + 0] = f0;
-    eo[4 * e + 1] = f1;
+    eo[ED * e + 0] = f0;
+    eo[ED * e + 1] = f1;
     ro[e] = m ? gi : pad;
     sno[e] = m ? 2 * NA + lane : pad;
     no[(16 + lane) * ND + 0] = hl.x;
@@ -1089,7 +1195,6 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
 // 10-wide edge features [s_i - s_j (7) | critical i -> i+1 | ||p_j^i|| | i_x_j] with
 // p_j^i = R_i^T (p_j - p_i).  One workgroup per env (any n, O, R, k); the LiDAR is the Lidar
 // engines' lidar_scan.  Same graph layout as LidarTarget (own-goal edges), edge rows 10 wide.
-constexpr int kOmniSD = 7, kOmniED = 10, kOmniNC = 5;
 
 // nodes (N, 10), states (N, 7), edges (E, 10), receivers / senders (E) of the graph on `nxt`
 __device__ void write_graph_omni(const dgppo_env_cfg& cfg, int n, int k, bool lidar, const float* nxt,
@@ -1711,6 +1816,14 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
     return DGPPO_EINVAL;
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  const bool wave_shape = lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK &&
+                          cfg->n_obs == 3 && wave_step_enabled();
+  if (cfg->engine == DGPPO_ENGINE_OMNI && wave_shape) {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<kOmniSD, 3>::total;
+    hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD, 3>),
+                       dim3((unsigned)((io->n_env + 3) / 4)), dim3(256), sh, (hipStream_t)stream, *cfg, *io);
+    return (int)hipGetLastError();
+  }
   if (cfg->engine == DGPPO_ENGINE_OMNI) {
     const size_t sh = omni_step_lds_bytes(*cfg);
     if (sh > 64 * 1024) return DGPPO_EINVAL;
@@ -1718,8 +1831,7 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
                        *io);
     return (int)hipGetLastError();
   }
-  if (lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
-      wave_step_enabled()) {
+  if (wave_shape) {
     const dim3 grid((unsigned)((io->n_env + 3) / 4)), block(256);
     const hipStream_t s = (hipStream_t)stream;
     const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;

@@ -10,6 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dgppo_fov_amd import _lib  # noqa: E402
 from dgppo_fov_amd.env import make_env  # noqa: E402
 
 n, O, B = 8, 3, 4096
@@ -32,21 +33,29 @@ def loop(m=64):
         cur = env.step_into(cur if i == 0 else outs[(i - 1) & 1], a, outs[i & 1], rew, cost)
 
 
-loop()
-torch.cuda.synchronize()
-cg = torch.cuda.CUDAGraph()
-with torch.cuda.graph(cg):
+def measure():
     loop()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-ts = []
-for _ in range(7):
-    e0.record()
-    cg.replay()
-    e1.record()
-    e1.synchronize()
-    ts.append(e0.elapsed_time(e1) / 64 * 1e3)
-us = sorted(ts)[len(ts) // 2]
-gbs = BYTES * B / us / 1e3
-print(json.dumps({"env": "LidarOmniTarget", "n": n, "n_obs": O, "n_env": B, "kernel": "omni_step_kernel<256>",
-                  "us_per_launch": round(us, 2), "env_steps_per_s": round(B / us * 1e6, 1),
-                  "bytes_per_env_step": BYTES, "achieved_GBs": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000, 4)}))
+    torch.cuda.synchronize()
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(cg):
+        loop()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(7):
+        e0.record()
+        cg.replay()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) / 64 * 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+lib = _lib.load()
+for mode, name in ((0, "wv::lidar_step_wave_kernel<OMNI,TARGET,7,3>"), (1, "omni_step_kernel<256>")):
+    lib.dgppo_env_set_step_kernel(mode)
+    us = measure()
+    gbs = BYTES * B / us / 1e3
+    print(json.dumps({"env": "LidarOmniTarget", "n": n, "n_obs": O, "n_env": B, "kernel": name,
+                      "us_per_launch": round(us, 2), "env_steps_per_s": round(B / us * 1e6, 1),
+                      "bytes_per_env_step": BYTES, "achieved_GBs": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000, 4)}))
+lib.dgppo_env_set_step_kernel(0)

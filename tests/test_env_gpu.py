@@ -245,16 +245,27 @@ def _adversarial_lidar_inputs(env, spec, B, seed, cuda):
             r = rng.integers(0, spec.n_rays)
             states[b, 0, :2] = np.clip(ob[b, 1, 8:10] - rays[r] * np.float32(0.5), 0, 1.5)
             states[b, 0, 2:4] = 0.0
-    a = rng.uniform(-1, 1, (B, n, 2)).astype(np.float32)
+    a = rng.uniform(-1, 1, (B, n, spec.ad)).astype(np.float32)
     a[kind == 1] = 0.0
     a[kind == 5, 0] = 0.0
     a[6, 0, 0] = np.nan
+    if spec.ad == 3:  # LidarOmniTarget: coincident agents (FoV norm 0), non-unit headings, rates at the
+        # limits, huge / non-finite alpha
+        for b in np.nonzero(kind == 6)[0]:
+            states[b, 1, :2] = states[b, 0, :2]
+            states[b, :n, 2:4] = [0.3, 0.4]
+        for b in np.nonzero(kind == 7)[0]:
+            states[b, :n, 6] = rng.choice([-99.0, 0.0, 99.0], size=n)
+            states[b, :n, 4:6] = rng.choice([-1.9, 2.5], size=(n, 2))
+        a[7, 1, 2] = 1e30
+        a[15, 2, 2] = -np.inf
+        a[23, 3, 2] = np.nan
     gin = env._assemble(g.nodes, g.edges, torch.from_numpy(states).to(cuda), g.receivers, g.senders,
                         torch.from_numpy(ob).to(cuda))
     return gin, states, ob, a
 
 
-@pytest.mark.parametrize("eid", ["LidarSpread", "LidarTarget", "LidarBicycleTarget"])
+@pytest.mark.parametrize("eid", ["LidarSpread", "LidarTarget", "LidarBicycleTarget", "LidarOmniTarget"])
 def test_wave_step_kernel_adversarial(cuda, eid):
     """The wave-per-env step kernel (exact ray culling + compacted ray cast) against the oracle and
     against the workgroup-per-env kernel, bit for bit, on adversarial inputs."""
