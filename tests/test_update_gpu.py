@@ -143,7 +143,7 @@ def _net_trees(algo, grad=False):
 
 
 @pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("MPESpread", 3, 3), ("LidarBicycleTarget", 2, 1),
-                                     ("LidarOmniTarget", 3, 2)])
+                                     ("LidarOmniTarget", 3, 2), ("LidarSpread", 32, 8)])
 def test_dgppo_update_matches_oracle(cuda, eid, n, obs):
     B, T, L = 4, 32, 16
     env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
