@@ -1,0 +1,95 @@
+"""Per-GPU throughput of every BASELINE.json config on one MI355X (the bench line covers configs[2]).
+
+For each config: the env-step kernel (average launch time from HIP events around 64 back-to-back
+launches captured in a hipGraph, ping-ponging two graph buffers) and, unless --no-ppo, one DGPPO
+collect + update at batch 16384 / rnn_step 16 (second call timed; the first captures graphs and grows
+workspaces).  Multi-GPU configs are measured at their per-GPU share (env-sharded, weak scaling).
+Random-init networks, synthetic resets and uniform random actions."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dgppo_fov_amd.algo import make_algo  # noqa: E402
+from dgppo_fov_amd.env import make_env  # noqa: E402
+
+# (label, env, n, obs, envs per GPU)
+CONFIGS = [
+    ("MPESpread n3 o3 x1024", "MPESpread", 3, 3, 1024),
+    ("LidarSpread n8 o3 x4096", "LidarSpread", 8, 3, 4096),
+    ("LidarBicycleTarget n8 o3 x4096/GPU (8-GPU config)", "LidarBicycleTarget", 8, 3, 4096),
+    ("LidarSpread n32 o8 x1024/GPU (8192 envs over 8 GPUs)", "LidarSpread", 32, 8, 1024),
+    ("LidarOmniTarget n8 o3 x4096", "LidarOmniTarget", 8, 3, 4096),
+]
+
+
+def step_us(env, B, dev, m=64):
+    g = env.reset(key=1, n_env=B)
+    a = torch.rand(B, env.num_agents, env.action_dim, device=dev) * 2 - 1
+    obst = getattr(g.env_states, "obstacle", None)  # Lidar: Rectangle records; MPE: obstacles live in the states
+    ob = obst.packed if obst is not None and hasattr(obst, "packed") else None
+    outs = [env.empty_graph((B,), dev) for _ in range(2)]
+    outs = [env._assemble(o.nodes, o.edges, o.states, o.receivers, o.senders, ob) for o in outs]
+    rew = torch.empty(B, device=dev)
+    cost = torch.empty(B, env.num_agents, env.n_cost, device=dev)
+
+    def loop():
+        for i in range(m):
+            env.step_into(g if i == 0 else outs[(i - 1) & 1], a, outs[i & 1], rew, cost)
+
+    loop()
+    torch.cuda.synchronize()
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(cg):
+        loop()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(5):
+        e0.record()
+        cg.replay()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) / m * 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+def ppo_ms(env, B, dev):
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=env.num_agents, batch_size=16384, rnn_step=16, seed=0,
+                     device=dev, train_steps=1000)
+    r = algo.collect(algo.params, 0, n_env=B)
+    algo.update(r, 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = algo.collect(algo.params, 1, n_env=B)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    algo.update(r, 1)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    return (t1 - t0) * 1e3, (t2 - t1) * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--no-ppo", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for label, eid, n, obs, B in CONFIGS:
+        env = make_env(eid, n, num_obs=obs, max_step=128, device=dev)
+        us = step_us(env, B, dev)
+        row = {"config": label, "env": eid, "n": n, "n_obs": obs, "envs_per_gpu": B, "env_step_us": round(us, 2),
+               "env_steps_per_s": round(B / us * 1e6, 1)}
+        if not args.no_ppo:
+            c, u = ppo_ms(env, B, dev)
+            row.update({"collect_ms": round(c, 2), "update_ms": round(u, 2),
+                        "minibatches": B * 128 // 16384})
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
