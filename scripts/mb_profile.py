@@ -41,15 +41,17 @@ from dgppo_fov_amd.env import make_env  # noqa: E402
 from dgppo_fov_amd.nn import kernels as K  # noqa: E402
 
 dev = torch.device("cuda:0")
-n, T, B = 8, 128, 1024
-env = make_env("LidarSpread", n, num_obs=3, max_step=T, device=dev)
+# MB_ENV / MB_N / MB_OBS pick another config (e.g. the dense LidarSpread n=32, 8 obstacles)
+EID, n, OBS = os.environ.get("MB_ENV", "LidarSpread"), int(os.environ.get("MB_N", 8)), int(os.environ.get("MB_OBS", 3))
+T, B = 128, 1024
+env = make_env(EID, n, num_obs=OBS, max_step=T, device=dev)
 algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
                  action_dim=env.action_dim, n_agents=n, batch_size=16384, device=dev, train_steps=100)
 r = algo.collect(algo.params, 0, n_env=B)
 envs = torch.arange(128, device=dev)
 g = algo._graphs(r.graph, envs)
 S, L = 128 * T // 16, 16
-acts = r.actions.index_select(0, envs).reshape(-1, 2).contiguous()
+acts = r.actions.index_select(0, envs).reshape(-1, env.action_dim).contiguous()
 hd = r.rnn_states.index_select(0, envs).reshape(-1, 64).contiguous()
 REPS = 5
 
