@@ -44,7 +44,8 @@ __device__ __forceinline__ float min_nan(float a, float b) {
   // jnp.min / jnp.minimum semantics: NaN wins
   return (a != a || a < b) ? a : b;
 }
-__device__ __forceinline__ float norm2(float dx, float dy) { return sqrtf(dx * dx + dy * dy); }
+__device__ __forceinline__ float sq2(float dx, float dy) { return dx * dx + dy * dy; }
+__device__ __forceinline__ float norm2(float dx, float dy) { return sqrtf(sq2(dx, dy)); }
 
 // ---- LDS carve (floats) -------------------------------------------------------------------------
 struct Carve {
@@ -773,14 +774,18 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
   if (gi == gj) daa = daa + 1e6f;
   const float dga = GOAL == DGPPO_GOAL_SPREAD ? norm2(gix - x[0], giy - x[1]) : norm2(gix - cix, giy - ciy);
   float dh;
-  if constexpr (OMNI) {  // every agent's current hits and the origin row (see oracle get_cost_omni)
+  if constexpr (OMNI) {
+    // every agent's current hits and the origin row (see oracle get_cost_omni): minimum of the squared
+    // norms, one sqrtf after it (sqrtf is correctly rounded and monotone, so sqrtf(min x) == min sqrtf(x);
+    // NaN propagates through min_nan either way)
     const float* ch = lds + C::hits;
-    dh = norm2(0.0f - cix, 0.0f - ciy);
+    float d2 = sq2(0.0f - cix, 0.0f - ciy);
 #pragma unroll
     for (int t = 0; t < NA; ++t) {
       const float2 hv = reinterpret_cast<const float2*>(ch)[gj + 8 * t];
-      dh = min_nan(dh, norm2(hv.x - cix, hv.y - ciy));
+      d2 = min_nan(d2, sq2(hv.x - cix, hv.y - ciy));
     }
+    dh = sqrtf(d2);
   } else {
     dh = norm2(hcx - cix, hcy - ciy);
   }
