@@ -965,7 +965,7 @@ constexpr int kRows = 16, kSR = 2, kQP = 100;
 // xs row pitch: x (DM floats; the pre-transform writes 32) then the edge features at column EC
 template <int DM>
 struct Pitch {
-  static constexpr int EC = DM <= 8 ? 8 : 32, XSP = EC + (DM <= 8 ? 4 : 8), AW = 64 * (XSP + 4);
+  static constexpr int EC = DM <= 8 ? 8 : (DM <= 16 ? 16 : 32), XSP = EC + (DM <= 16 ? 4 : 8), AW = 64 * (XSP + 4);
 };
 template <int DM>
 constexpr size_t lds_floats() {
@@ -979,7 +979,7 @@ __global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
   using lanes::wave_sync;
   constexpr int kRows = fwd2::kRows, kSR = fwd2::kSR, kQP = fwd2::kQP;
   constexpr int kXSP = fwd2::Pitch<DM>::XSP, EC = fwd2::Pitch<DM>::EC;
-  static_assert(DM == 8 || DM == 32, "fwd2 instantiations");
+  static_assert(DM == 8 || DM == 16 || DM == 32, "fwd2 instantiations");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* qts = lds;                 // [16][100]: qt_h (32-float stride per head) | beta_h at 96 + h
   float* preW = qts + kRows * kQP;  // [8][32]
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
   const int nrows = p.G * n;
   const int row0 = blockIdx.x * kRows;
   const bool agent = p.xa != nullptr;
-  const bool pre = DM > 8 && agent && p.pre_W != nullptr;  // the launcher sends pre mode to DM = 32
+  const bool pre = DM == 32 && agent && p.pre_W != nullptr;  // the launcher sends pre mode to DM = 32
   // ---- gathers of both sub-rounds
   float xv[kSR][DM];
   f32x4 efv[kSR];
@@ -1178,8 +1178,11 @@ bool fwd2_ok(const dgppo_gnn_attn_args* p) {
 void fwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const int64_t rows = (int64_t)p->G * p->n_agents;
   const unsigned grid = (unsigned)((rows + fwd2::kRows - 1) / fwd2::kRows);
-  if (p->D <= 8 && !(p->xa && p->pre_W))
+  const bool no_pre = !(p->xa && p->pre_W);
+  if (p->D <= 8 && no_pre)
     hipLaunchKernelGGL(attn_fwd2_kernel<8>, dim3(grid), dim3(256), fwd2::lds_floats<8>() * sizeof(float), s, *p);
+  else if (p->D <= 16 && no_pre)  // e.g. LidarOmniTarget's 10-wide first layer
+    hipLaunchKernelGGL(attn_fwd2_kernel<16>, dim3(grid), dim3(256), fwd2::lds_floats<16>() * sizeof(float), s, *p);
   else
     hipLaunchKernelGGL(attn_fwd2_kernel<32>, dim3(grid), dim3(256), fwd2::lds_floats<32>() * sizeof(float), s, *p);
 }
@@ -1200,8 +1203,8 @@ constexpr int kRows = 16, kSR = 2, kMaxBlocks = 1024;
 // per-head stride HS of the qt / dxbar rows, row pitches, xs pitch (x | x_raw | 1 in pre mode)
 template <int DM>
 struct Lay {
-  static constexpr int HS = DM <= 8 ? 8 : 32, QP = 3 * HS + 4, GP = 3 * HS + 16;
-  static constexpr int XSP = DM <= 8 ? 12 : 44, AW = 64 * (XSP + 4);
+  static constexpr int HS = DM <= 8 ? 8 : (DM <= 16 ? 16 : 32), QP = 3 * HS + 4, GP = 3 * HS + 16;
+  static constexpr int XSP = DM <= 8 ? 12 : (DM <= 16 ? 20 : 44), AW = 64 * (XSP + 4);
 };
 template <int DM>
 size_t lds_floats(int n, int D) {
@@ -1216,7 +1219,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
   using lanes::wave_sync;
   using LY = bwd2::Lay<DM>;
   constexpr int kRows = bwd2::kRows, kSR = bwd2::kSR, HS = LY::HS, kQP = LY::QP, kGP = LY::GP, kXSP = LY::XSP;
-  static_assert(DM == 8 || DM == 32, "bwd2 instantiations");
+  static_assert(DM == 8 || DM == 16 || DM == 32, "bwd2 instantiations");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* qts = lds;                 // [16][QP]: qt_h (HS-float stride per head)
   float* gs = qts + kRows * kQP;    // [16][GP]: dxbar_h (HS stride) | debar (3HS..+12) | dsig (3HS+12..+3)
@@ -1230,7 +1233,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
   const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = kH;
   const int gpb = kRows / n;
   const bool agent = p.xa != nullptr;
-  const bool pre = DM > 8 && agent && p.pre_W != nullptr;
+  const bool pre = DM == 32 && agent && p.pre_W != nullptr;  // the launcher sends pre mode to DM = 32
   const bool want_dxa = agent && p.dxa != nullptr;
   const bool want_pre = pre && p.dpre_part != nullptr;
   if (pre) {
@@ -1503,18 +1506,23 @@ int64_t bwd2_grid(const dgppo_gnn_attn_args* p, int64_t* nblk) {
 void bwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   int64_t nblk;
   const unsigned grid = (unsigned)bwd2_grid(p, &nblk);
-  const bool dm8 = p->D <= 8 && !(p->xa && p->pre_W);
-  const size_t bytes = (dm8 ? bwd2::lds_floats<8>(p->n_agents, p->D) : bwd2::lds_floats<32>(p->n_agents, p->D)) *
+  const bool no_pre = !(p->xa && p->pre_W);
+  const int v = p->D <= 8 && no_pre ? 0 : (p->D <= 16 && no_pre ? 1 : 2);  // DM 8 / 16 / 32
+  const size_t bytes = (v == 0   ? bwd2::lds_floats<8>(p->n_agents, p->D)
+                        : v == 1 ? bwd2::lds_floats<16>(p->n_agents, p->D)
+                                 : bwd2::lds_floats<32>(p->n_agents, p->D)) *
                        sizeof(float);
+  const void* fn = v == 0 ? (const void*)attn_bwd2_kernel<8>
+                          : (v == 1 ? (const void*)attn_bwd2_kernel<16> : (const void*)attn_bwd2_kernel<32>);
   if (bytes > 64 * 1024) {
-    static bool raised[2] = {false, false};
-    if (!raised[dm8]) {
-      (void)hipFuncSetAttribute(dm8 ? (const void*)attn_bwd2_kernel<8> : (const void*)attn_bwd2_kernel<32>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised[dm8] = true;
+    static bool raised[3] = {false, false, false};
+    if (!raised[v]) {
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised[v] = true;
     }
   }
-  if (dm8) hipLaunchKernelGGL(attn_bwd2_kernel<8>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+  if (v == 0) hipLaunchKernelGGL(attn_bwd2_kernel<8>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+  else if (v == 1) hipLaunchKernelGGL(attn_bwd2_kernel<16>, dim3(grid), dim3(256), bytes, s, *p, nblk);
   else hipLaunchKernelGGL(attn_bwd2_kernel<32>, dim3(grid), dim3(256), bytes, s, *p, nblk);
 }
 
@@ -1701,53 +1709,71 @@ extern "C" int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* p, void* stream) {
 // Edge columns past the first 4 (LidarOmniTarget's 10-wide edges).  The attention kernels keep their 4-wide edge
 // registers; the EX extra columns enter the value messages through xcat_x = sum_c attn * efx (edge_wsum, one
 // thread per output column) and the softmax backward through da_add (edge_da, one thread per (row, head, cand)).
-// Both are gather-bound over (G*n) x C x EX floats, a few % of the attention kernels' traffic.
+// Both are gather-bound over (G*n) x C x EX floats, a few % of the attention kernels' traffic.  EX <= 16.
 namespace dgppo {
 namespace {
 
+// one thread per (row, head): the candidate loop reads each edge's EX columns once (float2 pairs when EX is
+// even) and keeps the EX sums in registers
+template <int EXM>
 __global__ __launch_bounds__(256) void edge_wsum_kernel(int64_t R, int32_t n, int32_t C, int32_t H, int32_t EX,
                                                         int32_t E, const float* __restrict__ attn,
                                                         const int32_t* __restrict__ cand,
                                                         const int32_t* __restrict__ sidx,
                                                         const float* __restrict__ efx, float* __restrict__ out) {
-  const int W = H * EX;
-  const int64_t total = R * W;
+  const int64_t total = R * H;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
-    const int64_t r = t / W;
-    const int k = (int)(t - r * W), h = k / EX, j = k - h * EX;
+    const int64_t r = t / H;
+    const int h = (int)(t - r * H);
     const int64_t g = r / n;
     const int i = (int)(r - g * n);
-    const float* ar = attn + (r * H + h) * C;
-    const float* eg = efx + g * E * EX + j;
-    float acc = 0.0f;
+    const float* ar = attn + t * C;
+    const float* eg = efx + g * E * EX;
+    float acc[EXM];
+#pragma unroll
+    for (int j = 0; j < EXM; ++j) acc[j] = 0.0f;
     for (int c = 0; c < C; ++c) {
-      const int e = cand[i * C + c];
-      if (sidx[r * C + c] >= 0) acc += ar[c] * eg[(int64_t)e * EX];
+      if (sidx[r * C + c] < 0) continue;
+      const float a = ar[c];
+      const float* er = eg + (int64_t)cand[i * C + c] * EX;
+#pragma unroll
+      for (int j = 0; j < EXM; ++j)
+        if (j < EX) acc[j] += a * er[j];
     }
-    out[t] = acc;
+    float* o = out + r * H * EX + h * EX;
+#pragma unroll
+    for (int j = 0; j < EXM; ++j)
+      if (j < EX) o[j] = acc[j];
   }
 }
 
+// one thread per (row, candidate): the edge's EX columns read once, one dot product per head; consecutive
+// candidates of a row write consecutive floats of each head's da row
+template <int EXM>
 __global__ __launch_bounds__(256) void edge_da_kernel(int64_t R, int32_t n, int32_t C, int32_t H, int32_t EX,
                                                       int32_t E, const float* __restrict__ dxx,
                                                       const int32_t* __restrict__ cand,
                                                       const int32_t* __restrict__ sidx,
                                                       const float* __restrict__ efx, float* __restrict__ da) {
-  const int64_t total = R * H * C;
+  const int64_t total = R * C;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
-    const int c = (int)(t % C);
-    const int64_t rh = t / C;
-    const int h = (int)(rh % H);
-    const int64_t r = rh / H;
+    const int64_t r = t / C;
+    const int c = (int)(t - r * C);
     const int64_t g = r / n;
     const int i = (int)(r - g * n);
-    float acc = 0.0f;
-    if (sidx[r * C + c] >= 0) {
-      const float* er = efx + (g * E + cand[i * C + c]) * EX;
-      const float* gr = dxx + r * H * EX + h * EX;
-      for (int j = 0; j < EX; ++j) acc += gr[j] * er[j];
+    const bool ok = sidx[t] >= 0;
+    float ev[EXM];
+    const float* er = efx + (g * E + (ok ? cand[i * C + c] : 0)) * EX;
+#pragma unroll
+    for (int j = 0; j < EXM; ++j) ev[j] = (ok && j < EX) ? er[j] : 0.0f;
+    for (int h = 0; h < H; ++h) {
+      const float* gr = dxx + (r * H + h) * EX;
+      float acc = 0.0f;
+#pragma unroll
+      for (int j = 0; j < EXM; ++j)
+        if (j < EX) acc += gr[j] * ev[j];
+      da[(r * H + h) * C + c] = ok ? acc : 0.0f;
     }
-    da[t] = acc;
   }
 }
 
@@ -1766,8 +1792,14 @@ extern "C" int dgppo_gnn_edge_wsum(int32_t G, int32_t n_agents, int32_t C, int32
     return DGPPO_EINVAL;
   const int64_t R = (int64_t)G * n_agents;
   if (R == 0) return 0;
-  hipLaunchKernelGGL(dgppo::edge_wsum_kernel, dim3(dgppo::grid_for(R * H * EX)), dim3(256), 0, (hipStream_t)stream,
-                     R, n_agents, C, H, EX, E, attn, cand, sidx, efx, out);
+  if (EX > 16) return DGPPO_EINVAL;
+  const dim3 grid(dgppo::grid_for(R * H));
+  if (EX <= 8)
+    hipLaunchKernelGGL(dgppo::edge_wsum_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, R, n_agents, C, H, EX, E,
+                       attn, cand, sidx, efx, out);
+  else
+    hipLaunchKernelGGL(dgppo::edge_wsum_kernel<16>, grid, dim3(256), 0, (hipStream_t)stream, R, n_agents, C, H, EX,
+                       E, attn, cand, sidx, efx, out);
   return (int)hipGetLastError();
 }
 
@@ -1778,7 +1810,13 @@ extern "C" int dgppo_gnn_edge_da(int32_t G, int32_t n_agents, int32_t C, int32_t
     return DGPPO_EINVAL;
   const int64_t R = (int64_t)G * n_agents;
   if (R == 0) return 0;
-  hipLaunchKernelGGL(dgppo::edge_da_kernel, dim3(dgppo::grid_for(R * H * C)), dim3(256), 0, (hipStream_t)stream, R,
-                     n_agents, C, H, EX, E, dxx, cand, sidx, efx, da_add);
+  if (EX > 16) return DGPPO_EINVAL;
+  const dim3 grid(dgppo::grid_for(R * C));
+  if (EX <= 8)
+    hipLaunchKernelGGL(dgppo::edge_da_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, R, n_agents, C, H, EX, E,
+                       dxx, cand, sidx, efx, da_add);
+  else
+    hipLaunchKernelGGL(dgppo::edge_da_kernel<16>, grid, dim3(256), 0, (hipStream_t)stream, R, n_agents, C, H, EX, E,
+                       dxx, cand, sidx, efx, da_add);
   return (int)hipGetLastError();
 }

@@ -236,7 +236,7 @@ int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* args, void* stream);
  *   edge_wsum: out[r, h*EX + j] = sum_c attn[r, h, c] * efx[g, cand[i][c], j] over sidx[r][c] >= 0
  *              (the attention-weighted edge term of the value messages, dgppo/nn/gnn.py:99-104)
  *   edge_da:   da_add[r, h, c] = sum_j dxx[r, h*EX + j] * efx[g, cand[i][c], j] if sidx[r][c] >= 0 else 0
- * with r = g*n + i. */
+ * with r = g*n + i; EX <= 16. */
 int dgppo_gnn_edge_wsum(int32_t G, int32_t n_agents, int32_t C, int32_t H, int32_t EX, int32_t E, const float* attn,
                         const int32_t* cand, const int32_t* sidx, const float* efx, float* out, void* stream);
 int dgppo_gnn_edge_da(int32_t G, int32_t n_agents, int32_t C, int32_t H, int32_t EX, int32_t E, const float* dxx,
