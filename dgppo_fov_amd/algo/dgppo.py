@@ -406,7 +406,14 @@ class DGPPO:
                         "layout": [(n, s) for n, s, _ in net.ps.entries]}, os.path.join(d, f"{name}.pt"))
 
     def load(self, load_dir: str, step: int):
+        """models/<step>/{actor,Vl,Vh}.pt of this package, or reference-layout {actor,Vl,Vh}.npz flax
+        trees (utils/flax_ckpt.py; params only, Adam state kept)."""
         d = os.path.join(load_dir, str(step))
+        if not os.path.exists(os.path.join(d, "actor.pt")) and os.path.exists(os.path.join(d, "actor.npz")):
+            from ..utils.flax_ckpt import load_reference_npz
+
+            load_reference_npz(self, d)
+            return
         for name, net, opt in (("actor", self.actor, self.opt["policy"]), ("Vl", self.Vl, self.opt["Vl"]),
                                ("Vh", self.Vh, self.opt["Vh"])):
             ck = torch.load(os.path.join(d, f"{name}.pt"), weights_only=True)
