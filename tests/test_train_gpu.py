@@ -1,0 +1,47 @@
+"""End to end through the reference's entry points: train.py (make_env / make_algo / Trainer: collect,
+update, eval, checkpoint) for a few iterations, then test.py on the saved checkpoint (deterministic
+rollouts, returns / max cost / safe rate), in this process, for a Lidar env and LidarOmniTarget."""
+import glob
+import importlib.util
+import json
+import math
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+def _entry(name):  # the repo-root scripts by path (`test` would also name the stdlib package)
+    spec = importlib.util.spec_from_file_location(f"dgppo_entry_{name}", os.path.join(ROOT, f"{name}.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("LidarOmniTarget", 3, 2)])
+def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, n, obs):
+    test_py, train_py = _entry("test"), _entry("train")
+
+    argv = ["train.py", "--env", eid, "-n", str(n), "--algo", "dgppo", "--obs", str(obs), "--steps", "2",
+            "--n-env-train", "8", "--batch-size", "256", "--n-env-test", "4", "--eval-interval", "1",
+            "--save-interval", "2", "--log-dir", str(tmp_path)]
+    monkeypatch.setattr(sys, "argv", argv)
+    train_py.main()
+    runs = glob.glob(os.path.join(str(tmp_path), eid, "dgppo", "seed0_*"))
+    assert len(runs) == 1
+    run = runs[0]
+    assert os.path.exists(os.path.join(run, "config.yaml"))
+    assert sorted(os.listdir(os.path.join(run, "models"))) == ["0", "2"]
+    rows = [json.loads(x) for x in open(os.path.join(run, "log.jsonl"))]
+    assert rows and all(math.isfinite(v) for r in rows for v in r.values() if isinstance(v, float))
+    assert any("eval/safe_data" in r or "eval/unsafe_frac" in r for r in rows)
+    capsys.readouterr()
+    monkeypatch.setattr(sys, "argv", ["test.py", "--path", run, "--epi", "1", "--n-env", "4", "--max-step", "16"])
+    test_py.main()
+    out = capsys.readouterr().out
+    assert "safe_rate:" in out and "reward:" in out
