@@ -66,6 +66,26 @@ def read_pmc_traffic():
     return None
 
 
+def read_mfma_pmc():
+    """Executed-MFMA utilisation from the committed PMC profile (scripts/mfma_pmc.sh): SQ_INSTS_VALU_MFMA_MOPS_F32
+    x 512 per kernel family over one collect + update, against the fp32 MFMA peak."""
+    fn = os.path.join(ROOT, "profiles", "r01_mfma_util.json")
+    if not os.path.exists(fn):
+        return None
+    try:
+        d = json.load(open(fn))
+        fam = d["families"]
+        gemm_t = sum(fam[k]["time_ms"] for k in ("gemm_rows", "gemm_wgrad") if k in fam)
+        gemm_f = sum(fam[k]["mfma_tflop"] for k in ("gemm_rows", "gemm_wgrad") if k in fam)
+        return {"source": "profiles/r01_mfma_util.json (rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32)",
+                "gnn_gemm_executed_tflops": round(gemm_f / gemm_t * 1e3, 2),
+                "gnn_gemm_frac_of_peak": round(gemm_f / gemm_t * 1e3 / FP32_MFMA_PEAK_TFLOPS, 4),
+                "window_executed_tflops": d["total_mfma_tflops_over_window"],
+                "window_frac_of_peak": round(d["total_mfma_tflops_over_window"] / FP32_MFMA_PEAK_TFLOPS, 4)}
+    except Exception:
+        return None
+
+
 PPO_BATCH, RNN_STEP = 16384, 16  # BASELINE.md synthetic-input plan (batch_size, rnn_step)
 # SURVEY.md §8(d) official algorithmic flops (minimal node-level projection formulation), LidarSpread n8
 # B4096: one PPO update (det rollout excluded: prepass + SGD, fwd+bwd = 3x fwd) and the two rollouts'
@@ -123,7 +143,8 @@ def ppo_bench(env, dev, world, rank, iters):
             "iters": iters, "batch_size": PPO_BATCH * world, "rnn_step": RNN_STEP, "epoch_ppo": 1,
             "minibatches": B_PER_GPU * T * world // (PPO_BATCH * world),
             "gemm_tflop_per_update": round(gemm_flops / 1e12, 3),
-            "gemm_tflops_over_update": round(gemm_flops / t_upd / 1e12, 3), "fp32_mfma_peak_tflops": 157.3}
+            "gemm_tflops_over_update": round(gemm_flops / t_upd / 1e12, 3), "fp32_mfma_peak_tflops": 157.3,
+            "mfma_pmc": read_mfma_pmc()}
 
 
 def main():

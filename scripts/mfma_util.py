@@ -1,0 +1,58 @@
+"""Join scripts/mfma_pmc.sh's passes: per kernel family, executed fp32 MFMA flops (SQ_INSTS_VALU_MFMA_MOPS_F32
+x 512), kernel time from the un-instrumented trace, achieved TFLOP/s and the fraction of the 157.3 TFLOP/s
+fp32 MFMA peak, plus MFMA busy cycles / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs).  Only the last update_smoke
+iteration (the second collect + update) is counted: kernels are grouped by dispatch order halves."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+PEAK = 157.3e12
+
+
+def family(name):
+    n = name.replace("(anonymous namespace)::", "")
+    m = re.search(r"(gemm_rows|gemm_wgrad_reduce|gemm_wgrad|attn_\w+?_kernel|gru_seq_\w+?_kernel|policy_step_kernel|"
+                  r"lidar_step_wave_kernel|layernorm64_\w+?_kernel|gae_kernel|adam_kernel)", n)
+    return m.group(1) if m else "other"
+
+
+def second_half(rows, key):
+    rows = sorted(rows, key=key)
+    return rows[len(rows) // 2:]
+
+
+pmc = defaultdict(lambda: defaultdict(float))
+prow = list(csv.DictReader(open(glob.glob(os.path.join(root, "pmc", "**", "*counter_collection.csv"), recursive=True)[0])))
+disp = sorted({int(r["Dispatch_Id"]) for r in prow})
+keep = set(disp[len(disp) // 2:])
+for r in prow:
+    if int(r["Dispatch_Id"]) in keep:
+        pmc[family(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+trows = list(csv.DictReader(open(glob.glob(os.path.join(root, "trace", "**", "*kernel_trace.csv"), recursive=True)[0])))
+trows = second_half(trows, lambda r: int(r["Start_Timestamp"]))
+dur = defaultdict(float)
+for r in trows:
+    dur[family(r["Kernel_Name"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+span = (max(int(r["End_Timestamp"]) for r in trows) - min(int(r["Start_Timestamp"]) for r in trows)) * 1e-9
+out = {"peak_tflops_fp32_mfma": 157.3, "window": "second collect + update of update_smoke (LidarSpread n8, 4096 envs)",
+       "window_s": round(span, 4), "families": {}}
+tot_f = 0.0
+for fam in sorted(set(pmc) | set(dur), key=lambda f: -dur.get(f, 0)):
+    f = pmc[fam].get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) * 512
+    tot_f += f
+    t = dur.get(fam, 0.0)
+    g = pmc[fam].get("GRBM_GUI_ACTIVE", 0.0)
+    busy = pmc[fam].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+    out["families"][fam] = {"time_ms": round(t * 1e3, 3), "mfma_tflop": round(f / 1e12, 4),
+                            "achieved_tflops": round(f / t / 1e12, 2) if t else None,
+                            "frac_of_peak": round(f / t / PEAK, 4) if t else None,
+                            "mfma_busy_frac": round(busy / (g / 8 * 1024), 4) if g else None}
+out["total_mfma_tflop"] = round(tot_f / 1e12, 4)
+out["total_mfma_tflops_over_window"] = round(tot_f / span / 1e12, 2)
+print(json.dumps(out, indent=1))
+json.dump(out, open(os.path.join(root, "mfma_util.json"), "w"), indent=1)
