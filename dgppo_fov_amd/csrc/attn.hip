@@ -70,6 +70,36 @@ __device__ __forceinline__ float group_max(float v, float* scratch) {
   }
 }
 
+// group_sum / group_max of all kH heads at once: for CP = 128 one LDS exchange (3 barriers) serves every
+// head instead of one per head; same pairing and order as group_sum / group_max (bit-identical)
+template <int CP, bool MAX>
+__device__ __forceinline__ void group_red3(float (&v)[kH], float* scratch) {
+  if constexpr (CP <= 64) {
+#pragma unroll
+    for (int h = 0; h < kH; ++h) v[h] = MAX ? group_max<CP>(v[h], nullptr) : group_sum<CP>(v[h], nullptr);
+  } else {
+#pragma unroll
+    for (int h = 0; h < kH; ++h)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float w = __shfl_xor(v[h], o, 64);
+        v[h] = MAX ? fmaxf(v[h], w) : v[h] + w;
+      }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int h = 0; h < kH; ++h) scratch[w * kH + h] = v[h];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      const float a = scratch[(w & ~1) * kH + h], b = scratch[(w | 1) * kH + h];
+      v[h] = MAX ? fmaxf(a, b) : a + b;
+    }
+    __syncthreads();
+  }
+}
+
 struct Cand {
   int s, e;
 };
@@ -125,7 +155,7 @@ struct Carve {
     preW = base;
     preb = preW + kD0 * DM;
     scr = preb + DM;
-    qt = scr + 8;
+    qt = scr + 16;
     xs = qt + R * kH * DM;
     a = xs + R * CR * XP;
     ef = a + R * CR * kH;
@@ -134,7 +164,7 @@ struct Carve {
     dxs = x0s + (bwd ? R * CR * (kD0 + 1) : 0);
   }
   static size_t floats_fixed(int CR, bool bwd) {
-    return (size_t)kD0 * DM + DM + 8 + R * kH * DM + (size_t)R * CR * (XP + kH + 4) +
+    return (size_t)kD0 * DM + DM + 16 + R * kH * DM + (size_t)R * CR * (XP + kH + 4) +
            (bwd ? (size_t)R * kH * (DM + 5) + (size_t)R * CR * (kD0 + 1) : 0);
   }
 };
@@ -230,8 +260,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(dgppo_gnn_attn_args p, in
         float acc = 0.0f;
         if (active && h < H)
           for (int f = c; f < F; f += CP) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
-        beta[h] = group_sum<CP>(acc, L.scr);
+        beta[h] = acc;
       }
+      group_red3<CP, false>(beta, L.scr);
       __syncthreads();
       float lg[kH], mx[kH], a[kH];
 #pragma unroll
@@ -242,13 +273,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(dgppo_gnn_attn_args p, in
         for (int d = 0; d < DM; ++d)
           if (d < D) acc += qt[d] * x[d];
         lg[h] = (ok && h < H) ? (acc + beta[h]) * p.scale : -INFINITY;
-        mx[h] = group_max<CP>(lg[h], L.scr);
+        mx[h] = lg[h];
       }
+      group_red3<CP, true>(mx, L.scr);
+      float ex[kH], sm[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) sm[h] = ex[h] = ok && h < H ? expf(lg[h] - mx[h]) : 0.0f;
+      group_red3<CP, false>(sm, L.scr);
 #pragma unroll
       for (int h = 0; h < kH; ++h) {
-        const float ex = ok && h < H ? expf(lg[h] - mx[h]) : 0.0f;
-        const float sm = group_sum<CP>(ex, L.scr);
-        a[h] = ok && h < H ? ex / sm : 0.0f;
+        a[h] = ok && h < H ? ex[h] / sm[h] : 0.0f;
         if (active && c < C && h < H && p.attn) p.attn[(row * H + h) * C + c] = a[h];
       }
       // LDS transpose: candidates' rows and weights, then one output column per lane
@@ -299,7 +333,7 @@ struct BwdCarve {
     preW = base;
     preb = preW + kD0 * DM;
     scr = preb + DM;
-    qt = scr + 8;
+    qt = scr + 16;
     g = qt + R * kH * DM;
     xs = g + R * kH * (DM + 5);
     a = xs + R * CR * XP;
@@ -309,7 +343,7 @@ struct BwdCarve {
     dxs = cb + R * n * DM;
   }
   static size_t floats_fixed(int CR, int n) {
-    return (size_t)kD0 * DM + DM + 8 + R * kH * DM + R * kH * (DM + 5) + (size_t)R * CR * (2 * XP + kH + kD0 + 1) +
+    return (size_t)kD0 * DM + DM + 16 + R * kH * DM + R * kH * (DM + 5) + (size_t)R * CR * (2 * XP + kH + kD0 + 1) +
            (size_t)R * n * DM;
   }
 };
@@ -380,23 +414,25 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
       }
       __syncthreads();  // (1) qt / dxcat staged
       const float* gv = L.g + slot * kH * (DM + 5);  // dxbar (H*D) | debar (H*4) | dsig (H)
-      float dl[kH], dbeta[kH];
+      float dl[kH], dbeta[kH], da[kH], dot[kH];
 #pragma unroll
       for (int h = 0; h < kH; ++h) {
-        float da = 0.0f;
+        da[h] = 0.0f;
         if (ok && h < H) {
 #pragma unroll
           for (int d = 0; d < DM; ++d)
-            if (d < D) da += gv[h * D + d] * x[d];
+            if (d < D) da[h] += gv[h * D + d] * x[d];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) da += gv[H * D + h * 4 + j] * ef[j];
-          da += gv[H * D + H * 4 + h];
-          if (p.da_add) da += p.da_add[(row * H + h) * C + c];
+          for (int j = 0; j < 4; ++j) da[h] += gv[H * D + h * 4 + j] * ef[j];
+          da[h] += gv[H * D + H * 4 + h];
+          if (p.da_add) da[h] += p.da_add[(row * H + h) * C + c];
         }
-        const float dot = group_sum<CP>(a[h] * da, L.scr);
-        dl[h] = (ok && h < H) ? a[h] * (da - dot) * p.scale : 0.0f;
-        dbeta[h] = group_sum<CP>(dl[h], L.scr);
+        dot[h] = a[h] * da[h];
       }
+      group_red3<CP, false>(dot, L.scr);
+#pragma unroll
+      for (int h = 0; h < kH; ++h) dbeta[h] = dl[h] = (ok && h < H) ? a[h] * (da[h] - dot[h]) * p.scale : 0.0f;
+      group_red3<CP, false>(dbeta, L.scr);
       if (active && c == 0)
         for (int h = 0; h < H; ++h) p.dbeta[row * H + h] = dbeta[h];
       if (active)
