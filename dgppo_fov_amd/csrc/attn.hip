@@ -1676,7 +1676,214 @@ void launch_cp(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream
   }
 }
 
+// ================================================================================================
+// Forward, graph form, for candidate rows wider than the row-block kernels' 32 (dense graphs, e.g.
+// LidarSpread n = 32: 32 agent + 32 goal + 8 hit candidates per agent).  One workgroup per graph:
+// every sender row of the graph is staged ONCE in LDS (agent mode: the never-receivers' relu(x_raw W4
+// + b4) computed once per node instead of once per (receiver, candidate) pair), then each wave takes a
+// receiver row at a time with two candidates per lane (C <= 128): logits from LDS, softmax by wave
+// shuffles (no barriers), the row's weights / senders / edge features in a per-wave LDS buffer, and the
+// H (D + 5) weighted sums one output column per lane.
+// ================================================================================================
+namespace gfwd {
+constexpr int kMaxC = 128;
+// per-wave buffers: 4 x kMaxC x (kH + 1 + 4) floats, reused for the pre-mode staging (N D0 + D0 D + D)
+template <int DM>
+size_t wave_floats(int N) {
+  const size_t w = 4 * (size_t)kMaxC * (kH + 1 + 4), st = (size_t)N * kD0 + kD0 * DM + DM;
+  return w > st ? w : st;
+}
+template <int DM>
+size_t lds_floats(int N, int n) {
+  return (size_t)N * (DM + 1) + (size_t)n * (kH * DM + 4) + wave_floats<DM>(N);
+}
+}  // namespace gfwd
+
+template <int DM>
+__global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args p) {
+  using lanes::f32x4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int XP = DM + 1, QP = kH * DM + 4;
+  const int n = p.n_agents, N = p.N, D = p.D, F = p.F, C = p.C, H = kH;
+  const int64_t g = blockIdx.x;
+  float* X = lds;                         // [N][XP] sender rows
+  float* Q = X + (size_t)N * XP;          // [n][QP]: qt_h (DM stride) | beta_h at kH DM + h
+  float* Wb = Q + (size_t)n * QP;         // per wave: A [kMaxC][kH] | S [kMaxC] | E [kMaxC][4]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool agent = p.xa != nullptr;
+  // ---- stage the graph's sender rows (pre mode: raw rows and pre weights through LDS first, in the
+  // per-wave buffers that are free until the row loop)
+  const bool pre = agent && p.pre_W != nullptr;
+  const int D0 = p.D0;
+  float* R0 = Wb;                      // [N][D0] raw rows
+  float* PW = R0 + (size_t)N * D0;     // [D0][D] | b [D]
+  if (pre) {
+    for (int e = threadIdx.x; e < N * D0; e += 256) R0[e] = p.x[g * p.x_gstride + e];
+    for (int e = threadIdx.x; e < D0 * D; e += 256) PW[e] = p.pre_W[e];
+    for (int e = threadIdx.x; e < D; e += 256) PW[D0 * D + e] = p.pre_b[e];
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < N * D; e += 256) {
+    const int r = e / D, d = e - r * D;
+    float v;
+    if (!agent) {
+      v = p.x[g * p.x_gstride + (int64_t)r * D + d];
+    } else if (r < n) {
+      v = p.xa[g * p.xa_gstride + (int64_t)r * D + d];
+    } else if (pre) {
+      float acc = PW[D0 * D + d];
+      for (int k = 0; k < D0; ++k) acc += R0[r * D0 + k] * PW[k * D + d];
+      v = acc > 0.0f ? acc : 0.0f;
+    } else {  // raw rows used directly (D0 == D)
+      v = p.x[g * p.x_gstride + (int64_t)r * D0 + d];
+    }
+    X[r * XP + d] = v;
+  }
+  for (int e = threadIdx.x; e < n * H * D; e += 256) {
+    const int i = e / (H * D), k = e - i * (H * D), h = k / D, d = k - h * D;
+    Q[i * QP + h * DM + d] = p.qt[(g * n + i) * H * D + k];
+  }
+  for (int e = threadIdx.x; e < n * H; e += 256) {  // beta_h = q_h . bk_h
+    const int i = e / H, h = e - i * H;
+    const float* q = p.q + (g * n + i) * H * F + h * F;
+    float acc = 0.0f;
+    for (int f = 0; f < F; ++f) acc += q[f] * p.bk[h * F + f];
+    Q[i * QP + kH * DM + h] = acc;
+  }
+  __syncthreads();
+  constexpr int kMaxC = gfwd::kMaxC;
+  float* A = Wb + wave * kMaxC * (kH + 1 + 4);
+  int* S = reinterpret_cast<int*>(A + kMaxC * kH);
+  float* E = A + kMaxC * (kH + 1);
+  const int W = H * (D + 5);
+  // the next row's senders and edge features are requested while this row computes
+  int sn[2];
+  f32x4 en[2];
+  auto fetch = [&](int i) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = lane + 64 * u;
+      const bool in = i < n && c < C;
+      const int64_t row = g * n + (in ? i : 0);
+      const int sd = in ? p.sidx[row * C + c] : -1;
+      const int e = in ? p.cand[i * C + c] : 0;
+      sn[u] = sd;
+      en[u] = sd >= 0 ? *reinterpret_cast<const f32x4*>(p.ef + g * p.ef_gstride + (int64_t)e * 4)
+                      : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+  };
+  fetch(wave);
+  for (int i = wave; i < n; i += 4) {
+    const int64_t row = g * n + i;
+    int sv[2] = {sn[0], sn[1]};
+    const f32x4 ev[2] = {en[0], en[1]};
+    fetch(i + 4);
+    float lg[2][kH];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = lane + 64 * u;
+      const int sd = sv[u];
+      const bool ok = sd >= 0;
+      const float* xr = X + (ok ? sd : 0) * XP;
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        const float* qt = Q + i * QP + h * DM;
+        float acc = 0.0f;
+#pragma unroll
+        for (int d = 0; d < DM; ++d)
+          if (d < D) acc += qt[d] * xr[d];
+        lg[u][h] = ok ? (acc + Q[i * QP + kH * DM + h]) * p.scale : -INFINITY;
+      }
+      if (c < C) {
+        *reinterpret_cast<f32x4*>(E + c * 4) = ev[u];
+        S[c] = sd;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float mx = fmaxf(lg[0][h], lg[1][h]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      const float e0 = sv[0] >= 0 ? expf(lg[0][h] - mx) : 0.0f;
+      const float e1 = sv[1] >= 0 ? expf(lg[1][h] - mx) : 0.0f;
+      float sm = e0 + e1;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = lane + 64 * u;
+        const float a = sv[u] >= 0 ? (u == 0 ? e0 : e1) / sm : 0.0f;
+        if (c < C) {
+          A[c * kH + h] = a;
+          if (p.attn) p.attn[(row * H + h) * C + c] = a;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // weighted sums, 8 candidates per step with independent partial sums (the per-candidate LDS reads
+    // of one step do not wait on each other); masked candidates have weight 0 and read row 0
+    for (int o = lane; o < W; o += 64) {
+      const int kind = o < H * D ? 0 : (o < H * D + 4 * H ? 1 : 2);
+      const int h = kind == 0 ? o / D : (kind == 1 ? (o - H * D) >> 2 : o - H * D - 4 * H);
+      const int d = kind == 0 ? o - h * D : (kind == 1 ? (o - H * D) & 3 : 0);
+      float part[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      for (int c0 = 0; c0 < C; c0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int c = c0 + u;
+          if (c < C) {
+            const int sd = S[c];
+            const float a = A[c * kH + h];
+            const float v = kind == 0 ? X[(sd >= 0 ? sd : 0) * XP + d] : (kind == 1 ? E[c * 4 + d] : 1.0f);
+            part[u] += (sd >= 0 ? a : 0.0f) * v;
+          }
+        }
+      }
+      p.xcat[row * W + o] = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+bool gfwd_ok(const dgppo_gnn_attn_args* p) {
+  static const bool off = [] {
+    const char* e = getenv("DGPPO_ATTN_GRAPH");
+    return e && atoi(e) == 0;
+  }();
+  // measured (LidarSpread n = 32): 1.6 ms vs 3.1 ms for the block kernel at D <= 8; at D = 32 the LDS
+  // footprint (2 workgroups per CU) leaves it latency-bound and the block kernel is faster (5.3 vs 7.2 ms)
+  if (off || p->H != kH || p->C <= 32 || p->C > gfwd::kMaxC || p->D > 8 || !p->sidx) return false;
+  if (p->xa && p->D0 > kD0) return false;
+  const size_t bytes = (p->D <= 8 ? gfwd::lds_floats<8>(p->N, p->n_agents) : gfwd::lds_floats<32>(p->N, p->n_agents)) *
+                       sizeof(float);
+  return bytes <= 160 * 1024;
+}
+
+void gfwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
+  const bool d8 = p->D <= 8;
+  const size_t bytes = (d8 ? gfwd::lds_floats<8>(p->N, p->n_agents) : gfwd::lds_floats<32>(p->N, p->n_agents)) *
+                       sizeof(float);
+  if (bytes > 64 * 1024) {
+    static bool raised[2] = {false, false};
+    if (!raised[d8]) {
+      (void)hipFuncSetAttribute(d8 ? (const void*)attn_fwd_graph_kernel<8> : (const void*)attn_fwd_graph_kernel<32>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      raised[d8] = true;
+    }
+  }
+  if (d8) hipLaunchKernelGGL(attn_fwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
+  else hipLaunchKernelGGL(attn_fwd_graph_kernel<32>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
+}
+
 int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
+  if (!bwd && gfwd_ok(p)) {
+    if (p->G > 0) gfwd_launch(p, s);
+    return 0;
+  }
   if (!bwd && fwd2_ok(p)) {
     if (p->G > 0) fwd2_launch(p, s);
     return 0;
