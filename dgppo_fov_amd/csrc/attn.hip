@@ -1849,6 +1849,133 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
   }
 }
 
+// Backward, graph form, full mode without sender gradients (the first layer: its senders are the raw
+// node rows, whose gradient nobody needs): the same staging and row walk as attn_fwd_graph_kernel.
+// Per pair da_h = dxbar_h . x + debar_h . ef + dsig_h (+ da_add), dl_h = a_h (da_h - sum_c a_h da_h)
+// scale and dbeta_h = sum_c dl_h by wave shuffles; dqt_h = sum_c dl_h x_c one output column per lane.
+template <int DM>
+__global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args p) {
+  using lanes::f32x4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int XP = DM + 1, kMaxC = gfwd::kMaxC;
+  const int n = p.n_agents, N = p.N, D = p.D, F = p.F, C = p.C, H = kH;
+  const int W = H * (D + 5);
+  const int64_t g = blockIdx.x;
+  float* X = lds;                          // [N][XP]
+  float* G = X + (size_t)N * XP;           // [n][W] dxcat rows
+  float* Wb = G + (size_t)n * W;           // per wave: dl [kMaxC][kH] | S [kMaxC]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < N * D; e += 256) {
+    const int r = e / D, d = e - r * D;
+    X[r * XP + d] = p.x[g * p.x_gstride + (int64_t)r * D + d];
+  }
+  for (int e = threadIdx.x; e < n * W; e += 256) G[e] = p.dxcat[g * n * W + e];
+  __syncthreads();
+  float* Aw = Wb + wave * kMaxC * (kH + 1);
+  int* S = reinterpret_cast<int*>(Aw + kMaxC * kH);
+  for (int i = wave; i < n; i += 4) {
+    const int64_t row = g * n + i;
+    const float* gv = G + i * W;  // dxbar (H D) | debar (4 H) | dsig (H)
+    int sv[2];
+    float av[2][kH], da[2][kH];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = lane + 64 * u;
+      const int sd = c < C ? p.sidx[row * C + c] : -1;
+      sv[u] = sd;
+      const bool ok = sd >= 0;
+      const int e = c < C ? p.cand[i * C + c] : 0;
+      const f32x4 ef = ok ? *reinterpret_cast<const f32x4*>(p.ef + g * p.ef_gstride + (int64_t)e * 4)
+                          : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      const float* xr = X + (ok ? sd : 0) * XP;
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        av[u][h] = ok ? p.attn[(row * H + h) * C + c] : 0.0f;
+        float acc = 0.0f;
+#pragma unroll
+        for (int d = 0; d < DM; ++d)
+          if (d < D) acc += gv[h * D + d] * xr[d];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += gv[H * D + 4 * h + j] * ef[j];
+        acc += gv[H * D + 4 * H + h];
+        if (p.da_add && ok) acc += p.da_add[(row * H + h) * C + c];
+        da[u][h] = ok ? acc : 0.0f;
+      }
+      if (c < C) S[c] = sd;
+    }
+    float dbeta[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float dot = av[0][h] * da[0][h] + av[1][h] * da[1][h];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+      float db = 0.0f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = lane + 64 * u;
+        const float dl = sv[u] >= 0 ? av[u][h] * (da[u][h] - dot) * p.scale : 0.0f;
+        db += dl;
+        if (c < C) Aw[c * kH + h] = dl;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) db += __shfl_xor(db, o, 64);
+      dbeta[h] = db;
+    }
+    if (lane < kH) p.dbeta[row * H + lane] = lane == 0 ? dbeta[0] : (lane == 1 ? dbeta[1] : dbeta[2]);
+    for (int kk = lane; kk < H * F; kk += 64) {
+      const int h = kk / F;
+      p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int o = lane; o < H * D; o += 64) {  // dqt_h[d] = sum_c dl_h x_c[d]
+      const int h = o / D, d = o - h * D;
+      float part[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      for (int c0 = 0; c0 < C; c0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int c = c0 + u;
+          if (c < C) {
+            const int sd = S[c];
+            part[u] += (sd >= 0 ? Aw[c * kH + h] : 0.0f) * X[(sd >= 0 ? sd : 0) * XP + d];
+          }
+        }
+      }
+      p.dqt[row * H * D + o] = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+size_t gbwd_lds_floats(const dgppo_gnn_attn_args* p) {
+  return (size_t)p->N * (8 + 1) + (size_t)p->n_agents * kH * (p->D + 5) + 4 * (size_t)gfwd::kMaxC * (kH + 1);
+}
+
+bool gbwd_ok(const dgppo_gnn_attn_args* p) {
+  static const bool off = [] {
+    const char* e = getenv("DGPPO_ATTN_GRAPH");
+    return e && atoi(e) == 0;
+  }();
+  return !off && p->H == kH && p->C > 32 && p->C <= gfwd::kMaxC && p->D <= 8 && p->sidx && !p->xa && !p->dx &&
+         gbwd_lds_floats(p) * sizeof(float) <= 160 * 1024;
+}
+
+void gbwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
+  const size_t bytes = gbwd_lds_floats(p) * sizeof(float);
+  if (bytes > 64 * 1024) {
+    static bool raised = false;
+    if (!raised) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_graph_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      raised = true;
+    }
+  }
+  hipLaunchKernelGGL(attn_bwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
+}
+
 bool gfwd_ok(const dgppo_gnn_attn_args* p) {
   static const bool off = [] {
     const char* e = getenv("DGPPO_ATTN_GRAPH");
@@ -1886,6 +2013,10 @@ int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
   }
   if (!bwd && fwd2_ok(p)) {
     if (p->G > 0) fwd2_launch(p, s);
+    return 0;
+  }
+  if (bwd && gbwd_ok(p)) {
+    if (p->G > 0) gbwd_launch(p, s);
     return 0;
   }
   if (bwd && bwd2_ok(p)) {
