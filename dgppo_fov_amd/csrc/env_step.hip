@@ -1427,8 +1427,9 @@ static size_t omni_step_lds_bytes(const dgppo_env_cfg& c) {
 }
 
 // ---- reset ------------------------------------------------------------------------------------
-// Thread 0 runs the reference's sequential rejection sampler for its env (reset is once per
-// episode, amortised over T = 128 steps); then the whole workgroup ray-casts and writes the graph.
+// Thread 0 draws the obstacles, wave 0 runs the rejection sampler for agents and goals, thread 0 the
+// headings (reset is once per episode, amortised over T = 128 steps); then the whole workgroup
+// ray-casts and writes the graph.
 __device__ bool inside_any(const float* obst, int O, float px, float py, float r) {
   bool in = false;
   for (int o = 0; o < O; ++o) in = in || rect_inside(obst + o * DGPPO_OBST_FIELDS, px, py, r);
@@ -1455,61 +1456,73 @@ __device__ void make_rectangle(float* rec, float cx, float cy, float w, float h,
   }
 }
 
-// get_node_goal_rng (env/utils.py:139-244), dim 2, max_travel None; pos/goal are (n, 2) in LDS
-__device__ void node_goal_rng(Rng& rng, float side, int n, float min_dist, float r_in, const float* obst, int O,
-                              float* pos, float* gl) {
+// get_node_goal_rng (env/utils.py:139-244; dim 2, max_travel None; oracle/env.py node_goal_rng), the
+// reference's sequential rejection sampler, run by one 64-lane wave, exactly: within a phase (agent i, then goal i) the placed
+// points do not change and candidate t of the phase is the Philox draw pair at count p + 2 t, so lane l
+// tests candidate b + l of batch b and the phase takes the lowest accepted index (ballot); candidate
+// kMaxIter is taken regardless, as the sequential loop does.  Returns the phase's rejection count.
+__device__ int sample_phase(const Rng& rng, uint32_t& count, bool goals, float side, int n, float min_dist,
+                            float r_in, const float* obst, int O, const float* pts, float& ox, float& oy) {
   constexpr int kMaxIter = 1024;
-  for (int i = 0; i < 2 * n; ++i) {
-    pos[i] = 0.0f;
-    gl[i] = 0.0f;
+  const int lane = threadIdx.x & 63;
+  for (int b = 0;; b += 64) {
+    const int t = b + lane;
+    Rng r = rng;
+    r.count = count + 2u * (uint32_t)t;
+    const float cx = r.uniform(0.0f, side), cy = r.uniform(0.0f, side);
+    float dmin = 0.0f;
+    for (int j = 0; j < n; ++j) {
+      const float d = norm2(pts[2 * j] - cx, pts[2 * j + 1] - cy);
+      dmin = j == 0 ? d : min_nan(dmin, d);
+    }
+    bool bad = (dmin <= min_dist) || inside_any(obst, O, cx, cy, r_in);
+    if (goals) bad = bad || cx < 0.0f || cy < 0.0f || cx > side || cy > side;
+    const uint64_t m = __ballot((t <= kMaxIter) && (!bad || t == kMaxIter));
+    if (m) {
+      const int f = __ffsll((unsigned long long)m) - 1;
+      ox = __shfl(cx, f, 64);
+      oy = __shfl(cy, f, 64);
+      count += 2u * (uint32_t)(b + f + 1);
+      return b + f;
+    }
   }
+}
+
+__device__ void node_goal_rng_wave(Rng& rng, float side, int n, float min_dist, float r_in, const float* obst, int O,
+                                   float* pos, float* gl) {
+  constexpr int kMaxIter = 1024;
+  const int lane = threadIdx.x & 63;
+  auto clear = [&]() {
+    for (int i = lane; i < 2 * n; i += 64) {
+      pos[i] = 0.0f;
+      gl[i] = 0.0f;
+    }
+    wv::wave_sync();
+  };
+  clear();
+  uint32_t count = rng.count;
   int agent_id = 0;
   while (agent_id < n) {
-    float cx = rng.uniform(0.0f, side), cy = rng.uniform(0.0f, side);
-    int it = 0;
-    for (;;) {
-      float dmin = 0.0f;
-      for (int j = 0; j < n; ++j) {
-        const float d = norm2(pos[2 * j] - cx, pos[2 * j + 1] - cy);
-        dmin = j == 0 ? d : min_nan(dmin, d);
-      }
-      const bool collide = dmin <= min_dist;
-      const bool in = inside_any(obst, O, cx, cy, r_in);
-      if (!(collide || in) || it >= kMaxIter) break;
-      ++it;
-      cx = rng.uniform(0.0f, side);
-      cy = rng.uniform(0.0f, side);
+    float cx, cy, gx, gy;
+    const int it_agent = sample_phase(rng, count, false, side, n, min_dist, r_in, obst, O, pos, cx, cy);
+    if (lane == 0) {
+      pos[2 * agent_id] = cx;
+      pos[2 * agent_id + 1] = cy;
     }
-    const int it_agent = it;
-    pos[2 * agent_id] = cx;
-    pos[2 * agent_id + 1] = cy;
-    float gx = rng.uniform(0.0f, side), gy = rng.uniform(0.0f, side);
-    it = 0;
-    for (;;) {
-      float dmin = 0.0f;
-      for (int j = 0; j < n; ++j) {
-        const float d = norm2(gl[2 * j] - gx, gl[2 * j + 1] - gy);
-        dmin = j == 0 ? d : min_nan(dmin, d);
-      }
-      const bool collide = dmin <= min_dist;
-      const bool in = inside_any(obst, O, gx, gy, r_in);
-      const bool outside = gx < 0.0f || gy < 0.0f || gx > side || gy > side;
-      if (!(collide || in || outside) || it >= kMaxIter) break;
-      ++it;
-      gx = rng.uniform(0.0f, side);
-      gy = rng.uniform(0.0f, side);
+    wv::wave_sync();
+    const int it = sample_phase(rng, count, true, side, n, min_dist, r_in, obst, O, gl, gx, gy);
+    if (lane == 0) {
+      gl[2 * agent_id] = gx;
+      gl[2 * agent_id + 1] = gy;
     }
-    gl[2 * agent_id] = gx;
-    gl[2 * agent_id + 1] = gy;
+    wv::wave_sync();
     ++agent_id;
     if (it_agent >= kMaxIter || it >= kMaxIter) {  // no solution: start over (utils.py:229-232)
       agent_id = 0;
-      for (int i = 0; i < 2 * n; ++i) {
-        pos[i] = 0.0f;
-        gl[i] = 0.0f;
-      }
+      clear();
     }
   }
+  rng.count = count;
 }
 
 template <int ENGINE, int GOAL, int SD, int BLOCK>
@@ -1526,11 +1539,12 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
   float* goal = lds + cv.cur + n * SD;  // sampled goal states
   float* third = lds + cv.cur + 2 * n * SD;  // MPE obstacle states
   float* obst = lds + cv.obst;
+  __shared__ uint32_t rng_count;
+  Rng rng(io.seed_ptr ? *io.seed_ptr : io.seed, (uint32_t)(io.env_offset + env));
+  const float area = cfg.area_size;
+  float* pos = lds + cv.samp;
+  float* gl = pos + 2 * n;
   if (tid == 0) {
-    Rng rng(io.seed_ptr ? *io.seed_ptr : io.seed, (uint32_t)(io.env_offset + env));
-    const float area = cfg.area_size;
-    float* pos = lds + cv.samp;
-    float* gl = pos + 2 * n;
     if (!mpe && O > 0) {
       float tmp[4 * kMaxObs + kMaxObs];
       for (int o = 0; o < O; ++o) {
@@ -1546,7 +1560,17 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
         make_rectangle(obst + o * DGPPO_OBST_FIELDS, tmp[2 * o], tmp[2 * o + 1], tmp[2 * O + 2 * o],
                        tmp[2 * O + 2 * o + 1], tmp[4 * O + o]);
     }
-    node_goal_rng(rng, area, n, cfg.c_min_dist, cfg.c_inside_r, obst, mpe ? 0 : O, pos, gl);
+    rng_count = rng.count;
+  }
+  __syncthreads();
+  if (tid < 64) {  // agent / goal positions: the rejection sampler, one wave wide
+    rng.count = rng_count;
+    node_goal_rng_wave(rng, area, n, cfg.c_min_dist, cfg.c_inside_r, obst, mpe ? 0 : O, pos, gl);
+    if (tid == 0) rng_count = rng.count;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    rng.count = rng_count;
     for (int i = 0; i < n; ++i) {
       for (int c = 0; c < SD; ++c) {
         nxt[i * SD + c] = c < 2 ? pos[2 * i + c] : 0.0f;
