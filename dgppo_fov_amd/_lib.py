@@ -254,6 +254,9 @@ SIGNATURES = {
 _LIB = None
 
 
+ABI_VERSION = 2  # include/dgppo_hip.h DGPPO_ABI_VERSION
+
+
 def load() -> ctypes.CDLL:
     """Load the HIP library once (torch must be imported first so one HIP runtime is shared)."""
     global _LIB
@@ -273,6 +276,9 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.dgppo_abi_version() != ABI_VERSION:  # the ctypes mirrors below describe ABI_VERSION's structs
+        raise NativeLibraryError(f"{LIB_PATH} has ABI {lib.dgppo_abi_version()}, this package expects {ABI_VERSION}: "
+                                 "rebuild it (make)")
     _LIB = lib
     return lib
 
