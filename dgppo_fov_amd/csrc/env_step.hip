@@ -1461,15 +1461,26 @@ __device__ void make_rectangle(float* rec, float cx, float cy, float w, float h,
 // points do not change and candidate t of the phase is the Philox draw pair at count p + 2 t, so lane l
 // tests candidate b + l of batch b and the phase takes the lowest accepted index (ballot); candidate
 // kMaxIter is taken regardless, as the sequential loop does.  Returns the phase's rejection count.
-__device__ int sample_phase(const Rng& rng, uint32_t& count, bool goals, float side, int n, float min_dist,
-                            float r_in, const float* obst, int O, const float* pts, float& ox, float& oy) {
+constexpr int kSampTab = 256;  // candidate pairs drawn ahead by the whole workgroup (reset LDS tail)
+
+__device__ int sample_phase(const Rng& rng, uint32_t& count, uint32_t count0, const float* tab, bool goals,
+                            float side, int n, float min_dist, float r_in, const float* obst, int O,
+                            const float* pts, float& ox, float& oy) {
   constexpr int kMaxIter = 1024;
   const int lane = threadIdx.x & 63;
   for (int b = 0;; b += 64) {
     const int t = b + lane;
-    Rng r = rng;
-    r.count = count + 2u * (uint32_t)t;
-    const float cx = r.uniform(0.0f, side), cy = r.uniform(0.0f, side);
+    const uint32_t k = (count - count0) / 2u + (uint32_t)t;  // candidate pair index since count0
+    float cx, cy;
+    if (k < (uint32_t)kSampTab) {
+      cx = tab[2 * k];
+      cy = tab[2 * k + 1];
+    } else {
+      Rng r = rng;
+      r.count = count + 2u * (uint32_t)t;
+      cx = r.uniform(0.0f, side);
+      cy = r.uniform(0.0f, side);
+    }
     float dmin = 0.0f;
     for (int j = 0; j < n; ++j) {
       const float d = norm2(pts[2 * j] - cx, pts[2 * j + 1] - cy);
@@ -1488,8 +1499,8 @@ __device__ int sample_phase(const Rng& rng, uint32_t& count, bool goals, float s
   }
 }
 
-__device__ void node_goal_rng_wave(Rng& rng, float side, int n, float min_dist, float r_in, const float* obst, int O,
-                                   float* pos, float* gl) {
+__device__ void node_goal_rng_wave(Rng& rng, const float* tab, float side, int n, float min_dist, float r_in,
+                                   const float* obst, int O, float* pos, float* gl) {
   constexpr int kMaxIter = 1024;
   const int lane = threadIdx.x & 63;
   auto clear = [&]() {
@@ -1501,16 +1512,17 @@ __device__ void node_goal_rng_wave(Rng& rng, float side, int n, float min_dist, 
   };
   clear();
   uint32_t count = rng.count;
+  const uint32_t count0 = count;
   int agent_id = 0;
   while (agent_id < n) {
     float cx, cy, gx, gy;
-    const int it_agent = sample_phase(rng, count, false, side, n, min_dist, r_in, obst, O, pos, cx, cy);
+    const int it_agent = sample_phase(rng, count, count0, tab, false, side, n, min_dist, r_in, obst, O, pos, cx, cy);
     if (lane == 0) {
       pos[2 * agent_id] = cx;
       pos[2 * agent_id + 1] = cy;
     }
     wv::wave_sync();
-    const int it = sample_phase(rng, count, true, side, n, min_dist, r_in, obst, O, gl, gx, gy);
+    const int it = sample_phase(rng, count, count0, tab, true, side, n, min_dist, r_in, obst, O, gl, gx, gy);
     if (lane == 0) {
       gl[2 * agent_id] = gx;
       gl[2 * agent_id + 1] = gy;
@@ -1563,9 +1575,18 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
     rng_count = rng.count;
   }
   __syncthreads();
+  // the first kSampTab candidate pairs of the sampler's stream, drawn by every thread at once
+  float* tab = lds + cv.total;
+  for (int k = tid; k < kSampTab; k += BLOCK) {
+    Rng r = rng;
+    r.count = rng_count + 2u * (uint32_t)k;
+    tab[2 * k] = r.uniform(0.0f, area);
+    tab[2 * k + 1] = r.uniform(0.0f, area);
+  }
+  __syncthreads();
   if (tid < 64) {  // agent / goal positions: the rejection sampler, one wave wide
     rng.count = rng_count;
-    node_goal_rng_wave(rng, area, n, cfg.c_min_dist, cfg.c_inside_r, obst, mpe ? 0 : O, pos, gl);
+    node_goal_rng_wave(rng, tab, area, n, cfg.c_min_dist, cfg.c_inside_r, obst, mpe ? 0 : O, pos, gl);
     if (tid == 0) rng_count = rng.count;
   }
   __syncthreads();
@@ -1890,7 +1911,7 @@ extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_i
   if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                  cfg->engine != DGPPO_ENGINE_MPE);
-  const size_t shmem = (size_t)cv.total * sizeof(float);
+  const size_t shmem = ((size_t)cv.total + 2 * kSampTab) * sizeof(float);  // + the sampler's candidate table
   dispatch_reset(*cfg, *io, shmem, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
