@@ -665,7 +665,8 @@ struct Carve {
   static constexpr int total = (uni + uni_size + 3) & ~3;
 };
 
-template <int ENGINE, int GOAL, int SD, int O>
+// REBUILD: the graph of the given states (reset: y = x, no reward / cost), else one env step.
+template <int ENGINE, int GOAL, int SD, int O, bool REBUILD = false>
 __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
   static_assert(O >= 1 && O <= 4, "obstacle records are staged by one load per lane");
   // LidarOmniTarget (SD 7, own goals): omni dynamics, 5 costs, 10-wide edges; same LiDAR and graph rows
@@ -731,7 +732,10 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     ev = rec[8 + 2 * ((e + 3) & 3) + c] - rec[8 + 2 * e + c];  // (x4 - x3, y4 - y3)
   }
   float y[SD];
-  if constexpr (OMNI) {  // agent_step_euler (lidar_omni_target.py:146-197)
+  if constexpr (REBUILD) {
+#pragma unroll
+    for (int c = 0; c < SD; ++c) y[c] = x[c];
+  } else if constexpr (OMNI) {  // agent_step_euler (lidar_omni_target.py:146-197)
     const float acc_x = a0 * 10.0f, acc_y = a1 * 10.0f, alw = aw * 5.0f;
     const float theta = atan2_32(x[3], x[2]);
     const float new_theta = theta + x[6] * cfg.dt;
@@ -761,8 +765,10 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     y[2] = (a0 * 10.0f) * cfg.dt + x[2];
     y[3] = (a1 * 10.0f) * cfg.dt + x[3];
   }
+  if constexpr (!REBUILD) {
 #pragma unroll
-  for (int c = 0; c < SD; ++c) y[c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+    for (int c = 0; c < SD; ++c) y[c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+  }
   if (lane < NA) {
 #pragma unroll
     for (int c = 0; c < SD; ++c) nxt[lane * SD + c] = y[c];
@@ -811,7 +817,7 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     float v = q == 0 ? cq[0] : (q == 1 ? cq[1] : (q == 2 ? cq[2] : (q == 3 ? cq[3] : cq[4])));
     v = v <= 0.0f ? v - 0.1f : v + 0.1f;
     v = clampf_nan(v, -1.0f, 1.0f);
-    if (live & (gj < kOmniNC)) io.cost[env * io.cost_stride + kOmniNC * gi + gj] = v;
+    if (!REBUILD && live & (gj < kOmniNC)) io.cost[env * io.cost_stride + kOmniNC * gi + gj] = v;
     const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
     const float w2 = aw * aw, o2 = x[6] * x[6];
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f, s4 = 0.0f;
@@ -823,7 +829,7 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
       s3 = s3 + rlf(w2, i);
       s4 = s4 + rlf(o2, i);
     }
-    if (live & (lane == 0)) {  // get_reward (lidar_omni_target.py:295-336)
+    if (!REBUILD && live & (lane == 0)) {  // get_reward (lidar_omni_target.py:295-336)
       const float nn = (float)NA;
       float r = 0.0f - (s0 / nn) * 0.01f;
       r = r - (s1 / nn) * 0.001f;
@@ -839,7 +845,7 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     c1 = c1 <= 0.0f ? c1 - 0.5f : c1 + 0.5f;
     c0 = clampf_nan(c0, -1.0f, 1.0f);
     c1 = clampf_nan(c1, -1.0f, 1.0f);
-    if (live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = gj == 0 ? c0 : c1;
+    if (!REBUILD && live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = gj == 0 ? c0 : c1;
     const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
     float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
 #pragma unroll
@@ -848,7 +854,7 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
       sf = sf + rlf(far, 8 * i);
       sa = sa + rlf(a2, i);  // lane i holds agent j = i
     }
-    if (live & (lane == 0)) {
+    if (!REBUILD && live & (lane == 0)) {
       const float nn = (float)NA;
       float r = 0.0f - (sd_ / nn) * 0.01f;
       r = r - (sf / nn) * 0.001f;
@@ -1538,7 +1544,7 @@ __device__ void node_goal_rng_wave(Rng& rng, const float* tab, float side, int n
 }
 
 template <int ENGINE, int GOAL, int SD, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgppo_env_reset_io io) {
+__global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgppo_env_reset_io io, int states_only) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const bool mpe = ENGINE == DGPPO_ENGINE_MPE;
   const Dims<0, -1, 0, 0> d(cfg);
@@ -1640,6 +1646,15 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
     }
   }
   __syncthreads();
+  if (states_only) {  // the wave step kernel builds the graph from these rows (dgppo_env_reset)
+    if (lidar) {
+      float* ob = io.obstacles + env * io.obstacles_stride;
+      for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) ob[idx] = obst[idx];
+    }
+    float* so = io.out_states + env * io.out_states_stride;
+    for (int idx = tid; idx < 2 * n * SD; idx += BLOCK) so[idx] = idx < n * SD ? nxt[idx] : goal[idx - n * SD];
+    return;
+  }
   if (lidar) {
     float* ob = io.obstacles + env * io.obstacles_stride;
     for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) ob[idx] = obst[idx];
@@ -1728,30 +1743,32 @@ static void dispatch_step(const dgppo_env_cfg& c, const dgppo_env_step_io& io, s
 }
 
 template <int ENGINE, int GOAL, int SD>
-static void dispatch_reset_sized(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s) {
+static void dispatch_reset_sized(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s,
+                                 int states_only) {
   const dim3 grid((unsigned)io.n_env);
   if (ENGINE == DGPPO_ENGINE_MPE)
-    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 64>), grid, dim3(64), shmem, s, c, io);
+    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 64>), grid, dim3(64), shmem, s, c, io, states_only);
   else if (c.n_agents * c.n_rays >= 256)
-    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 256>), grid, dim3(256), shmem, s, c, io);
+    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 256>), grid, dim3(256), shmem, s, c, io, states_only);
   else
-    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 128>), grid, dim3(128), shmem, s, c, io);
+    hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 128>), grid, dim3(128), shmem, s, c, io, states_only);
 }
 
-static void dispatch_reset(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s) {
+static void dispatch_reset(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s,
+                           int so) {
   const bool spread = c.goal_mode == DGPPO_GOAL_SPREAD;
   switch (c.engine) {
     case DGPPO_ENGINE_MPE:
-      return spread ? dispatch_reset_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
-                    : dispatch_reset_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
+      return spread ? dispatch_reset_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s, so)
+                    : dispatch_reset_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s, so);
     case DGPPO_ENGINE_BICYCLE:
-      return spread ? dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, io, shmem, s)
-                    : dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, io, shmem, s);
+      return spread ? dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, io, shmem, s, so)
+                    : dispatch_reset_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, io, shmem, s, so);
     case DGPPO_ENGINE_OMNI:
-      return dispatch_reset_sized<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD>(c, io, shmem, s);
+      return dispatch_reset_sized<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD>(c, io, shmem, s, so);
     default:
-      return spread ? dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s)
-                    : dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s);
+      return spread ? dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, io, shmem, s, so)
+                    : dispatch_reset_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, io, shmem, s, so);
   }
 }
 
@@ -1912,6 +1929,56 @@ extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_i
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                  cfg->engine != DGPPO_ENGINE_MPE);
   const size_t shmem = ((size_t)cv.total + 2 * kSampTab) * sizeof(float);  // + the sampler's candidate table
-  dispatch_reset(*cfg, *io, shmem, (hipStream_t)stream);
+  const hipStream_t s = (hipStream_t)stream;
+  const bool wave = lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK &&
+                    cfg->n_obs == 3 && wave_step_enabled();
+  if (!wave) {
+    dispatch_reset(*cfg, *io, shmem, s, 0);
+    return (int)hipGetLastError();
+  }
+  // sampled agent / goal rows and obstacles, then the wave-per-env step kernel in REBUILD mode builds
+  // the initial graph from them in place (same LiDAR and graph code as every step)
+  dispatch_reset(*cfg, *io, shmem, s, 1);
+  dgppo_env_step_io st{};
+  st.states = io->out_states;
+  st.states_stride = io->out_states_stride;
+  st.obstacles = io->obstacles;
+  st.obstacles_stride = io->obstacles_stride;
+  st.action = io->out_states;  // read, never used in REBUILD
+  st.action_stride = io->out_states_stride;
+  st.ray_dirs = io->ray_dirs;
+  st.nodes = io->nodes;
+  st.nodes_stride = io->nodes_stride;
+  st.edges = io->edges;
+  st.edges_stride = io->edges_stride;
+  st.out_states = io->out_states;
+  st.out_states_stride = io->out_states_stride;
+  st.receivers = io->receivers;
+  st.senders = io->senders;
+  st.edge_index_stride = io->edge_index_stride;
+  st.n_env = io->n_env;
+  const dim3 grid((unsigned)((io->n_env + 3) / 4)), block(256);
+  const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
+  if (cfg->engine == DGPPO_ENGINE_OMNI) {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<kOmniSD, 3>::total;
+    hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD, 3, true>), grid, block,
+                       sh, s, *cfg, st);
+  } else if (cfg->engine == DGPPO_ENGINE_BICYCLE) {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<5, 3>::total;
+    if (spread)
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+    else
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+  } else {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<4, 3>::total;
+    if (spread)
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+    else
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+  }
   return (int)hipGetLastError();
 }
