@@ -1746,7 +1746,9 @@ template <int ENGINE, int GOAL, int SD>
 static void dispatch_reset_sized(const dgppo_env_cfg& c, const dgppo_env_reset_io& io, size_t shmem, hipStream_t s,
                                  int states_only) {
   const dim3 grid((unsigned)io.n_env);
-  if (ENGINE == DGPPO_ENGINE_MPE)
+  // MPE and states-only resets need one wave (sampler; no workgroup ray cast): 64 threads, so many more
+  // envs are resident per CU and their sequential sampling latencies overlap
+  if (ENGINE == DGPPO_ENGINE_MPE || states_only)
     hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 64>), grid, dim3(64), shmem, s, c, io, states_only);
   else if (c.n_agents * c.n_rays >= 256)
     hipLaunchKernelGGL((env_reset_kernel<ENGINE, GOAL, SD, 256>), grid, dim3(256), shmem, s, c, io, states_only);
