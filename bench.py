@@ -271,7 +271,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "wv::lidar_step_wave_kernel<LIDAR,SPREAD,4,3>",
+                "kernel": "wv::lidar_step_wave_kernel<LIDAR,SPREAD,4,3,false>",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "cpu_baseline": None if args.no_cpu_baseline or world > 1 else cpu_baseline(),
