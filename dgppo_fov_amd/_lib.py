@@ -234,6 +234,8 @@ SIGNATURES = {
     "dgppo_policy_prepare": (ctypes.c_int, [_V, _V]),
     "dgppo_policy_step": (ctypes.c_int, [_V, _V]),
     "dgppo_gnn_sender_table": (ctypes.c_int, [_I32, _I32, _I32, _I32, _V, _V, _V, _V, _V]),
+    "dgppo_cost_shaped_loss": (ctypes.c_int, [_V, _V, ctypes.c_float, _V, _I32, _I32, _I32, _I32, _V]),
+    "dgppo_informarl_advantages": (ctypes.c_int, [_V, _V, _V, _I32, _I32, _I32, _V]),
     "dgppo_gnn_edge_wsum": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _V, _V, _V, _V, _V, _V]),
     "dgppo_gnn_edge_da": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _V, _V, _V, _V, _V, _V]),
     "dgppo_gru_seq_fwd": (ctypes.c_int, [_V, _V]),

@@ -1,10 +1,13 @@
 """Algorithm registry (dgppo/algo/__init__.py:8-18)."""
 from .dgppo import DGPPO
+from .informarl import InforMARL
 
 
 def make_algo(algo: str, **kwargs):
     if algo == "dgppo":
         return DGPPO(**kwargs)
-    if algo in ("informarl", "informarl_lagr", "hcbfcrpo"):
+    if algo == "informarl":
+        return InforMARL(**kwargs)
+    if algo in ("informarl_lagr", "hcbfcrpo"):
         raise NotImplementedError(f"{algo} is not built on the MI355X path yet (DESIGN.md: next rows)")
     raise ValueError(f"Unknown algorithm: {algo}")

@@ -902,6 +902,78 @@ extern "C" int dgppo_dgppo_advantages(const dgppo_adv_args* p, void* stream) {
   return (int)hipGetLastError();
 }
 
+// ---- InforMARL (dgppo/algo/informarl.py:310-340): cost-shaped loss and normalised advantages --------
+// l[b, t] = -r[b, t] + w * sum_a sum_h max(c[b, t, a, h], 0)   (sum over h first, then a)
+__global__ __launch_bounds__(256) void shaped_loss_kernel(const float* __restrict__ r, const float* __restrict__ c,
+                                                          float w, float* __restrict__ l, int64_t BT, int32_t n,
+                                                          int32_t nh) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < BT; t += (int64_t)gridDim.x * 256) {
+    const float* cr = c + t * n * nh;
+    float sa = 0.0f;
+    for (int a = 0; a < n; ++a) {
+      float sh = 0.0f;
+      for (int h = 0; h < nh; ++h) sh += fmaxf(cr[a * nh + h], 0.0f);
+      sa += sh;
+    }
+    l[t] = -r[t] + w * sa;
+  }
+}
+
+// one workgroup per env: Al = Ql - Vl[:T], A[t, a] = -(Al - mean_t Al) / (std_t Al + 1e-8) for every agent
+// (jnp.std: population); fixed-order block reductions
+__global__ __launch_bounds__(256) void informarl_adv_kernel(const float* __restrict__ Ql, const float* __restrict__ Vl,
+                                                            float* __restrict__ A, int32_t T, int32_t n) {
+  __shared__ float red[256];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* q = Ql + b * T;
+  const float* v = Vl + b * (T + 1);
+  float s = 0.0f;
+  for (int t = tid; t < T; t += 256) s += q[t] - v[t];
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  const float mean = red[0] / (float)T;
+  __syncthreads();
+  float s2 = 0.0f;
+  for (int t = tid; t < T; t += 256) {
+    const float d = (q[t] - v[t]) - mean;
+    s2 += d * d;
+  }
+  red[tid] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  const float den = sqrtf(red[0] / (float)T) + 1e-8f;
+  for (int e = tid; e < T * n; e += 256) {
+    const int t = e / n;
+    A[b * T * n + e] = -(((q[t] - v[t]) - mean) / den);
+  }
+}
+
+extern "C" int dgppo_cost_shaped_loss(const float* rewards, const float* costs, float cost_weight, float* l, int32_t B,
+                                      int32_t T, int32_t n_agents, int32_t n_h, void* stream) {
+  if (B < 0 || T < 1 || n_agents < 1 || n_h < 1 || !rewards || !costs || !l) return DGPPO_EINVAL;
+  const int64_t BT = (int64_t)B * T;
+  if (BT == 0) return 0;
+  hipLaunchKernelGGL(shaped_loss_kernel, dim3(grid_for(BT)), dim3(256), 0, DG_STREAM(stream), rewards, costs,
+                     cost_weight, l, BT, n_agents, n_h);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_informarl_advantages(const float* Ql, const float* Vl, float* A, int32_t B, int32_t T,
+                                          int32_t n_agents, void* stream) {
+  if (B < 0 || T < 1 || n_agents < 1 || !Ql || !Vl || !A) return DGPPO_EINVAL;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(informarl_adv_kernel, dim3((unsigned)B), dim3(256), 0, DG_STREAM(stream), Ql, Vl, A, T, n_agents);
+  return (int)hipGetLastError();
+}
+
 extern "C" int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace, void* stream) {
   if (n < 0 || !grad || !state || !workspace) return DGPPO_EINVAL;
   hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kLossBlocks), dim3(256), 0, DG_STREAM(stream), grad, n, workspace);

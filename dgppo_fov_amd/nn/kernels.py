@@ -205,6 +205,18 @@ def normal_(out, seed=0, stream_id=0, seed_tensor=None):
     return out
 
 
+def cost_shaped_loss(rewards, costs, cost_weight, out):
+    B, T, n, nh = costs.shape
+    _chk(_lib.load().dgppo_cost_shaped_loss(_p(rewards), _p(costs), float(cost_weight), _p(out), int(B), int(T), int(n),
+                                            int(nh), _stream(out)), "dgppo_cost_shaped_loss")
+
+
+def informarl_advantages(Ql, Vl, A):
+    B, T, n = A.shape
+    _chk(_lib.load().dgppo_informarl_advantages(_p(Ql), _p(Vl), _p(A), int(B), int(T), int(n), _stream(A)),
+         "dgppo_informarl_advantages")
+
+
 def dgppo_advantages(Ql, Vl, Vh, A, safe_count, dt, alpha, cbf_eps, cbf_weight):
     B, T = Ql.shape
     _, _, n, nh = Vh.shape

@@ -404,6 +404,14 @@ int dgppo_dgppo_advantages(const dgppo_adv_args* args, void* stream);
 
 /* compute_norm_and_clip + optax.adam + apply_if_finite (dgppo/trainer/utils.py:105-118,
  * informarl.py:131-137): state = [global norm, non-finite count, adam step] on the device */
+/* InforMARL (dgppo/algo/informarl.py:310-340): the GAE's cost-shaped loss
+ *   l[b,t] = -rewards[b,t] + cost_weight * sum_a sum_h max(costs[b,t,a,h], 0)
+ * and the per-env normalised advantages A[b,t,a] = -(Al - mean_t Al) / (std_t Al + 1e-8), Al = Ql - Vl[:, :T]
+ * (Ql (B, T), Vl (B, T+1), A (B, T, n_agents)). */
+int dgppo_cost_shaped_loss(const float* rewards, const float* costs, float cost_weight, float* l, int32_t B,
+                           int32_t T, int32_t n_agents, int32_t n_h, void* stream);
+int dgppo_informarl_advantages(const float* Ql, const float* Vl, float* A, int32_t B, int32_t T, int32_t n_agents,
+                               void* stream);
 int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace, void* stream);
 int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, float b1,
                float b2, float eps, float max_norm, void* stream);

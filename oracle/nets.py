@@ -252,3 +252,18 @@ def ppo_policy_loss(log_pis, log_pis_old, A, entropy, clip_eps=0.25, coef_ent=1e
     loss = np.maximum(l1, l2).mean() - coef_ent * entropy.mean()
     return loss, dict(clip_frac=(l2 > l1).mean(), entropy=entropy.mean(),
                       total_variation_dist=0.5 * np.abs(ratio - 1.0).mean())
+
+
+# ---- InforMARL (dgppo/algo/informarl.py) ------------------------------------------------------------
+def informarl_shaped_l(rewards, costs, cost_weight):
+    """T_l of informarl.py:329: -reward + w * sum over (agent, cost) of max(cost, 0), (B, T)."""
+    r = np.asarray(rewards, np.float64)
+    c = np.maximum(np.asarray(costs, np.float64), 0.0)
+    return -r + cost_weight * c.sum(-1).sum(-1)
+
+
+def informarl_advantages(Ql, Vl, n_agents):
+    """informarl.py:334-337: Al = Ql - Vl[:, :T] normalised over T per env (population std), A = -Al per agent."""
+    Al = np.asarray(Ql, np.float64) - np.asarray(Vl, np.float64)[:, :-1]
+    Al = (Al - Al.mean(axis=1, keepdims=True)) / (Al.std(axis=1, keepdims=True) + 1e-8)
+    return -np.repeat(Al[:, :, None], n_agents, axis=-1)

@@ -23,16 +23,17 @@ def _entry(name):  # the repo-root scripts by path (`test` would also name the s
     return mod
 
 
-@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("LidarOmniTarget", 3, 2)])
-def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, n, obs):
+@pytest.mark.parametrize("eid,n,obs,algo", [("LidarSpread", 3, 2, "dgppo"), ("LidarOmniTarget", 3, 2, "dgppo"),
+                                            ("LidarSpread", 3, 2, "informarl")])
+def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, n, obs, algo):
     test_py, train_py = _entry("test"), _entry("train")
 
-    argv = ["train.py", "--env", eid, "-n", str(n), "--algo", "dgppo", "--obs", str(obs), "--steps", "2",
+    argv = ["train.py", "--env", eid, "-n", str(n), "--algo", algo, "--obs", str(obs), "--steps", "2",
             "--n-env-train", "8", "--batch-size", "256", "--n-env-test", "4", "--eval-interval", "1",
             "--save-interval", "2", "--log-dir", str(tmp_path)]
     monkeypatch.setattr(sys, "argv", argv)
     train_py.main()
-    runs = glob.glob(os.path.join(str(tmp_path), eid, "dgppo", "seed0_*"))
+    runs = glob.glob(os.path.join(str(tmp_path), eid, algo, "seed0_*"))
     assert len(runs) == 1
     run = runs[0]
     assert os.path.exists(os.path.join(run, "config.yaml"))
