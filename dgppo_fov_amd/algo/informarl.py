@@ -42,12 +42,30 @@ class InforMARL(DGPPO):
                 w *= 5
         return w
 
-    def update(self, rollout: Rollout, step: int) -> dict:
+    def _targets(self, rollout: Rollout, Vl: torch.Tensor, step: int):
+        """GAE on the cost-shaped loss with Vh = Vl broadcast, normalised advantages (informarl.py:324-340).
+        Returns Ql (B, T), A (B, T, n) and extra info entries."""
         env, dev = self._env, self.device
         B, T = rollout.rewards.shape
         n = self._n_agents
+        costs = rollout.costs.contiguous()
+        l = torch.empty((B, T), device=dev)
+        K.cost_shaped_loss(rollout.rewards.contiguous(), costs, self.cost_weight_at(step), l)
+        Vh = Vl[:, :, None, None].expand(B, T + 1, n, env.n_cost).contiguous()
+        Qh = torch.empty((B, T, n, env.n_cost), device=dev)
+        Ql = torch.empty((B, T), device=dev)
+        K.gae(costs, l, Vh, Vl, Qh, Ql, self.gamma, self.gae_lambda)
+        A = torch.empty((B, T, n), device=dev)
+        K.informarl_advantages(Ql, Vl, A)
+        if self.trace is not None:
+            self.trace.update(Vl=Vl.clone(), l=l.clone(), Ql=Ql.clone(), A=A.clone())
+        return Ql, A, {}
+
+    def update(self, rollout: Rollout, step: int) -> dict:
+        dev = self.device
+        B, T = rollout.rewards.shape
         chunk = max(1, min(B, 65536 // T))
-        info = {}
+        info, extra = {}, {}
         for _ in range(self.epoch_ppo):
             # Vl scan over the whole episode + final Vl (informarl.py:310-322)
             Vl = torch.empty((B, T + 1), device=dev)
@@ -59,18 +77,7 @@ class InforMARL(DGPPO):
                 vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
                                            keep_cache=False)
                 Vl[e0:e1, T].copy_(vf[:, 0])
-            # GAE on the cost-shaped loss with Vh = Vl broadcast, normalised advantages (informarl.py:324-340)
-            costs = rollout.costs.contiguous()
-            l = torch.empty((B, T), device=dev)
-            K.cost_shaped_loss(rollout.rewards.contiguous(), costs, self.cost_weight_at(step), l)
-            Vh = Vl[:, :, None, None].expand(B, T + 1, n, env.n_cost).contiguous()
-            Qh = torch.empty((B, T, n, env.n_cost), device=dev)
-            Ql = torch.empty((B, T), device=dev)
-            K.gae(costs, l, Vh, Vl, Qh, Ql, self.gamma, self.gae_lambda)
-            A = torch.empty((B, T, n), device=dev)
-            K.informarl_advantages(Ql, Vl, A)
-            if self.trace is not None:
-                self.trace.update(Vl=Vl.clone(), l=l.clone(), Ql=Ql.clone(), A=A.clone())
+            Ql, A, extra = self._targets(rollout, Vl, step)
             # minibatches (informarl.py:342-355)
             L = self.rnn_step
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
@@ -104,6 +111,7 @@ class InforMARL(DGPPO):
                     self.opt[name].step()
                 info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
                         "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
+        info.update(extra)
         out = self._finish_info(info)
         for k in ("Vh/grad_Vh_norm", "Vh/grad_Vh_has_nan"):
             out.pop(k, None)

@@ -267,3 +267,18 @@ def informarl_advantages(Ql, Vl, n_agents):
     Al = np.asarray(Ql, np.float64) - np.asarray(Vl, np.float64)[:, :-1]
     Al = (Al - Al.mean(axis=1, keepdims=True)) / (Al.std(axis=1, keepdims=True) + 1e-8)
     return -np.repeat(Al[:, :, None], n_agents, axis=-1)
+
+
+def merged_cbf_advantages(Ql, Vl, Vh, n_agents, dt, alpha, cbf_eps, cbf_weight):
+    """DGPPO's merged advantage (dgppo.py:239-259, identical in hcbfcrpo.py:163-183): Al = Ql - Vl[:, :T]
+    normalised over T; deriv = (Vh[t+1] - Vh[t]) / dt + alpha Vh[t]; Acbf = max(deriv + eps, 0);
+    A = -(where(all_h deriv <= 0, Al, 0) + max_h Acbf * w).  Returns (A (B, T, n), safe fraction)."""
+    Ql, Vl, Vh = (np.asarray(x, np.float64) for x in (Ql, Vl, Vh))
+    T = Ql.shape[1]
+    Al = Ql - Vl[:, :T]
+    Al = (Al - Al.mean(axis=1, keepdims=True)) / (Al.std(axis=1, keepdims=True) + 1e-8)
+    deriv = (Vh[:, 1:] - Vh[:, :T]) / dt + alpha * Vh[:, :T]
+    Acbf = np.maximum(deriv + cbf_eps, 0.0)
+    safe = (deriv <= 0).min(-1)
+    A = -(np.where(safe, np.repeat(Al[:, :, None], n_agents, -1), 0.0) + Acbf.max(-1) * cbf_weight)
+    return A, safe.mean(), deriv

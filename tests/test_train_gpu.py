@@ -24,7 +24,7 @@ def _entry(name):  # the repo-root scripts by path (`test` would also name the s
 
 
 @pytest.mark.parametrize("eid,n,obs,algo", [("LidarSpread", 3, 2, "dgppo"), ("LidarOmniTarget", 3, 2, "dgppo"),
-                                            ("LidarSpread", 3, 2, "informarl")])
+                                            ("LidarSpread", 3, 2, "informarl"), ("LidarSpread", 3, 2, "hcbfcrpo")])
 def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, n, obs, algo):
     test_py, train_py = _entry("test"), _entry("train")
 
