@@ -2,7 +2,8 @@
 
 Workload (BASELINE.json metric "env-steps/sec + PPO-updates/sec, LidarSpread n=8 x4096 envs"):
 LidarSpread, n=8 agents, 3 obstacles, 32 rays, 4096 parallel envs per GPU.  One bench "step" is
-one episode of the rollout hot path: env reset + T=128 fused env steps over all 4096 envs, with
+one episode of the rollout hot path: env reset + T=128 fused env steps over all 4096 envs (stepped as
+2 slices of 2048 envs on 2 HIP streams inside one hipGraph, DGPPO_BENCH_LANES), with
 synthetic random actions already resident in HBM, writing the full (B, T+1) graph rollout buffer
 (the reference's `collect` minus the policy).  `value` = env transitions per second over all
 ranks.  The "ppo" object times full DGPPO training iterations at the same config (policy rollout
@@ -177,7 +178,8 @@ def main():
     from dgppo_fov_amd.trainer.rollout import RolloutEngine
 
     env = make_env(ENV_ID, N_AGENTS, num_obs=N_OBS, device=dev)
-    eng = RolloutEngine(env, B_PER_GPU, T, dev, env_offset=rank * B_PER_GPU)
+    lanes = int(os.environ.get("DGPPO_BENCH_LANES", "2"))
+    eng = RolloutEngine(env, B_PER_GPU, T, dev, env_offset=rank * B_PER_GPU, lanes=lanes)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
     eng.actions.uniform_(-1.0, 1.0, generator=gen)  # synthetic actions, resident before timing
@@ -259,9 +261,11 @@ def main():
                 "workload": f"{ENV_ID} n={N_AGENTS} obs={N_OBS} rays=32 top_k=8, {B_PER_GPU} envs/GPU, "
                             f"1 step = reset + T={T} fused env steps into the (B,T+1) rollout buffer",
                 "env": ENV_ID, "num_agents": N_AGENTS, "n_obs": N_OBS, "n_env_per_gpu": B_PER_GPU, "T": T,
-                "hip_graph": use_graph, "parallelism": f"dp{world} (env-sharded, no collective)",
+                "hip_graph": use_graph, "stream_lanes": lanes, "parallelism": f"dp{world} (env-sharded, no collective)",
             },
             "env_step_kernel_us": round(step_ms * 1e3, 3),
+            # whole timed region (reset + T steps, 2 env slices on 2 streams) at the per-transition bytes
+            "rollout_effective_hbm_gbs": round(value / world * BYTES_PER_ENV_STEP / 1e9, 1),
             "ppo_updates_per_s": None if ppo is None else ppo["updates_per_s"],
             "ppo": ppo,
             "roofline": {

@@ -28,9 +28,12 @@ class RolloutEngine:
     MODE_RANDOM, MODE_SAMPLE, MODE_DET = -1, 1, 0
 
     def __init__(self, env: MultiAgentEnv, n_env: int, T: Optional[int] = None, device=None, env_offset: int = 0,
-                 actor=None, mode: int = -1):
+                 actor=None, mode: int = -1, lanes: int = 1):
         """actor: an ActorNet (or None); mode: MODE_SAMPLE (stochastic policy, sample_action),
-        MODE_DET (deterministic policy, get_action) or MODE_RANDOM (keep `self.actions` as given)."""
+        MODE_DET (deterministic policy, get_action) or MODE_RANDOM (keep `self.actions` as given).
+        lanes (MODE_RANDOM only): split the envs into that many contiguous slices, each stepped T
+        times on its own HIP stream after the shared reset, so one slice's launch ramp and store
+        drain overlap the other's compute (envs are independent: results are identical)."""
         self.env = env
         self.B = int(n_env)
         self.T = int(T or env.max_episode_steps)
@@ -52,6 +55,13 @@ class RolloutEngine:
             self.log_pis = torch.zeros((T, B, n), dtype=torch.float32, device=dev)
             self.noise = torch.empty((B * n, env.action_dim), dtype=torch.float32, device=dev)
         self._hip_graph = None
+        self.lanes = int(lanes)
+        if self.lanes > 1:
+            if self.mode != self.MODE_RANDOM:
+                raise ValueError("lanes > 1 is for env-only rollouts (MODE_RANDOM)")
+            if B % self.lanes:
+                raise ValueError(f"n_env {B} is not a multiple of lanes {self.lanes}")
+            self._streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]
 
     def graph_at(self, t: int) -> GraphsTuple:
         b = self.buf
@@ -80,7 +90,26 @@ class RolloutEngine:
         for t in range(self.T):
             if self.mode != self.MODE_RANDOM:
                 self._act(t)
-            cur = env.step_into(cur, self.actions[t], self.graph_at(t + 1), self.rewards[t], self.costs[t])
+            if self.lanes == 1:
+                cur = env.step_into(cur, self.actions[t], self.graph_at(t + 1), self.rewards[t], self.costs[t])
+        if self.lanes > 1:
+            self._run_lanes()
+
+    def _run_lanes(self):
+        env, b, main = self.env, self.buf, torch.cuda.current_stream(self.device)
+        w = self.B // self.lanes
+        for k, s in enumerate(self._streams):
+            sl = slice(k * w, (k + 1) * w)
+            obst = self.obstacles[sl] if self.obstacles is not None else None
+            at = lambda t: env._assemble(b.nodes[t][sl], b.edges[t][sl], b.states[t][sl],  # noqa: E731
+                                         b.receivers[t][sl], b.senders[t][sl], obst)
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                cur = at(0)
+                for t in range(self.T):
+                    cur = env.step_into(cur, self.actions[t][sl], at(t + 1), self.rewards[t][sl], self.costs[t][sl])
+        for s in self._streams:
+            main.wait_stream(s)
 
     def capture(self):
         """Record reset + T x (actor, step) into one hipGraph (after one eager warm-up run)."""

@@ -100,3 +100,28 @@ def test_rollout_shards_use_disjoint_noise(cuda):
         eng.run(5)
         acts.append(eng.actions.clone())
     assert not torch.equal(acts[0], acts[1])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_env_rollout_lanes_bit_exact(cuda, graph):
+    """Env-only rollout stepped as 2 env slices on 2 streams (RolloutEngine lanes=2) writes the same
+    (T+1, B) buffer, rewards and costs as the single-stream rollout, bit for bit."""
+    env = make_env("LidarSpread", 8, num_obs=3, device=cuda)
+    B, T = 256, 12
+    outs = []
+    for lanes in (1, 2):
+        eng = RolloutEngine(env, B, T, cuda, lanes=lanes)
+        gen = torch.Generator(device=cuda)
+        gen.manual_seed(5)
+        eng.actions.uniform_(-1.0, 1.0, generator=gen)
+        if graph:
+            eng.capture()
+        eng.run(key=3)
+        torch.cuda.synchronize(cuda)
+        b = eng.buf
+        outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders,
+                                              eng.rewards, eng.costs)])
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y)
+    with pytest.raises(ValueError):
+        RolloutEngine(env, 255, T, cuda, lanes=2)
