@@ -212,11 +212,18 @@ class DGPPO:
         a, lp, h2 = self.actor.act(g, rnn_state.reshape(B * n, 64).contiguous(), 1, noise=noise)
         return a.view(B, n, -1), lp.view(B, n), h2.view(B, 1, n, 1, 64)
 
+    def _rollout_lanes(self, n_env: int) -> int:
+        """Env slices on separate streams (RolloutEngine lanes): DGPPO_ROLLOUT_LANES when the slices are
+        whole (the engine itself keeps one stream where the fused policy step does not cover the env)."""
+        lanes = int(os.environ.get("DGPPO_ROLLOUT_LANES", "1"))
+        return 1 if lanes <= 1 or n_env % lanes or self.device.type != "cuda" else lanes
+
     def _engine(self, n_env: int, mode: int) -> RolloutEngine:
         k = (n_env, mode)
         if k not in self._engines:
             eng = RolloutEngine(self._env, n_env, self._env.max_episode_steps, self.device,
-                                env_offset=self.rank * n_env, actor=self.actor, mode=mode)
+                                env_offset=self.rank * n_env, actor=self.actor, mode=mode,
+                                lanes=self._rollout_lanes(n_env))
             if os.environ.get("DGPPO_NO_GRAPH", "0") != "1":
                 eng.capture()
             self._engines[k] = eng

@@ -15,8 +15,11 @@ from __future__ import annotations
 
 from typing import Optional
 
+import ctypes
+
 import torch
 
+from .. import _lib
 from ..env.base import MultiAgentEnv
 from ..nn import kernels as K
 from ..nn.layers import GraphBatch
@@ -31,9 +34,11 @@ class RolloutEngine:
                  actor=None, mode: int = -1, lanes: int = 1):
         """actor: an ActorNet (or None); mode: MODE_SAMPLE (stochastic policy, sample_action),
         MODE_DET (deterministic policy, get_action) or MODE_RANDOM (keep `self.actions` as given).
-        lanes (MODE_RANDOM only): split the envs into that many contiguous slices, each stepped T
-        times on its own HIP stream after the shared reset, so one slice's launch ramp and store
-        drain overlap the other's compute (envs are independent: results are identical)."""
+        lanes: split the envs into that many contiguous slices, each running its T (act, step) pairs
+        on its own HIP stream after the shared reset, so one slice's launch ramp and store drain
+        overlap the other's compute (envs are independent: results are identical).  With an actor
+        this needs the fused policy step (it reads only the prepared query-key workspace); the T
+        sampling-noise tensors are drawn up front with the same Philox stream ids."""
         self.env = env
         self.B = int(n_env)
         self.T = int(T or env.max_episode_steps)
@@ -57,20 +62,34 @@ class RolloutEngine:
         self._hip_graph = None
         self.lanes = int(lanes)
         if self.lanes > 1:
-            if self.mode != self.MODE_RANDOM:
-                raise ValueError("lanes > 1 is for env-only rollouts (MODE_RANDOM)")
             if B % self.lanes:
                 raise ValueError(f"n_env {B} is not a multiple of lanes {self.lanes}")
             self._streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]
+            if self.mode == self.MODE_SAMPLE:
+                self.noise_all = torch.empty((T, B * n, env.action_dim), dtype=torch.float32, device=dev)
 
     def graph_at(self, t: int) -> GraphsTuple:
         b = self.buf
         return self.env._assemble(b.nodes[t], b.edges[t], b.states[t], b.receivers[t], b.senders[t], self.obstacles)
 
-    def _act(self, t: int):
+    def _batch(self, t: int, sl=slice(None)) -> GraphBatch:
         env, b = self.env, self.buf
-        g = GraphBatch(b.nodes[t], b.edges[t], b.receivers[t], b.senders[t], env.num_agents,
-                       env.agent_candidates(self.device), raw_cols=env.nonagent_feature_cols)
+        return GraphBatch(b.nodes[t][sl], b.edges[t][sl], b.receivers[t][sl], b.senders[t][sl], env.num_agents,
+                          env.agent_candidates(self.device), raw_cols=env.nonagent_feature_cols)
+
+    def _act_slice(self, t: int, sl: slice, k: int):
+        n, A, w = self.env.num_agents, self.env.action_dim, sl.stop - sl.start
+        h = self.rnn[t][sl].view(w * n, 64)
+        kw = dict(action_out=self.actions[t][sl].view(-1, A), h_out=self.rnn[t + 1][sl].view(w * n, 64), prepare=False)
+        if self.mode == self.MODE_SAMPLE:
+            self.actor.act(self._batch(t, sl), h, 1, noise=self.noise_all[t][k * w * n:(k + 1) * w * n],
+                           log_pi_out=self.log_pis[t][sl].view(-1), **kw)
+        else:
+            self.actor.act(self._batch(t, sl), h, 0, **kw)
+
+    def _act(self, t: int):
+        env = self.env
+        g = self._batch(t)
         n = env.num_agents
         h = self.rnn[t].view(self.B * n, 64)
         if self.mode == self.MODE_SAMPLE:
@@ -87,17 +106,26 @@ class RolloutEngine:
         env = self.env
         cur = env.reset(self.key, n_env=self.B, env_offset=self.env_offset, out=self.graph_at(0),
                         obstacles_out=self.obstacles)
+        if self.lanes > 1 and self._run_lanes():
+            return
         for t in range(self.T):
             if self.mode != self.MODE_RANDOM:
                 self._act(t)
-            if self.lanes == 1:
-                cur = env.step_into(cur, self.actions[t], self.graph_at(t + 1), self.rewards[t], self.costs[t])
-        if self.lanes > 1:
-            self._run_lanes()
+            cur = env.step_into(cur, self.actions[t], self.graph_at(t + 1), self.rewards[t], self.costs[t])
 
     def _run_lanes(self):
         env, b, main = self.env, self.buf, torch.cuda.current_stream(self.device)
         w = self.B // self.lanes
+        if self.actor is not None:
+            fa = self.actor._fused_args(self._batch(0))
+            if fa is None:  # the unfused actor path shares GEMM workspaces: one stream only
+                self.lanes = 1
+                return False
+            K._chk(_lib.load().dgppo_policy_prepare(ctypes.byref(fa), _lib.stream_handle(self.device)),
+                   "dgppo_policy_prepare")
+            if self.mode == self.MODE_SAMPLE:
+                for t in range(self.T):
+                    K.normal_(self.noise_all[t], stream_id=(self.env_offset << 32) | t, seed_tensor=self.key)
         for k, s in enumerate(self._streams):
             sl = slice(k * w, (k + 1) * w)
             obst = self.obstacles[sl] if self.obstacles is not None else None
@@ -107,9 +135,12 @@ class RolloutEngine:
             with torch.cuda.stream(s):
                 cur = at(0)
                 for t in range(self.T):
+                    if self.actor is not None:
+                        self._act_slice(t, sl, k)
                     cur = env.step_into(cur, self.actions[t][sl], at(t + 1), self.rewards[t][sl], self.costs[t][sl])
         for s in self._streams:
             main.wait_stream(s)
+        return True
 
     def capture(self):
         """Record reset + T x (actor, step) into one hipGraph (after one eager warm-up run)."""

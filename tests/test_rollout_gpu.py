@@ -125,3 +125,25 @@ def test_env_rollout_lanes_bit_exact(cuda, graph):
         assert np.array_equal(x, y)
     with pytest.raises(ValueError):
         RolloutEngine(env, 255, T, cuda, lanes=2)
+
+
+@pytest.mark.parametrize("env_id", ["LidarSpread", "LidarOmniTarget"])
+def test_policy_rollout_lanes_bit_exact(cuda, env_id):
+    """Policy rollouts (sample and det) stepped as 2 env slices on 2 streams write the same actions,
+    log_pi, carries and graphs as one stream, bit for bit (LidarOmniTarget: no fused policy step,
+    the engine keeps one stream)."""
+    env = make_env(env_id, 8, num_obs=3, device=cuda)
+    B, T = 64, 6
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=8, batch_size=B * T, rnn_step=3, seed=4, device=cuda)
+    for mode in (RolloutEngine.MODE_SAMPLE, RolloutEngine.MODE_DET):
+        outs = []
+        for lanes in (1, 2):
+            eng = RolloutEngine(env, B, T, cuda, env_offset=0, actor=algo.actor, mode=mode, lanes=lanes)
+            eng.capture()
+            eng.run(key=11)
+            torch.cuda.synchronize(cuda)
+            outs.append([x.cpu().numpy() for x in (eng.buf.states, eng.buf.edges, eng.actions, eng.log_pis,
+                                                  eng.rnn, eng.rewards, eng.costs)])
+        for x, y in zip(*outs):
+            assert np.array_equal(x, y)
