@@ -249,14 +249,14 @@ SIGNATURES = {
     "dgppo_gae": (ctypes.c_int, [ctypes.POINTER(GaeArgs), ctypes.c_void_p]),
     "dgppo_dgppo_advantages": (ctypes.c_int, [ctypes.POINTER(AdvArgs), ctypes.c_void_p]),
     "dgppo_grad_norm": (ctypes.c_int, [_V, _I64, _V, _V, _V]),
-    "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, _F32, _F32, _F32, _F32, _V]),
+    "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, ctypes.c_double, ctypes.c_double, _F32, _F32, _V]),
     "dgppo_normal": (ctypes.c_int, [_V, _I64, _V, ctypes.c_uint64, ctypes.c_uint64, _V]),
 }
 
 _LIB = None
 
 
-ABI_VERSION = 2  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 3  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

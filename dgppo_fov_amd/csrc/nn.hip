@@ -648,8 +648,8 @@ __global__ __launch_bounds__(64) void norm_final_kernel(const float* part, int n
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(float* param, const float* grad, float* m, float* v, int64_t n,
-                                                   const float* state, float lr, float b1, float b2, float eps,
-                                                   float max_norm) {
+                                                   const float* state, float lr, float b1, float omb1, float b2,
+                                                   float omb2, float eps, float max_norm) {
   if (state[1] != 0.0f) return;  // apply_if_finite: skip the whole update
   const float gnorm = state[0];
   const float c = fmaxf(max_norm, gnorm);
@@ -658,8 +658,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* param, const float* gr
   const float bc2 = 1.0f - powf(b2, t);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float g = (grad[i] / c) * max_norm;
-    const float mi = b1 * m[i] + (1.0f - b1) * g;
-    const float vi = b2 * v[i] + (1.0f - b2) * g * g;
+    const float mi = b1 * m[i] + omb1 * g;  // optax: (1 - decay) folded in double, then rounded (weak type)
+    const float vi = b2 * v[i] + omb2 * (g * g);
     m[i] = mi;
     v[i] = vi;
     param[i] = param[i] - lr * ((mi / bc1) / (sqrtf(vi / bc2) + eps));
@@ -982,10 +982,10 @@ extern "C" int dgppo_grad_norm(const float* grad, int64_t n, float* state, float
 }
 
 extern "C" int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr,
-                          float b1, float b2, float eps, float max_norm, void* stream) {
+                          double b1, double b2, float eps, float max_norm, void* stream) {
   if (n < 0 || !param || !grad || !m || !v || !state) return DGPPO_EINVAL;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), param, grad, m, v, n, state, lr,
-                     b1, b2, eps, max_norm);
+                     (float)b1, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, max_norm);
   hipLaunchKernelGGL(adam_count_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), state);
   return (int)hipGetLastError();
 }

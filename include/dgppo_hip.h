@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 2  /* 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 3  /* 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -413,8 +413,10 @@ int dgppo_cost_shaped_loss(const float* rewards, const float* costs, float cost_
 int dgppo_informarl_advantages(const float* Ql, const float* Vl, float* A, int32_t B, int32_t T, int32_t n_agents,
                                void* stream);
 int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace, void* stream);
-int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, float b1,
-               float b2, float eps, float max_norm, void* stream);
+/* b1 / b2 are doubles: (1 - b) is formed in double and rounded once, as optax's weakly typed
+ * `(1 - decay) * g` does (ABI 3) */
+int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, double b1,
+               double b2, float eps, float max_norm, void* stream);
 
 /* standard normal noise from Philox4x32-10 (Box-Muller); seed from *seed_ptr when non-NULL */
 int dgppo_normal(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed, uint64_t stream_id, void* stream);

@@ -74,19 +74,22 @@ def graph_transformer(p, nodes, edges, recv, send, n_heads, out_dim):
 
 
 def gnn(layers, graph, n_agents, out_dim=64, msg_dim=32, n_heads=3):
-    outs = []
-    L = len(layers)
+    """GraphTransformerGNN + type_nodes(agent) over a batch of G graphs, evaluated as ONE disjoint
+    union graph (node ids offset by g * N): segment softmax / segment sum never cross graphs, so this
+    is the per-graph computation of gnn.py:133-142 vmapped, as XLA runs it."""
     nodes = torch.as_tensor(graph["nodes"], dtype=T64)
     edges = torch.as_tensor(graph["edges"], dtype=T64)
-    recv = torch.as_tensor(graph["receivers"]).long()
-    send = torch.as_tensor(graph["senders"]).long()
-    for g in range(nodes.shape[0]):
-        x = nodes[g]
-        for i in range(L):
-            od = out_dim if i == L - 1 else msg_dim
-            x = graph_transformer(layers[i], x, edges[g], recv[g], send[g], n_heads, od)
-        outs.append(x[:n_agents])
-    return torch.stack(outs)
+    G, N = nodes.shape[:2]
+    off = (torch.arange(G, dtype=torch.long) * N)[:, None]
+    recv = (torch.as_tensor(graph["receivers"]).long() + off).reshape(-1)
+    send = (torch.as_tensor(graph["senders"]).long() + off).reshape(-1)
+    x = nodes.reshape(G * N, -1)
+    e = edges.reshape(-1, edges.shape[-1])
+    L = len(layers)
+    for i in range(L):
+        od = out_dim if i == L - 1 else msg_dim
+        x = graph_transformer(layers[i], x, e, recv, send, n_heads, od)
+    return x.reshape(G, N, -1)[:, :n_agents]
 
 
 STD_INIT_INV = math.log(math.exp(0.5) - 1.0)

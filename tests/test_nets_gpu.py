@@ -130,7 +130,8 @@ def _graphs(cuda, eid, n, obs, S, L, seed=0):
     return env, gb, host
 
 
-CASES = [("LidarSpread", 8, 3), ("MPETarget", 3, 0), ("MPESpread", 3, 3), ("LidarBicycleTarget", 4, 2)]
+CASES = [("LidarSpread", 8, 3), ("MPETarget", 3, 0), ("MPESpread", 3, 3), ("LidarBicycleTarget", 4, 2),
+         ("LidarBicycleTarget", 8, 3)]  # BASELINE's bicycle config at its own n = 8, obs = 3
 # 10-wide nodes and edges, 3-d actions: edge columns 4.. through edge_wsum / edge_da, agent-mode raw columns
 OMNI = [("LidarOmniTarget", 3, 2), ("LidarOmniTarget", 8, 3)]
 # BASELINE's dense-graph config: 72 candidate edges per agent (past the row-block kernels' 32)
@@ -172,7 +173,7 @@ def test_actor_eval_seq_fwd_bwd(cuda, eid, n, obs):
         _grad_close(a, b, "actor grad " + path)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES[:2] + OMNI[:1])
+@pytest.mark.parametrize("eid,n,obs", CASES[:2] + CASES[4:] + OMNI[:1])
 def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
     S, L = 3, 5
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=4)
@@ -194,7 +195,7 @@ def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
         _grad_close(a, b, "Vl grad " + path)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES[:3] + OMNI[:1] + DENSE)
+@pytest.mark.parametrize("eid,n,obs", CASES[:3] + CASES[4:] + OMNI[:1] + DENSE)
 def test_vh_fwd_bwd(cuda, eid, n, obs):
     S, L = 2, 3
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=6)
@@ -236,6 +237,13 @@ def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
     p = R.to_t(net.flax())
     h2_ref = R.actor_carry(p, host, h.cpu().double().reshape(S * L, n, 64), n)
     mu, sd = R.policy_dist(p, h2_ref)
+    try:  # the same oracle in float32: the noise floor of an fp32 evaluation (module docstring)
+        R.T64 = torch.float32
+        p32 = R.to_t(net.flax())
+        h2_32 = R.actor_carry(p32, host, h.cpu().float().reshape(S * L, n, 64), n)
+        mu32, sd32 = R.policy_dist(p32, h2_32)
+    finally:
+        R.T64 = torch.float64
     for mode in (0, 1):
         a, lp, h2 = net.act(gb, h, mode, noise=noise if mode else None)
         torch.cuda.synchronize()
@@ -243,5 +251,37 @@ def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
         pre = mu + sd * noise.cpu().double().reshape(S * L, n, A) if mode else mu
         a_ref = torch.tanh(pre)
         _close(a.cpu().numpy(), a_ref.numpy().reshape(rows, A), what=f"action mode {mode}")
-        lp_ref = R.tanh_normal_log_prob(a.cpu().double().reshape(S * L, n, A), mu, sd)
-        _close(lp.cpu().numpy(), lp_ref.numpy().reshape(rows), rtol=3e-5, atol=3e-5, what=f"log_pi mode {mode}")
+        a_host = a.cpu().double().reshape(S * L, n, A)
+        lp_ref = R.tanh_normal_log_prob(a_host, mu, sd).numpy().reshape(rows)
+        lp_32 = R.tanh_normal_log_prob(a_host.float(), mu32.double(), sd32.double()).numpy().reshape(rows)
+        # log pi of the GPU's own fp32 action: 1e-5 (1 + |ref|) plus 8x the float32-oracle floor (the
+        # atanh / log(1 - a^2) terms amplify the mean / std rounding near |a| -> 1)
+        err = np.abs(lp.cpu().numpy() - lp_ref)
+        floor = np.abs(lp_32 - lp_ref)
+        assert (err - 1e-5 * (1 + np.abs(lp_ref)) - 8 * floor).max() <= 0, \
+            f"log_pi mode {mode}: max abs err {err.max():.3e}, fp32 floor {floor.max():.3e}"
+
+
+# ---- known-answer test on the attention kernels ----------------------------------
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("MPESpread", 3, 3), ("LidarSpread", 32, 8)])
+def test_attention_uniform_logits_give_inverse_in_degree(cuda, eid, n, obs):
+    """Wq = 0, bq = 0 makes every logit q.k/sqrt(F) zero, so jraph.segment_softmax gives each of a
+    receiver's in-edges weight exactly 1 / in-degree (masked candidates 0), in both layers (the
+    first reads raw sender rows, the second is the agent-mode kernel)."""
+    S, L = 2, 3
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=9)
+    net = ActorNet(env.node_dim, n, cuda, seed=1, action_dim=env.action_dim, **_nets_kw(env))
+    for layer in net.gnn.layers:
+        layer.v("Wq").zero_()
+        layer.v("bq").zero_()
+    _, caches = net.gnn.fwd(gb)
+    torch.cuda.synchronize()
+    recv = host["receivers"]
+    deg = np.stack([(recv == i).sum(1) for i in range(n)], 1).reshape(-1)  # (G*n,) in-degree of agent rows
+    valid = gb.sidx.cpu().numpy() >= 0  # (G*n, C)
+    assert (valid.sum(1) == deg).all()
+    for li, c in enumerate(caches):
+        attn = c[4].cpu().numpy()  # (G*n, H, C)
+        want = np.where(valid[:, None, :], 1.0 / np.maximum(deg, 1)[:, None, None], 0.0)
+        want = np.broadcast_to(want, attn.shape)
+        np.testing.assert_allclose(attn, want, rtol=2e-7, atol=0, err_msg=f"layer {li}")
