@@ -13,7 +13,11 @@ weak scaling.
 roofline: the dominant kernel is the env-step kernel (HBM-bound).  Algorithmic bytes per env
 transition = 8,856 B; per launch = 8,856 * 4096.  Its average duration is measured
 live with HIP events around back-to-back step launches on the launch stream.
-cpu_baseline: the NumPy oracle (oracle/env.py, single thread) on a bounded sample.
+cpu_baseline: the NumPy oracle (oracle/env.py) on the host cores (one process per core), warm-up 3 and
+median of 10; cpu_baseline_update: the torch-CPU fp32 network oracle (oracle/nets_t.py) on a sample of the
+update's minibatch work, scaled to one update (both run before the GPU is touched).
+GPU timing: `value` = env transitions / wall time of exactly K steps between barriers; the per-step
+median from HIP events is reported beside it (warm-up 10, median of 50 = the defaults).
 """
 import argparse
 import json
@@ -34,27 +38,146 @@ BYTES_PER_ENV_STEP = 8856  # SURVEY.md §8(d), LidarSpread n8 O3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def cpu_baseline(budget_s=12.0):
-    """NumPy oracle (1 thread, vectorised over envs) on a bounded sample of the same workload."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_workers() -> int:
+    """Host cores to use: the process's CPU share (16 on the GPU box, whose nproc shows the whole
+    machine; OMP_NUM_THREADS is set to that share there), else the affinity mask."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(share, aff) if share > 0 else aff)
+
+
+CPU_STEPS_PER_ITER, CPU_WARMUP, CPU_ITERS = 16, 3, 10  # BASELINE.md: warm-up 3, median of 10
+
+
+def _cpu_env_worker(args):
+    """One shard of the CPU env baseline (forked before any GPU use): NumPy oracle env steps over its
+    envs, CPU_WARMUP untimed + CPU_ITERS timed iterations of CPU_STEPS_PER_ITER steps."""
+    w, n_env = args
+    os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import env as O
 
     spec = O.Spec(ENV_ID, N_AGENTS, N_OBS)
-    Bs = 1024
-    ag, gl, third = O.env_reset(spec, 1, Bs)
+    ag, gl, third = O.env_reset(spec, 1, n_env, env_offset=w * n_env)
+    states = O.initial_graph(spec, ag, gl, third)["states"]
+    rng = np.random.default_rng(1000 + w)
+    times = []
+    for it in range(CPU_WARMUP + CPU_ITERS):
+        acts = rng.uniform(-1, 1, (CPU_STEPS_PER_ITER, n_env, N_AGENTS, 2)).astype(np.float32)
+        t0 = time.perf_counter()
+        for k in range(CPU_STEPS_PER_ITER):
+            states = O.env_step(spec, states, third, acts[k])["states"]
+        if it >= CPU_WARMUP:
+            times.append(time.perf_counter() - t0)
+    return times
+
+
+def cpu_baseline():
+    """The NumPy oracle (oracle/env.py, the reference's env step restated, fp32, vectorised over envs)
+    on the host cores: the bench's 4096 LidarSpread n=8 envs sharded over one forked process per core
+    (all host cores, warm-up 3, median of 10).  Runs BEFORE the process touches the GPU."""
+    import multiprocessing as mp
+
+    P = _cpu_workers()
+    B = 4096 if P >= 8 else 1024  # the bench width on the GPU box's 16-core share
+    per = [B // P + (1 if w < B % P else 0) for w in range(P)]
+    with mp.get_context("fork").Pool(P) as pool:
+        res = pool.map(_cpu_env_worker, list(enumerate(per)))
+    # throughput = sum over shards of envs x steps / that shard's median iteration time
+    value = sum(nw * CPU_STEPS_PER_ITER / float(np.median(ts)) for nw, ts in zip(per, res))
+    tot = sum(sum(ts) for ts in res) / P
+    return {"value": round(value, 1), "unit": "env-steps/s", "cores": P, "kind": "port", "cpu": _cpu_model(),
+            "sample": f"oracle/env.py NumPy fp32, {B} LidarSpread n=8 o=3 envs sharded over {P} processes "
+                      f"(1 thread each); per shard {CPU_WARMUP} warm-up + median of {CPU_ITERS} iterations of "
+                      f"{CPU_STEPS_PER_ITER} env steps ({tot:.1f} s timed per process, reset excluded)"}
+
+
+def cpu_baseline_update():
+    """torch-CPU fp32 of the DGPPO update's minibatch work (oracle/nets_t.py: the reference's per-edge
+    GraphTransformer, MLP, GRU, TanhNormal restated, every graph of the batch evaluated as one disjoint
+    union graph as vmap does): update_Vl + update_Vh + update_policy forward + backward on a bounded
+    sample of SAMPLE_ENVS envs x T steps, torch.set_num_threads(host cores), warm-up 3, median of 10.
+    Scaled to one update = 32 minibatches x (16,384 / sample graphs) x t_sample; the prepass (Vl / Vh
+    over the rollouts) and the deterministic rollout are NOT counted, so the CPU figure is optimistic."""
+    import torch as th
+
+    from oracle import env as O
+    from oracle import nets_t as R
+
+    P = _cpu_workers()
+    th.set_num_threads(P)
+    SAMPLE_ENVS, L = 2, RNN_STEP
+    spec = O.Spec(ENV_ID, N_AGENTS, N_OBS)
+    ag, gl, third = O.env_reset(spec, 3, SAMPLE_ENVS)
     g = O.initial_graph(spec, ag, gl, third)
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(2)
+    seq = {k: [] for k in ("nodes", "edges", "receivers", "senders")}
     states = g["states"]
-    n_steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and n_steps < T:
-        a = rng.uniform(-1, 1, (Bs, N_AGENTS, 2)).astype(np.float32)
-        out = O.env_step(spec, states, third, a)
-        states = out["states"]
-        n_steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(Bs * n_steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/env.py NumPy fp32, {Bs} envs x {n_steps} LidarSpread n=8 steps "
-                      f"({dt:.1f} s, reset excluded), 1 thread"}
+    for t in range(T):
+        for k in seq:
+            seq[k].append(g[k])
+        g = O.env_step(spec, states, third, rng.uniform(-1, 1, (SAMPLE_ENVS, N_AGENTS, 2)).astype(np.float32))
+        states = g["states"]
+    graph = {k: np.stack(v, 1).reshape((SAMPLE_ENVS * T,) + v[0].shape[1:]) for k, v in seq.items()}
+    G = SAMPLE_ENVS * T
+    S = G // L
+    n = N_AGENTS
+    R.T64 = th.float32
+    try:
+        trees = _random_flax_trees(spec)
+        acts = rng.uniform(-0.99, 0.99, (G * n, 2)).astype(np.float32)
+        eps = rng.standard_normal((n, 2)).astype(np.float32)
+        h_act = (rng.standard_normal((G, n, 64)) * 0.3).astype(np.float32)
+        tgt_l = th.tensor(rng.standard_normal((S, L)), dtype=th.float32)
+        tgt_h = th.tensor(rng.standard_normal((G, n, 2)), dtype=th.float32)
+        adv = rng.standard_normal((S, L, n)).astype(np.float32)
+        lp_old = rng.standard_normal((S, L, n)).astype(np.float32) - 2.0
+
+        def one():
+            pa, pl, ph = (R.to_t(x, requires_grad=True) for x in trees)
+            v = R.vl_seq(pl, graph, S, L, n)
+            (0.5 * (v - tgt_l) ** 2).mean().backward()
+            out = R.vh(ph, graph, h_act, n)
+            (0.5 * (out - tgt_h) ** 2).mean().backward()
+            lp, ent = R.actor_eval_seq(pa, graph, S, L, n, acts, eps)
+            R.ppo_loss(lp, lp_old, adv, ent).backward()
+
+        times = []
+        for it in range(CPU_WARMUP + CPU_ITERS):
+            t0 = time.perf_counter()
+            one()
+            if it >= CPU_WARMUP:
+                times.append(time.perf_counter() - t0)
+    finally:
+        R.T64 = th.float64
+    t_sample = float(np.median(times))
+    t_update = t_sample * (PPO_BATCH / G) * (B_PER_GPU * T // PPO_BATCH)
+    return {"value": round(1.0 / t_update, 6), "unit": "PPO-updates/s", "cores": P, "kind": "port",
+            "cpu": _cpu_model(), "sample_ms": round(t_sample * 1e3, 2),
+            "sample": f"oracle/nets_t.py torch-CPU fp32 ({P} threads): Vl + Vh + policy forward+backward on "
+                      f"{SAMPLE_ENVS} envs x T={T} LidarSpread n=8 graphs ({S} rnn_step-{L} chunks), warm-up "
+                      f"{CPU_WARMUP}, median of {CPU_ITERS} = {t_sample * 1e3:.1f} ms; scaled x{PPO_BATCH // G} "
+                      f"to a 16,384-graph minibatch and x{B_PER_GPU * T // PPO_BATCH} minibatches per update "
+                      f"(prepass and deterministic rollout not counted)"}
+
+
+def _random_flax_trees(spec):
+    """Random-init actor / Vl / Vh parameter trees in the reference's flax layout (built on the host)."""
+    from dgppo_fov_amd.algo.module.nets import ActorNet, VhNet, VlNet
+
+    nd = spec.nd  # node features: state + 3 indicator columns (lidar_env/base.py:227-271)
+    return [ActorNet(nd, N_AGENTS, "cpu", seed=6).flax(), VlNet(nd, N_AGENTS, "cpu", seed=7).flax(),
+            VhNet(nd, N_AGENTS, 2, "cpu", seed=8).flax()]
 
 
 def read_pmc_traffic():
@@ -112,7 +235,7 @@ def ppo_bench(env, dev, world, rank, iters):
     algo.update(r, 0)
     gemm_flops = sum(2.0 * M * N * Kd * b for (M, N, Kd, b, *_rest) in K.GEMM_LOG)
     K.GEMM_LOG = None
-    t_col = t_upd = 0.0
+    cols, upds = [], []
     for it in range(iters):
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -126,15 +249,17 @@ def ppo_bench(env, dev, world, rank, iters):
         if world > 1:
             dist.barrier()
         t2 = time.perf_counter()
-        t_col += t1 - t0
-        t_upd += t2 - t1
-    t = torch.tensor([t_col, t_upd], device=dev, dtype=torch.float64)
+        cols.append(t1 - t0)
+        upds.append(t2 - t1)
+    t = torch.tensor([cols, upds], device=dev, dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_col, t_upd = (float(x) / iters for x in t.tolist())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # per iteration, the slowest rank
+    t_col, t_upd = (float(x) for x in t.median(dim=1).values.tolist())
+    t_upd_mean = float(t[1].mean())
     upd_tf = UPDATE_TFLOP_PER_4096_ENVS * (B_PER_GPU / 4096) * world + ROLLOUT_TFLOP_PER_4096_ENVS / 2 * (
         B_PER_GPU / 4096) * world  # the update runs the deterministic rollout too
     return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),
+            "update_ms_mean": round(t_upd_mean * 1e3, 2), "timing": f"median of {iters} iterations after 2 warm-up updates",
             "update_roofline": {"bound": "mfma", "algorithmic_tflop": round(upd_tf, 2),
                                 "achieved": round(upd_tf / t_upd, 2), "peak": FP32_MFMA_PEAK_TFLOPS * world,
                                 "unit": "TFLOP/s", "frac": round(upd_tf / t_upd / (FP32_MFMA_PEAK_TFLOPS * world), 4),
@@ -151,15 +276,21 @@ def ppo_bench(env, dev, world, rank, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)  # warm-up 10, median of 50
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--ppo-iters", type=int, default=3, help="timed DGPPO collect+update iterations (0: skip)")
+    ap.add_argument("--ppo-iters", type=int, default=10, help="timed DGPPO collect+update iterations (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # CPU baselines first: forked workers must never inherit an initialised GPU context
+    cpu_env = cpu_upd = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_env = cpu_baseline()
+        cpu_upd = cpu_baseline_update() if args.ppo_iters > 0 else None
+
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     local = local % ndev if ndev > 0 else local  # identity on a full node; wraps for one-GPU rehearsals
@@ -191,10 +322,14 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    stream = torch.cuda.current_stream(dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
+        evs[s].record(stream)
         eng.run(key=10_000 + s)
+    evs[-1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -204,9 +339,9 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    step_ms_median = float(np.median([evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]))
 
     # ---- live kernel timing for the roofline: back-to-back step launches on the launch stream ----
-    stream = torch.cuda.current_stream(dev)
     n_launch = 4 * T
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     g_step = None
@@ -225,7 +360,7 @@ def main():
         with torch.cuda.graph(g_step):
             step_loop()
     kern_ms = []
-    for rep in range(3):
+    for rep in range(5):
         ev0.record(stream)
         if g_step is not None:
             g_step.replay()
@@ -252,6 +387,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step_median": round(step_ms_median, 4),  # HIP events around each step, rank 0
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -278,7 +414,8 @@ def main():
                 "kernel": "wv::lidar_step_wave_kernel<LIDAR,SPREAD,4,3,false>",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
-            "cpu_baseline": None if args.no_cpu_baseline or world > 1 else cpu_baseline(),
+            "cpu_baseline": cpu_env,
+            "cpu_baseline_update": cpu_upd,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -230,13 +230,19 @@ class DGPPO:
         return self._engines[k]
 
     def collect(self, params, key, n_env: Optional[int] = None) -> Rollout:
-        """jit(vmap(rollout_fn))(params, keys): `key` is an int seed (or a sequence whose length is n_env)."""
+        """jit(vmap(rollout_fn))(params, keys): `key` is an int seed (or a sequence whose length is n_env).
+
+        The returned Rollout is a set of VIEWS into the buffers of a RolloutEngine cached per n_env:
+        the next collect() with the same n_env overwrites it in place (the reference returns fresh
+        arrays).  Clone the fields to keep a rollout across collects."""
+        assert params is None or params is self.params
         if n_env is None:
             n_env = len(key) if hasattr(key, "__len__") else 128
         seed = int(np.asarray(key).reshape(-1)[0]) if hasattr(key, "__len__") else int(key)
         return self._engine(n_env, RolloutEngine.MODE_SAMPLE).run(seed)
 
     def det_rollout(self, n_env: int, key: int) -> Rollout:
+        """test_rollout with the deterministic policy; the same aliasing as collect() applies."""
         return self._engine(n_env, RolloutEngine.MODE_DET).run(key)
 
     # ---- update ------------------------------------------------------------------------------

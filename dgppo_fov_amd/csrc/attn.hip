@@ -19,6 +19,8 @@
 // Sender gradients accumulate in an LDS image of the block's graphs in fixed receiver order, and
 // every reduction has a fixed order: bitwise-deterministic, no atomics.
 #include <hip/hip_runtime.h>
+
+#include "lds_attr.h"
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1550,13 +1552,7 @@ void bwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
                        sizeof(float);
   const void* fn = v == 0 ? (const void*)attn_bwd2_kernel<8>
                           : (v == 1 ? (const void*)attn_bwd2_kernel<16> : (const void*)attn_bwd2_kernel<32>);
-  if (bytes > 64 * 1024) {
-    static bool raised[3] = {false, false, false};
-    if (!raised[v]) {
-      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised[v] = true;
-    }
-  }
+  if (bytes > 64 * 1024) allow_lds(fn);
   if (v == 0) hipLaunchKernelGGL(attn_bwd2_kernel<8>, dim3(grid), dim3(256), bytes, s, *p, nblk);
   else if (v == 1) hipLaunchKernelGGL(attn_bwd2_kernel<16>, dim3(grid), dim3(256), bytes, s, *p, nblk);
   else hipLaunchKernelGGL(attn_bwd2_kernel<32>, dim3(grid), dim3(256), bytes, s, *p, nblk);
@@ -1629,25 +1625,12 @@ Plan make_plan(const dgppo_gnn_attn_args* p, bool bwd) {
 
 template <int CP, int DM>
 void launch_t(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream_t s) {
-  if (pl.bytes > 64 * 1024) {  // once per instantiation: allow up to the CU's 160 KB
-    static bool raised[2] = {false, false};
-    if (!raised[bwd]) {
-      (void)hipFuncSetAttribute(bwd ? (const void*)attn_bwd_kernel<CP, DM> : (const void*)attn_fwd_kernel<CP, DM>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised[bwd] = true;
-    }
-  }
+  if (pl.bytes > 64 * 1024)  // allow up to the CU's 160 KB
+    allow_lds(bwd ? (const void*)attn_bwd_kernel<CP, DM> : (const void*)attn_fwd_kernel<CP, DM>);
   if (pl.wave) {
     if constexpr (CP <= 64) {
-      if (pl.bytes > 64 * 1024) {
-        static bool raised_w[2] = {false, false};
-        if (!raised_w[bwd]) {
-          (void)hipFuncSetAttribute(
-              bwd ? (const void*)attn_bwd_wave_kernel<CP, DM> : (const void*)attn_fwd_wave_kernel<CP, DM>,
-              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          raised_w[bwd] = true;
-        }
-      }
+      if (pl.bytes > 64 * 1024)
+        allow_lds(bwd ? (const void*)attn_bwd_wave_kernel<CP, DM> : (const void*)attn_fwd_wave_kernel<CP, DM>);
       if (bwd)
         hipLaunchKernelGGL((attn_bwd_wave_kernel<CP, DM>), dim3((unsigned)pl.grid), dim3(256), pl.bytes, s, *p,
                            pl.gpb, pl.nblk, pl.wfloats);
@@ -1965,14 +1948,7 @@ bool gbwd_ok(const dgppo_gnn_attn_args* p) {
 
 void gbwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const size_t bytes = gbwd_lds_floats(p) * sizeof(float);
-  if (bytes > 64 * 1024) {
-    static bool raised = false;
-    if (!raised) {
-      (void)hipFuncSetAttribute((const void*)attn_bwd_graph_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      raised = true;
-    }
-  }
+  if (bytes > 64 * 1024) allow_lds((const void*)attn_bwd_graph_kernel<8>);
   hipLaunchKernelGGL(attn_bwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
 }
 
@@ -1994,14 +1970,7 @@ void gfwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const bool d8 = p->D <= 8;
   const size_t bytes = (d8 ? gfwd::lds_floats<8>(p->N, p->n_agents) : gfwd::lds_floats<32>(p->N, p->n_agents)) *
                        sizeof(float);
-  if (bytes > 64 * 1024) {
-    static bool raised[2] = {false, false};
-    if (!raised[d8]) {
-      (void)hipFuncSetAttribute(d8 ? (const void*)attn_fwd_graph_kernel<8> : (const void*)attn_fwd_graph_kernel<32>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised[d8] = true;
-    }
-  }
+  if (bytes > 64 * 1024) allow_lds(d8 ? (const void*)attn_fwd_graph_kernel<8> : (const void*)attn_fwd_graph_kernel<32>);
   if (d8) hipLaunchKernelGGL(attn_fwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
   else hipLaunchKernelGGL(attn_fwd_graph_kernel<32>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
 }

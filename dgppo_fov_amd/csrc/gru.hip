@@ -16,6 +16,8 @@
 // gradient (column sum of dn*r) is reduced per workgroup in fixed order.  Every global load of a
 // step is issued before the step's stores (no load-after-store serialisation).
 #include <hip/hip_runtime.h>
+
+#include "lds_attr.h"
 #include <stdint.h>
 
 #include "../../include/dgppo_hip.h"
@@ -268,12 +270,7 @@ extern "C" int dgppo_gru_seq_fwd(const dgppo_gru_seq_args* p, void* stream) {
       (p->Q % p->n_agents) != 0)
     return DGPPO_EINVAL;
   if (p->Q == 0) return 0;
-  static bool raised = false;
-  if (!raised) {
-    (void)hipFuncSetAttribute((const void*)dgppo::gru_seq_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    raised = true;
-  }
+  dgppo::allow_lds((const void*)dgppo::gru_seq_fwd_kernel);
   hipLaunchKernelGGL(dgppo::gru_seq_fwd_kernel, dim3((unsigned)dgppo_gru_seq_blocks(p->Q)), dim3(dgppo::kThreads),
                      dgppo::fwd_lds(), (hipStream_t)stream, *p);
   return (int)hipGetLastError();
@@ -284,12 +281,7 @@ extern "C" int dgppo_gru_seq_bwd(const dgppo_gru_seq_args* p, void* stream) {
       !p->dhs || !p->dgi || !p->dgh || (p->Q % p->n_agents) != 0)
     return DGPPO_EINVAL;
   if (p->Q == 0) return 0;
-  static bool raised = false;
-  if (!raised) {
-    (void)hipFuncSetAttribute((const void*)dgppo::gru_seq_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    raised = true;
-  }
+  dgppo::allow_lds((const void*)dgppo::gru_seq_bwd_kernel);
   hipLaunchKernelGGL(dgppo::gru_seq_bwd_kernel, dim3((unsigned)dgppo_gru_seq_blocks(p->Q)), dim3(dgppo::kThreads),
                      dgppo::bwd_lds(), (hipStream_t)stream, *p);
   return (int)hipGetLastError();

@@ -12,6 +12,8 @@
 // (GEMMs over all agents of the batch, dgppo_gemm) plus this O(C * H * D) gather core.  The
 // result equals the reference's up to fp32 rounding.
 #include <hip/hip_runtime.h>
+
+#include "lds_attr.h"
 #include <math.h>
 #include <stdint.h>
 
@@ -877,13 +879,9 @@ extern "C" int dgppo_gae(const dgppo_gae_args* p, void* stream) {
   const dim3 grid((unsigned)p->B), block(256);
   const hipStream_t s = DG_STREAM(stream);
   if (shmem > 64 * 1024) {
-    static bool raised = false;
-    if (!raised) {
-      const void* fns[4] = {(const void*)gae_kernel<16>, (const void*)gae_kernel<32>, (const void*)gae_kernel<64>,
-                            (const void*)gae_kernel<128>};
-      for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      raised = true;
-    }
+    const void* fns[4] = {(const void*)gae_kernel<16>, (const void*)gae_kernel<32>, (const void*)gae_kernel<64>,
+                          (const void*)gae_kernel<128>};
+    for (const void* f : fns) allow_lds(f);
   }
   if (epl <= 16) hipLaunchKernelGGL(gae_kernel<16>, grid, block, shmem, s, *p, C);
   else if (epl <= 32) hipLaunchKernelGGL(gae_kernel<32>, grid, block, shmem, s, *p, C);

@@ -4,7 +4,7 @@
 //   GNN (GraphTransformer x L, per receiving agent) -> MLP head (Dense+LN+ReLU x 2) -> GRUCell ->
 //   ScaleHid -> mean / std Dense -> TanhNormal sample (or mode) + log-prob
 //
-// A 256-thread workgroup owns 32 agent rows (32 / n whole graphs) and keeps every activation of the
+// A 256-thread workgroup owns kRowsG = 16 agent rows (16 / n whole graphs) and keeps every activation of the
 // chain in LDS: the ~20 launches and HBM round trips of the unfused step collapse into one kernel
 // whose HBM traffic is the graph rows it gathers, the carries and the outputs.  The kernel is
 // latency-bound (a chain of dependent gathers and small GEMMs per workgroup), so the design
@@ -24,6 +24,8 @@
 // Same math as the unfused path (nn/layers.py, algo/module/nets.py); summation orders differ, so
 // results agree to fp32 rounding (tests/test_rollout_gpu.py checks both against float64).
 #include <hip/hip_runtime.h>
+
+#include "lds_attr.h"
 #include <stdint.h>
 
 #include "../../include/dgppo_hip.h"
@@ -707,12 +709,7 @@ extern "C" int dgppo_policy_step(const dgppo_policy_step_args* p, void* stream) 
       !p->h_in || !p->h_out || !p->action || (p->mode == 1 && !p->noise) || !p->work || p->G < 0)
     return DGPPO_EINVAL;
   if (p->G == 0) return 0;
-  static bool raised = false;
-  if (!raised) {
-    (void)hipFuncSetAttribute((const void*)dgppo::policy_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    raised = true;
-  }
+  dgppo::allow_lds((const void*)dgppo::policy_step_kernel);
   const int gpg = dgppo::kRowsG / p->n_agents;
   const int64_t ngroups = (p->G + gpg - 1) / gpg;
   if (ngroups > INT32_MAX) return DGPPO_EINVAL;

@@ -61,9 +61,11 @@ class RolloutEngine:
             self.noise = torch.empty((B * n, env.action_dim), dtype=torch.float32, device=dev)
         self._hip_graph = None
         self.lanes = int(lanes)
+        if self.lanes > 1 and B % self.lanes:
+            raise ValueError(f"n_env {B} is not a multiple of lanes {self.lanes}")
+        if self.lanes > 1 and actor is not None and actor._fused_args(self._batch(0)) is None:
+            self.lanes = 1  # the unfused actor path shares GEMM workspaces: one stream only
         if self.lanes > 1:
-            if B % self.lanes:
-                raise ValueError(f"n_env {B} is not a multiple of lanes {self.lanes}")
             self._streams = [torch.cuda.Stream(dev) for _ in range(self.lanes)]
             if self.mode == self.MODE_SAMPLE:
                 self.noise_all = torch.empty((T, B * n, env.action_dim), dtype=torch.float32, device=dev)
@@ -106,7 +108,8 @@ class RolloutEngine:
         env = self.env
         cur = env.reset(self.key, n_env=self.B, env_offset=self.env_offset, out=self.graph_at(0),
                         obstacles_out=self.obstacles)
-        if self.lanes > 1 and self._run_lanes():
+        if self.lanes > 1:
+            self._run_lanes()
             return
         for t in range(self.T):
             if self.mode != self.MODE_RANDOM:
@@ -117,10 +120,7 @@ class RolloutEngine:
         env, b, main = self.env, self.buf, torch.cuda.current_stream(self.device)
         w = self.B // self.lanes
         if self.actor is not None:
-            fa = self.actor._fused_args(self._batch(0))
-            if fa is None:  # the unfused actor path shares GEMM workspaces: one stream only
-                self.lanes = 1
-                return False
+            fa = self.actor._fused_args(self._batch(0))  # not None: checked in __init__
             K._chk(_lib.load().dgppo_policy_prepare(ctypes.byref(fa), _lib.stream_handle(self.device)),
                    "dgppo_policy_prepare")
             if self.mode == self.MODE_SAMPLE:
@@ -140,7 +140,6 @@ class RolloutEngine:
                     cur = env.step_into(cur, self.actions[t][sl], at(t + 1), self.rewards[t][sl], self.costs[t][sl])
         for s in self._streams:
             main.wait_stream(s)
-        return True
 
     def capture(self):
         """Record reset + T x (actor, step) into one hipGraph (after one eager warm-up run)."""

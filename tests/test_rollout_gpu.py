@@ -127,11 +127,12 @@ def test_env_rollout_lanes_bit_exact(cuda, graph):
         RolloutEngine(env, 255, T, cuda, lanes=2)
 
 
+@pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("env_id", ["LidarSpread", "LidarOmniTarget"])
-def test_policy_rollout_lanes_bit_exact(cuda, env_id):
+def test_policy_rollout_lanes_bit_exact(cuda, env_id, graph):
     """Policy rollouts (sample and det) stepped as 2 env slices on 2 streams write the same actions,
-    log_pi, carries and graphs as one stream, bit for bit (LidarOmniTarget: no fused policy step,
-    the engine keeps one stream)."""
+    log_pi, carries and graphs as one stream, bit for bit, replayed from a hipGraph and eager
+    (LidarOmniTarget: no fused policy step, the engine keeps one stream)."""
     env = make_env(env_id, 8, num_obs=3, device=cuda)
     B, T = 64, 6
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
@@ -140,7 +141,10 @@ def test_policy_rollout_lanes_bit_exact(cuda, env_id):
         outs = []
         for lanes in (1, 2):
             eng = RolloutEngine(env, B, T, cuda, env_offset=0, actor=algo.actor, mode=mode, lanes=lanes)
-            eng.capture()
+            if lanes == 2:
+                assert eng.lanes == (2 if env_id == "LidarSpread" else 1)
+            if graph:
+                eng.capture()
             eng.run(key=11)
             torch.cuda.synchronize(cuda)
             outs.append([x.cpu().numpy() for x in (eng.buf.states, eng.buf.edges, eng.actions, eng.log_pis,
