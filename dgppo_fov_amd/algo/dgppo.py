@@ -190,13 +190,21 @@ class DGPPO:
             w *= 2
         return w
 
+    def _check_params(self, params):
+        """The kernels read the nets' own parameter buffers: `params` must be None or this algorithm's
+        `params` (the same flat tensors), never a foreign parameter set."""
+        if params is not None:
+            mine = self.params
+            assert set(params) == set(mine) and all(params[k] is mine[k] for k in mine), \
+                "params must be this algorithm's own parameter buffers (self.params)"
+
     # ---- acting ----------------------------------------------------------------------------------
     def _gb(self, graph) -> GraphBatch:
         return GraphBatch.from_graph(graph, self._env)
 
     def act(self, graph, rnn_state: torch.Tensor, params=None):
         """get_action for a batch of graphs: rnn_state (B, 1, n, 1, 64) -> (action (B, n, A), rnn)."""
-        assert params is None or params is self.params
+        self._check_params(params)
         g = self._gb(graph)
         B, n = g.G, self._n_agents
         h = rnn_state.reshape(B * n, 64).contiguous()
@@ -235,7 +243,7 @@ class DGPPO:
         The returned Rollout is a set of VIEWS into the buffers of a RolloutEngine cached per n_env:
         the next collect() with the same n_env overwrites it in place (the reference returns fresh
         arrays).  Clone the fields to keep a rollout across collects."""
-        assert params is None or params is self.params
+        self._check_params(params)
         if n_env is None:
             n_env = len(key) if hasattr(key, "__len__") else 128
         seed = int(np.asarray(key).reshape(-1)[0]) if hasattr(key, "__len__") else int(key)
