@@ -18,7 +18,7 @@ from typing import NamedTuple, Optional, Tuple
 import numpy as np
 import torch
 
-from .. import _lib
+from .. import _lib, ops
 from ..utils.graph import GraphsTuple
 
 
@@ -65,6 +65,7 @@ class MultiAgentEnv(ABC):
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         self._cfg = self._make_cfg()
+        self._cfg_handle = ops.register_env_cfg(self._cfg)  # the torch.ops.dgppo env ops take this handle
         self._dev_cache = {}
 
     # ---- reference properties --------------------------------------------------------------
@@ -283,38 +284,23 @@ class MultiAgentEnv(ABC):
 
         `key` is an int, or a 1-element uint64/int64 device tensor read by the kernel at run time
         (so a captured hipGraph can be replayed with fresh keys)."""
-        lib = _lib.load()
         dev = self.device if out is None else out.nodes.device
         _lib.require_gpu(dev, "env.reset")
         g = self.empty_graph((n_env,), dev) if out is None else out
         ob = obstacles_out
         if ob is None and self._obstacle_fields() > 0:
             ob = torch.empty((n_env, max(self.n_obs, 1), self._obstacle_fields()), dtype=torch.float32, device=dev)
-        io = _lib.EnvResetIO()
-        if isinstance(key, torch.Tensor):
-            if key.device != dev or key.numel() != 1 or key.dtype not in (torch.int64, torch.uint64):
-                raise ValueError("tensor key must be a 1-element int64 tensor on the env's device")
-            io.seed, io.seed_ptr = 0, key.data_ptr()
-        else:
-            io.seed, io.seed_ptr = int(key) & 0xFFFFFFFFFFFFFFFF, None
-        io.env_offset = int(env_offset)
-        io.obstacles = _lib.ptr(ob)
-        io.obstacles_stride = ob.stride(0) if ob is not None else 0
-        io.ray_dirs = _lib.ptr(self._ray_table(dev))
-        io.nodes, io.nodes_stride = _lib.ptr(g.nodes), self._env_stride(g.nodes, 2)
-        io.edges, io.edges_stride = _lib.ptr(g.edges), self._env_stride(g.edges, 2)
-        io.out_states, io.out_states_stride = _lib.ptr(g.states), self._env_stride(g.states, 2)
-        io.receivers, io.senders = _lib.ptr(g.receivers), _lib.ptr(g.senders)
-        io.edge_index_stride = self._env_stride(g.receivers, 1)
-        io.n_env = int(n_env)
-        _lib.check(lib.dgppo_env_reset(ctypes.byref(self._cfg), ctypes.byref(io), _lib.stream_handle(dev)),
-                   "dgppo_env_reset")
+        tkey = key if isinstance(key, torch.Tensor) else None
+        seed = 0 if tkey is not None else int(key) & 0xFFFFFFFFFFFFFFFF
+        torch.ops.dgppo.env_reset(self._cfg_handle, tkey, seed if seed < 2 ** 63 else seed - 2 ** 64,
+                                  int(env_offset), int(n_env), ob, self._ray_table(dev), g.nodes, g.edges, g.states,
+                                  g.receivers, g.senders)
         return self._assemble(g.nodes, g.edges, g.states, g.receivers, g.senders, ob)
 
     def step_into(self, graph: GraphsTuple, action: torch.Tensor, out: GraphsTuple,
                   reward: torch.Tensor, cost: torch.Tensor) -> GraphsTuple:
-        """One fused HIP step writing into caller-owned buffers (views into a rollout buffer)."""
-        lib = _lib.load()
+        """One fused HIP step (torch.ops.dgppo.env_step) writing into caller-owned buffers (views into a
+        rollout buffer)."""
         _lib.require_gpu(graph.states.device, "env.step")
         if graph.states.dim() != 3:
             raise ValueError("step expects one leading env axis: states (B, N, state_dim)")
@@ -329,22 +315,8 @@ class MultiAgentEnv(ABC):
         A = self.action_dim
         action = action if action.stride(-1) == 1 and action.stride(-2) == A else action.contiguous()
         ob = self._obstacles_of(graph)
-        io = _lib.EnvStepIO()
-        io.states, io.states_stride = _lib.ptr(graph.states), self._env_stride(graph.states, 2)
-        io.obstacles = _lib.ptr(ob)
-        io.obstacles_stride = ob.stride(-3) if ob is not None else 0
-        io.action, io.action_stride = _lib.ptr(action), self._env_stride(action, 2)
-        io.ray_dirs = _lib.ptr(self._ray_table(graph.states.device))
-        io.nodes, io.nodes_stride = _lib.ptr(out.nodes), self._env_stride(out.nodes, 2)
-        io.edges, io.edges_stride = _lib.ptr(out.edges), self._env_stride(out.edges, 2)
-        io.out_states, io.out_states_stride = _lib.ptr(out.states), self._env_stride(out.states, 2)
-        io.receivers, io.senders = _lib.ptr(out.receivers), _lib.ptr(out.senders)
-        io.edge_index_stride = self._env_stride(out.receivers, 1)
-        io.reward, io.reward_stride = _lib.ptr(reward), (reward.stride(0) if reward.dim() > 0 else 1)
-        io.cost, io.cost_stride = _lib.ptr(cost), self._env_stride(cost, 2)
-        io.n_env = int(B)
-        _lib.check(lib.dgppo_env_step(ctypes.byref(self._cfg), ctypes.byref(io),
-                                      _lib.stream_handle(graph.states.device)), "dgppo_env_step")
+        torch.ops.dgppo.env_step(self._cfg_handle, graph.states, ob, action, self._ray_table(graph.states.device),
+                                 out.nodes, out.edges, out.states, out.receivers, out.senders, reward, cost)
         return self._assemble(out.nodes, out.edges, out.states, out.receivers, out.senders, ob)
 
     def _obstacles_of(self, graph: GraphsTuple) -> Optional[torch.Tensor]:

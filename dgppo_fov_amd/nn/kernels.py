@@ -1,4 +1,5 @@
-"""Typed wrappers over the hot-path-(2) C-ABI (include/dgppo_hip.h) for torch device tensors.
+"""Typed wrappers over the hot-path-(2) C-ABI (include/dgppo_hip.h) for torch device tensors (the
+registered torch.ops.dgppo ops where one exists, dgppo_fov_amd/ops.py).
 
 Every function launches on torch's current stream and returns immediately; there is no CPU
 path (non-CUDA tensors raise NativeLibraryError)."""
@@ -9,7 +10,7 @@ import math
 
 import torch
 
-from .. import _lib
+from .. import _lib, ops  # noqa: F401  (ops registers torch.ops.dgppo.*)
 
 _WS = {}
 
@@ -134,12 +135,6 @@ def agent_mean_bwd(dy, dx, G, n, F, dx_gstride):
          "dgppo_agent_mean_bwd")
 
 
-def gnn_attn(args: _lib.GnnAttnArgs, backward: bool, device):
-    lib = _lib.load()
-    fn = lib.dgppo_gnn_attn_bwd if backward else lib.dgppo_gnn_attn_fwd
-    _chk(fn(ctypes.byref(args), _lib.stream_handle(device)), "dgppo_gnn_attn")
-
-
 def sender_table(G, n, C, E, cand, receivers, senders, out):
     _chk(_lib.load().dgppo_gnn_sender_table(int(G), int(n), int(C), int(E), _p(cand), _p(receivers), _p(senders),
                                             _p(out), _stream(out)), "dgppo_gnn_sender_table")
@@ -153,10 +148,6 @@ def edge_wsum(G, n, C, H, EX, E, attn, cand, sidx, efx, out):
 def edge_da(G, n, C, H, EX, E, dxx, cand, sidx, efx, out):
     _chk(_lib.load().dgppo_gnn_edge_da(int(G), int(n), int(C), int(H), int(EX), int(E), _p(dxx), _p(cand),
                                        _p(sidx), _p(efx), _p(out), _stream(out)), "dgppo_gnn_edge_da")
-
-
-def gnn_attn_partial_blocks(args: _lib.GnnAttnArgs) -> int:
-    return int(_lib.load().dgppo_gnn_attn_partial_blocks(ctypes.byref(args)))
 
 
 def tanh_normal(args: _lib.TanhNormalArgs, device):
@@ -179,24 +170,15 @@ def l2_loss(pred, target, dpred, loss):
 
 
 def gae(hs, l, Vh, Vl, Qh, Ql, gamma, lam):
-    B, T, n, nh = hs.shape
-    a = _lib.GaeArgs()
-    a.B, a.T, a.n_agents, a.n_h = int(B), int(T), int(n), int(nh)
-    a.hs, a.l, a.Vh, a.Vl, a.Qh, a.Ql = _p(hs), _p(l), _p(Vh), _p(Vl), _p(Qh), _p(Ql)
-    a.gamma = float(gamma)
-    setattr(a, "lambda", float(lam))
-    _chk(_lib.load().dgppo_gae(ctypes.byref(a), _stream(hs)), "dgppo_gae")
+    torch.ops.dgppo.gae(hs, l, Vh, Vl, Qh, Ql, float(gamma), float(lam))
 
 
 def grad_norm(grad, state):
-    lib = _lib.load()
-    ws = workspace(lib.dgppo_loss_workspace_floats(), grad.device, "norm")
-    _chk(lib.dgppo_grad_norm(_p(grad), int(grad.numel()), _p(state), _p(ws), _stream(grad)), "dgppo_grad_norm")
+    torch.ops.dgppo.grad_norm(grad, state)
 
 
 def adam(param, grad, m, v, state, lr, b1=0.9, b2=0.999, eps=1e-8, max_norm=2.0):
-    _chk(_lib.load().dgppo_adam(_p(param), _p(grad), _p(m), _p(v), int(param.numel()), _p(state), float(lr),
-                                float(b1), float(b2), float(eps), float(max_norm), _stream(param)), "dgppo_adam")
+    torch.ops.dgppo.adam(param, grad, m, v, state, float(lr), float(b1), float(b2), float(eps), float(max_norm))
 
 
 def normal_(out, seed=0, stream_id=0, seed_tensor=None):

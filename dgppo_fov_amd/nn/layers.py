@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
+from .. import ops
 from . import kernels as K
 
 
@@ -372,30 +373,23 @@ class GraphTransformer:
              "Dense_4": {"kernel": orthogonal(rng, (D, F)), "bias": np.zeros(F, np.float32)}}
         self.load_flax(d)
 
-    def _attn_args(self, g: "GraphBatch", xa=None, pre=None):
-        """Kernel arguments; returns (args, tensors the pointers refer to, kept alive over the launch)."""
-        a = K._lib.GnnAttnArgs()
-        G, N = g.G, g.N
-        a.G, a.N, a.E, a.n_agents = G, N, g.E, g.n
-        a.D, a.F, a.H, a.C = self.D, self.F, self.H, g.C
-        a.cand, a.receivers, a.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
-        a.sidx = K._p(g.sidx)
-        a.ef, a.ef_gstride = K._p(g.edges_head), g.E * 4
-        a.bk = K._p(self.v("bk"))
-        a.scale = 1.0 / math.sqrt(self.F)
-        keep = []
+    def _attn_args(self, g: "GraphBatch", Q, QT, xa=None, pre=None) -> dict:
+        """Inputs of torch.ops.dgppo.gnn_attn_fwd / _bwd for this layer on graph batch g."""
+        D0 = 0
+        pre_W = pre_b = None
         if xa is None:
-            a.x, a.x_gstride = K._p(g.nodes), N * g.nodes.shape[2]
+            x, x_gs = g.nodes, g.N * g.nodes.shape[2]
         else:  # agent mode: agents from xa, other senders = pre's Dense_4 + ReLU of raw rows
             raw, cols = g.sender_raw
             D0 = raw.shape[2]
-            a.x, a.x_gstride, a.D0 = K._p(raw), N * D0, D0
-            a.xa, a.xa_gstride = K._p(xa), g.n * self.D
+            x, x_gs = raw, g.N * D0
             if pre is not None:
-                W = pre.v("Wu") if cols is None else pre.v("Wu").index_select(0, cols)
-                keep.append(W)
-                a.pre_W, a.pre_b = K._p(W), K._p(pre.v("bu"))
-        return a, keep
+                pre_W = pre.v("Wu") if cols is None else pre.v("Wu").index_select(0, cols)
+                pre_b = pre.v("bu")
+        return dict(dims=[g.G, g.N, g.E, g.n, self.D, self.F, self.H, g.C, D0], cand=g.cand, receivers=g.receivers,
+                    senders=g.senders, sidx=g.sidx, x=x, x_gstride=x_gs, ef=g.edges_head, ef_gstride=g.E * 4, q=Q,
+                    qt=QT, bk=self.v("bk"), scale=1.0 / math.sqrt(self.F), xa=xa, xa_gstride=g.n * self.D,
+                    pre_W=pre_W, pre_b=pre_b)
 
     def fwd(self, g: "GraphBatch", xa=None, pre=None):
         """One layer on the graph batch.  xa None: senders read the raw nodes (G, N, D) (first layer);
@@ -414,10 +408,7 @@ class GraphTransformer:
         K.gemm(Q, self.v("Wkt"), QT, R, D, F, lda=H * F, sa=F, ldb=D, sb=F * D, ldc=H * D, sc=D, batch=H)
         attn = torch.empty((R, H, C), device=dev)
         xcat = torch.empty((R, H * (D + 5)), device=dev)
-        a, keep = self._attn_args(g, xa, pre)
-        a.q, a.qt, a.attn, a.xcat = K._p(Q), K._p(QT), K._p(attn), K._p(xcat)
-        K.gnn_attn(a, False, dev)
-        del keep
+        torch.ops.dgppo.gnn_attn_fwd(**self._attn_args(g, Q, QT, xa, pre), attn=attn, xcat=xcat)
         M = torch.empty((R, F), device=dev)
         K.gemm(xcat, self.v("Wcat"), M, R, F, H * (D + 5), alpha=1.0 / H)
         xcx = None
@@ -456,24 +447,18 @@ class GraphTransformer:
         dQ = torch.empty((R, H * F), device=dev)
         dbeta = torch.empty((R, H), device=dev)
         dXa = torch.zeros((R, D), device=dev) if xa is not None else None
-        a, keep = self._attn_args(g, xa, pre)
-        a.q, a.qt, a.attn = K._p(Q), K._p(QT), K._p(attn)
-        a.dxcat, a.dqt, a.dq, a.dbeta = K._p(dxcat), K._p(dQT), K._p(dQ), K._p(dbeta)
-        a.da_add = K._p(da_add)
+        args = self._attn_args(g, Q, QT, xa, pre)
         part = None
-        if xa is not None:
-            a.dxa, a.dxa_gstride = K._p(dXa), n * D
-            if pre is not None:
-                nb = K.gnn_attn_partial_blocks(a)
-                PK = a.D0 * D + D
-                part = K.workspace(nb * PK, dev, "attn_pre")
-                a.dpre_part = K._p(part)
-        K.gnn_attn(a, True, dev)
-        del keep
+        if xa is not None and pre is not None:
+            nb = ops.gnn_attn_partial_blocks(**args)
+            PK = args["dims"][8] * D + D
+            part = K.workspace(nb * PK, dev, "attn_pre")
+        torch.ops.dgppo.gnn_attn_bwd(**args, attn=attn, dxcat=dxcat, da_add=da_add, dqt=dQT, dq=dQ, dbeta=dbeta,
+                                     dxa=dXa, dxa_gstride=n * D, dpre_part=part)
         if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre (Wu rows = the raw columns used)
             cols = g.sender_raw[1]
             ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
-            nw = a.D0 * D
+            nw = args["dims"][8] * D
             if ob == ow + nw and cols is None:
                 K.colsum(part, nb, PK, pre.ps.grad[ow:ow + PK], beta=1.0)
             else:
@@ -482,7 +467,7 @@ class GraphTransformer:
                 if cols is None:
                     pre.ps.grad[ow:ow + nw].add_(tmp[:nw])
                 else:
-                    pre.v("Wu", True).index_add_(0, cols, tmp[:nw].view(a.D0, D))
+                    pre.v("Wu", True).index_add_(0, cols, tmp[:nw].view(args["dims"][8], D))
                 pre.ps.grad[ob:ob + D].add_(tmp[nw:])
         K.gemm(dbeta, Q, self.v("bk", True), 1, F, R, ta=True, lda=H, sa=1, ldb=H * F, sb=F, ldc=F, sc=F,
                batch=H, beta=1.0)

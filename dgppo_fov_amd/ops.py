@@ -1,0 +1,255 @@
+"""PyTorch-ROCm custom ops over libdgppo_hip.so: `torch.ops.dgppo.*`.
+
+The hot-path kernels are registered with `torch.library` so the torch dispatcher, FakeTensor /
+meta tracing (torch.compile, export) and CUDA-graph capture all see them as ordinary ops.  Each op
+is a thin shim over the C-ABI entry point declared in include/dgppo_hip.h (the same function a
+cgo / JNI / ctypes binding would call); outputs are caller-allocated and written
+in place (`mutates_args`), launches go on torch's current stream, and there is no CPU kernel: a
+non-CUDA tensor raises NativeLibraryError (`_lib.require_gpu`).
+
+  dgppo::env_reset      dgppo_env_reset      vmap(env.reset)      lidar_env/base.py:89-124, mpe/base.py:81-127
+  dgppo::env_step       dgppo_env_step       vmap(env.step)       lidar_env/base.py:151-174, mpe/base.py:137-158
+  dgppo::gnn_attn_fwd   dgppo_gnn_attn_fwd   GraphTransformer attention core, gnn.py:83-117
+  dgppo::gnn_attn_bwd   dgppo_gnn_attn_bwd   its gradient (the jax.grad of update_Vl / update_policy)
+  dgppo::gae            dgppo_gae            compute_dec_ocp_gae, algo/utils.py:11-79
+  dgppo::grad_norm      dgppo_grad_norm      compute_norm + has_any_nan_or_inf, trainer/utils.py:105-118
+  dgppo::adam           dgppo_adam           clip + optax.apply_if_finite(optax.adam), informarl.py:131-137
+
+An env's static configuration (dgppo_env_cfg: engine, sizes, radii, limits) is not a tensor; it is
+registered once per env instance and the ops take its integer handle.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+_CFGS: dict = {}
+
+
+def register_env_cfg(cfg: _lib.EnvCfg) -> int:
+    """Keep `cfg` alive for the process and return the handle the env ops take."""
+    h = len(_CFGS) + 1
+    _CFGS[h] = cfg
+    return h
+
+
+def env_cfg(handle: int) -> _lib.EnvCfg:
+    try:
+        return _CFGS[int(handle)]
+    except KeyError:
+        raise ValueError(f"unknown env cfg handle {handle}") from None
+
+
+def _stride(t: Tensor, inner: int) -> int:
+    """Per-env element stride of t, requiring the trailing `inner` dims to be contiguous."""
+    tail = 1
+    for d in range(t.dim() - 1, t.dim() - 1 - inner, -1):
+        if t.stride(d) != tail:
+            raise ValueError("trailing dims must be contiguous")
+        tail *= t.shape[d]
+    return t.stride(t.dim() - 1 - inner) if t.dim() > inner else tail
+
+
+def _p(t: Optional[Tensor]) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _stream(t: Tensor) -> int:
+    return _lib.stream_handle(t.device)
+
+
+# ---- env -------------------------------------------------------------------------------------------
+@torch.library.custom_op("dgppo::env_step", mutates_args=("nodes", "edges", "out_states", "receivers", "senders",
+                                                           "reward", "cost"))
+def env_step(cfg: int, states: Tensor, obstacles: Optional[Tensor], action: Tensor, ray_dirs: Tensor, nodes: Tensor,
+             edges: Tensor, out_states: Tensor, receivers: Tensor, senders: Tensor, reward: Tensor,
+             cost: Tensor) -> None:
+    """One fused env step for B envs: states (B, N, sd) [+ obstacles (B, O, 16)] and actions (B, n, A)
+    -> next graph rows, reward (B,), cost (B, n, n_cost).  Per-env strides are free (views into a
+    time-major rollout buffer); the trailing dims must be contiguous."""
+    _lib.require_gpu(states.device, "dgppo::env_step")
+    io = _lib.EnvStepIO()
+    io.states, io.states_stride = _p(states), _stride(states, 2)
+    io.obstacles = _p(obstacles)
+    io.obstacles_stride = obstacles.stride(-3) if obstacles is not None else 0
+    io.action, io.action_stride = _p(action), _stride(action, 2)
+    io.ray_dirs = _p(ray_dirs)
+    io.nodes, io.nodes_stride = _p(nodes), _stride(nodes, 2)
+    io.edges, io.edges_stride = _p(edges), _stride(edges, 2)
+    io.out_states, io.out_states_stride = _p(out_states), _stride(out_states, 2)
+    io.receivers, io.senders = _p(receivers), _p(senders)
+    io.edge_index_stride = _stride(receivers, 1)
+    io.reward, io.reward_stride = _p(reward), (reward.stride(0) if reward.dim() > 0 else 1)
+    io.cost, io.cost_stride = _p(cost), _stride(cost, 2)
+    io.n_env = int(states.shape[0])
+    _lib.check(_lib.load().dgppo_env_step(ctypes.byref(env_cfg(cfg)), ctypes.byref(io), _stream(states)),
+               "dgppo_env_step")
+
+
+@env_step.register_fake
+def _env_step_fake(cfg, states, obstacles, action, ray_dirs, nodes, edges, out_states, receivers, senders, reward,
+                   cost) -> None:
+    return None
+
+
+@torch.library.custom_op("dgppo::env_reset", mutates_args=("obstacles", "nodes", "edges", "out_states", "receivers",
+                                                            "senders"))
+def env_reset(cfg: int, key: Optional[Tensor], seed: int, env_offset: int, n_env: int, obstacles: Optional[Tensor],
+              ray_dirs: Tensor, nodes: Tensor, edges: Tensor, out_states: Tensor, receivers: Tensor,
+              senders: Tensor) -> None:
+    """Reset n_env envs (env b draws from Philox keyed (seed or *key, env_offset + b)) and write the
+    initial graph.  `key`: optional 1-element int64 device tensor read at run time (hipGraph replays)."""
+    _lib.require_gpu(nodes.device, "dgppo::env_reset")
+    io = _lib.EnvResetIO()
+    if key is not None:
+        if key.device != nodes.device or key.numel() != 1 or key.dtype not in (torch.int64, torch.uint64):
+            raise ValueError("tensor key must be a 1-element int64 tensor on the env's device")
+        io.seed, io.seed_ptr = 0, key.data_ptr()
+    else:
+        io.seed, io.seed_ptr = int(seed) & 0xFFFFFFFFFFFFFFFF, None
+    io.env_offset = int(env_offset)
+    io.obstacles = _p(obstacles)
+    io.obstacles_stride = obstacles.stride(0) if obstacles is not None else 0
+    io.ray_dirs = _p(ray_dirs)
+    io.nodes, io.nodes_stride = _p(nodes), _stride(nodes, 2)
+    io.edges, io.edges_stride = _p(edges), _stride(edges, 2)
+    io.out_states, io.out_states_stride = _p(out_states), _stride(out_states, 2)
+    io.receivers, io.senders = _p(receivers), _p(senders)
+    io.edge_index_stride = _stride(receivers, 1)
+    io.n_env = int(n_env)
+    _lib.check(_lib.load().dgppo_env_reset(ctypes.byref(env_cfg(cfg)), ctypes.byref(io), _stream(nodes)),
+               "dgppo_env_reset")
+
+
+@env_reset.register_fake
+def _env_reset_fake(cfg, key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states, receivers,
+                    senders) -> None:
+    return None
+
+
+# ---- GraphTransformer attention core -------------------------------------------------------------------
+def _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa, xa_gstride,
+                 pre_W, pre_b) -> _lib.GnnAttnArgs:
+    a = _lib.GnnAttnArgs()
+    a.G, a.N, a.E, a.n_agents, a.D, a.F, a.H, a.C, a.D0 = (int(v) for v in dims)
+    a.cand, a.receivers, a.senders, a.sidx = _p(cand), _p(receivers), _p(senders), _p(sidx)
+    a.x, a.x_gstride = _p(x), int(x_gstride)
+    a.ef, a.ef_gstride = _p(ef), int(ef_gstride)
+    a.q, a.qt, a.bk = _p(q), _p(qt), _p(bk)
+    a.scale = float(scale)
+    a.xa, a.xa_gstride = _p(xa), int(xa_gstride)
+    a.pre_W, a.pre_b = _p(pre_W), _p(pre_b)
+    return a
+
+
+@torch.library.custom_op("dgppo::gnn_attn_fwd", mutates_args=("attn", "xcat"))
+def gnn_attn_fwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
+                 x_gstride: int, ef: Tensor, ef_gstride: int, q: Tensor, qt: Tensor, bk: Tensor, scale: float,
+                 xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor], pre_b: Optional[Tensor],
+                 attn: Tensor, xcat: Tensor) -> None:
+    """Per-receiving-agent attention of one GraphTransformer layer (dims = [G, N, E, n, D, F, H, C, D0]):
+    attn (G*n, H, C) = segment softmax of (q . k)/sqrt(F) over each agent's candidate edges, xcat
+    (G*n, H*(D+5)) = the attention-weighted [sender rows | edge rows | 1] per head (nn/layers.py)."""
+    _lib.require_gpu(q.device, "dgppo::gnn_attn_fwd")
+    a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
+                     xa_gstride, pre_W, pre_b)
+    a.attn, a.xcat = _p(attn), _p(xcat)
+    _lib.check(_lib.load().dgppo_gnn_attn_fwd(ctypes.byref(a), _stream(q)), "dgppo_gnn_attn_fwd")
+
+
+@gnn_attn_fwd.register_fake
+def _gnn_attn_fwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
+                       xa_gstride, pre_W, pre_b, attn, xcat) -> None:
+    return None
+
+
+@torch.library.custom_op("dgppo::gnn_attn_bwd", mutates_args=("dqt", "dq", "dbeta", "dxa", "dpre_part"))
+def gnn_attn_bwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
+                 x_gstride: int, ef: Tensor, ef_gstride: int, q: Tensor, qt: Tensor, bk: Tensor, scale: float,
+                 xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor], pre_b: Optional[Tensor],
+                 attn: Tensor, dxcat: Tensor, da_add: Optional[Tensor], dqt: Tensor, dq: Tensor, dbeta: Tensor,
+                 dxa: Optional[Tensor], dxa_gstride: int, dpre_part: Optional[Tensor]) -> None:
+    """Backward of gnn_attn_fwd given dL/dxcat (+ da_add, extra dL/dattn of edge columns past 4): dqt, dq,
+    dbeta (dL/d(q . bk)); in agent mode dxa (accumulated, agent senders) and the partial Dense_4
+    gradients of the recomputed never-receiving senders (dpre_part, one row per workgroup)."""
+    _lib.require_gpu(q.device, "dgppo::gnn_attn_bwd")
+    a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
+                     xa_gstride, pre_W, pre_b)
+    a.attn, a.dxcat, a.da_add = _p(attn), _p(dxcat), _p(da_add)
+    a.dqt, a.dq, a.dbeta = _p(dqt), _p(dq), _p(dbeta)
+    a.dxa, a.dxa_gstride, a.dpre_part = _p(dxa), int(dxa_gstride), _p(dpre_part)
+    _lib.check(_lib.load().dgppo_gnn_attn_bwd(ctypes.byref(a), _stream(q)), "dgppo_gnn_attn_bwd")
+
+
+@gnn_attn_bwd.register_fake
+def _gnn_attn_bwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
+                       xa_gstride, pre_W, pre_b, attn, dxcat, da_add, dqt, dq, dbeta, dxa, dxa_gstride,
+                       dpre_part) -> None:
+    return None
+
+
+def gnn_attn_partial_blocks(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
+                            xa_gstride, pre_W, pre_b) -> int:
+    """Rows of the dpre_part workspace gnn_attn_bwd writes for these arguments (host query)."""
+    a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
+                     xa_gstride, pre_W, pre_b)
+    return int(_lib.load().dgppo_gnn_attn_partial_blocks(ctypes.byref(a)))
+
+
+# ---- GAE, clip + Adam ------------------------------------------------------------------------------------
+@torch.library.custom_op("dgppo::gae", mutates_args=("Qh", "Ql"))
+def gae(hs: Tensor, l: Tensor, Vh: Tensor, Vl: Tensor, Qh: Tensor, Ql: Tensor, gamma: float, lam: float) -> None:
+    """Dec-OCP GAE per env: hs (B, T, n, nh) costs, l (B, T) losses, Vh (B, T+1, n, nh), Vl (B, T+1)
+    -> Qh (B, T, n, nh), Ql (B, T) (the reference's O(T^2) row scan, literally)."""
+    _lib.require_gpu(hs.device, "dgppo::gae")
+    for t in (hs, l, Vh, Vl, Qh, Ql):
+        if not t.is_contiguous():
+            raise ValueError("dgppo::gae needs contiguous tensors")
+    B, T, n, nh = hs.shape
+    a = _lib.GaeArgs()
+    a.B, a.T, a.n_agents, a.n_h = int(B), int(T), int(n), int(nh)
+    a.hs, a.l, a.Vh, a.Vl, a.Qh, a.Ql = _p(hs), _p(l), _p(Vh), _p(Vl), _p(Qh), _p(Ql)
+    a.gamma = float(gamma)
+    setattr(a, "lambda", float(lam))
+    _lib.check(_lib.load().dgppo_gae(ctypes.byref(a), _stream(hs)), "dgppo_gae")
+
+
+@gae.register_fake
+def _gae_fake(hs, l, Vh, Vl, Qh, Ql, gamma, lam) -> None:
+    return None
+
+
+@torch.library.custom_op("dgppo::grad_norm", mutates_args=("state",))
+def grad_norm(grad: Tensor, state: Tensor) -> None:
+    """state[0] = global L2 norm of grad, state[1] = number of non-finite entries (state[2]: Adam count)."""
+    _lib.require_gpu(grad.device, "dgppo::grad_norm")
+    lib = _lib.load()
+    from .nn.kernels import workspace
+
+    ws = workspace(lib.dgppo_loss_workspace_floats(), grad.device, "norm")
+    _lib.check(lib.dgppo_grad_norm(_p(grad), int(grad.numel()), _p(state), _p(ws), _stream(grad)), "dgppo_grad_norm")
+
+
+@grad_norm.register_fake
+def _grad_norm_fake(grad, state) -> None:
+    return None
+
+
+@torch.library.custom_op("dgppo::adam", mutates_args=("param", "m", "v", "state"))
+def adam(param: Tensor, grad: Tensor, m: Tensor, v: Tensor, state: Tensor, lr: float, b1: float, b2: float,
+         eps: float, max_norm: float) -> None:
+    """g <- g * max_norm / max(max_norm, |g|) and one optax adam step, skipped entirely (apply_if_finite)
+    when state[1] (non-finite count from dgppo::grad_norm) is non-zero; state[2] counts applied steps."""
+    _lib.require_gpu(param.device, "dgppo::adam")
+    _lib.check(_lib.load().dgppo_adam(_p(param), _p(grad), _p(m), _p(v), int(param.numel()), _p(state), float(lr),
+                                      float(b1), float(b2), float(eps), float(max_norm), _stream(param)), "dgppo_adam")
+
+
+@adam.register_fake
+def _adam_fake(param, grad, m, v, state, lr, b1, b2, eps, max_norm) -> None:
+    return None
