@@ -52,7 +52,8 @@ def _raw_env_step(env, g, action, out, reward, cost):
     """The same step through the C-ABI directly (ctypes), bypassing the torch op."""
     io = _lib.EnvStepIO()
     io.states, io.states_stride = g.states.data_ptr(), ops._stride(g.states, 2)
-    io.obstacles, io.obstacles_stride = 0, 0
+    ob = env._obstacles_of(g)
+    io.obstacles, io.obstacles_stride = ob.data_ptr(), ob.stride(-3)
     io.action, io.action_stride = action.data_ptr(), ops._stride(action, 2)
     io.ray_dirs = env._ray_table(g.states.device).data_ptr()
     io.nodes, io.nodes_stride = out.nodes.data_ptr(), ops._stride(out.nodes, 2)
@@ -81,7 +82,7 @@ def test_env_step_op_matches_c_abi_and_captures(cuda):
         r = torch.empty(B, device=cuda)
         c = torch.empty((B, 8, 2), device=cuda)
         if path == "op":
-            torch.ops.dgppo.env_step(env._cfg_handle, g.states, None, a, env._ray_table(cuda), out.nodes, out.edges,
+            torch.ops.dgppo.env_step(env._cfg_handle, g.states, env._obstacles_of(g), a, env._ray_table(cuda), out.nodes, out.edges,
                                      out.states, out.receivers, out.senders, r, c)
         elif path == "raw":
             _raw_env_step(env, g, a, out, r, c)
