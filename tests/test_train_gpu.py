@@ -42,7 +42,17 @@ def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, 
     assert rows and all(math.isfinite(v) for r in rows for v in r.values() if isinstance(v, float))
     assert any("eval/safe_data" in r or "eval/unsafe_frac" in r for r in rows)
     capsys.readouterr()
-    monkeypatch.setattr(sys, "argv", ["test.py", "--path", run, "--epi", "1", "--n-env", "4", "--max-step", "16"])
+    monkeypatch.setattr(sys, "argv", ["test.py", "--path", run, "--epi", "4", "--max-step", "16", "--no-video"])
     test_py.main()
     out = capsys.readouterr().out
-    assert "safe_rate:" in out and "reward:" in out
+    assert "safe_rate:" in out and "reward:" in out and out.count("epi: ") == 4
+    # the reference's generalisation eval: more agents / obstacles than training, skip 1 episode, log a csv row
+    argv = ["test.py", "--path", run, "--epi", "5", "--offset", "1", "-n", str(n + 1), "--obs", str(obs + 1),
+            "--max-step", "16", "--log", "--no-video"]
+    monkeypatch.setattr(sys, "argv", argv)
+    test_py.main()
+    out = capsys.readouterr().out
+    assert out.count("epi: ") == 4 and "epi: 0," not in out and "epi: 4," in out
+    row = open(os.path.join(run, "test_log.csv")).read().strip().split(",")
+    assert len(row) == 7 and row[0] == str(n + 1) and row[1] == "5" and row[2] == "16" and row[4] == str(obs + 1)
+    assert 0.0 <= float(row[5]) <= 100.0
