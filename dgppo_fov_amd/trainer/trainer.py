@@ -80,6 +80,8 @@ class Trainer:
                 self.algo.save(self.model_dir, step)
             key = int(self.rng.integers(0, 2 ** 62))
             rollouts = self.algo.collect(self.algo.params, key, n_env=self.n_env_train)
+            train_info = {k.replace("eval/", "train/"): v for k, v in eval_info(rollouts.rewards, rollouts.costs).items()
+                          if k in ("eval/reward", "eval/unsafe_frac")}  # the stochastic rollouts' own metrics
             update_info = self.algo.update(rollouts, step)
-            self._log({"step": self.update_steps, **update_info})
+            self._log({"step": self.update_steps, **update_info, **train_info})
             self.update_steps += 1

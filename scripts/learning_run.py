@@ -35,13 +35,13 @@ def main():
     ap.add_argument("--epi", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/learn")
-    a = ap.parse_args()
+    a, extra = ap.parse_known_args()  # anything else goes to train.py (e.g. --lr-actor 1e-4)
     os.makedirs(a.out, exist_ok=True)
     train, test = _entry("train"), _entry("test")
     t0 = time.time()
     sys.argv = ["train.py", "--env", a.env, "-n", str(a.n), "--algo", a.algo, "--obs", str(a.obs), "--steps",
                 str(a.steps), "--eval-interval", str(a.eval_interval), "--save-interval", str(a.steps),
-                "--seed", str(a.seed), "--log-dir", os.path.join(a.out, "logs")]
+                "--seed", str(a.seed), "--log-dir", os.path.join(a.out, "logs")] + extra
     train.main()
     t_train = time.time() - t0
     (run,) = glob.glob(os.path.join(a.out, "logs", a.env, a.algo, f"seed{a.seed}_*"))
@@ -51,10 +51,12 @@ def main():
     for step in (0, a.steps):
         res[step] = test.test(argparse.Namespace(**{**vars(_test_args(test)), "path": run, "epi": a.epi, "step": step,
                                                     "log": True}))
-    out = {"env": a.env, "n": a.n, "obs": a.obs, "algo": a.algo, "steps": a.steps, "train_wall_s": round(t_train, 1),
+    out = {"env": a.env, "n": a.n, "obs": a.obs, "algo": a.algo, "steps": a.steps, "train_args": extra, "train_wall_s": round(t_train, 1),
            "s_per_iteration": round(t_train / (a.steps + 1), 4),
            "eval_curve": [{k: r[k] for k in ("step", "eval/reward", "eval/cost", "eval/unsafe_frac")} for r in evals],
            "test_untrained_step0": res[0], f"test_step{a.steps}": res[a.steps], "test_epi": a.epi,
+           "train_curve": [(r["step"], round(r["train/reward"], 4), round(r["train/unsafe_frac"], 3)) for r in rows
+                           if "train/reward" in r][::max(1, a.steps // 20)],
            "update_tail": [{k: v for k, v in r.items() if not k.startswith("eval/")} for r in rows
                            if "Vl/loss" in r][-3:]}
     with open(os.path.join(a.out, "learning_run.json"), "w") as f:

@@ -285,3 +285,17 @@ def test_attention_uniform_logits_give_inverse_in_degree(cuda, eid, n, obs):
         want = np.where(valid[:, None, :], 1.0 / np.maximum(deg, 1)[:, None, None], 0.0)
         want = np.broadcast_to(want, attn.shape)
         np.testing.assert_allclose(attn, want, rtol=2e-7, atol=0, err_msg=f"layer {li}")
+
+
+@pytest.mark.parametrize("S,L", [(3, 128), (2, 200)])
+def test_vl_long_scan_matches_oracle(cuda, S, L):
+    """The update's prepass scans Vl over a whole episode (L = T = 128, scan_Vl informarl.py:281-293):
+    every step of a long GRU scan against the float64 oracle."""
+    env, gb, host = _graphs(cuda, "LidarSpread", 4, 2, S, L, seed=11)
+    net = VlNet(env.node_dim, 4, cuda, seed=12, **_nets_kw(env))
+    v, hT, _ = net.seq_fwd(gb, S, L, keep_cache=False)
+    p = R.to_t(net.flax())
+    rv, rh = R.vl_seq(p, host, S, L, 4, return_h=True)
+    torch.cuda.synchronize()
+    _close(v.cpu().numpy(), rv.detach().numpy(), what="Vl over a long scan")
+    _close(hT.cpu().numpy(), rh.detach().numpy(), what="final carry")
