@@ -180,8 +180,8 @@ def _random_flax_trees(spec):
             VhNet(nd, N_AGENTS, 2, "cpu", seed=8).flax()]
 
 
-def read_pmc_traffic():
-    fn = os.path.join(ROOT, "profiles", "env_step_pmc.json")
+def read_pmc_traffic(fn="env_step_pmc.json"):
+    fn = os.path.join(ROOT, "profiles", fn)
     if os.path.exists(fn):
         try:
             return json.load(open(fn)).get("hbm_bytes_per_launch")
@@ -309,7 +309,7 @@ def main():
     from dgppo_fov_amd.trainer.rollout import RolloutEngine
 
     env = make_env(ENV_ID, N_AGENTS, num_obs=N_OBS, device=dev)
-    lanes = int(os.environ.get("DGPPO_BENCH_LANES", "2"))
+    lanes = int(os.environ.get("DGPPO_BENCH_LANES", "1"))  # 1: states-only reset + ONE persistent rollout launch
     eng = RolloutEngine(env, B_PER_GPU, T, dev, env_offset=rank * B_PER_GPU, lanes=lanes)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -341,9 +341,23 @@ def main():
         elapsed = float(t.item())
     step_ms_median = float(np.median([evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]))
 
-    # ---- live kernel timing for the roofline: back-to-back step launches on the launch stream ----
-    n_launch = 4 * T
+    # ---- live kernel timing for the roofline (HIP events on the launch stream) ----
+    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # (a) the dominant kernel: the persistent rollout kernel alone (T steps from the loaded graph 0)
+    roll_ms = None
+    if eng.fused and lanes == 1:
+        rms = []
+        for rep in range(6):
+            ev0.record(stream)
+            env.rollout_into(eng.buf, eng.obstacles, eng.actions, eng.rewards, eng.costs, rebuild_first=False)
+            ev1.record(stream)
+            ev1.synchronize()
+            if rep:
+                rms.append(ev0.elapsed_time(ev1))
+        roll_ms = float(np.median(rms))
+    # (b) the per-step kernel (policy rollouts use it): back-to-back step launches in a hipGraph
+    n_launch = 4 * T
     g_step = None
     cur = eng.graph_at(0)
     outs = [eng.graph_at(1), eng.graph_at(2)]
@@ -373,9 +387,17 @@ def main():
 
     env_steps = args.steps * B_PER_GPU * T * world
     value = env_steps / elapsed
-    bytes_per_launch = BYTES_PER_ENV_STEP * B_PER_GPU
-    achieved = bytes_per_launch / (step_ms * 1e-3) / 1e9
-    traffic = read_pmc_traffic()
+    if roll_ms is not None:  # T transitions per launch
+        bytes_per_launch = BYTES_PER_ENV_STEP * B_PER_GPU * T
+        achieved = bytes_per_launch / (roll_ms * 1e-3) / 1e9
+        kname = "wv::lidar_rollout_wave_kernel<LIDAR,SPREAD,4,3> (persistent: T=128 steps per launch)"
+    else:
+        bytes_per_launch = BYTES_PER_ENV_STEP * B_PER_GPU
+        achieved = bytes_per_launch / (step_ms * 1e-3) / 1e9
+        kname = "wv::lidar_step_wave_kernel<LIDAR,SPREAD,4,3,false>"
+    step_achieved = BYTES_PER_ENV_STEP * B_PER_GPU / (step_ms * 1e-3) / 1e9
+    traffic = read_pmc_traffic("r02_env_rollout_pmc.json" if roll_ms is not None else "env_step_pmc.json")
+    fused = eng.fused and lanes == 1
     del eng, outs, cur, g_step
     ppo = ppo_bench(env, dev, world, rank, args.ppo_iters) if args.ppo_iters > 0 else None
     if rank == 0:
@@ -397,9 +419,12 @@ def main():
                 "workload": f"{ENV_ID} n={N_AGENTS} obs={N_OBS} rays=32 top_k=8, {B_PER_GPU} envs/GPU, "
                             f"1 step = reset + T={T} fused env steps into the (B,T+1) rollout buffer",
                 "env": ENV_ID, "num_agents": N_AGENTS, "n_obs": N_OBS, "n_env_per_gpu": B_PER_GPU, "T": T,
-                "hip_graph": use_graph, "stream_lanes": lanes, "parallelism": f"dp{world} (env-sharded, no collective)",
+                "hip_graph": use_graph, "stream_lanes": lanes, "persistent_rollout": fused,
+                "parallelism": f"dp{world} (env-sharded, no collective)",
             },
             "env_step_kernel_us": round(step_ms * 1e3, 3),
+            "env_step_kernel_gbs": round(step_achieved, 1),  # the per-step kernel the policy rollouts launch
+            "env_rollout_kernel_us": None if roll_ms is None else round(roll_ms * 1e3, 2),
             # whole timed region (reset + T steps, 2 env slices on 2 streams) at the per-transition bytes
             "rollout_effective_hbm_gbs": round(value / world * BYTES_PER_ENV_STEP / 1e9, 1),
             "ppo_updates_per_s": None if ppo is None else ppo["updates_per_s"],
@@ -411,7 +436,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "wv::lidar_step_wave_kernel<LIDAR,SPREAD,4,3,false>",
+                "kernel": kname,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "cpu_baseline": cpu_env,

@@ -104,6 +104,16 @@ class EnvResetIO(ctypes.Structure):
     ]
 
 
+class EnvRolloutIO(ctypes.Structure):
+    _fields_ = [
+        ("step", EnvStepIO),
+        ("T", ctypes.c_int32), ("rebuild_first", ctypes.c_int32),
+        ("t_states", ctypes.c_int64), ("t_nodes", ctypes.c_int64), ("t_edges", ctypes.c_int64),
+        ("t_index", ctypes.c_int64), ("t_action", ctypes.c_int64), ("t_reward", ctypes.c_int64),
+        ("t_cost", ctypes.c_int64),
+    ]
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32), ("batch", ctypes.c_int32),
@@ -215,6 +225,8 @@ SIGNATURES = {
     "dgppo_env_step": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvStepIO), ctypes.c_void_p]),
     "dgppo_env_set_step_kernel": (ctypes.c_int, [ctypes.c_int]),
     "dgppo_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvResetIO), ctypes.c_void_p]),
+    "dgppo_env_reset_states": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvResetIO), ctypes.c_void_p]),
+    "dgppo_env_rollout": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvRolloutIO), ctypes.c_void_p]),
     "dgppo_gemm_workspace_floats": (ctypes.c_int64, [ctypes.POINTER(GemmArgs)]),
     "dgppo_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), ctypes.c_void_p]),
     "dgppo_gnn_attn_fwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
@@ -256,7 +268,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 3  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 4  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

@@ -665,9 +665,15 @@ struct Carve {
   static constexpr int total = (uni + uni_size + 3) & ~3;
 };
 
-// REBUILD: the graph of the given states (reset: y = x, no reward / cost), else one env step.
-template <int ENGINE, int GOAL, int SD, int O, bool REBUILD = false>
-__global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+// One env step of the wave-per-env kernel for this wave's env (the 4 waves of a workgroup pool their
+// ray casts, so all four call it together).  REBUILD: the graph of the given states (reset: y = x, no
+// reward / cost), else one env step.  LOAD: read the current agent / goal rows, current hits,
+// obstacles and ray table from HBM (io.states / io.obstacles / io.ray_dirs); otherwise they are the
+// LDS state the previous call left (persistent rollout: next agent rows and next hits become current,
+// obstacles and rays stay staged), and only the action comes from HBM.
+template <int ENGINE, int GOAL, int SD, int O, bool REBUILD, bool LOAD>
+__device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_env_step_io& io, float* smem,
+                                          int* wg_items) {
   static_assert(O >= 1 && O <= 4, "obstacle records are staged by one load per lane");
   // LidarOmniTarget (SD 7, own goals): omni dynamics, 5 costs, 10-wide edges; same LiDAR and graph rows
   constexpr bool OMNI = ENGINE == DGPPO_ENGINE_OMNI;
@@ -675,13 +681,15 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
   constexpr int AD = OMNI ? 3 : 2;   // action width
   constexpr int ED = OMNI ? 10 : 4;  // edge width
   constexpr int XS = 16 * SD - 64;   // agent + goal state floats past the first 64
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int wg_items[4];
   using C = Carve<SD, O>;
   constexpr int N = C::N, ND = C::ND, pad = N - 1;
   constexpr int n_ag = GOAL == DGPPO_GOAL_SPREAD ? NA * NA : NA;
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  int tid = threadIdx.x;
+  // persistent loop: an opaque thread id per step keeps the per-lane addressing inside the loop (hoisted,
+  // it costs ~80 VGPRs and a wave per SIMD of occupancy)
+  if constexpr (!LOAD) asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid) >> 6;
   const int64_t env_raw = (int64_t)blockIdx.x * 4 + wid;
   // a wave past the last env replays the last env without storing anything: it must still join
   // the two workgroup barriers around the pooled ray cast
@@ -691,25 +699,34 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
   const int gi = lane >> 3, gj = lane & 7;
 
   // ---- A: every global load first (unconditional, clamped addresses), then stage in LDS -------
-  const float* st = io.states + env * io.states_stride;
-  const float* ob = io.obstacles + env * io.obstacles_stride;
   const float* ac = io.action + env * io.action_stride;
-  const float cv0 = st[lane];
-  const int xsl = 64 + (lane < XS ? lane : XS - 1);
-  const float cv1 = XS > 0 ? st[xsl] : 0.0f;
-  const float hcx = st[(16 + lane) * SD + 0], hcy = st[(16 + lane) * SD + 1];
-  const float obv = ob[lane < O * DGPPO_OBST_FIELDS ? lane : 0];
-  const float rdv = io.ray_dirs[lane];
   const float a0 = clampf_nan(ac[AD * gj + 0], -1.0f, 1.0f), a1 = clampf_nan(ac[AD * gj + 1], -1.0f, 1.0f);
   const float aw = OMNI ? clampf_nan(ac[AD * gj + AD - 1], -1000.0f, 1000.0f) : 0.0f;  // omni alpha
-  // unconditional LDS stores: a store under a lane predicate lets the compiler sink its global load
-  // into the predicated block, serialising a second HBM round trip
-  lds[C::cur + lane] = cv0;
-  if (XS > 0) lds[C::cur + xsl] = cv1;
-  // omni obstacle cost reads every current hit: staged in the next-hit rows (rewritten in E)
-  if (OMNI) reinterpret_cast<float2*>(lds + C::hits)[lane] = make_float2(hcx, hcy);
-  lds[C::obst + lane] = obv;  // lanes >= 16 O land in evec / rays, both written after this
-  lds[C::rays + lane] = rdv;
+  float hcx, hcy;
+  if constexpr (LOAD) {
+    const float* st = io.states + env * io.states_stride;
+    const float* ob = io.obstacles + env * io.obstacles_stride;
+    const float cv0 = st[lane];
+    const int xsl = 64 + (lane < XS ? lane : XS - 1);
+    const float cv1 = XS > 0 ? st[xsl] : 0.0f;
+    hcx = st[(16 + lane) * SD + 0], hcy = st[(16 + lane) * SD + 1];
+    const float obv = ob[lane < O * DGPPO_OBST_FIELDS ? lane : 0];
+    const float rdv = io.ray_dirs[lane];
+    // unconditional LDS stores: a store under a lane predicate lets the compiler sink its global load
+    // into the predicated block, serialising a second HBM round trip
+    lds[C::cur + lane] = cv0;
+    if (XS > 0) lds[C::cur + xsl] = cv1;
+    // omni obstacle cost reads every current hit: staged in the next-hit rows (rewritten in E)
+    if (OMNI) reinterpret_cast<float2*>(lds + C::hits)[lane] = make_float2(hcx, hcy);
+    lds[C::obst + lane] = obv;  // lanes >= 16 O land in evec / rays, both written after this
+    lds[C::rays + lane] = rdv;
+  } else {
+    // persistent rollout: the previous step's next agent rows are this step's current rows (goals,
+    // obstacles and rays unchanged); its hits (rows 16 + lane of its graph) are the current hits
+    if (lane < NA * SD) lds[C::cur + lane] = lds[C::nxt + lane];
+    const float2 hc = reinterpret_cast<const float2*>(lds + C::hits)[lane];
+    hcx = hc.x, hcy = hc.y;
+  }
   wave_sync();
   const float* cur = lds + C::cur;
   const float* goal = cur + NA * SD;
@@ -1177,10 +1194,9 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     }
   }
   wave_sync();
-  if (!live) return;
 
   // ---- F2: the lidar-dependent columns: hit coordinates, agent-lidar edge offsets and masks -------
-  {
+  if (live) {
     const float2 hl = reinterpret_cast<const float2*>(hits)[lane];
     const float f0 = si[0] - hl.x;
     const float f1 = si[1] - hl.y;
@@ -1195,6 +1211,71 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
     no[(16 + lane) * ND + 1] = hl.y;
     so[(16 + lane) * SD + 0] = hl.x;
     so[(16 + lane) * SD + 1] = hl.y;
+  }
+}
+
+// One env step (REBUILD: the graph of the given states) for io.n_env envs, 4 per workgroup.
+template <int ENGINE, int GOAL, int SD, int O, bool REBUILD = false>
+__global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int wg_items[4];
+  wave_body<ENGINE, GOAL, SD, O, REBUILD, true>(cfg, io, smem, wg_items);
+}
+
+// Persistent rollout: T env steps per launch, a wave per env for the whole episode (the reference's
+// lax.scan over env.step, trainer/utils.py:45-55, with the actions given).  Agent rows, hits,
+// obstacles and rays stay in LDS between steps: per step the wave reads its env's actions (T, B, n, A)
+// and writes graph t+1's rows into the time-major (T+1, B) buffer, reward[t] and cost[t].  No launch
+// per step, and the 4096 waves drift out of phase, so one wave's store drain overlaps another's compute.
+// rebuild_first: graph 0 is first built from its agent / goal / obstacle rows (after a states-only
+// reset), else its current rows are loaded.
+// (4 waves per SIMD: the whole 4096-env batch resident at once, as for the per-step kernel; without the
+// bound the loop's hoisted addressing takes ~150 VGPRs and a quarter of the workgroups would run after
+// the rest had finished their episodes)
+template <int ENGINE, int GOAL, int SD, int O>
+__global__ __launch_bounds__(256) void lidar_rollout_wave_kernel(
+    dgppo_env_cfg cfg, dgppo_env_rollout_io r) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int wg_items[4];
+  const dgppo_env_step_io& g0 = r.step;
+  if (r.rebuild_first) {
+    wave_body<ENGINE, GOAL, SD, O, true, true>(cfg, g0, smem, wg_items);
+  } else {  // stage graph 0's rows exactly as the LOAD prologue of a step does
+    using C = Carve<SD, O>;
+    constexpr int XS = 16 * SD - 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t env_raw = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t env = env_raw < g0.n_env ? env_raw : g0.n_env - 1;
+    float* lds = smem + wid * C::total;
+    const float* st = g0.states + env * g0.states_stride;
+    const float* ob = g0.obstacles + env * g0.obstacles_stride;
+    const float cv0 = st[lane];
+    const int xsl = 64 + (lane < XS ? lane : XS - 1);
+    const float cv1 = XS > 0 ? st[xsl] : 0.0f;
+    const float hcx = st[(16 + lane) * SD + 0], hcy = st[(16 + lane) * SD + 1];
+    const float obv = ob[lane < O * DGPPO_OBST_FIELDS ? lane : 0];
+    const float rdv = g0.ray_dirs[lane];
+    reinterpret_cast<float2*>(lds + C::hits)[lane] = make_float2(hcx, hcy);
+    lds[C::obst + lane] = obv;
+    lds[C::rays + lane] = rdv;
+    // the current agent rows go to the NEXT-row slot: the first step copies them over (goals in place)
+    if (lane < NA * SD) lds[C::nxt + lane] = cv0;
+    lds[C::cur + lane] = cv0;
+    if (XS > 0) lds[C::cur + xsl] = cv1;
+    wave_sync();
+  }
+#pragma clang loop unroll(disable)
+  for (int t = 0; t < r.T; ++t) {
+    dgppo_env_step_io q = g0;
+    q.action = g0.action + t * r.t_action;
+    q.nodes = g0.nodes + (t + 1) * r.t_nodes;
+    q.edges = g0.edges + (t + 1) * r.t_edges;
+    q.out_states = g0.out_states + (t + 1) * r.t_states;
+    q.receivers = g0.receivers + (t + 1) * r.t_index;
+    q.senders = g0.senders + (t + 1) * r.t_index;
+    q.reward = g0.reward + t * r.t_reward;
+    q.cost = g0.cost + t * r.t_cost;
+    wave_body<ENGINE, GOAL, SD, O, false, false>(cfg, q, smem, wg_items);
   }
 }
 
@@ -1920,6 +2001,68 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
   const size_t shmem = (size_t)cv.total * sizeof(float);
   dispatch_step(*cfg, *io, shmem, (hipStream_t)stream);
   return (int)hipGetLastError();
+}
+
+static bool wave_config(const dgppo_env_cfg* cfg) {
+  const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
+  return lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
+         wave_step_enabled();
+}
+
+extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {
+  if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
+  if (!wave_config(cfg)) return dgppo_env_reset(cfg, io, stream);
+  if (io->n_env == 0) return 0;
+  if (!io->out_states || !io->obstacles) return DGPPO_EINVAL;
+  const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k, true);
+  const size_t shmem = ((size_t)cv.total + 2 * kSampTab) * sizeof(float);
+  dispatch_reset(*cfg, *io, shmem, (hipStream_t)stream, 1);
+  return (int)hipGetLastError();
+}
+
+template <int ENGINE, int GOAL, int SD>
+static void launch_rollout(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, hipStream_t s) {
+  const size_t sh = 4 * sizeof(float) * wv::Carve<SD, 3>::total;
+  hipLaunchKernelGGL((wv::lidar_rollout_wave_kernel<ENGINE, GOAL, SD, 3>), dim3((unsigned)((r.step.n_env + 3) / 4)),
+                     dim3(256), sh, s, c, r);
+}
+
+extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollout_io* r, void* stream) {
+  if (validate(cfg) || !r || r->T < 0 || r->step.n_env < 0) return DGPPO_EINVAL;
+  const dgppo_env_step_io& io = r->step;
+  if (r->T == 0 && !r->rebuild_first) return 0;
+  if (io.n_env == 0) return 0;
+  if (!io.states || !io.action || !io.nodes || !io.edges || !io.out_states || !io.receivers || !io.senders ||
+      !io.reward || !io.cost)
+    return DGPPO_EINVAL;
+  const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
+  if (lidar && (!io.obstacles || !io.ray_dirs)) return DGPPO_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  if (wave_config(cfg)) {
+    const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
+    if (cfg->engine == DGPPO_ENGINE_OMNI) launch_rollout<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD>(*cfg, *r, s);
+    else if (cfg->engine == DGPPO_ENGINE_BICYCLE && spread) launch_rollout<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(*cfg, *r, s);
+    else if (cfg->engine == DGPPO_ENGINE_BICYCLE) launch_rollout<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(*cfg, *r, s);
+    else if (spread) launch_rollout<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(*cfg, *r, s);
+    else launch_rollout<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(*cfg, *r, s);
+    return (int)hipGetLastError();
+  }
+  // other configs: the per-step kernel T times (a rebuild_first request got a full reset already)
+  for (int t = 0; t < r->T; ++t) {
+    dgppo_env_step_io q = io;
+    q.states = io.out_states + t * r->t_states;
+    q.action = io.action + t * r->t_action;
+    q.nodes = io.nodes + (t + 1) * r->t_nodes;
+    q.edges = io.edges + (t + 1) * r->t_edges;
+    q.out_states = io.out_states + (t + 1) * r->t_states;
+    q.receivers = io.receivers + (t + 1) * r->t_index;
+    q.senders = io.senders + (t + 1) * r->t_index;
+    q.reward = io.reward + t * r->t_reward;
+    q.cost = io.cost + t * r->t_cost;
+    const int rc = dgppo_env_step(cfg, &q, stream);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {

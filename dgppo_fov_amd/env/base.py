@@ -297,6 +297,38 @@ class MultiAgentEnv(ABC):
                                   g.receivers, g.senders)
         return self._assemble(g.nodes, g.edges, g.states, g.receivers, g.senders, ob)
 
+    def reset_states(self, key, n_env: int, env_offset: int = 0, out: Optional[GraphsTuple] = None,
+                     obstacles_out: Optional[torch.Tensor] = None) -> GraphsTuple:
+        """The sampling half of `reset` (torch.ops.dgppo.env_reset_states): obstacles and the agent / goal
+        state rows only; `rollout_into(..., rebuild_first=True)` builds graph 0 from them.  Configs
+        without the persistent rollout kernel get the full reset."""
+        dev = self.device if out is None else out.nodes.device
+        _lib.require_gpu(dev, "env.reset_states")
+        g = self.empty_graph((n_env,), dev) if out is None else out
+        ob = obstacles_out
+        if ob is None and self._obstacle_fields() > 0:
+            ob = torch.empty((n_env, max(self.n_obs, 1), self._obstacle_fields()), dtype=torch.float32, device=dev)
+        tkey = key if isinstance(key, torch.Tensor) else None
+        seed = 0 if tkey is not None else int(key) & 0xFFFFFFFFFFFFFFFF
+        torch.ops.dgppo.env_reset_states(self._cfg_handle, tkey, seed if seed < 2 ** 63 else seed - 2 ** 64,
+                                         int(env_offset), int(n_env), ob, self._ray_table(dev), g.nodes, g.edges,
+                                         g.states, g.receivers, g.senders)
+        return self._assemble(g.nodes, g.edges, g.states, g.receivers, g.senders, ob)
+
+    def rollout_into(self, buf: GraphsTuple, obstacles: Optional[torch.Tensor], actions: torch.Tensor,
+                     rewards: torch.Tensor, costs: torch.Tensor, rebuild_first: bool = False) -> None:
+        """T env steps with the given actions (T, B, n, A) in one call (torch.ops.dgppo.env_rollout): buf is
+        a time-major (T+1, B, ...) graph buffer, step t reads buf[t] and writes buf[t+1], rewards[t],
+        costs[t] -- the env half of the reference's rollout scan (trainer/utils.py:45-55)."""
+        _lib.require_gpu(buf.states.device, "env.rollout")
+        n, A = self._num_agents, self.action_dim
+        T = actions.shape[0]
+        if actions.shape[-2:] != (n, A) or buf.states.shape[0] != T + 1 or buf.states.dim() != 4:
+            raise ValueError("rollout_into: actions (T, B, n, A) and a (T+1, B, N, sd) graph buffer")
+        torch.ops.dgppo.env_rollout(self._cfg_handle, bool(rebuild_first), obstacles, actions,
+                                    self._ray_table(buf.states.device), buf.nodes, buf.edges, buf.states,
+                                    buf.receivers, buf.senders, rewards, costs)
+
     def step_into(self, graph: GraphsTuple, action: torch.Tensor, out: GraphsTuple,
                   reward: torch.Tensor, cost: torch.Tensor) -> GraphsTuple:
         """One fused HIP step (torch.ops.dgppo.env_step) writing into caller-owned buffers (views into a

@@ -9,6 +9,8 @@ non-CUDA tensor raises NativeLibraryError (`_lib.require_gpu`).
 
   dgppo::env_reset      dgppo_env_reset      vmap(env.reset)      lidar_env/base.py:89-124, mpe/base.py:81-127
   dgppo::env_step       dgppo_env_step       vmap(env.step)       lidar_env/base.py:151-174, mpe/base.py:137-158
+  dgppo::env_reset_states dgppo_env_reset_states  the sampling half of env_reset (no graph)
+  dgppo::env_rollout    dgppo_env_rollout    lax.scan of env.step over T given actions, trainer/utils.py:45-55
   dgppo::gnn_attn_fwd   dgppo_gnn_attn_fwd   GraphTransformer attention core, gnn.py:83-117
   dgppo::gnn_attn_bwd   dgppo_gnn_attn_bwd   its gradient (the jax.grad of update_Vl / update_policy)
   dgppo::gae            dgppo_gae            compute_dec_ocp_gae, algo/utils.py:11-79
@@ -105,9 +107,21 @@ def env_reset(cfg: int, key: Optional[Tensor], seed: int, env_offset: int, n_env
     """Reset n_env envs (env b draws from Philox keyed (seed or *key, env_offset + b)) and write the
     initial graph.  `key`: optional 1-element int64 device tensor read at run time (hipGraph replays)."""
     _lib.require_gpu(nodes.device, "dgppo::env_reset")
+    io = _reset_io(key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states, receivers, senders)
+    _lib.check(_lib.load().dgppo_env_reset(ctypes.byref(env_cfg(cfg)), ctypes.byref(io), _stream(nodes)),
+               "dgppo_env_reset")
+
+
+@env_reset.register_fake
+def _env_reset_fake(cfg, key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states, receivers,
+                    senders) -> None:
+    return None
+
+
+def _reset_io(key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states, receivers, senders):
     io = _lib.EnvResetIO()
     if key is not None:
-        if key.device != nodes.device or key.numel() != 1 or key.dtype not in (torch.int64, torch.uint64):
+        if key.device != out_states.device or key.numel() != 1 or key.dtype not in (torch.int64, torch.uint64):
             raise ValueError("tensor key must be a 1-element int64 tensor on the env's device")
         io.seed, io.seed_ptr = 0, key.data_ptr()
     else:
@@ -122,13 +136,67 @@ def env_reset(cfg: int, key: Optional[Tensor], seed: int, env_offset: int, n_env
     io.receivers, io.senders = _p(receivers), _p(senders)
     io.edge_index_stride = _stride(receivers, 1)
     io.n_env = int(n_env)
-    _lib.check(_lib.load().dgppo_env_reset(ctypes.byref(env_cfg(cfg)), ctypes.byref(io), _stream(nodes)),
-               "dgppo_env_reset")
+    return io
 
 
-@env_reset.register_fake
-def _env_reset_fake(cfg, key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states, receivers,
-                    senders) -> None:
+@torch.library.custom_op("dgppo::env_reset_states", mutates_args=("obstacles", "nodes", "edges", "out_states",
+                                                                   "receivers", "senders"))
+def env_reset_states(cfg: int, key: Optional[Tensor], seed: int, env_offset: int, n_env: int,
+                     obstacles: Optional[Tensor], ray_dirs: Tensor, nodes: Tensor, edges: Tensor, out_states: Tensor,
+                     receivers: Tensor, senders: Tensor) -> None:
+    """env_reset's sampling half: obstacle records and agent / goal state rows (configs without the
+    persistent rollout kernel: the full reset).  Pair with env_rollout(rebuild_first=True)."""
+    _lib.require_gpu(out_states.device, "dgppo::env_reset_states")
+    io = _reset_io(key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states, receivers, senders)
+    _lib.check(_lib.load().dgppo_env_reset_states(ctypes.byref(env_cfg(cfg)), ctypes.byref(io), _stream(out_states)),
+               "dgppo_env_reset_states")
+
+
+@env_reset_states.register_fake
+def _env_reset_states_fake(cfg, key, seed, env_offset, n_env, obstacles, ray_dirs, nodes, edges, out_states,
+                           receivers, senders) -> None:
+    return None
+
+
+@torch.library.custom_op("dgppo::env_rollout", mutates_args=("nodes", "edges", "states", "receivers", "senders",
+                                                              "reward", "cost"))
+def env_rollout(cfg: int, rebuild_first: bool, obstacles: Optional[Tensor], actions: Tensor, ray_dirs: Tensor,
+                nodes: Tensor, edges: Tensor, states: Tensor, receivers: Tensor, senders: Tensor, reward: Tensor,
+                cost: Tensor) -> None:
+    """T env steps with given actions (T, B, n, A) through time-major graph buffers (T+1, B, ...):
+    step t reads graph t and writes graph t+1, reward[t] (T, B), cost[t] (T, B, n, n_cost).
+    rebuild_first: graph 0's rows are first built from its agent / goal states (env_reset_states)."""
+    _lib.require_gpu(states.device, "dgppo::env_rollout")
+    T = int(actions.shape[0])
+    if states.shape[0] != T + 1 or reward.shape[0] != T or cost.shape[0] != T:
+        raise ValueError("env_rollout: graph buffers must hold T+1 graphs, actions / reward / cost T steps")
+    r = _lib.EnvRolloutIO()
+    io = r.step
+    io.states, io.states_stride = _p(states), _stride(states[0], 2)
+    io.obstacles = _p(obstacles)
+    io.obstacles_stride = obstacles.stride(-3) if obstacles is not None else 0
+    io.action, io.action_stride = _p(actions), _stride(actions[0], 2)
+    io.ray_dirs = _p(ray_dirs)
+    io.nodes, io.nodes_stride = _p(nodes), _stride(nodes[0], 2)
+    io.edges, io.edges_stride = _p(edges), _stride(edges[0], 2)
+    io.out_states, io.out_states_stride = _p(states), _stride(states[0], 2)
+    io.receivers, io.senders = _p(receivers), _p(senders)
+    io.edge_index_stride = _stride(receivers[0], 1)
+    io.reward, io.reward_stride = _p(reward), reward.stride(1)
+    io.cost, io.cost_stride = _p(cost), _stride(cost[0], 2)
+    io.n_env = int(states.shape[1])
+    r.T, r.rebuild_first = T, int(bool(rebuild_first))
+    r.t_states, r.t_nodes, r.t_edges = states.stride(0), nodes.stride(0), edges.stride(0)
+    if receivers.stride(0) != senders.stride(0):
+        raise ValueError("env_rollout: receivers and senders need the same time stride")
+    r.t_index, r.t_action, r.t_reward, r.t_cost = receivers.stride(0), actions.stride(0), reward.stride(0), cost.stride(0)
+    _lib.check(_lib.load().dgppo_env_rollout(ctypes.byref(env_cfg(cfg)), ctypes.byref(r), _stream(states)),
+               "dgppo_env_rollout")
+
+
+@env_rollout.register_fake
+def _env_rollout_fake(cfg, rebuild_first, obstacles, actions, ray_dirs, nodes, edges, states, receivers, senders,
+                      reward, cost) -> None:
     return None
 
 

@@ -31,14 +31,16 @@ class RolloutEngine:
     MODE_RANDOM, MODE_SAMPLE, MODE_DET = -1, 1, 0
 
     def __init__(self, env: MultiAgentEnv, n_env: int, T: Optional[int] = None, device=None, env_offset: int = 0,
-                 actor=None, mode: int = -1, lanes: int = 1):
+                 actor=None, mode: int = -1, lanes: int = 1, fused: bool = True):
         """actor: an ActorNet (or None); mode: MODE_SAMPLE (stochastic policy, sample_action),
         MODE_DET (deterministic policy, get_action) or MODE_RANDOM (keep `self.actions` as given).
         lanes: split the envs into that many contiguous slices, each running its T (act, step) pairs
         on its own HIP stream after the shared reset, so one slice's launch ramp and store drain
         overlap the other's compute (envs are independent: results are identical).  With an actor
         this needs the fused policy step (it reads only the prepared query-key workspace); the T
-        sampling-noise tensors are drawn up front with the same Philox stream ids."""
+        sampling-noise tensors are drawn up front with the same Philox stream ids.
+        fused: an env-only (MODE_RANDOM, one lane) rollout runs as a states-only reset plus one persistent
+        dgppo_env_rollout launch for all T steps (else reset + T step launches; identical results)."""
         self.env = env
         self.B = int(n_env)
         self.T = int(T or env.max_episode_steps)
@@ -60,6 +62,7 @@ class RolloutEngine:
             self.log_pis = torch.zeros((T, B, n), dtype=torch.float32, device=dev)
             self.noise = torch.empty((B * n, env.action_dim), dtype=torch.float32, device=dev)
         self._hip_graph = None
+        self.fused = bool(fused)
         self.lanes = int(lanes)
         if self.lanes > 1 and B % self.lanes:
             raise ValueError(f"n_env {B} is not a multiple of lanes {self.lanes}")
@@ -106,6 +109,13 @@ class RolloutEngine:
 
     def _run(self):
         env = self.env
+        if self.mode == self.MODE_RANDOM and self.lanes == 1 and self.fused:
+            # env-only rollout: the states-only reset + ONE persistent launch for all T steps (graph 0 built
+            # by the rollout kernel; configs without it loop the step kernel inside the call)
+            env.reset_states(self.key, n_env=self.B, env_offset=self.env_offset, out=self.graph_at(0),
+                             obstacles_out=self.obstacles)
+            env.rollout_into(self.buf, self.obstacles, self.actions, self.rewards, self.costs, rebuild_first=True)
+            return
         cur = env.reset(self.key, n_env=self.B, env_offset=self.env_offset, out=self.graph_at(0),
                         obstacles_out=self.obstacles)
         if self.lanes > 1:

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 3  /* 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 4  /* 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -148,6 +148,29 @@ typedef struct dgppo_env_reset_io {
 } dgppo_env_reset_io;
 
 int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream);
+
+/* The sampling half of dgppo_env_reset: obstacle records and the agent / goal rows of `out_states`
+ * only (no graph); dgppo_env_rollout with rebuild_first = 1 then builds graph 0 itself.  Configs
+ * without a persistent rollout kernel get the full reset (the graph is written too). */
+int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream);
+
+/* T env steps with given actions in one call: replaces the env half of the reference's rollout scan
+ * `lax.scan(body, ...)` over env.step (dgppo/trainer/utils.py:45-55) for a fixed action sequence.
+ * `step` describes graph 0 and step 0: graph t's rows live at the graph pointers + t * t_<field>
+ * (states / nodes / edges / receivers+senders, element strides, e.g. a time-major (T+1, B, ...)
+ * buffer), the actions of step t at action + t * t_action, reward[t] / cost[t] at + t * t_reward /
+ * t_cost.  Step t reads graph t and writes graph t+1, reward[t], cost[t]; rebuild_first = 1 first
+ * writes graph 0's rows from its agent / goal states and obstacles (after dgppo_env_reset_states).
+ * Lidar configs at n = 8, 32 rays, top-8, 3 obstacles run one persistent kernel (a wave per env for
+ * all T steps, state in LDS); others loop dgppo_env_step (identical results). */
+typedef struct dgppo_env_rollout_io {
+  dgppo_env_step_io step;   /* graph 0 in / out (states == out_states), actions / reward / cost of step 0 */
+  int32_t T;
+  int32_t rebuild_first;
+  int64_t t_states, t_nodes, t_edges, t_index, t_action, t_reward, t_cost;
+} dgppo_env_rollout_io;
+
+int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollout_io* io, void* stream);
 
 /* ---- hot path (2): DGPPO update building blocks ------------------------------------------------
  * Batched fp32 GEMM on the matrix cores (v_mfma_f32_32x32x2_f32):

@@ -151,3 +151,49 @@ def test_policy_rollout_lanes_bit_exact(cuda, env_id, graph):
                                                   eng.rnn, eng.rewards, eng.costs)])
         for x, y in zip(*outs):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("eid,n,obs,B", [("LidarSpread", 8, 3, 255), ("LidarTarget", 8, 3, 64),
+                                         ("LidarBicycleTarget", 8, 3, 130), ("LidarOmniTarget", 8, 3, 97),
+                                         ("MPESpread", 3, 3, 33), ("LidarSpread", 4, 2, 20)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_persistent_env_rollout_bit_exact(cuda, eid, n, obs, B, graph):
+    """The env-only rollout as ONE persistent launch (states-only reset + dgppo_env_rollout, a wave per
+    env for all T steps with its state in LDS) writes the same (T+1, B) graphs, rewards and costs as
+    reset + T single-step launches, bit for bit -- also for partial workgroups and, through the
+    per-step fallback, configs without the persistent kernel."""
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    T = 24
+    outs = []
+    for fused in (False, True):
+        eng = RolloutEngine(env, B, T, cuda, fused=fused)
+        gen = torch.Generator(device=cuda)
+        gen.manual_seed(9)
+        eng.actions.uniform_(-1.2, 1.2, generator=gen)  # includes out-of-range actions (clipped)
+        if graph:
+            eng.capture()
+        eng.run(key=21)
+        torch.cuda.synchronize(cuda)
+        b = eng.buf
+        outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders, eng.rewards,
+                                              eng.costs)])
+    for k, (x, y) in enumerate(zip(*outs)):
+        assert np.array_equal(x, y), k
+
+
+def test_persistent_env_rollout_from_a_loaded_graph(cuda):
+    """rebuild_first = False: the kernel loads graph 0's rows (a full reset) instead of rebuilding them."""
+    env = make_env("LidarSpread", 8, num_obs=3, device=cuda)
+    B, T = 64, 10
+    ref = RolloutEngine(env, B, T, cuda, fused=False)
+    ref.actions.uniform_(-1, 1)
+    ref.run(key=4)
+    buf = env.empty_graph((T + 1, B), cuda)
+    g0 = env.reset(4, n_env=B, out=env._assemble(buf.nodes[0], buf.edges[0], buf.states[0], buf.receivers[0],
+                                                 buf.senders[0], None))
+    rw, cs = torch.empty_like(ref.rewards), torch.empty_like(ref.costs)
+    env.rollout_into(buf, env._obstacles_of(g0), ref.actions, rw, cs, rebuild_first=False)
+    torch.cuda.synchronize(cuda)
+    for f in ("nodes", "edges", "states", "receivers", "senders"):
+        assert torch.equal(getattr(buf, f), getattr(ref.buf, f)), f
+    assert torch.equal(rw, ref.rewards) and torch.equal(cs, ref.costs)
