@@ -291,6 +291,21 @@ class DGPPO:
     def _allreduce_grads(self):
         allreduce_mean_(self.grad_flat, self.world)
 
+    def _start_reduce(self, net, pending: list):
+        """Start the (sum) all-reduce of one net's gradient bucket as soon as its backward is done, so it
+        travels over xGMI (RCCL's stream) while the next net's forward / backward runs; `_finish_reduce`
+        waits for every bucket and scales by 1/world before clip + Adam (same result as one flat
+        all-reduce: each bucket is reduced exactly once)."""
+        if self.world > 1:
+            pending.append(dist.all_reduce(net.ps.grad, op=dist.ReduceOp.SUM, async_op=True))
+
+    def _finish_reduce(self, pending: list):
+        if self.world > 1:
+            for w in pending:
+                w.wait()
+            pending.clear()
+            self.grad_flat.mul_(1.0 / self.world)
+
     def update(self, rollout: Rollout, step: int) -> dict:
         env, dev = self._env, self.device
         B, T = rollout.rewards.shape
@@ -354,6 +369,8 @@ class DGPPO:
                 ph.mark("Vl_fwd")
                 self.Vl.seq_bwd(cache, dv)
                 del cache
+                pending = []
+                self._start_reduce(self.Vl, pending)
                 ph.mark("Vl_bwd")
                 # update_Vh (dgppo.py:296-321) on the deterministic rollout
                 gd = self._graphs(det.graph, envs)
@@ -365,6 +382,7 @@ class DGPPO:
                 ph.mark("Vh_fwd")
                 self.Vh.bwd(cache, dvh)
                 del cache
+                self._start_reduce(self.Vh, pending)
                 ph.mark("Vh_bwd")
                 # update_policy (informarl.py:405-457)
                 acts = rollout.actions.index_select(0, envs).reshape(-1, self._action_dim).contiguous()
@@ -378,9 +396,11 @@ class DGPPO:
                 ph.mark("pi_fwd")
                 self.actor.eval_seq_bwd(cache, dlp, dent)
                 del cache
+                self._start_reduce(self.actor, pending)
                 ph.mark("pi_bwd")
-                # one all-reduce for the three nets, then clip + finite check + Adam per net
-                self._allreduce_grads()
+                # the three gradient buckets reduced (overlapped with the later nets' passes), then clip +
+                # finite check + Adam per net
+                self._finish_reduce(pending)
                 if self.trace is not None:
                     self.trace["mb"].append(dict(
                         envs=bi.copy(), grad=self.grad_flat.clone(), vl_loss=vl_loss.clone(), vh_loss=vh_loss.clone(),

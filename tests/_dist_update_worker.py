@@ -1,0 +1,53 @@
+"""One rank of tests/test_distributed_gpu.py (started as a subprocess with RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT set): gloo process group, all ranks on cuda:0, DGPPO collect on the rank's
+env shard + one traced update; saves the shard's rollouts, the reduced minibatch gradient and the
+parameters after Adam to <out>/rank<r>.pt.  Test infrastructure, not a product entry point."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from dgppo_fov_amd.algo import make_algo  # noqa: E402
+from dgppo_fov_amd.env import make_env  # noqa: E402
+
+ENV, N, OBS, B_LOCAL, T, L = "LidarSpread", 3, 2, 4, 32, 16
+
+
+def host(r):
+    f = lambda G: {k: getattr(G, k).detach().cpu().clone() for k in ("nodes", "edges", "states", "receivers",  # noqa
+                                                                     "senders")}
+    return dict(graph=f(r.graph), next_graph=f(r.next_graph), actions=r.actions.cpu().clone(),
+                rnn_states=r.rnn_states.cpu().clone(), rewards=r.rewards.cpu().clone(), costs=r.costs.cpu().clone(),
+                dones=r.dones.cpu().clone(), log_pis=None if r.log_pis is None else r.log_pis.cpu().clone())
+
+
+def main(out):
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    env = make_env(ENV, N, num_obs=OBS, max_step=T, device=dev)
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=N, batch_size=B_LOCAL * T * world, rnn_step=L,
+                     train_steps=100, seed=1, device=dev)
+    assert algo.world == world and algo.rank == rank
+    roll = algo.collect(algo.params, 7, n_env=B_LOCAL)  # env shard [rank B, (rank + 1) B)
+    saved = host(roll)
+    algo.trace = {}
+    info = algo.update(roll, 3)
+    torch.cuda.synchronize()
+    (mb,) = algo.trace["mb"]
+    torch.save(dict(roll=saved, det=host(algo.trace["det"]), envs=torch.as_tensor(mb["envs"]),
+                    grad=mb["grad"].cpu(), before={k: v.cpu() for k, v in mb["before"].items()},
+                    after={k: o.ps.flat.cpu().clone() for k, o in algo.opt.items()},
+                    safe=info["eval/safe_data"]), os.path.join(out, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,0 +1,78 @@
+"""Multi-rank DGPPO.update on the GPU (dgppo.py:275-289): two ranks (gloo, both on
+cuda:0) each update on their own env shard; the all-reduced minibatch gradient equals the
+single-process gradient of the same minibatch loss on the union of the two shards (the mean of
+the shard gradients = the full-batch gradient, within fp32 summation-order tolerance), and the
+parameters after clip + Adam are bit-identical across the ranks."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from dgppo_fov_amd.algo import make_algo
+from dgppo_fov_amd.env import make_env
+from dgppo_fov_amd.trainer.data import Rollout
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _dist_update_worker as W  # noqa: E402
+
+
+def _cat(parts, dev):
+    return torch.cat([p.to(dev) for p in parts], 0)
+
+
+def test_two_rank_update_equals_single_process_union(cuda, tmp_path):
+    world, port = 2, 29700 + os.getpid() % 200
+    procs = []
+    for r in range(world):
+        envv = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                    MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_update_worker.py"), str(tmp_path)],
+                                      env=envv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        out, _ = p.communicate(timeout=150)
+        assert p.returncode == 0, out.decode()[-3000:]
+    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=False) for r in range(world)]
+    # replicas: identical reduced gradient and bit-identical parameters after Adam
+    assert torch.equal(res[0]["grad"], res[1]["grad"])
+    for k in res[0]["after"]:
+        assert torch.equal(res[0]["after"][k], res[1]["after"][k]), k
+    assert res[0]["safe"] == res[1]["safe"]
+
+    # single process on the union of the shards: the same minibatch loss, gradient of the full batch
+    env = make_env(W.ENV, W.N, num_obs=W.OBS, max_step=W.T, device=cuda)
+    B = W.B_LOCAL * world
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=W.N, batch_size=B * W.T, rnn_step=W.L, train_steps=100,
+                     seed=1, device=cuda)
+    for k, o in algo.opt.items():  # the ranks' starting parameters (same seed -> same init)
+        assert torch.equal(o.ps.flat.cpu(), res[0]["before"][k])
+
+    def rollout(key):
+        d = [r[key] for r in res]
+        g = lambda f: env._assemble(*[_cat([x[f][k] for x in d], cuda) for k in  # noqa: E731
+                                      ("nodes", "edges", "states", "receivers", "senders")], None)
+        return Rollout(g("graph"), _cat([x["actions"] for x in d], cuda), _cat([x["rnn_states"] for x in d], cuda),
+                       _cat([x["rewards"] for x in d], cuda), _cat([x["costs"] for x in d], cuda),
+                       _cat([x["dones"] for x in d], cuda),
+                       None if d[0]["log_pis"] is None else _cat([x["log_pis"] for x in d], cuda), g("next_graph"))
+
+    roll, det = rollout("roll"), rollout("det")
+    algo.det_rollout = lambda n_env, key: det  # the ranks' deterministic rollouts, concatenated
+    algo.trace = {}
+    info = algo.update(roll, 3)
+    torch.cuda.synchronize()
+    (mb,) = algo.trace["mb"]
+    assert sorted(mb["envs"].tolist()) == list(range(B))
+    g1, g2 = mb["grad"].cpu().double().numpy(), res[0]["grad"].double().numpy()
+    off = 0
+    for name, net in (("Vl", algo.Vl), ("Vh", algo.Vh), ("policy", algo.actor)):
+        a, b = g2[off:off + net.ps.size], g1[off:off + net.ps.size]
+        off += net.ps.size
+        err = np.abs(a - b).max()
+        assert err <= 1e-5 * np.abs(b).max() + 1e-7, f"{name}: shard-mean vs full-batch gradient {err:.3e}"
+    assert abs(info["eval/safe_data"] - res[0]["safe"]) < 1e-6
