@@ -114,6 +114,11 @@ class EnvRolloutIO(ctypes.Structure):
     ]
 
 
+class GatherField(ctypes.Structure):
+    _fields_ = [("src", c_f32p), ("dst", c_f32p), ("row_elems", ctypes.c_int64), ("src_tstride", ctypes.c_int64),
+                ("src_estride", ctypes.c_int64)]
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32), ("batch", ctypes.c_int32),
@@ -182,6 +187,8 @@ class GnnAttnArgs(ctypes.Structure):
         ("xa", c_f32p), ("xa_gstride", ctypes.c_int64), ("pre_W", c_f32p), ("pre_b", c_f32p),
         ("dxa", c_f32p), ("dxa_gstride", ctypes.c_int64), ("dpre_part", c_f32p), ("sidx", c_f32p),
         ("da_add", c_f32p),
+        ("beta", c_f32p), ("beta_ld", ctypes.c_int64),
+        ("qt_ld", ctypes.c_int64), ("dqt_ld", ctypes.c_int64), ("dbeta_ld", ctypes.c_int64),
     ]
 
 
@@ -263,12 +270,13 @@ SIGNATURES = {
     "dgppo_grad_norm": (ctypes.c_int, [_V, _I64, _V, _V, _V]),
     "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, ctypes.c_double, ctypes.c_double, _F32, _F32, _V]),
     "dgppo_normal": (ctypes.c_int, [_V, _I64, _V, ctypes.c_uint64, ctypes.c_uint64, _V]),
+    "dgppo_gather_env_steps": (ctypes.c_int, [ctypes.POINTER(GatherField), _I32, _V, _I32, _I32, _V]),
 }
 
 _LIB = None
 
 
-ABI_VERSION = 4  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 5  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

@@ -254,9 +254,26 @@ class DGPPO:
         return self._engine(n_env, RolloutEngine.MODE_DET).run(key)
 
     # ---- update ------------------------------------------------------------------------------
+    @staticmethod
+    def _gather(envs: torch.Tensor, *fields):
+        """Contiguous (len(envs), T, ...) copies of (B, T, ...) rollout fields for the selected envs, one
+        torch.ops.dgppo.gather_env_steps launch per 8 fields (the minibatch's x[idx])."""
+        out = [torch.empty((envs.shape[0],) + tuple(f.shape[1:]), dtype=f.dtype, device=f.device) for f in fields]
+        for i in range(0, len(fields), 8):
+            torch.ops.dgppo.gather_env_steps(list(fields[i:i + 8]), out[i:i + 8], envs)
+        return out
+
+    def _graph_batch(self, nodes, edges, recv, send) -> GraphBatch:
+        Be, T = nodes.shape[:2]
+        return GraphBatch(nodes.view(Be * T, *nodes.shape[2:]), edges.view(Be * T, *edges.shape[2:]),
+                          recv.view(Be * T, -1), send.view(Be * T, -1), self._n_agents,
+                          self._env.agent_candidates(self.device), raw_cols=self._env.nonagent_feature_cols)
+
     def _graphs(self, graph, envs) -> GraphBatch:
         """(Be, T, ...) graphs of the selected envs, env-major -> contiguous GraphBatch."""
-        sel = lambda x: x.index_select(0, envs) if not isinstance(envs, slice) else x[envs]  # noqa: E731
+        if not isinstance(envs, slice):
+            return self._graph_batch(*self._gather(envs, graph.nodes, graph.edges, graph.receivers, graph.senders))
+        sel = lambda x: x[envs]  # noqa: E731
         nodes, edges = sel(graph.nodes).contiguous(), sel(graph.edges).contiguous()
         recv, send = sel(graph.receivers).contiguous(), sel(graph.senders).contiguous()
         Be, T = nodes.shape[:2]
@@ -359,10 +376,17 @@ class DGPPO:
                 envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
                 Bm = len(bi)
                 self.grad_flat.zero_()
+                # the minibatch's rows of both rollouts (x[idx] of dgppo.py:278-279): two gather launches
+                rg = rollout.graph
+                nodes, edges, recv, send, acts, lp_old, adv, tgt = self._gather(
+                    envs, rg.nodes, rg.edges, rg.receivers, rg.senders, rollout.actions, rollout.log_pis, A, Ql)
+                g = self._graph_batch(nodes, edges, recv, send)
+                dg = det.graph
+                dnodes, dedges, drecv, dsend, hd, qhd = self._gather(
+                    envs, dg.nodes, dg.edges, dg.receivers, dg.senders, det.rnn_states, Qh_det)
                 # update_Vl (informarl.py:357-385)
-                g = self._graphs(rollout.graph, envs)
                 v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
-                tgt = Ql.index_select(0, envs).view(Bm * S_per_env, L)
+                tgt = tgt.view(Bm * S_per_env, L)
                 dv = torch.empty_like(v)
                 vl_loss = torch.empty(1, device=dev)
                 K.l2_loss(v, tgt, dv, vl_loss)
@@ -373,21 +397,18 @@ class DGPPO:
                 self._start_reduce(self.Vl, pending)
                 ph.mark("Vl_bwd")
                 # update_Vh (dgppo.py:296-321) on the deterministic rollout
-                gd = self._graphs(det.graph, envs)
-                hd = det.rnn_states.index_select(0, envs).reshape(Bm * T * n, 64).contiguous()
-                vh, cache = self.Vh.fwd(gd, hd)
+                gd = self._graph_batch(dnodes, dedges, drecv, dsend)
+                vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, 64))
                 dvh = torch.empty_like(vh)
                 vh_loss = torch.empty(1, device=dev)
-                K.l2_loss(vh, Qh_det.index_select(0, envs).reshape(-1, env.n_cost), dvh, vh_loss)
+                K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, vh_loss)
                 ph.mark("Vh_fwd")
                 self.Vh.bwd(cache, dvh)
                 del cache
                 self._start_reduce(self.Vh, pending)
                 ph.mark("Vh_bwd")
                 # update_policy (informarl.py:405-457)
-                acts = rollout.actions.index_select(0, envs).reshape(-1, self._action_dim).contiguous()
-                lp_old = rollout.log_pis.index_select(0, envs).reshape(-1).contiguous()
-                adv = A.index_select(0, envs).reshape(-1).contiguous()
+                acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
                 lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
                 dlp = torch.empty_like(lp)
                 dent = torch.empty_like(ent)

@@ -86,17 +86,18 @@ class InforMARL(DGPPO):
                 envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
                 Bm = len(bi)
                 self.grad_flat.zero_()
-                g = self._graphs(rollout.graph, envs)
+                rg = rollout.graph
+                nodes, edges, recv, send, acts, lp_old, adv, tgt = self._gather(
+                    envs, rg.nodes, rg.edges, rg.receivers, rg.senders, rollout.actions, rollout.log_pis, A, Ql)
+                g = self._graph_batch(nodes, edges, recv, send)
                 v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
-                tgt = Ql.index_select(0, envs).view(Bm * S_per_env, L)
+                tgt = tgt.view(Bm * S_per_env, L)
                 dv = torch.empty_like(v)
                 vl_loss = torch.empty(1, device=dev)
                 K.l2_loss(v, tgt, dv, vl_loss)
                 self.Vl.seq_bwd(cache, dv)
                 del cache
-                acts = rollout.actions.index_select(0, envs).reshape(-1, self._action_dim).contiguous()
-                lp_old = rollout.log_pis.index_select(0, envs).reshape(-1).contiguous()
-                adv = A.index_select(0, envs).reshape(-1).contiguous()
+                acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
                 lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
                 dlp = torch.empty_like(lp)
                 dent = torch.empty_like(ent)

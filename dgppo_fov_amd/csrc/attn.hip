@@ -28,6 +28,20 @@
 #include "lanes.h"
 
 namespace dgppo {
+
+// Row strides of qt / dqt / dbeta (0: packed) and beta_h = q_h . bk_h: precomputed (p.beta, Q-free form) or
+// the dot over this thread's f-stripe [f0, F) step `stride` (the caller reduces the stripes).
+__device__ __forceinline__ int64_t qt_ld(const dgppo_gnn_attn_args& p) { return p.qt_ld ? p.qt_ld : (int64_t)p.H * p.D; }
+__device__ __forceinline__ int64_t dqt_ld(const dgppo_gnn_attn_args& p) {
+  return p.dqt_ld ? p.dqt_ld : (int64_t)p.H * p.D;
+}
+__device__ __forceinline__ int64_t dbeta_ld(const dgppo_gnn_attn_args& p) { return p.dbeta_ld ? p.dbeta_ld : p.H; }
+__device__ __forceinline__ float q_dot_bk(const dgppo_gnn_attn_args& p, int64_t row, int h, int f0, int stride) {
+  if (p.beta) return f0 == 0 ? p.beta[row * p.beta_ld + h] : 0.0f;
+  float acc = 0.0f;
+  for (int f = f0; f < p.F; f += stride) acc += p.q[row * p.H * p.F + h * p.F + f] * p.bk[h * p.F + f];
+  return acc;
+}
 namespace {
 
 constexpr int kH = 3;         // heads (GraphTransformer num_heads of the reference GNN)
@@ -254,14 +268,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(dgppo_gnn_attn_args p, in
       // stage qt; beta_h = q_h . bk_h as a group dot product
       for (int e = t; e < R * H * D; e += 256) {
         const int rr = e / (H * D), kk = e - rr * (H * D);
-        if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
+        if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * qt_ld(p) + kk];
       }
       float beta[kH];
 #pragma unroll
       for (int h = 0; h < kH; ++h) {
         float acc = 0.0f;
         if (active && h < H)
-          for (int f = c; f < F; f += CP) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
+          acc = q_dot_bk(p, row, h, c, CP);
         beta[h] = acc;
       }
       group_red3<CP, false>(beta, L.scr);
@@ -408,7 +422,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
       for (int h = 0; h < kH; ++h) a[h] = (ok && h < H) ? p.attn[(row * H + h) * C + c] : 0.0f;
       for (int e = t; e < R * H * D; e += 256) {
         const int rr = e / (H * D), kk = e - rr * (H * D);
-        if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
+        if (r0 + rr < nrec) L.qt[rr * kH * DM + kk] = p.qt[(g0 * n + r0 + rr) * qt_ld(p) + kk];
       }
       for (int e = t; e < R * W; e += 256) {
         const int rr = e / W, kk = e - rr * W;
@@ -436,11 +450,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
       for (int h = 0; h < kH; ++h) dbeta[h] = dl[h] = (ok && h < H) ? a[h] * (da[h] - dot[h]) * p.scale : 0.0f;
       group_red3<CP, false>(dbeta, L.scr);
       if (active && c == 0)
-        for (int h = 0; h < H; ++h) p.dbeta[row * H + h] = dbeta[h];
+        for (int h = 0; h < H; ++h) p.dbeta[row * dbeta_ld(p) + h] = dbeta[h];
       if (active)
         for (int kk = c; kk < H * F; kk += CP) {
           const int h = kk / F;
-          p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+          if (p.dq) p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
         }
       // sender contribution dx_s[d] = sum_h a_h dxbar_h[d] + dl_h qt_h[d]
       float contrib[DM];
@@ -481,7 +495,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(dgppo_gnn_attn_args p, in
           float acc = 0.0f;
           #pragma unroll 8
           for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
-          p.dqt[row * H * D + o] = acc;
+          p.dqt[row * dqt_ld(p) + o] = acc;
         }
       }
       if (want_dxa) {  // agent j of each graph in this round: sum of its receivers' slot-j rows, in order
@@ -712,14 +726,14 @@ __global__ __launch_bounds__(256) void attn_fwd_wave_kernel(dgppo_gnn_attn_args 
 #pragma unroll
     for (int u = 0; u < (RW * kH * DM + 63) / 64; ++u) {
       const int e = lane + 64 * u, rr = e / (H * D), kk = e - rr * (H * D);
-      qv[u] = (e < RW * H * D && r0 + rr < nrec) ? p.qt[(g0 * n + r0 + rr) * H * D + kk] : 0.0f;
+      qv[u] = (e < RW * H * D && r0 + rr < nrec) ? p.qt[(g0 * n + r0 + rr) * qt_ld(p) + kk] : 0.0f;
     }
     float bacc[kH];
 #pragma unroll
     for (int h = 0; h < kH; ++h) {
       float acc = 0.0f;
       if (active && h < H)
-        for (int f = c; f < F; f += CP) acc += p.q[row * H * F + h * F + f] * p.bk[h * F + f];
+        acc = q_dot_bk(p, row, h, c, CP);
       bacc[h] = acc;
     }
     if (j + 1 < J) {
@@ -848,7 +862,7 @@ __global__ __launch_bounds__(256) void attn_bwd_wave_kernel(dgppo_gnn_attn_args 
       for (int h = 0; h < kH; ++h) a[h] = (ok && h < H) ? p.attn[(row * H + h) * C + c] : 0.0f;
       for (int e = lane; e < RW * H * D; e += 64) {
         const int rr = e / (H * D), kk = e - rr * (H * D);
-        if (r0 + rr < nrec) L.qt[rr * QP + kk] = p.qt[(g0 * n + r0 + rr) * H * D + kk];
+        if (r0 + rr < nrec) L.qt[rr * QP + kk] = p.qt[(g0 * n + r0 + rr) * qt_ld(p) + kk];
       }
       for (int e = lane; e < RW * W; e += 64) {  // dxcat row -> [dxbar | debar | dsig] at aligned offsets
         const int rr = e / W, kk = e - rr * W;
@@ -877,11 +891,11 @@ __global__ __launch_bounds__(256) void attn_bwd_wave_kernel(dgppo_gnn_attn_args 
         dbeta[h] = group_sum<CP>(dl[h], nullptr);
       }
       if (active && c == 0)
-        for (int h = 0; h < H; ++h) p.dbeta[row * H + h] = dbeta[h];
+        for (int h = 0; h < H; ++h) p.dbeta[row * dbeta_ld(p) + h] = dbeta[h];
       if (active)
         for (int kk = c; kk < H * F; kk += CP) {
           const int h = kk / F;
-          p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+          if (p.dq) p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
         }
       float contrib[DM];
       {
@@ -909,7 +923,7 @@ __global__ __launch_bounds__(256) void attn_bwd_wave_kernel(dgppo_gnn_attn_args 
           float acc = 0.0f;
           #pragma unroll 8
           for (int cc = 0; cc < CR; ++cc) acc += L.a[(base + cc) * kH + h] * L.xs[(base + cc) * XP + d];
-          p.dqt[row * H * D + o] = acc;
+          p.dqt[row * dqt_ld(p) + o] = acc;
         }
       }
       if (want_dxa) {  // agent senders: the wave's graph image, slots in fixed order
@@ -1064,7 +1078,7 @@ __global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
   // ---- stage qt (zero padded per head), beta_h = q_h . bk_h, pre weights
   for (int e = threadIdx.x; e < kRows * 96; e += 256) {
     const int r = e / 96, k = e - r * 96, h = k >> 5, d = k & 31;
-    qts[r * kQP + k] = (row0 + r < nrows && d < D) ? p.qt[(int64_t)(row0 + r) * H * D + h * D + d] : 0.0f;
+    qts[r * kQP + k] = (row0 + r < nrows && d < D) ? p.qt[(int64_t)(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
   }
   {
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
@@ -1073,7 +1087,7 @@ __global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
     for (int h = 0; h < kH; ++h) {
       float acc = 0.0f;
       if (act)
-        for (int f = j; f < F; f += 16) acc += p.q[(int64_t)(row0 + r) * H * F + h * F + f] * p.bk[h * F + f];
+        acc = q_dot_bk(p, (int64_t)(row0 + r), h, j, 16);
       acc = lanes::sum16(acc);
       if (j == 0) qts[r * kQP + 96 + h] = acc;
     }
@@ -1338,7 +1352,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
     // ---- block staging: qt rows, dxcat rows (split at aligned offsets), agent image cleared
     for (int e = threadIdx.x; e < kRows * 3 * HS; e += 256) {
       const int r = e / (3 * HS), k = e - r * (3 * HS), h = k / HS, d = k - h * HS;
-      qts[r * kQP + k] = (r < nrec && d < D) ? p.qt[(row0 + r) * H * D + h * D + d] : 0.0f;
+      qts[r * kQP + k] = (r < nrec && d < D) ? p.qt[(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
     }
     for (int e = threadIdx.x; e < kRows * kGP; e += 256) {
       const int r = e / kGP, k = e - r * kGP;
@@ -1426,10 +1440,10 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
         dbeta[h] = lanes::sum32(dl[h]);
       }
       if (active) {
-        if (c < kH) p.dbeta[row * H + c] = c == 0 ? dbeta[0] : c == 1 ? dbeta[1] : dbeta[2];
+        if (c < kH) p.dbeta[row * dbeta_ld(p) + c] = c == 0 ? dbeta[0] : c == 1 ? dbeta[1] : dbeta[2];
         for (int kk = c; kk < H * F; kk += 32) {
           const int h = kk / F;
-          p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+          if (p.dq) p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
         }
       }
 #pragma unroll
@@ -1453,7 +1467,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 8
         for (int cc = 0; cc < 32; ++cc) acc += ab[cc * 4] * *(const f32x4*)(xb + cc * kXSP + 4 * tk_q);
-        float* o = p.dqt + row * H * D + tk_h * D;
+        float* o = p.dqt + row * dqt_ld(p) + tk_h * D;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (4 * tk_q + j < D) o[4 * tk_q + j] = acc[j];
@@ -1724,14 +1738,11 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
   }
   for (int e = threadIdx.x; e < n * H * D; e += 256) {
     const int i = e / (H * D), k = e - i * (H * D), h = k / D, d = k - h * D;
-    Q[i * QP + h * DM + d] = p.qt[(g * n + i) * H * D + k];
+    Q[i * QP + h * DM + d] = p.qt[(g * n + i) * qt_ld(p) + k];
   }
   for (int e = threadIdx.x; e < n * H; e += 256) {  // beta_h = q_h . bk_h
     const int i = e / H, h = e - i * H;
-    const float* q = p.q + (g * n + i) * H * F + h * F;
-    float acc = 0.0f;
-    for (int f = 0; f < F; ++f) acc += q[f] * p.bk[h * F + f];
-    Q[i * QP + kH * DM + h] = acc;
+    Q[i * QP + kH * DM + h] = q_dot_bk(p, g * n + i, h, 0, 1);
   }
   __syncthreads();
   constexpr int kMaxC = gfwd::kMaxC;
@@ -1904,10 +1915,10 @@ __global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args
       for (int o = 32; o > 0; o >>= 1) db += __shfl_xor(db, o, 64);
       dbeta[h] = db;
     }
-    if (lane < kH) p.dbeta[row * H + lane] = lane == 0 ? dbeta[0] : (lane == 1 ? dbeta[1] : dbeta[2]);
+    if (lane < kH) p.dbeta[row * dbeta_ld(p) + lane] = lane == 0 ? dbeta[0] : (lane == 1 ? dbeta[1] : dbeta[2]);
     for (int kk = lane; kk < H * F; kk += 64) {
       const int h = kk / F;
-      p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+      if (p.dq) p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1925,7 +1936,7 @@ __global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args
           }
         }
       }
-      p.dqt[row * H * D + o] = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
+      p.dqt[row * dqt_ld(p) + o] = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2002,7 +2013,11 @@ int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
 
 bool valid(const dgppo_gnn_attn_args* p) {
   if (!p || p->H < 1 || p->H > kH || p->D < 1 || p->D > 64 || p->F < 1 || p->F > 64 || p->C < 1 || p->C > 128 ||
-      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->q || !p->bk || !p->cand || !p->receivers || !p->senders)
+      p->n_agents < 1 || !p->x || !p->ef || !p->qt || !p->bk || !p->cand || !p->receivers || !p->senders)
+    return false;
+  if (!p->q && !(p->beta && p->beta_ld >= p->H)) return false;  // beta = q . bk from q, or precomputed
+  if ((p->qt_ld && p->qt_ld < (int64_t)p->H * p->D) || (p->dqt_ld && p->dqt_ld < (int64_t)p->H * p->D) ||
+      (p->dbeta_ld && p->dbeta_ld < p->H))
     return false;
   if (p->xa && (p->D0 < 1 || p->D0 > kD0 || (!p->pre_W && p->D0 != p->D) || (p->pre_W && !p->pre_b)))
     return false;
@@ -2042,7 +2057,7 @@ extern "C" int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* p, void* stream) {
 }
 
 extern "C" int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* p, void* stream) {
-  if (!dgppo::valid(p) || !p->attn || !p->dxcat || !p->dqt || !p->dq || !p->dbeta) return DGPPO_EINVAL;
+  if (!dgppo::valid(p) || !p->attn || !p->dxcat || !p->dqt || !p->dbeta) return DGPPO_EINVAL;
   if (p->G == 0) return 0;
   if (dgppo::run(p, true, (hipStream_t)stream)) return DGPPO_EINVAL;
   return (int)hipGetLastError();

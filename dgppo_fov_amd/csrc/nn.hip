@@ -996,3 +996,45 @@ extern "C" int dgppo_normal(float* out, int64_t n, const uint64_t* seed_ptr, uin
                      stream_id);
   return (int)hipGetLastError();
 }
+
+// ---- minibatch assembly: gather the (env, t) rows of the selected envs (DGPPO.update, dgppo.py:275-289) ---
+// jtu.tree_map(lambda x: x[idx], rollout) of the reference's minibatch scan: for every field, output row
+// o = e * T + t (e over the selected envs, t over the episode) is the source row of env envs[e] at step t,
+// wherever the rollout keeps it (time-major buffers: t stride B * row, env stride row).  One wave per output
+// row and field, 16-byte moves where a row allows it (rows of 4-byte elements).
+namespace dgppo {
+struct GatherFields {
+  dgppo_gather_field f[8];
+};
+__global__ __launch_bounds__(256) void gather_env_steps_kernel(GatherFields fs, const int64_t* __restrict__ envs,
+                                                             int32_t T, int64_t rows) {
+  const dgppo_gather_field& f = fs.f[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= rows) return;
+  const int64_t e = o / T, t = o - e * T;
+  const float* src = reinterpret_cast<const float*>(f.src) + t * f.src_tstride + envs[e] * f.src_estride;
+  float* dst = reinterpret_cast<float*>(f.dst) + o * f.row_elems;
+  const int64_t L = f.row_elems;
+  if ((L & 3) == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+    for (int64_t j = lane; j < L / 4; j += 64) reinterpret_cast<float4*>(dst)[j] = reinterpret_cast<const float4*>(src)[j];
+  } else {
+    for (int64_t j = lane; j < L; j += 64) dst[j] = src[j];
+  }
+}
+}  // namespace dgppo
+
+extern "C" int dgppo_gather_env_steps(const dgppo_gather_field* fields, int32_t n_fields, const int64_t* envs,
+                                      int32_t n_sel, int32_t T, void* stream) {
+  if (n_fields < 1 || n_fields > 8 || !fields || !envs || n_sel < 0 || T < 1) return DGPPO_EINVAL;
+  const int64_t rows = (int64_t)n_sel * T;
+  if (rows == 0) return 0;
+  dgppo::GatherFields fs{};
+  for (int i = 0; i < n_fields; ++i) {
+    if (!fields[i].src || !fields[i].dst || fields[i].row_elems < 1) return DGPPO_EINVAL;
+    fs.f[i] = fields[i];
+  }
+  hipLaunchKernelGGL(dgppo::gather_env_steps_kernel, dim3((unsigned)((rows + 3) / 4), (unsigned)n_fields), dim3(256),
+                     0, DG_STREAM(stream), fs, envs, T, rows);
+  return (int)hipGetLastError();
+}

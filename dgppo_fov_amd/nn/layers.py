@@ -373,8 +373,9 @@ class GraphTransformer:
              "Dense_4": {"kernel": orthogonal(rng, (D, F)), "bias": np.zeros(F, np.float32)}}
         self.load_flax(d)
 
-    def _attn_args(self, g: "GraphBatch", Q, QT, xa=None, pre=None) -> dict:
-        """Inputs of torch.ops.dgppo.gnn_attn_fwd / _bwd for this layer on graph batch g."""
+    def _attn_args(self, g: "GraphBatch", QB, xa=None, pre=None) -> dict:
+        """Inputs of torch.ops.dgppo.gnn_attn_fwd / _bwd for this layer on graph batch g, Q-free form:
+        QB (R, H*D + H) = [qt | beta] rows (see qb_weights)."""
         D0 = 0
         pre_W = pre_b = None
         if xa is None:
@@ -386,10 +387,33 @@ class GraphTransformer:
             if pre is not None:
                 pre_W = pre.v("Wu") if cols is None else pre.v("Wu").index_select(0, cols)
                 pre_b = pre.v("bu")
+        HD = self.H * self.D
+        W = HD + self.H
         return dict(dims=[g.G, g.N, g.E, g.n, self.D, self.F, self.H, g.C, D0], cand=g.cand, receivers=g.receivers,
-                    senders=g.senders, sidx=g.sidx, x=x, x_gstride=x_gs, ef=g.edges_head, ef_gstride=g.E * 4, q=Q,
-                    qt=QT, bk=self.v("bk"), scale=1.0 / math.sqrt(self.F), xa=xa, xa_gstride=g.n * self.D,
-                    pre_W=pre_W, pre_b=pre_b)
+                    senders=g.senders, sidx=g.sidx, x=x, x_gstride=x_gs, ef=g.edges_head, ef_gstride=g.E * 4, q=None,
+                    qt=QB, bk=self.v("bk"), scale=1.0 / math.sqrt(self.F), xa=xa, xa_gstride=g.n * self.D,
+                    pre_W=pre_W, pre_b=pre_b, beta=QB[:, HD:], beta_ld=W, qt_ld=W)
+
+    def _aug(self, w: str, b: str, grad=False) -> torch.Tensor:
+        """[W; b] as one ((in+1), out) view: the flat buffer stores a Dense's kernel then its bias."""
+        ow, ob = self.ps.offsets[self.name + "." + w], self.ps.offsets[self.name + "." + b]
+        rows, cols = self.ps.view(self.name + "." + w).shape
+        assert ob == ow + rows * cols, "bias must follow its kernel in the flat buffer"
+        buf = self.ps.grad if grad else self.ps.flat
+        return buf[ow:ow + (rows + 1) * cols].view(rows + 1, cols)
+
+    def qb_weights(self) -> torch.Tensor:
+        """QBW ((D+1), H*D + H): with q_h = x Wq_h + bq_h, the attention needs only qt_h = q_h Wkt_h (its
+        logits are (qt_h . x_s + q_h . bk_h) / sqrt(F)) and beta_h = q_h . bk_h, both affine in x:
+        [x 1] QBW = [qt | beta] with QBW[:, hD:(h+1)D] = [Wq_h; bq_h] Wkt_h and QBW[:, HD + h] =
+        [Wq_h; bq_h] bk_h.  Two small batched GEMMs on the weights replace materialising q (R, H*F)."""
+        D, F, H = self.D, self.F, self.H
+        W = H * D + H
+        Waug = self._aug("Wq", "bq")
+        QBW = torch.empty((D + 1, W), device=Waug.device)
+        K.gemm(Waug, self.v("Wkt"), QBW, D + 1, D, F, lda=H * F, sa=F, ldb=D, sb=F * D, ldc=W, sc=D, batch=H)
+        K.gemm(Waug, self.v("bk"), QBW, D + 1, 1, F, lda=H * F, sa=F, ldb=1, sb=F, ldc=W, sc=1, c_off=H * D, batch=H)
+        return QBW
 
     def fwd(self, g: "GraphBatch", xa=None, pre=None):
         """One layer on the graph batch.  xa None: senders read the raw nodes (G, N, D) (first layer);
@@ -402,13 +426,13 @@ class GraphTransformer:
         dev = g.nodes.device
         R = G * n
         A, akw = (g.nodes, dict(lda=D, a_grp=n, a_gs=N * D)) if xa is None else (xa, dict(lda=D))
-        Q = torch.empty((R, H * F), device=dev)
-        K.gemm(A, self.v("Wq"), Q, R, H * F, D, bias=self.v("bq"), **akw)
-        QT = torch.empty((R, H * D), device=dev)
-        K.gemm(Q, self.v("Wkt"), QT, R, D, F, lda=H * F, sa=F, ldb=D, sb=F * D, ldc=H * D, sc=D, batch=H)
+        QBW = self.qb_weights()
+        W = H * D + H
+        QB = torch.empty((R, W), device=dev)  # [qt | beta] per receiving agent: one GEMM, q never stored
+        K.gemm(A, QBW, QB, R, W, D, bias=QBW[D], **akw)
         attn = torch.empty((R, H, C), device=dev)
         xcat = torch.empty((R, H * (D + 5)), device=dev)
-        torch.ops.dgppo.gnn_attn_fwd(**self._attn_args(g, Q, QT, xa, pre), attn=attn, xcat=xcat)
+        torch.ops.dgppo.gnn_attn_fwd(**self._attn_args(g, QB, xa, pre), attn=attn, xcat=xcat)
         M = torch.empty((R, F), device=dev)
         K.gemm(xcat, self.v("Wcat"), M, R, F, H * (D + 5), alpha=1.0 / H)
         xcx = None
@@ -418,17 +442,18 @@ class GraphTransformer:
             K.gemm(xcx, self.v("Wex"), M, R, F, H * self.EX, alpha=1.0 / H, beta=1.0)
         Y = torch.empty((R, F), device=dev)
         K.gemm(A, self.v("Wu"), Y, R, F, D, bias=self.v("bu"), addend=M, relu=True, **akw)
-        return Y, (xa, pre, Q, QT, attn, xcat, xcx, Y)
+        return Y, (xa, pre, QBW, QB, attn, xcat, xcx, Y)
 
     def bwd(self, cache, dY, g: "GraphBatch"):
         """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, else None;
         accumulates this layer's grads and, in agent mode with `pre`, pre's Dense_4 grads from the
         transformed senders."""
-        xa, pre, Q, QT, attn, xcat, xcx, Y = cache
+        xa, pre, QBW, QB, attn, xcat, xcx, Y = cache
         G, N, n = g.G, g.N, g.n
         D, F, H, C = self.D, self.F, self.H, g.C
         R = G * n
         W = H * (D + 5)
+        HD, WQ = H * D, H * D + H
         dev = dY.device
         A, akw = (g.nodes, dict(lda=D, a_grp=n, a_gs=N * D)) if xa is None else (xa, dict(lda=D))
         K.relu_bwd_(dY, Y)  # dY := dZ
@@ -443,18 +468,17 @@ class GraphTransformer:
             K.gemm(xcx, dY, self.v("Wex", True), WX, F, R, ta=True, lda=WX, alpha=1.0 / H, beta=1.0)
             da_add = torch.empty((R, H, C), device=dev)
             K.edge_da(G, n, C, H, self.EX, g.E, dxx, g.cand, g.sidx, g.edges_x, da_add)
-        dQT = torch.empty((R, H * D), device=dev)
-        dQ = torch.empty((R, H * F), device=dev)
-        dbeta = torch.empty((R, H), device=dev)
+        dQB = torch.empty((R, WQ), device=dev)  # [dqt | dbeta]
         dXa = torch.zeros((R, D), device=dev) if xa is not None else None
-        args = self._attn_args(g, Q, QT, xa, pre)
+        args = self._attn_args(g, QB, xa, pre)
         part = None
         if xa is not None and pre is not None:
             nb = ops.gnn_attn_partial_blocks(**args)
             PK = args["dims"][8] * D + D
             part = K.workspace(nb * PK, dev, "attn_pre")
-        torch.ops.dgppo.gnn_attn_bwd(**args, attn=attn, dxcat=dxcat, da_add=da_add, dqt=dQT, dq=dQ, dbeta=dbeta,
-                                     dxa=dXa, dxa_gstride=n * D, dpre_part=part)
+        torch.ops.dgppo.gnn_attn_bwd(**args, attn=attn, dxcat=dxcat, da_add=da_add, dqt=dQB, dq=None,
+                                     dbeta=dQB[:, HD:], dxa=dXa, dxa_gstride=n * D, dpre_part=part, dqt_ld=WQ,
+                                     dbeta_ld=WQ)
         if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre (Wu rows = the raw columns used)
             cols = g.sender_raw[1]
             ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
@@ -469,17 +493,26 @@ class GraphTransformer:
                 else:
                     pre.v("Wu", True).index_add_(0, cols, tmp[:nw].view(args["dims"][8], D))
                 pre.ps.grad[ob:ob + D].add_(tmp[nw:])
-        K.gemm(dbeta, Q, self.v("bk", True), 1, F, R, ta=True, lda=H, sa=1, ldb=H * F, sb=F, ldc=F, sc=F,
+        # Q-free parameter gradients: Gaug = [x 1]^T [dqt | dbeta] ((D+1) x (HD+H)), one pass over the rows;
+        # then, per head, with Waug_h = [Wq_h; bq_h] ((D+1) x F):
+        #   [dWq_h; dbq_h] += Gaug[:, hD:(h+1)D] Wkt_h^T + Gaug[:, HD+h] bk_h^T
+        #   dWkt_h += Waug_h^T Gaug[:, hD:(h+1)D],   dbk_h += Waug_h^T Gaug[:, HD+h]
+        # (q_h = x Wq_h + bq_h is affine in the layer input, so every sum over rows of q collapses into Gaug)
+        Gaug = torch.empty((D + 1, WQ), device=dev)
+        K.gemm(A, dQB, Gaug, D, WQ, R, ta=True, bias_grad=Gaug[D], **akw)
+        Waug, dWaug = self._aug("Wq", "bq"), self._aug("Wq", "bq", grad=True)
+        K.gemm(Gaug, self.v("Wkt"), dWaug, D + 1, F, D, lda=WQ, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
                batch=H, beta=1.0)
-        K.gemm(Q, dQT, self.v("Wkt", True), F, D, R, ta=True, lda=H * F, sa=F, ldb=H * D, sb=D, ldc=D, sc=F * D,
+        K.gemm(Gaug, self.v("bk"), dWaug, D + 1, F, 1, lda=WQ, a_off=HD, sa=1, ldb=F, sb=F, ldc=H * F, sc=F,
                batch=H, beta=1.0)
-        K.gemm(dQT, self.v("Wkt"), dQ, R, F, D, lda=H * D, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
-               batch=H, beta=1.0)
-        K.gemm(A, dQ, self.v("Wq", True), D, H * F, R, ta=True, beta=1.0, bias_grad=self.v("bq", True), **akw)
+        K.gemm(Waug, Gaug, self.v("Wkt", True), F, D, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, sb=D, ldc=D,
+               sc=F * D, batch=H, beta=1.0)
+        K.gemm(Waug, Gaug, self.v("bk", True), F, 1, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, b_off=HD, sb=1,
+               ldc=1, sc=F, batch=H, beta=1.0)
         K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
         if dXa is not None:
             K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
-            K.gemm(dQ, self.v("Wq"), dXa, R, D, H * F, tb=True, ldb=H * F, beta=1.0)
+            K.gemm(dQB, QBW, dXa, R, D, WQ, tb=True, ldb=WQ, beta=1.0)  # d[qt | beta] / dx = QBW[:D]^T
         return dXa
 
 

@@ -16,6 +16,7 @@ non-CUDA tensor raises NativeLibraryError (`_lib.require_gpu`).
   dgppo::gae            dgppo_gae            compute_dec_ocp_gae, algo/utils.py:11-79
   dgppo::grad_norm      dgppo_grad_norm      compute_norm + has_any_nan_or_inf, trainer/utils.py:105-118
   dgppo::adam           dgppo_adam           clip + optax.apply_if_finite(optax.adam), informarl.py:131-137
+  dgppo::gather_env_steps dgppo_gather_env_steps  tree_map(lambda x: x[idx], rollout), dgppo.py:275-289
 
 An env's static configuration (dgppo_env_cfg: engine, sizes, radii, limits) is not a tensor; it is
 registered once per env instance and the ops take its integer handle.
@@ -202,7 +203,7 @@ def _env_rollout_fake(cfg, rebuild_first, obstacles, actions, ray_dirs, nodes, e
 
 # ---- GraphTransformer attention core -------------------------------------------------------------------
 def _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa, xa_gstride,
-                 pre_W, pre_b) -> _lib.GnnAttnArgs:
+                 pre_W, pre_b, beta=None, beta_ld=0, qt_ld=0) -> _lib.GnnAttnArgs:
     a = _lib.GnnAttnArgs()
     a.G, a.N, a.E, a.n_agents, a.D, a.F, a.H, a.C, a.D0 = (int(v) for v in dims)
     a.cand, a.receivers, a.senders, a.sidx = _p(cand), _p(receivers), _p(senders), _p(sidx)
@@ -212,60 +213,67 @@ def _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstr
     a.scale = float(scale)
     a.xa, a.xa_gstride = _p(xa), int(xa_gstride)
     a.pre_W, a.pre_b = _p(pre_W), _p(pre_b)
+    a.beta, a.beta_ld, a.qt_ld = _p(beta), int(beta_ld), int(qt_ld)
     return a
 
 
 @torch.library.custom_op("dgppo::gnn_attn_fwd", mutates_args=("attn", "xcat"))
 def gnn_attn_fwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
-                 x_gstride: int, ef: Tensor, ef_gstride: int, q: Tensor, qt: Tensor, bk: Tensor, scale: float,
-                 xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor], pre_b: Optional[Tensor],
-                 attn: Tensor, xcat: Tensor) -> None:
+                 x_gstride: int, ef: Tensor, ef_gstride: int, q: Optional[Tensor], qt: Tensor, bk: Tensor,
+                 scale: float, xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor],
+                 pre_b: Optional[Tensor], attn: Tensor, xcat: Tensor, beta: Optional[Tensor] = None,
+                 beta_ld: int = 0, qt_ld: int = 0) -> None:
     """Per-receiving-agent attention of one GraphTransformer layer (dims = [G, N, E, n, D, F, H, C, D0]):
     attn (G*n, H, C) = segment softmax of (q . k)/sqrt(F) over each agent's candidate edges, xcat
-    (G*n, H*(D+5)) = the attention-weighted [sender rows | edge rows | 1] per head (nn/layers.py)."""
-    _lib.require_gpu(q.device, "dgppo::gnn_attn_fwd")
+    (G*n, H*(D+5)) = the attention-weighted [sender rows | edge rows | 1] per head (nn/layers.py).
+    Q-free form: q None and beta (G*n, H) = q_h . bk_h given (row stride beta_ld); qt_ld = qt's row stride."""
+    _lib.require_gpu(qt.device, "dgppo::gnn_attn_fwd")
     a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
-                     xa_gstride, pre_W, pre_b)
+                     xa_gstride, pre_W, pre_b, beta, beta_ld, qt_ld)
     a.attn, a.xcat = _p(attn), _p(xcat)
-    _lib.check(_lib.load().dgppo_gnn_attn_fwd(ctypes.byref(a), _stream(q)), "dgppo_gnn_attn_fwd")
+    _lib.check(_lib.load().dgppo_gnn_attn_fwd(ctypes.byref(a), _stream(qt)), "dgppo_gnn_attn_fwd")
 
 
 @gnn_attn_fwd.register_fake
 def _gnn_attn_fwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
-                       xa_gstride, pre_W, pre_b, attn, xcat) -> None:
+                       xa_gstride, pre_W, pre_b, attn, xcat, beta=None, beta_ld=0, qt_ld=0) -> None:
     return None
 
 
 @torch.library.custom_op("dgppo::gnn_attn_bwd", mutates_args=("dqt", "dq", "dbeta", "dxa", "dpre_part"))
 def gnn_attn_bwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
-                 x_gstride: int, ef: Tensor, ef_gstride: int, q: Tensor, qt: Tensor, bk: Tensor, scale: float,
-                 xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor], pre_b: Optional[Tensor],
-                 attn: Tensor, dxcat: Tensor, da_add: Optional[Tensor], dqt: Tensor, dq: Tensor, dbeta: Tensor,
-                 dxa: Optional[Tensor], dxa_gstride: int, dpre_part: Optional[Tensor]) -> None:
+                 x_gstride: int, ef: Tensor, ef_gstride: int, q: Optional[Tensor], qt: Tensor, bk: Tensor,
+                 scale: float, xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor],
+                 pre_b: Optional[Tensor], attn: Tensor, dxcat: Tensor, da_add: Optional[Tensor], dqt: Tensor,
+                 dq: Optional[Tensor], dbeta: Tensor, dxa: Optional[Tensor], dxa_gstride: int,
+                 dpre_part: Optional[Tensor], beta: Optional[Tensor] = None, beta_ld: int = 0, qt_ld: int = 0,
+                 dqt_ld: int = 0, dbeta_ld: int = 0) -> None:
     """Backward of gnn_attn_fwd given dL/dxcat (+ da_add, extra dL/dattn of edge columns past 4): dqt, dq,
     dbeta (dL/d(q . bk)); in agent mode dxa (accumulated, agent senders) and the partial Dense_4
-    gradients of the recomputed never-receiving senders (dpre_part, one row per workgroup)."""
-    _lib.require_gpu(q.device, "dgppo::gnn_attn_bwd")
+    gradients of the recomputed never-receiving senders (dpre_part, one row per workgroup).  Q-free form:
+    dq None (not written), dqt / dbeta row strides dqt_ld / dbeta_ld (e.g. one [dqt | dbeta] buffer)."""
+    _lib.require_gpu(qt.device, "dgppo::gnn_attn_bwd")
     a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
-                     xa_gstride, pre_W, pre_b)
+                     xa_gstride, pre_W, pre_b, beta, beta_ld, qt_ld)
+    a.dqt_ld, a.dbeta_ld = int(dqt_ld), int(dbeta_ld)
     a.attn, a.dxcat, a.da_add = _p(attn), _p(dxcat), _p(da_add)
     a.dqt, a.dq, a.dbeta = _p(dqt), _p(dq), _p(dbeta)
     a.dxa, a.dxa_gstride, a.dpre_part = _p(dxa), int(dxa_gstride), _p(dpre_part)
-    _lib.check(_lib.load().dgppo_gnn_attn_bwd(ctypes.byref(a), _stream(q)), "dgppo_gnn_attn_bwd")
+    _lib.check(_lib.load().dgppo_gnn_attn_bwd(ctypes.byref(a), _stream(qt)), "dgppo_gnn_attn_bwd")
 
 
 @gnn_attn_bwd.register_fake
 def _gnn_attn_bwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
-                       xa_gstride, pre_W, pre_b, attn, dxcat, da_add, dqt, dq, dbeta, dxa, dxa_gstride,
-                       dpre_part) -> None:
+                       xa_gstride, pre_W, pre_b, attn, dxcat, da_add, dqt, dq, dbeta, dxa, dxa_gstride, dpre_part,
+                       beta=None, beta_ld=0, qt_ld=0, dqt_ld=0, dbeta_ld=0) -> None:
     return None
 
 
 def gnn_attn_partial_blocks(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
-                            xa_gstride, pre_W, pre_b) -> int:
+                            xa_gstride, pre_W, pre_b, beta=None, beta_ld=0, qt_ld=0) -> int:
     """Rows of the dpre_part workspace gnn_attn_bwd writes for these arguments (host query)."""
     a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
-                     xa_gstride, pre_W, pre_b)
+                     xa_gstride, pre_W, pre_b, beta, beta_ld, qt_ld)
     return int(_lib.load().dgppo_gnn_attn_partial_blocks(ctypes.byref(a)))
 
 
@@ -320,4 +328,38 @@ def adam(param: Tensor, grad: Tensor, m: Tensor, v: Tensor, state: Tensor, lr: f
 
 @adam.register_fake
 def _adam_fake(param, grad, m, v, state, lr, b1, b2, eps, max_norm) -> None:
+    return None
+
+
+# ---- minibatch assembly ---------------------------------------------------------------------------------
+@torch.library.custom_op("dgppo::gather_env_steps", mutates_args=("dst",))
+def gather_env_steps(src: List[Tensor], dst: List[Tensor], envs: Tensor) -> None:
+    """dst[i][e, t] = src[i][envs[e], t] for (B, T, ...) rollout fields (any strides on B and T, e.g. views
+    of time-major buffers; contiguous trailing dims; 4-byte dtypes) into contiguous (Bm, T, ...) outputs:
+    the reference's `jtu.tree_map(lambda x: x[idx], rollout)` as one launch for up to 8 fields."""
+    if not src or len(src) != len(dst) or len(src) > 8:
+        raise ValueError("gather_env_steps: 1..8 (src, dst) pairs")
+    _lib.require_gpu(envs.device, "dgppo::gather_env_steps")
+    if envs.dtype != torch.int64 or envs.dim() != 1:
+        raise ValueError("envs must be a 1-d int64 tensor")
+    T = int(src[0].shape[1])
+    fields = (_lib.GatherField * len(src))()
+    for f, a, b in zip(fields, src, dst):
+        if a.element_size() != 4 or b.element_size() != 4 or a.dim() < 2 or a.shape[1] != T:
+            raise ValueError("gather_env_steps: (B, T, ...) fields of 4-byte elements")
+        if tuple(b.shape) != (envs.shape[0],) + tuple(a.shape[1:]) or not b.is_contiguous():
+            raise ValueError("gather_env_steps: dst must be contiguous (len(envs), T, ...)")
+        inner = 1
+        for d in range(a.dim() - 1, 1, -1):
+            if a.shape[d] != 1 and a.stride(d) != inner:
+                raise ValueError("gather_env_steps: trailing dims must be contiguous")
+            inner *= a.shape[d]
+        f.src, f.dst, f.row_elems = _p(a), _p(b), inner
+        f.src_tstride, f.src_estride = a.stride(1), a.stride(0)
+    _lib.check(_lib.load().dgppo_gather_env_steps(fields, len(src), _p(envs), int(envs.shape[0]), T, _stream(envs)),
+               "dgppo_gather_env_steps")
+
+
+@gather_env_steps.register_fake
+def _gather_env_steps_fake(src, dst, envs) -> None:
     return None

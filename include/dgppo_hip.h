@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 4  /* 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 5  /* 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -245,6 +245,11 @@ typedef struct dgppo_gnn_attn_args {
   const int32_t* sidx;  /* optional (G*n, C) sender table from dgppo_gnn_sender_table (else resolved per use) */
   const float* da_add;  /* optional (G*n, H, C) extra dL/d attn added in the softmax backward: the edge columns
                            past the first 4 (dgppo_gnn_edge_da) */
+  /* Q-free form (ABI 5): beta (G*n, H) with row stride beta_ld = q_h . bk_h precomputed (then q is not
+   * read and may be NULL); row strides of qt / dqt / dbeta (0 = packed H*D / H*D / H), so [qt | beta]
+   * and [dqt | dbeta] can share one (G*n, H*D + H) buffer; dq == NULL skips the (G*n, H*F) dq rows. */
+  const float* beta; int64_t beta_ld;
+  int64_t qt_ld, dqt_ld, dbeta_ld;
 } dgppo_gnn_attn_args;
 
 int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
@@ -440,6 +445,18 @@ int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace
  * `(1 - decay) * g` does (ABI 3) */
 int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, double b1,
                double b2, float eps, float max_norm, void* stream);
+
+/* Minibatch assembly (the reference's `jtu.tree_map(lambda x: x[idx], rollout)`, dgppo.py:275-289): for
+ * each field, output row o = e * T + t (e < n_sel) = the source row of env envs[e] at step t, read at
+ * src + t * src_tstride + envs[e] * src_estride (elements), written contiguously (row_elems elements).
+ * Fields (at most 8, a HOST array) are rows of 4-byte elements (fp32 / int32); `envs` is a DEVICE array. */
+typedef struct dgppo_gather_field {
+  const void* src; void* dst;
+  int64_t row_elems, src_tstride, src_estride;
+} dgppo_gather_field;
+
+int dgppo_gather_env_steps(const dgppo_gather_field* fields, int32_t n_fields, const int64_t* envs, int32_t n_sel,
+                           int32_t T, void* stream);
 
 /* standard normal noise from Philox4x32-10 (Box-Muller); seed from *seed_ptr when non-NULL */
 int dgppo_normal(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed, uint64_t stream_id, void* stream);
