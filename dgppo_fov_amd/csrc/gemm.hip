@@ -23,6 +23,7 @@
 //  tile   everything else: 64 x 64 LDS-tiled MFMA, optional split-K (the original kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dgppo_hip.h"
 
@@ -321,8 +322,8 @@ constexpr int kWWaves = 8;
 constexpr int kWMaxChunks = 256;
 constexpr int kWMinRows = 512;
 
-__host__ __device__ inline int wgrad_chunks(int64_t K) {
-  int64_t c = (K + kWMinRows - 1) / kWMinRows;
+__host__ __device__ inline int wgrad_chunks(int64_t K, int min_rows = kWMinRows) {
+  int64_t c = (K + min_rows - 1) / min_rows;
   if (c > kWMaxChunks) c = kWMaxChunks;
   return c < 1 ? 1 : (int)c;
 }
@@ -481,6 +482,22 @@ __global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int 
 namespace {
 enum GemmPath { kPathTile = 0, kPathRows = 1, kPathWgrad = 2 };
 
+int env_knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+// wgrad launch shape (measured, scripts/gemm_knobs.sh): at most 4 accumulator tiles per wave (M64 x N192 over
+// 131072 rows: 96 -> 67 us; more workgroups across N beat re-reading the row chunk once) and >= 128 rows per
+// chunk (small-K weight gradients such as the GRU's dWh over 16384 rows: 88 -> 65 us)
+int wgrad_min_rows() {
+  static int v = env_knob("DGPPO_WGRAD_MINROWS", 128);
+  return v;
+}
+int wgrad_max_acc() {
+  static int v = env_knob("DGPPO_WGRAD_MAXACC", 4);
+  return v;
+}
+
 GemmPath gemm_path(const dgppo_gemm_args* p) {
   if (p->trans_a && !p->trans_b && p->N <= 192 && p->M <= 4096 && !p->bias && !p->addend && !p->relu)
     return kPathWgrad;
@@ -495,9 +512,11 @@ GemmPath gemm_path(const dgppo_gemm_args* p) {
 // (MT, NT) tile-group shape for the wgrad kernel: MT * NT <= 12 accumulators of 16 per lane
 void wgrad_shape(int M, int N, int* MT, int* NT) {
   const int mt = (M + 31) / 32, nt = (N + 31) / 32;
+  const int macc = wgrad_max_acc();
   *NT = nt >= 6 ? 6 : nt >= 3 ? 3 : nt;   // 1, 2, 3 or 6 (groups of 3/6 cover larger N)
   if (nt == 4 || nt == 5) *NT = 3;
-  const int mmax = 12 / *NT;
+  while (*NT > 1 && *NT > macc) *NT = *NT == 6 ? 3 : (*NT == 3 ? 1 : *NT - 1);
+  const int mmax = macc / *NT > 0 ? macc / *NT : 1;
   *MT = mt < mmax ? mt : mmax;
   if (*MT > 4) *MT = 4;
   if (*MT == 3 && *NT == 6) *MT = 2;
@@ -514,7 +533,7 @@ void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
 int launch_wgrad(const dgppo_gemm_args* p, hipStream_t s) {
   int MT, NT;
   wgrad_shape(p->M, p->N, &MT, &NT);
-  const int chunks = dgppo::wgrad_chunks(p->K);
+  const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows());
   if (chunks > 1 && !p->workspace) return DGPPO_EINVAL;
 #define DG_W(a, b) \
   if (MT == a && NT == b) { launch_wgrad_t<a, b>(p, chunks, s); goto launched; }
@@ -545,6 +564,12 @@ void launch_rows_t(const dgppo_gemm_args* p, int ncg, hipStream_t s) {
   const int64_t units = (int64_t)((p->M + 31) / 32) * ncg;
   int per_cu = (int)((160 * 1024) / (lds > 0 ? lds : 1));
   per_cu = per_cu < 1 ? 1 : per_cu > 5 ? 5 : per_cu;
+  static int knob = -2;
+  if (knob == -2) {
+    const char* v = getenv("DGPPO_ROWS_WG_PER_CU");
+    knob = v ? atoi(v) : -1;
+  }
+  if (knob > 0 && knob < per_cu) per_cu = knob;
   const int64_t want = (units + 3) / 4, cap = 256LL * per_cu;
   const int grid = (int)(want < cap ? want : cap);
   const bool vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
@@ -570,7 +595,7 @@ extern "C" int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* p) {
   if (!p) return 0;
   switch (gemm_path(p)) {
     case kPathWgrad: {
-      const int chunks = dgppo::wgrad_chunks(p->K);
+      const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows());
       return chunks > 1 ? (int64_t)chunks * p->batch * ((int64_t)p->M * p->N + p->N) : 0;
     }
     case kPathRows:
