@@ -270,6 +270,9 @@ SIGNATURES = {
     "dgppo_grad_norm": (ctypes.c_int, [_V, _I64, _V, _V, _V]),
     "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, ctypes.c_double, ctypes.c_double, _F32, _F32, _V]),
     "dgppo_normal": (ctypes.c_int, [_V, _I64, _V, ctypes.c_uint64, ctypes.c_uint64, _V]),
+    "dgppo_clip_min0": (ctypes.c_int, [_V, _V, _I64, _V]),
+    "dgppo_lagr_advantages": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _I32, _I32, _I32, _I32, _V]),
+    "dgppo_lagr_update": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _I64, _I32, _I32, _F32, _F32, _V]),
     "dgppo_gather_env_steps": (ctypes.c_int, [ctypes.POINTER(GatherField), _I32, _V, _I32, _I32, _V]),
 }
 

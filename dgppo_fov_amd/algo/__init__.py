@@ -2,6 +2,7 @@
 from .dgppo import DGPPO
 from .hcbfcrpo import HCBFCRPO
 from .informarl import InforMARL
+from .informarl_lagr import InforMARLLagr
 
 
 def make_algo(algo: str, **kwargs):
@@ -12,5 +13,5 @@ def make_algo(algo: str, **kwargs):
     if algo == "hcbfcrpo":
         return HCBFCRPO(**kwargs)
     if algo == "informarl_lagr":
-        raise NotImplementedError(f"{algo} is not built on the MI355X path yet (DESIGN.md: next rows)")
+        return InforMARLLagr(**kwargs)
     raise ValueError(f"Unknown algorithm: {algo}")

@@ -95,6 +95,8 @@ class _Opt:
 
 
 class DGPPO:
+    VH_NET = VhNet  # the cost critic's network class (InforMARL-Lagr: VhGlobalNet)
+
     def __init__(self, env: MultiAgentEnv, node_dim: int, edge_dim: int, state_dim: int, action_dim: int,
                  n_agents: int, actor_gnn_layers: int = 2, Vl_gnn_layers: int = 2, Vh_gnn_layers: int = 1,
                  gamma: float = 0.99, lr_actor: float = 3e-4, lr_Vl: float = 1e-3, lr_Vh: float = 1e-3,
@@ -122,8 +124,8 @@ class DGPPO:
         self.actor = ActorNet(node_dim, n_agents, dev, seed=seed * 3 + 0, gnn_layers=actor_gnn_layers,
                               action_dim=action_dim, edge_dim=edge_dim)
         self.Vl = VlNet(node_dim, n_agents, dev, seed=seed * 3 + 1, gnn_layers=Vl_gnn_layers, edge_dim=edge_dim)
-        self.Vh = VhNet(node_dim, n_agents, env.n_cost, dev, seed=seed * 3 + 2, gnn_layers=Vh_gnn_layers,
-                        edge_dim=edge_dim)
+        self.Vh = self.VH_NET(node_dim, n_agents, env.n_cost, dev, seed=seed * 3 + 2, gnn_layers=Vh_gnn_layers,
+                              edge_dim=edge_dim)
         # one flat gradient buffer for the three nets (one all-reduce per minibatch)
         sizes = [self.Vl.ps.size, self.Vh.ps.size, self.actor.ps.size]
         self.grad_flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
@@ -287,6 +289,21 @@ class DGPPO:
                           self._n_agents, self._env.agent_candidates(self.device),
                           raw_cols=self._env.nonagent_feature_cols)
 
+    def _vl_all(self, rollout: Rollout, chunk: int) -> torch.Tensor:
+        """scan_Vl over every env's whole episode from the zero carry, plus the final Vl at next_graph[:, -1]
+        from the scan's last carry (final_Vl_fn_, dgppo.py:203-216): (B, T+1)."""
+        B, T = rollout.rewards.shape
+        Vl = torch.empty((B, T + 1), device=self.device)
+        for e0 in range(0, B, chunk):
+            e1 = min(B, e0 + chunk)
+            g = self._graphs(rollout.graph, slice(e0, e1))
+            v, hT, _ = self.Vl.seq_fwd(g, e1 - e0, T, keep_cache=False)
+            Vl[e0:e1, :T].copy_(v)
+            vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
+                                       keep_cache=False)
+            Vl[e0:e1, T].copy_(vf[:, 0])
+        return Vl
+
     def _vh_all(self, rollout: Rollout, chunk: int):
         """Vh on every (env, t) graph with the stored actor carries, plus the final Vh (dgppo.py:218-228)."""
         B, T, n = rollout.rewards.shape[0], rollout.rewards.shape[1], self._n_agents
@@ -336,15 +353,7 @@ class DGPPO:
         info = {}
         for _ in range(self.epoch_ppo):
             # ---- prepass: Vl scan over the whole episode + final Vl (dgppo.py:203-216)
-            Vl = torch.empty((B, T + 1), device=dev)
-            for e0 in range(0, B, chunk):
-                e1 = min(B, e0 + chunk)
-                g = self._graphs(rollout.graph, slice(e0, e1))
-                v, hT, _ = self.Vl.seq_fwd(g, e1 - e0, T, keep_cache=False)
-                Vl[e0:e1, :T].copy_(v)
-                vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
-                                           keep_cache=False)
-                Vl[e0:e1, T].copy_(vf[:, 0])
+            Vl = self._vl_all(rollout, chunk)
             ph.mark("prepass_Vl")
             Vh = self._vh_all(rollout, chunk)
             Vh_det = self._vh_all(det, chunk)

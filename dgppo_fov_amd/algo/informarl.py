@@ -68,15 +68,7 @@ class InforMARL(DGPPO):
         info, extra = {}, {}
         for _ in range(self.epoch_ppo):
             # Vl scan over the whole episode + final Vl (informarl.py:310-322)
-            Vl = torch.empty((B, T + 1), device=dev)
-            for e0 in range(0, B, chunk):
-                e1 = min(B, e0 + chunk)
-                g = self._graphs(rollout.graph, slice(e0, e1))
-                v, hT, _ = self.Vl.seq_fwd(g, e1 - e0, T, keep_cache=False)
-                Vl[e0:e1, :T].copy_(v)
-                vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
-                                           keep_cache=False)
-                Vl[e0:e1, T].copy_(vf[:, 0])
+            Vl = self._vl_all(rollout, chunk)
             Ql, A, extra = self._targets(rollout, Vl, step)
             # minibatches (informarl.py:342-355)
             L = self.rnn_step

@@ -278,3 +278,78 @@ class VhNet(_Net):
         dy, _ = self.gru.seq_bwd(rc, dh2)
         dz = self.head.bwd(hc, dy)
         self.gnn.bwd(gc, dz, g)
+
+
+class VhGlobalNet(_Net):
+    """InforMARL-Lagr's cost critic: ValueNet(n_out=n_cost, decompose=True, use_global_info=True)
+    (DecRStateFn, value.py:47-79; informarl_lagr.py:68-79): GNN(agent rows) -> [x | mean over agents of x]
+    (n, 128) -> MLP(64, 64) -> GRUCell with its OWN carries (scan_Vh, informarl_lagr.py:152-163) ->
+    Dense(n_cost).  The concat never materialises: head Dense_0 = x W[:64] + b + broadcast(mean(x) W[64:])
+    (one GEMM of the agent-mean rows, added per graph through the GEMM addend's row grouping)."""
+
+    def __init__(self, node_dim: int, n_agents: int, n_cost: int, device, seed: int = 2, gnn_layers: int = 1,
+                 edge_dim: int = 4):
+        self.n, self.n_cost = n_agents, n_cost
+        ps = self.ps = ParamSpace()
+        self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
+        self.head = MLPHead(ps, "head", d_in=128)
+        self.gru = GRUCell(ps, "gru")
+        self.out = Dense(ps, "out", 64, n_cost)
+        self.modules = [self.gnn, self.head, self.gru, self.out]
+        ps.build(device)
+        self.init_host(seed)
+        self.device = torch.device(device)
+
+    def flax(self):
+        return {"gnn": self.gnn.flax(), "head": self.head.flax(), "gru": self.gru.flax(), "out": self.out.flax()}
+
+    def load_flax(self, d):
+        self.gnn.load_flax(d["gnn"]), self.head.load_flax(d["head"]), self.gru.load_flax(d["gru"])
+        self.out.load_flax(d["out"])
+
+    def seq_fwd(self, g: GraphBatch, S: int, L: int, h0=None, keep_cache=True):
+        """scan_Vh over S sequences of L graphs (zero carries unless h0 (S*n, 64)): values (S*L*n, n_cost) rows
+        (s, t, agent), final carries (S*n, 64) and the cache for seq_bwd."""
+        n, dev = self.n, g.nodes.device
+        G = S * L
+        rows = G * n
+        z, gc = self.gnn.fwd(g)  # (rows, 64)
+        zm = torch.empty((G, 64), device=dev)
+        K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
+        W0 = self.head.d0.W()
+        m = torch.empty((G, 64), device=dev)
+        K.gemm(zm, W0[64:], m, G, 64, 64)
+        h0pre = torch.empty((rows, 64), device=dev)
+        K.gemm(z, W0[:64], h0pre, rows, 64, 64, bias=self.head.d0.b(), addend=m, ld_add=0, add_grp=n, add_gs=64)
+        hd = self.head
+        y0, c0 = hd.ln0.fwd(h0pre)
+        h1 = hd.d1.fwd(y0, rows)
+        y1, c1 = hd.ln1.fwd(h1)
+        hT = torch.empty((S * n, 64), device=dev)
+        Hs, gcs = self.gru.seq_fwd(y1, S * n, L, n, h0=h0, hT_out=hT)
+        out = self.out.fwd(Hs, rows)
+        cache = (g, S, L, gc, z, zm, y0, c0, c1, gcs, Hs) if keep_cache else None
+        return out, hT, cache
+
+    def seq_bwd(self, cache, dout):
+        g, S, L, gc, z, zm, y0, c0, c1, gcs, Hs = cache
+        n, dev = self.n, dout.device
+        G = S * L
+        rows = G * n
+        hd = self.head
+        dH = self.out.bwd(Hs, dout, rows)
+        dy1, _ = self.gru.seq_bwd(gcs, dH)
+        dh1 = hd.ln1.bwd(c1, dy1)
+        dy0 = hd.d1.bwd(y0, dh1, rows)
+        dh0 = hd.ln0.bwd(c0, dy0)  # d(head Dense_0 output) (rows, 64)
+        W0, dW0 = hd.d0.W(), hd.d0.W(True)
+        K.gemm(z, dh0, dW0[:64], 64, 64, rows, ta=True, beta=1.0, bias_grad=hd.d0.b(True))
+        sm = torch.empty((G, 64), device=dev)  # per-graph mean of dh0; the agent SUM is n x it
+        K.agent_mean_fwd(dh0, sm, G, n, 64, n * 64)
+        K.gemm(zm, sm, dW0[64:], 64, 64, G, ta=True, alpha=float(n), beta=1.0)
+        # dz = dh0 W[:64]^T + (sum_agents dh0) W[64:]^T / n  (the mean's backward), one GEMM with a per-graph addend
+        dzm = torch.empty((G, 64), device=dev)
+        K.gemm(sm, W0[64:], dzm, G, 64, 64, tb=True, ldb=64)
+        dz = torch.empty_like(z)
+        K.gemm(dh0, W0[:64], dz, rows, 64, 64, tb=True, ldb=64, addend=dzm, ld_add=0, add_grp=n, add_gs=64)
+        self.gnn.bwd(gc, dz, g)

@@ -1038,3 +1038,128 @@ extern "C" int dgppo_gather_env_steps(const dgppo_gather_field* fields, int32_t 
                      0, DG_STREAM(stream), fs, envs, T, rows);
   return (int)hipGetLastError();
 }
+
+// ---- InforMARL-Lagr (dgppo/algo/informarl_lagr.py:125-309) ------------------------------------------------
+namespace dgppo {
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  const float s = red[0];
+  __syncthreads();
+  return s;
+}
+
+__global__ void clip_min0_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = x[i];
+    y[i] = v < 0.0f ? 0.0f : v;  // jnp.clip(costs, a_min=0): NaN passes through
+  }
+}
+
+// one workgroup per env: Al = -(norm_t (Ql - Vl)), Ah = norm_t (Qh - Vh) per (agent, h) (population std + 1e-8),
+// A[t, a] = Al[t] - mean_h (Ah[t, a, h] lagr[a, h])   (informarl_lagr.py:205-221)
+__global__ __launch_bounds__(256) void lagr_adv_kernel(const float* __restrict__ Ql, const float* __restrict__ Vl,
+                                                       const float* __restrict__ Qh, const float* __restrict__ Vh,
+                                                       const float* __restrict__ lagr, float* __restrict__ A,
+                                                       float* __restrict__ Ah, int32_t T, int32_t n, int32_t nh) {
+  __shared__ float red[256];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* q = Ql + b * T;
+  const float* v = Vl + b * (T + 1);
+  float s = 0.0f;
+  for (int t = tid; t < T; t += 256) s += q[t] - v[t];
+  const float mean = block_sum256(s, red) / (float)T;
+  float s2 = 0.0f;
+  for (int t = tid; t < T; t += 256) {
+    const float d = (q[t] - v[t]) - mean;
+    s2 += d * d;
+  }
+  const float den = sqrtf(block_sum256(s2, red) / (float)T) + 1e-8f;
+  // constraint advantages: (agent, h) columns, each normalised over t; Vh row stride (T+1) n nh
+  const float* qh = Qh + b * T * n * nh;
+  const float* vh = Vh + b * (int64_t)(T + 1) * n * nh;
+  float* ah = Ah + b * T * n * nh;
+  for (int col = 0; col < n * nh; ++col) {
+    float cs = 0.0f;
+    for (int t = tid; t < T; t += 256) cs += qh[t * n * nh + col] - vh[t * n * nh + col];
+    const float cm = block_sum256(cs, red) / (float)T;
+    float cs2 = 0.0f;
+    for (int t = tid; t < T; t += 256) {
+      const float d = (qh[t * n * nh + col] - vh[t * n * nh + col]) - cm;
+      cs2 += d * d;
+    }
+    const float cden = sqrtf(block_sum256(cs2, red) / (float)T) + 1e-8f;
+    for (int t = tid; t < T; t += 256) ah[t * n * nh + col] = ((qh[t * n * nh + col] - vh[t * n * nh + col]) - cm) / cden;
+  }
+  __syncthreads();
+  for (int e = tid; e < T * n; e += 256) {
+    const int t = e / n, a = e - t * n;
+    float m = 0.0f;
+    for (int h = 0; h < nh; ++h) m += ah[(int64_t)t * n * nh + a * nh + h] * lagr[a * nh + h];
+    A[b * T * n + e] = -(((q[t] - v[t]) - mean) / den) - m / (float)nh;
+  }
+}
+
+// one workgroup per (agent, h): delta = -mean_{b,t} (Vh (1 - gamma) + ratio Ah), ratio = exp(log_pi - log_pi_old);
+// lagr = relu(lagr - lr delta)   (update_lagr, informarl_lagr.py:283-305).  Fixed-order block reduction.
+__global__ __launch_bounds__(256) void lagr_update_kernel(const float* __restrict__ lp, const float* __restrict__ lp_old,
+                                                          const float* __restrict__ Vh, const float* __restrict__ Ah,
+                                                          float* __restrict__ lagr, float* __restrict__ lagr_mean_out,
+                                                          int64_t rows, int32_t n, int32_t nh, float gamma, float lr) {
+  __shared__ float red[256];
+  const int col = blockIdx.x, a = col / nh;
+  float s = 0.0f;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) {
+    const float ratio = expf(lp[r * n + a] - lp_old[r * n + a]);
+    s += Vh[r * n * nh + col] * (1.0f - gamma) + ratio * Ah[r * n * nh + col];
+  }
+  const float delta = -(block_sum256(s, red) / (float)rows);
+  if (threadIdx.x == 0) {
+    const float l = lagr[col] - delta * lr;
+    lagr[col] = l > 0.0f ? l : 0.0f;
+  }
+  (void)lagr_mean_out;
+}
+
+__global__ void mean_kernel(const float* __restrict__ x, int32_t n, float* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int i = 0; i < n; ++i) s += x[i];
+    out[0] = s / (float)n;
+  }
+}
+}  // namespace dgppo
+
+extern "C" int dgppo_clip_min0(const float* x, float* y, int64_t n, void* stream) {
+  if (n < 0 || !x || !y) return DGPPO_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dgppo::clip_min0_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), x, y, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_lagr_advantages(const float* Ql, const float* Vl, const float* Qh, const float* Vh,
+                                     const float* lagr, float* A, float* Ah, int32_t B, int32_t T, int32_t n_agents,
+                                     int32_t n_h, void* stream) {
+  if (B < 0 || T < 1 || n_agents < 1 || n_h < 1 || !Ql || !Vl || !Qh || !Vh || !lagr || !A || !Ah) return DGPPO_EINVAL;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(dgppo::lagr_adv_kernel, dim3((unsigned)B), dim3(256), 0, DG_STREAM(stream), Ql, Vl, Qh, Vh, lagr,
+                     A, Ah, T, n_agents, n_h);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_lagr_update(const float* log_pi, const float* log_pi_old, const float* Vh, const float* Ah,
+                                 float* lagr, float* lagr_mean, int64_t rows, int32_t n_agents, int32_t n_h,
+                                 float gamma, float lr, void* stream) {
+  if (rows < 1 || n_agents < 1 || n_h < 1 || !log_pi || !log_pi_old || !Vh || !Ah || !lagr) return DGPPO_EINVAL;
+  hipLaunchKernelGGL(dgppo::lagr_update_kernel, dim3((unsigned)(n_agents * n_h)), dim3(256), 0, DG_STREAM(stream),
+                     log_pi, log_pi_old, Vh, Ah, lagr, lagr_mean, rows, n_agents, n_h, gamma, lr);
+  if (lagr_mean)
+    hipLaunchKernelGGL(dgppo::mean_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), lagr, n_agents * n_h, lagr_mean);
+  return (int)hipGetLastError();
+}

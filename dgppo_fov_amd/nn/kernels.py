@@ -207,3 +207,19 @@ def dgppo_advantages(Ql, Vl, Vh, A, safe_count, dt, alpha, cbf_eps, cbf_weight):
     a.Ql, a.Vl, a.Vh, a.A, a.safe_count = _p(Ql), _p(Vl), _p(Vh), _p(A), _p(safe_count)
     a.dt, a.alpha, a.cbf_eps, a.cbf_weight = float(dt), float(alpha), float(cbf_eps), float(cbf_weight)
     _chk(_lib.load().dgppo_dgppo_advantages(ctypes.byref(a), _stream(Ql)), "dgppo_dgppo_advantages")
+
+
+def clip_min0(x, y):
+    _chk(_lib.load().dgppo_clip_min0(_p(x), _p(y), int(x.numel()), _stream(y)), "dgppo_clip_min0")
+
+
+def lagr_advantages(Ql, Vl, Qh, Vh, lagr, A, Ah):
+    B, T, n, nh = Qh.shape
+    _chk(_lib.load().dgppo_lagr_advantages(_p(Ql), _p(Vl), _p(Qh), _p(Vh), _p(lagr), _p(A), _p(Ah), int(B), int(T),
+                                           int(n), int(nh), _stream(A)), "dgppo_lagr_advantages")
+
+
+def lagr_update(log_pi, log_pi_old, Vh, Ah, lagr, lagr_mean, rows, gamma, lr):
+    n, nh = lagr.shape
+    _chk(_lib.load().dgppo_lagr_update(_p(log_pi), _p(log_pi_old), _p(Vh), _p(Ah), _p(lagr), _p(lagr_mean), int(rows),
+                                       int(n), int(nh), float(gamma), float(lr), _stream(lagr)), "dgppo_lagr_update")

@@ -446,6 +446,18 @@ int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace
 int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, double b1,
                double b2, float eps, float max_norm, void* stream);
 
+/* InforMARL-Lagr (dgppo/algo/informarl_lagr.py:125-309): y = max(x, 0) (the GAE's clipped costs, :196);
+ * the merged advantage A = -norm_t(Ql - Vl) - mean_h(lagr norm_t(Qh - Vh)) with Ah = norm_t(Qh - Vh) out
+ * (Ql (B,T), Vl (B,T+1), Qh (B,T,n,nh), Vh (B,T+1,n,nh), lagr (n,nh), :205-221); and update_lagr (:283-305):
+ * lagr = relu(lagr - lr delta), delta = -mean over `rows` (env, t) of Vh (1 - gamma) + exp(log_pi -
+ * log_pi_old) Ah, with lagr_mean (optional) = mean of the new multipliers. */
+int dgppo_clip_min0(const float* x, float* y, int64_t n, void* stream);
+int dgppo_lagr_advantages(const float* Ql, const float* Vl, const float* Qh, const float* Vh, const float* lagr,
+                          float* A, float* Ah, int32_t B, int32_t T, int32_t n_agents, int32_t n_h, void* stream);
+int dgppo_lagr_update(const float* log_pi, const float* log_pi_old, const float* Vh, const float* Ah, float* lagr,
+                      float* lagr_mean, int64_t rows, int32_t n_agents, int32_t n_h, float gamma, float lr,
+                      void* stream);
+
 /* Minibatch assembly (the reference's `jtu.tree_map(lambda x: x[idx], rollout)`, dgppo.py:275-289): for
  * each field, output row o = e * T + t (e < n_sel) = the source row of env envs[e] at step t, read at
  * src + t * src_tstride + envs[e] * src_estride (elements), written contiguously (row_elems elements).

@@ -269,6 +269,27 @@ def informarl_advantages(Ql, Vl, n_agents):
     return -np.repeat(Al[:, :, None], n_agents, axis=-1)
 
 
+def lagr_advantages(Ql, Vl, Qh, Vh, lagr):
+    """InforMARL-Lagr (informarl_lagr.py:205-221): Al = Ql - Vl[:, :T] normalised over T per env;
+    Ah = Qh - Vh[:, :T] normalised over T per (env, agent, cost); A = -Al - mean_h(Ah * lagr).
+    Returns (A (B, T, n), Ah (B, T, n, nh))."""
+    Ql, Vl, Qh, Vh, lagr = (np.asarray(x, np.float64) for x in (Ql, Vl, Qh, Vh, lagr))
+    T = Ql.shape[1]
+    Al = Ql - Vl[:, :T]
+    Al = (Al - Al.mean(axis=1, keepdims=True)) / (Al.std(axis=1, keepdims=True) + 1e-8)
+    Ah = Qh - Vh[:, :T]
+    Ah = (Ah - Ah.mean(axis=1, keepdims=True)) / (Ah.std(axis=1, keepdims=True) + 1e-8)
+    return -Al[:, :, None] - (Ah * lagr[None, None]).mean(-1), Ah
+
+
+def lagr_update(lagr, log_pi, log_pi_old, Vh, Ah, gamma, lr):
+    """update_lagr (informarl_lagr.py:283-305): ratio = exp(log_pi - log_pi_old) (B, T, n);
+    delta = -mean_{b,t}(Vh (1 - gamma) + ratio Ah) (n, nh); lagr <- relu(lagr - lr delta)."""
+    ratio = np.exp(np.asarray(log_pi, np.float64) - np.asarray(log_pi_old, np.float64))
+    delta = -(np.asarray(Vh, np.float64) * (1 - gamma) + ratio[..., None] * np.asarray(Ah, np.float64)).mean((0, 1))
+    return np.maximum(np.asarray(lagr, np.float64) - delta * lr, 0.0)
+
+
 def merged_cbf_advantages(Ql, Vl, Vh, n_agents, dt, alpha, cbf_eps, cbf_weight):
     """DGPPO's merged advantage (dgppo.py:239-259, identical in hcbfcrpo.py:163-183): Al = Ql - Vl[:, :T]
     normalised over T; deriv = (Vh[t+1] - Vh[t]) / dt + alpha Vh[t]; Acbf = max(deriv + eps, 0);

@@ -152,6 +152,21 @@ def vl_seq(p, graph, S, L, n, h0=None, return_h=False):
     return (v, h) if return_h else v
 
 
+def vh_global_seq(p, graph, S, L, n, h0=None, return_h=False):
+    """scan_Vh of InforMARL-Lagr's ValueNet(decompose=True, use_global_info=True) (DecRStateFn,
+    value.py:47-79) over S sequences of L graphs, zero carries unless h0 (S, n, 64): values (S, L, n, n_out)."""
+    x = gnn(p["gnn"], graph, n)  # (G, n, 64)
+    x = torch.cat([x, x.mean(1, keepdim=True).expand(-1, n, -1)], -1)
+    y = mlp_head(x, p["head"]).reshape(S, L, n, 64)
+    h = torch.zeros((S, n, 64), dtype=T64) if h0 is None else torch.as_tensor(h0, dtype=T64)
+    vs = []
+    for t in range(L):
+        h = gru_cell(p["gru"], h, y[:, t])
+        vs.append(dense(h, p["out"]))
+    v = torch.stack(vs, 1)
+    return (v, h) if return_h else v
+
+
 def actor_carry(p, graph, h, n):
     """act(): the policy GRU carry after one graph (policy.py:61-74), h (G, n, 64)."""
     y = mlp_head(gnn(p["gnn"], graph, n), p["head"])

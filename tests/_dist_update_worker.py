@@ -25,15 +25,16 @@ def host(r):
                 dones=r.dones.cpu().clone(), log_pis=None if r.log_pis is None else r.log_pis.cpu().clone())
 
 
-def main(out):
+def main(out, algo_name="dgppo"):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     env = make_env(ENV, N, num_obs=OBS, max_step=T, device=dev)
-    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+    extra = dict(lagr_init=0.5, lr_lagr=0.1) if algo_name == "informarl_lagr" else {}
+    algo = make_algo(algo_name, env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
                      action_dim=env.action_dim, n_agents=N, batch_size=B_LOCAL * T * world, rnn_step=L,
-                     train_steps=100, seed=1, device=dev)
+                     train_steps=100, seed=1, device=dev, **extra)
     assert algo.world == world and algo.rank == rank
     roll = algo.collect(algo.params, 7, n_env=B_LOCAL)  # env shard [rank B, (rank + 1) B)
     saved = host(roll)
@@ -41,13 +42,16 @@ def main(out):
     info = algo.update(roll, 3)
     torch.cuda.synchronize()
     (mb,) = algo.trace["mb"]
-    torch.save(dict(roll=saved, det=host(algo.trace["det"]), envs=torch.as_tensor(mb["envs"]),
+    torch.save(dict(roll=saved, det=host(algo.trace["det"]) if "det" in algo.trace else None,
+                    envs=torch.as_tensor(mb["envs"]),
                     grad=mb["grad"].cpu(), before={k: v.cpu() for k, v in mb["before"].items()},
                     after={k: o.ps.flat.cpu().clone() for k, o in algo.opt.items()},
-                    safe=info["eval/safe_data"]), os.path.join(out, f"rank{rank}.pt"))
+                    safe=info.get("eval/safe_data"),
+                    lagr=algo.ah_lagr.cpu().clone() if hasattr(algo, "ah_lagr") else None),
+               os.path.join(out, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *sys.argv[2:3])

@@ -25,13 +25,17 @@ def _cat(parts, dev):
     return torch.cat([p.to(dev) for p in parts], 0)
 
 
-def test_two_rank_update_equals_single_process_union(cuda, tmp_path):
+@pytest.mark.parametrize("algo_name", ["dgppo", "informarl_lagr"])
+def test_two_rank_update_equals_single_process_union(cuda, tmp_path, algo_name):
+    """informarl_lagr adds the sharded multiplier step (per-rank delta, one all-reduce, same relu step on
+    every rank): multipliers identical across ranks and equal to the single-process union's."""
     world, port = 2, 29700 + os.getpid() % 200
     procs = []
     for r in range(world):
         envv = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                     MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_update_worker.py"), str(tmp_path)],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_update_worker.py"), str(tmp_path),
+                                       algo_name],
                                       env=envv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     for p in procs:
         out, _ = p.communicate(timeout=150)
@@ -46,9 +50,10 @@ def test_two_rank_update_equals_single_process_union(cuda, tmp_path):
     # single process on the union of the shards: the same minibatch loss, gradient of the full batch
     env = make_env(W.ENV, W.N, num_obs=W.OBS, max_step=W.T, device=cuda)
     B = W.B_LOCAL * world
-    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+    extra = dict(lagr_init=0.5, lr_lagr=0.1) if algo_name == "informarl_lagr" else {}
+    algo = make_algo(algo_name, env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
                      action_dim=env.action_dim, n_agents=W.N, batch_size=B * W.T, rnn_step=W.L, train_steps=100,
-                     seed=1, device=cuda)
+                     seed=1, device=cuda, **extra)
     for k, o in algo.opt.items():  # the ranks' starting parameters (same seed -> same init)
         assert torch.equal(o.ps.flat.cpu(), res[0]["before"][k])
 
@@ -61,8 +66,10 @@ def test_two_rank_update_equals_single_process_union(cuda, tmp_path):
                        _cat([x["dones"] for x in d], cuda),
                        None if d[0]["log_pis"] is None else _cat([x["log_pis"] for x in d], cuda), g("next_graph"))
 
-    roll, det = rollout("roll"), rollout("det")
-    algo.det_rollout = lambda n_env, key: det  # the ranks' deterministic rollouts, concatenated
+    roll = rollout("roll")
+    if res[0]["det"] is not None:
+        det = rollout("det")
+        algo.det_rollout = lambda n_env, key: det  # the ranks' deterministic rollouts, concatenated
     algo.trace = {}
     info = algo.update(roll, 3)
     torch.cuda.synchronize()
@@ -75,4 +82,10 @@ def test_two_rank_update_equals_single_process_union(cuda, tmp_path):
         off += net.ps.size
         err = np.abs(a - b).max()
         assert err <= 1e-5 * np.abs(b).max() + 1e-7, f"{name}: shard-mean vs full-batch gradient {err:.3e}"
-    assert abs(info["eval/safe_data"] - res[0]["safe"]) < 1e-6
+    if algo_name == "dgppo":
+        assert abs(info["eval/safe_data"] - res[0]["safe"]) < 1e-6
+    else:
+        assert torch.equal(res[0]["lagr"], res[1]["lagr"])
+        lg = algo.ah_lagr.cpu()
+        assert not torch.equal(lg, torch.full_like(lg, 0.5))  # the step moved the multipliers
+        assert (lg - res[0]["lagr"]).abs().max().item() <= 1e-5 * lg.abs().max().item() + 1e-7

@@ -207,3 +207,23 @@ def test_ppo_clipped_loss_hand_values():
     assert abs(loss - (-1.0 / 12 - 0.004)) < 1e-12
     assert abs(info["clip_frac"] - 2 / 3) < 1e-12
     assert abs(info["total_variation_dist"] - 0.5 * (0.5 + 0.5 + 0.0) / 3) < 1e-12
+
+
+def test_lagr_advantages_and_update_kat():
+    """InforMARL-Lagr by hand (informarl_lagr.py:205-221, 283-305): Ql - Vl = [0, 2] per env normalises to
+    [-1, 1]; Qh - Vh = [1, 3] likewise; A = -Al - mean_h(Ah lagr). With log pi = old log pi (ratio 1),
+    Vh = c and Ah with zero mean over (b, t), delta = -c (1 - gamma): lagr + lr c (1 - gamma)."""
+    Ql = np.array([[0.0, 2.0]])
+    Vl = np.zeros((1, 3))
+    Qh = np.array([[1.0, 3.0]])[:, :, None, None] * np.ones((1, 2, 1, 2))
+    Vh = np.zeros((1, 3, 1, 2))
+    lagr = np.array([[0.5, 1.5]])
+    A, Ah = O.lagr_advantages(Ql, Vl, Qh, Vh, lagr)
+    np.testing.assert_allclose(Ah[0, :, 0, 0], [-1.0, 1.0], atol=1e-7)
+    np.testing.assert_allclose(A[0, :, 0], [1.0 + 1.0, -1.0 - 1.0], atol=1e-7)  # mean_h(lagr) = 1
+    lp = np.zeros((1, 2, 1))
+    out = O.lagr_update(lagr, lp, lp, np.full((1, 2, 1, 2), 3.0), Ah, 0.9, 0.1)
+    np.testing.assert_allclose(out, lagr + 0.1 * 3.0 * 0.1, atol=1e-12)
+    # relu: a large negative Vh drives the multiplier to zero
+    out = O.lagr_update(lagr, lp, lp, np.full((1, 2, 1, 2), -1e3), Ah, 0.9, 0.1)
+    assert (out == 0).all()
