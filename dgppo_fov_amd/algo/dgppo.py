@@ -256,6 +256,15 @@ class DGPPO:
         return self._engine(n_env, RolloutEngine.MODE_DET).run(key)
 
     # ---- update ------------------------------------------------------------------------------
+    def _env_ids(self, batches):
+        """Every minibatch's env ids in ONE host-to-device copy (a per-minibatch copy from pageable memory
+        synchronises the stream and stalls the launch pipeline); yields (len(bi),) device views."""
+        flat = torch.as_tensor(np.concatenate(batches).astype(np.int64), device=self.device)
+        off = 0
+        for bi in batches:
+            yield flat[off:off + len(bi)]
+            off += len(bi)
+
     @staticmethod
     def _gather(envs: torch.Tensor, *fields):
         """Contiguous (len(envs), T, ...) copies of (B, T, ...) rollout fields for the selected envs, one
@@ -340,24 +349,62 @@ class DGPPO:
             pending.clear()
             self.grad_flat.mul_(1.0 / self.world)
 
+    def _aux_streams(self, k: int):
+        """k auxiliary HIP streams for the update's independent passes (None when DGPPO_STREAMS=0 or
+        when DGPPO_PROFILE phase timing is on, which synchronises between passes)."""
+        if k <= 0 or os.environ.get("DGPPO_STREAMS", "1") == "0" or os.environ.get("DGPPO_PROFILE", "0") == "1":
+            return None
+        aux = getattr(self, "_aux", None)
+        if aux is None or len(aux) < k:
+            aux = self._aux = [torch.cuda.Stream(self.device) for _ in range(k)]
+        return aux[:k]
+
+    def _parallel(self, jobs):
+        """Run independent closures concurrently and return their results: job 0 on the current stream,
+        job i > 0 on auxiliary stream i - 1.  Every auxiliary stream first waits for all work enqueued so
+        far and the current stream then waits for every auxiliary stream, so results are used, and
+        buffers freed, only after the producing stream's work.  Each job's kernels keep their order, so
+        the results are bit-identical to running the jobs one after another."""
+        aux = self._aux_streams(len(jobs) - 1)
+        if aux is None:
+            return [job() for job in jobs]
+        main = torch.cuda.current_stream(self.device)
+        for st in aux:
+            st.wait_stream(main)
+        out = [None] * len(jobs)
+        for k, job in enumerate(jobs[1:]):
+            with torch.cuda.stream(aux[k]):
+                out[k + 1] = job()
+        out[0] = jobs[0]()
+        for st in aux:
+            main.wait_stream(st)
+        return out
+
     def update(self, rollout: Rollout, step: int) -> dict:
         env, dev = self._env, self.device
         B, T = rollout.rewards.shape
         n = self._n_agents
         ph = _Phases(dev)
         ph.mark()
-        det = self.det_rollout(B, int(self.key.integers(0, 2 ** 62)))
-        ph.mark("det_rollout")
+        det_key = int(self.key.integers(0, 2 ** 62))
         assert B * T * self.world >= self.batch_size
         chunk = max(1, min(B, 65536 // T))
         info = {}
+        det = None
         for _ in range(self.epoch_ppo):
-            # ---- prepass: Vl scan over the whole episode + final Vl (dgppo.py:203-216)
-            Vl = self._vl_all(rollout, chunk)
-            ph.mark("prepass_Vl")
-            Vh = self._vh_all(rollout, chunk)
-            Vh_det = self._vh_all(det, chunk)
-            ph.mark("prepass_Vh")
+            # ---- prepass (dgppo.py:203-228): Vl scan over the whole episode + final Vl; Vh on every graph of
+            # the rollout and of the deterministic rollout.  Independent passes on three streams: the det
+            # rollout (a latency-bound 128-step launch chain) and its Vh overlap the rollout's Vl / Vh passes.
+            if det is None:
+                def det_job():
+                    d = self.det_rollout(B, det_key)
+                    return d, self._vh_all(d, chunk)
+
+                Vl, (det, Vh_det), Vh = self._parallel([lambda: self._vl_all(rollout, chunk), det_job,
+                                                        lambda: self._vh_all(rollout, chunk)])
+            else:
+                Vl, Vh, Vh_det = self._vl_all(rollout, chunk), self._vh_all(rollout, chunk), self._vh_all(det, chunk)
+            ph.mark("prepass")
             # ---- GAE + advantages
             costs = rollout.costs.contiguous()
             l = (-rollout.rewards).contiguous()
@@ -381,55 +428,61 @@ class DGPPO:
             L = self.rnn_step
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
             S_per_env = T // L
+            env_ids = self._env_ids(batches)
             for bi in batches:
-                envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
+                envs = next(env_ids)
                 Bm = len(bi)
                 self.grad_flat.zero_()
                 # the minibatch's rows of both rollouts (x[idx] of dgppo.py:278-279): two gather launches
                 rg = rollout.graph
                 nodes, edges, recv, send, acts, lp_old, adv, tgt = self._gather(
                     envs, rg.nodes, rg.edges, rg.receivers, rg.senders, rollout.actions, rollout.log_pis, A, Ql)
-                g = self._graph_batch(nodes, edges, recv, send)
+                g = self._graph_batch(nodes, edges, recv, send).prepare()
                 dg = det.graph
                 dnodes, dedges, drecv, dsend, hd, qhd = self._gather(
                     envs, dg.nodes, dg.edges, dg.receivers, dg.senders, det.rnn_states, Qh_det)
-                # update_Vl (informarl.py:357-385)
-                v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
+                gd = self._graph_batch(dnodes, dedges, drecv, dsend).prepare()
                 tgt = tgt.view(Bm * S_per_env, L)
-                dv = torch.empty_like(v)
-                vl_loss = torch.empty(1, device=dev)
-                K.l2_loss(v, tgt, dv, vl_loss)
-                ph.mark("Vl_fwd")
-                self.Vl.seq_bwd(cache, dv)
-                del cache
-                pending = []
-                self._start_reduce(self.Vl, pending)
-                ph.mark("Vl_bwd")
-                # update_Vh (dgppo.py:296-321) on the deterministic rollout
-                gd = self._graph_batch(dnodes, dedges, drecv, dsend)
-                vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, 64))
-                dvh = torch.empty_like(vh)
-                vh_loss = torch.empty(1, device=dev)
-                K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, vh_loss)
-                ph.mark("Vh_fwd")
-                self.Vh.bwd(cache, dvh)
-                del cache
-                self._start_reduce(self.Vh, pending)
-                ph.mark("Vh_bwd")
-                # update_policy (informarl.py:405-457)
                 acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
-                lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
-                dlp = torch.empty_like(lp)
-                dent = torch.empty_like(ent)
-                stats = torch.empty(4, device=dev)
-                K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, stats)
-                ph.mark("pi_fwd")
-                self.actor.eval_seq_bwd(cache, dlp, dent)
-                del cache
-                self._start_reduce(self.actor, pending)
-                ph.mark("pi_bwd")
-                # the three gradient buckets reduced (overlapped with the later nets' passes), then clip +
-                # finite check + Adam per net
+                pending = []
+
+                def vl_job():  # update_Vl (informarl.py:357-385)
+                    v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
+                    dv = torch.empty_like(v)
+                    loss = torch.empty(1, device=dev)
+                    K.l2_loss(v, tgt, dv, loss)
+                    ph.mark("Vl_fwd")
+                    self.Vl.seq_bwd(cache, dv)
+                    self._start_reduce(self.Vl, pending)  # the bucket's all-reduce overlaps the other passes
+                    ph.mark("Vl_bwd")
+                    return loss
+
+                def vh_job():  # update_Vh (dgppo.py:296-321) on the deterministic rollout
+                    vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, 64))
+                    dvh = torch.empty_like(vh)
+                    loss = torch.empty(1, device=dev)
+                    K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)
+                    ph.mark("Vh_fwd")
+                    self.Vh.bwd(cache, dvh)
+                    self._start_reduce(self.Vh, pending)
+                    ph.mark("Vh_bwd")
+                    return loss
+
+                def pi_job():  # update_policy (informarl.py:405-457)
+                    lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
+                    dlp = torch.empty_like(lp)
+                    dent = torch.empty_like(ent)
+                    st = torch.empty(4, device=dev)
+                    K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, st)
+                    ph.mark("pi_fwd")
+                    self.actor.eval_seq_bwd(cache, dlp, dent)
+                    self._start_reduce(self.actor, pending)
+                    ph.mark("pi_bwd")
+                    return st
+
+                # the three passes are independent (own parameters and gradient slices): concurrent streams
+                stats, vl_loss, vh_loss = self._parallel([pi_job, vl_job, vh_job])
+                # gradient buckets all-reduced (sum, then / world), clip + finite check + Adam per net
                 self._finish_reduce(pending)
                 if self.trace is not None:
                     self.trace["mb"].append(dict(

@@ -74,8 +74,10 @@ class InforMARL(DGPPO):
             L = self.rnn_step
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
             S_per_env = T // L
-            for bi in minibatch_plan(B, T, self.world, self.batch_size, self.np_rng):
-                envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
+            batches = minibatch_plan(B, T, self.world, self.batch_size, self.np_rng)
+            env_ids = self._env_ids(batches)
+            for bi in batches:
+                envs = next(env_ids)
                 Bm = len(bi)
                 self.grad_flat.zero_()
                 rg = rollout.graph

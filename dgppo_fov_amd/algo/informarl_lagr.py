@@ -77,8 +77,10 @@ class InforMARLLagr(InforMARL):
             S_per_env = T // L
             Vh_T = Vh[:, :T]
             lagr_mean = torch.empty(1, device=dev)
-            for bi in minibatch_plan(B, T, self.world, self.batch_size, self.np_rng):
-                envs = torch.as_tensor(bi, device=dev, dtype=torch.long)
+            batches = minibatch_plan(B, T, self.world, self.batch_size, self.np_rng)
+            env_ids = self._env_ids(batches)
+            for bi in batches:
+                envs = next(env_ids)
                 Bm = len(bi)
                 self.grad_flat.zero_()
                 rg = rollout.graph

@@ -16,8 +16,9 @@ _WS = {}
 
 
 def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
-    """Grow-only scratch buffer per (device, slot); safe to reuse across sequential launches."""
-    key = (str(device), slot)
+    """Grow-only scratch buffer per (device, slot, current stream): reused by the sequential launches of
+    one stream, never shared by launches that may run concurrently on different streams."""
+    key = (str(device), slot, _lib.stream_handle(device))
     t = _WS.get(key)
     if t is None or t.numel() < nfloats:
         t = torch.empty(max(int(nfloats), 1024), dtype=torch.float32, device=device)

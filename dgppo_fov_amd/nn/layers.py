@@ -553,6 +553,12 @@ class GraphBatch:
         self._sidx = None
         self._edges_head = self._edges_x = self._sender_raw = None
 
+    def prepare(self):
+        """Build every lazily derived table (sender table, edge splits, raw sender rows) now, on the
+        current stream, so the batch can be read by passes running concurrently on other streams."""
+        _ = self.sidx, self.edges_head, self.edges_x, self.sender_raw
+        return self
+
     @property
     def sidx(self) -> torch.Tensor:
         """(G*n, C) resolved sender of every candidate edge (-1 if masked), built once per batch and

@@ -13,6 +13,7 @@ M = int(os.environ.get("ROWS", "131072"))
 # (label, M, N, K, ta, tb, batch, bias, beta)
 SHAPES = [
     ("fwd N192 K64 +b", M, 192, 64, 0, 0, 1, True, 0.0),
+    ("fwd N64 K64 relu K64", M, 64, 64, 0, 0, 1, True, 0.0),
     ("fwd N64 K64 +b", M, 64, 64, 0, 0, 1, True, 0.0),
     ("dx N64 K192 tb", M, 64, 192, 0, 1, 1, False, 0.0),
     ("dx N64 K64 tb", M, 64, 64, 0, 1, 1, False, 0.0),
