@@ -33,6 +33,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBM = 64, kBN = 64, kBK = 32, kPitch = kBM + 1;
 
+// 64 zero bytes in global memory: out-of-range lanes of the streamed A loads read these instead of
+// taking a branch or a select, so the prefetch stays a plain straight-line load
+__device__ float4 g_zero_row[4];
+
 struct GemmTileArgs {
   int M, N, K, k_begin, k_end;
   bool ta, tb;
@@ -213,17 +217,23 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
     rok = uu < nunits && row < M;
     return A + (rok ? row_off(row, p.lda, p.a_grp, p.a_gstride) : 0) + 8 * h;
   };
+  // branch-free loads: an out-of-range lane reads A's first element and zeroes it afterwards, so the
+  // loads stay straight-line code and the compiler waits only for the chunk it consumes (a guarded load
+  // becomes a branch, after which every use waits for ALL loads in flight, prefetch included)
   auto load8 = [&](const float* Ar, bool rok, int c, float (&a)[8]) {
     const int k0 = 16 * c + 8 * h;
     if (VEC) {  // K % 8 == 0 and 16-byte aligned rows: a lane's 8 values are all in or all out
       const bool ok = rok && k0 < K;
-      const float4 v0 = ok ? *(const float4*)(Ar + 16 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 v1 = ok ? *(const float4*)(Ar + 16 * c + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float* src = ok ? Ar + 16 * c : (const float*)g_zero_row;
+      const float4 v0 = *(const float4*)src, v1 = *(const float4*)(src + 4);
       a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w;
       a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
     } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) a[q] = (rok && k0 + q < K) ? Ar[16 * c + q] : 0.0f;
+      for (int q = 0; q < 8; ++q) {
+        const bool ok = rok && k0 + q < K;
+        a[q] = *(ok ? Ar + 16 * c + q : (const float*)g_zero_row);
+      }
     }
   };
   int64_t u = (int64_t)blockIdx.x * 4 + wave;
@@ -281,6 +291,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
         Arn = row_ptr(u + ustep, rokn);
         load8(Arn, rokn, 0, a1);
       }
+      __builtin_amdgcn_sched_barrier(0);  // the prefetch is issued here, not sunk to its use
       const float* brow = bcol + 16 * c * NP;
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -306,6 +317,130 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
           float v = p.alpha * acc[t][r];
           if (p.beta != 0.0f) v += p.beta * *cp;
           v += bv;
+          if (Dd) v += Dd[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
+          if (p.relu) v = v > 0.0f ? v : 0.0f;
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
+// ================================================================================================
+// rows, B-in-registers form (N <= 64: one column group; K <= 16 NCH <= 64): op(B) is staged in LDS once
+// per workgroup as above, then every lane copies ITS MFMA B operands (NCH x 8 x NTW values) into
+// registers, so the main loop issues MFMAs fed by the streamed A chunks and registers only (no LDS
+// read per MFMA).  Same unit walk, A chunk pipeline and epilogue as gemm_rows_kernel.
+// ================================================================================================
+template <int NTW, int NCH>
+__global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) {
+  extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
+  constexpr int NC = 32 * NTW, NP = NC + 1, K16 = 16 * NCH;
+  const int K = p.K, N = p.N, M = p.M;
+  const int b = blockIdx.z;
+  const float* A = p.A + (int64_t)b * p.stride_a;
+  const float* B = p.B + (int64_t)b * p.stride_b;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t nunits = (M + 31) / 32;
+  const int64_t ustep = (int64_t)gridDim.x * 4;
+  auto row_ptr = [&](int64_t uu, bool& rok) -> const float* {
+    const int row = (int)uu * 32 + i;
+    rok = uu < nunits && row < M;
+    return A + (rok ? row_off(row, p.lda, p.a_grp, p.a_gstride) : 0) + 8 * h;
+  };
+  auto load8 = [&](const float* Ar, bool rok, int c, float (&a)[8]) {  // branch-free, as gemm_rows_kernel
+    const bool ok = rok && 16 * c + 8 * h < K;  // K % 8 == 0: a lane's 8 values are all in or all out
+    const float* src = ok ? Ar + 16 * c : (const float*)g_zero_row;
+    const float4 v0 = *(const float4*)src, v1 = *(const float4*)(src + 4);
+    a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w;
+    a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
+  };
+  int64_t u = (int64_t)blockIdx.x * 4 + wave;
+  bool rok;
+  const float* Ar = row_ptr(u, rok);
+  float a0[8], a1[8];
+  load8(Ar, rok, 0, a0);
+  {
+    const int total = K16 * NC;
+    const int dv = p.trans_b ? K16 : NC;
+    const float inv = 1.0f / (float)dv;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * 16) {
+      float v[16];
+#pragma unroll
+      for (int uu = 0; uu < 16; ++uu) {
+        const int e = e0 + uu * 256;
+        const int mj = (int)(((float)e + 0.5f) * inv), mn = e - mj * dv;
+        const int k = p.trans_b ? mn : mj, n = p.trans_b ? mj : mn;
+        v[uu] = (e < total && k < K && n < N)
+                    ? (p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k]
+                                 : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n])
+                    : 0.0f;
+      }
+#pragma unroll
+      for (int uu = 0; uu < 16; ++uu) {
+        const int e = e0 + uu * 256;
+        if (e < total) {
+          const int mj = (int)(((float)e + 0.5f) * inv), mn = e - mj * dv;
+          const int k = p.trans_b ? mn : mj, n = p.trans_b ? mj : mn;
+          Bs[k * NP + n] = v[uu];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float bf[NCH][8][NTW];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) bf[c][q][t] = Bs[(16 * c + 8 * h + q) * NP + 32 * t + i];
+  float* C = p.C + (int64_t)b * p.stride_c;
+  const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  float bv[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) bv[t] = (p.bias && 32 * t + i < N) ? p.bias[32 * t + i] : 0.0f;
+  for (; u < nunits; u += ustep) {
+    const int m0 = (int)u * 32;
+    f32x16 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    bool rokn = false;
+    const float* Arn = Ar;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + 1 < NCH) {
+        load8(Ar, rok, c + 1, a1);
+      } else {
+        Arn = row_ptr(u + ustep, rokn);
+        load8(Arn, rokn, 0, a1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[q], bf[c][q][t], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a0[q] = a1[q];
+    }
+    Ar = Arn;
+    rok = rokn;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      const int col = t * 32 + i;
+      if (col >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < M) {
+          float* cp = C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
+          float v = p.alpha * acc[t][r];
+          if (p.beta != 0.0f) v += p.beta * *cp;
+          v += bv[t];
           if (Dd) v += Dd[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
           if (p.relu) v = v > 0.0f ? v : 0.0f;
           *cp = v;
@@ -552,7 +687,10 @@ launched:
 // column-tile groups: NTW tiles per wave unit, ncg groups across N
 void rows_split(int N, int* ntw, int* ncg) {
   const int nt = (N + 31) / 32;  // two tiles per unit keep the operands within 168 registers
+  static const int wide = env_knob("DGPPO_ROWS_NTW", 0);  // experiment: tiles per unit for N > 64
   if (nt <= 2) { *ntw = nt; *ncg = 1; }
+  else if (wide == 3 && nt % 3 == 0) { *ntw = 3; *ncg = nt / 3; }
+  else if (wide == 6 && nt == 6) { *ntw = 6; *ncg = 1; }
   else if (nt == 3) { *ntw = 1; *ncg = 3; }
   else { *ntw = 2; *ncg = (nt + 1) / 2; }
 }
@@ -574,6 +712,16 @@ void launch_rows_t(const dgppo_gemm_args* p, int ncg, hipStream_t s) {
   const int grid = (int)(want < cap ? want : cap);
   const bool vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
                    (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
+  static const int breg = env_knob("DGPPO_ROWS_BREG", 1);
+  if (vec && breg && ncg == 1 && K16 <= 64) {
+#define DG_RB(c)                                                                                              \
+  if (K16 == 16 * c) {                                                                                        \
+    hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); \
+    return;                                                                                                   \
+  }
+    DG_RB(1) DG_RB(2) DG_RB(3) DG_RB(4)
+#undef DG_RB
+  }
   if (vec)
     hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, true>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
   else
@@ -586,6 +734,8 @@ int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {
   switch (ntw) {
     case 1: launch_rows_t<1>(p, ncg, s); return 0;
     case 2: launch_rows_t<2>(p, ncg, s); return 0;
+    case 3: launch_rows_t<3>(p, ncg, s); return 0;
+    case 6: launch_rows_t<6>(p, ncg, s); return 0;
   }
   return DGPPO_EINVAL;
 }

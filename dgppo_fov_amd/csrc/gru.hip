@@ -30,6 +30,12 @@ constexpr int kHid = 64, kG3 = 192, kRows = 16, kWP = 193, kHP = 65, kThreads = 
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// sink for the stores of padding rows (q >= Q): every store stays an unconditional straight-line
+// instruction, so the compiler's wait counts stay exact (a guarded store or load is a branch, after
+// which the next use waits for EVERY memory operation in flight)
+__device__ float g_row_sink[kG3];
+__device__ float4 g_zero_rows[16];  // a zero hidden row (64 floats) for padding rows / no initial carry
+
 __device__ __forceinline__ int64_t seq_row(int q, int t, int L, int n) {
   return ((int64_t)(q / n) * L + t) * n + (q % n);
 }
@@ -114,34 +120,43 @@ __global__ __launch_bounds__(kThreads) void gru_seq_fwd_kernel(dgppo_gru_seq_arg
     __syncthreads();  // previous block's readers of hb are done
     store_rows16(hb, h0v);
     __syncthreads();
-    for (int t = 0; t < L; ++t) {
-      const float* hcur = hb + (t & 1) * kRows * kHP;
-      float* hnext = hb + ((t + 1) & 1) * kRows * kHP;
-      float gr_[4], gz_[4], gn_[4];
+    // gi of step t + 1 is loaded during step t (register double buffer); padding rows read row 0 and
+    // store into the sink, so neither loads nor stores branch
+    float gc[3][4], gx[3][4];
+    auto load_gi = [&](int t, float (&g)[3][4]) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = q0 + lane_row(lane, r);
-        const float* g = p.gi + (q < Q ? seq_row(q, t, L, n) : 0) * kG3;
-        gr_[r] = q < Q ? g[col] : 0.0f;
-        gz_[r] = q < Q ? g[kHid + col] : 0.0f;
-        gn_[r] = q < Q ? g[2 * kHid + col] : 0.0f;
+        const float* gp = p.gi + (q < Q ? seq_row(q, t, L, n) : 0) * kG3 + col;
+        g[0][r] = gp[0];
+        g[1][r] = gp[kHid];
+        g[2][r] = gp[2 * kHid];
       }
+    };
+    load_gi(0, gc);
+    for (int t = 0; t < L; ++t) {
+      const float* hcur = hb + (t & 1) * kRows * kHP;
+      float* hnext = hb + ((t + 1) & 1) * kRows * kHP;
+      load_gi(t + 1 < L ? t + 1 : t, gx);
+      __builtin_amdgcn_sched_barrier(0);
       f32x4 ar, az, an;
       gh_tiles(hcur, Whs, col, lane, ar, az, an);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = lane_row(lane, r), q = q0 + row;
-        float hn = 0.0f;
-        if (q < Q) {
-          const float rg = sigm(gr_[r] + ar[r]);
-          const float zg = sigm(gz_[r] + az[r]);
-          const float ng = tanhf(gn_[r] + rg * (an[r] + bn));
-          hn = (1.0f - zg) * ng + zg * hcur[row * kHP + col];
-          p.hs[seq_row(q, t, L, n) * kHid + col] = hn;
-          if (t == L - 1 && p.hT) p.hT[(int64_t)q * kHid + col] = hn;
-        }
+        const bool ok = q < Q;
+        const float rg = sigm(gc[0][r] + ar[r]);
+        const float zg = sigm(gc[1][r] + az[r]);
+        const float ng = tanhf(gc[2][r] + rg * (an[r] + bn));
+        const float hn = ok ? (1.0f - zg) * ng + zg * hcur[row * kHP + col] : 0.0f;
+        *(ok ? p.hs + seq_row(q, t, L, n) * kHid + col : g_row_sink + col) = hn;
+        if (t == L - 1 && p.hT) *(ok ? p.hT + (int64_t)q * kHid + col : g_row_sink + col) = hn;
         hnext[row * kHP + col] = hn;
       }
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gc[k][r] = gx[k][r];
       __syncthreads();
     }
   }
@@ -164,24 +179,40 @@ __global__ __launch_bounds__(kThreads) void gru_seq_bwd_kernel(dgppo_gru_seq_arg
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     const int q0 = blk * kRows;
     float dh[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int t = L - 1; t >= 0; --t) {
-      // this step's loads first: h_{t-1} rows, gi and upstream grads of the lane's 4 rows
-      const float4 hv = load_rows16([&](int r) -> const float* {
-        const int q = q0 + r;
-        if (q >= Q) return nullptr;
-        if (t > 0) return p.hs + seq_row(q, t - 1, L, n) * kHid;
-        return p.h0 ? p.h0 + (int64_t)q * kHid : nullptr;
-      });
-      float gr_[4], gz_[4], gn_[4], dd_[4];
+    // step t's loads (h_{t-1} rows, gi and upstream grads of the lane's 4 rows) are issued during step
+    // t + 1 (register double buffer), branch-free: padding rows / the zero initial carry read the zero row
+    float4 hv, hvx;
+    float gc[4][4], gx[4][4];  // [r, z, n, dhs][row]
+    auto load_step = [&](int t, float4& h, float (&g)[4][4]) {
+      {
+        const int q = q0 + (threadIdx.x >> 4);
+        const float* hr = (const float*)g_zero_rows;
+        if (q < Q) hr = t > 0 ? p.hs + seq_row(q, t - 1, L, n) * kHid : (p.h0 ? p.h0 + (int64_t)q * kHid : hr);
+        h = ((const float4*)hr)[threadIdx.x & 15];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = q0 + lane_row(lane, r);
         const int64_t grow = q < Q ? seq_row(q, t, L, n) : 0;
-        const float* g = p.gi + grow * kG3;
-        gr_[r] = q < Q ? g[col] : 0.0f;
-        gz_[r] = q < Q ? g[kHid + col] : 0.0f;
-        gn_[r] = q < Q ? g[2 * kHid + col] : 0.0f;
-        dd_[r] = q < Q ? p.dhs[grow * kHid + col] : 0.0f;
+        const float* gp = p.gi + grow * kG3 + col;
+        g[0][r] = gp[0];
+        g[1][r] = gp[kHid];
+        g[2][r] = gp[2 * kHid];
+        g[3][r] = p.dhs[grow * kHid + col];
+      }
+    };
+    load_step(L - 1, hv, gc);
+    for (int t = L - 1; t >= 0; --t) {
+      load_step(t > 0 ? t - 1 : t, hvx, gx);
+      __builtin_amdgcn_sched_barrier(0);
+      float gr_[4], gz_[4], gn_[4], dd_[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = q0 + lane_row(lane, r) < Q;
+        gr_[r] = ok ? gc[0][r] : 0.0f;
+        gz_[r] = ok ? gc[1][r] : 0.0f;
+        gn_[r] = ok ? gc[2][r] : 0.0f;
+        dd_[r] = ok ? gc[3][r] : 0.0f;
       }
       __syncthreads();  // previous step's readers of hp / dg are done
       store_rows16(hp, hv);
@@ -233,6 +264,11 @@ __global__ __launch_bounds__(kThreads) void gru_seq_bwd_kernel(dgppo_gru_seq_arg
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) dh[r] += acc[r];
+      hv = hvx;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gc[k][r] = gx[k][r];
     }
     if (p.dh0) {
 #pragma unroll
