@@ -16,6 +16,8 @@ LIB_PATH = pathlib.Path(os.environ.get("DGPPO_HIP_LIB", PKG_DIR / "lib" / "libdg
 DGPPO_EINVAL = -22
 DGPPO_ENGINE_LIDAR, DGPPO_ENGINE_BICYCLE, DGPPO_ENGINE_MPE, DGPPO_ENGINE_OMNI = 0, 1, 2, 3
 DGPPO_GOAL_SPREAD, DGPPO_GOAL_TARGET = 0, 1
+(DGPPO_VARIANT_NONE, DGPPO_VARIANT_LINE, DGPPO_VARIANT_FORMATION, DGPPO_VARIANT_CORRIDOR,
+ DGPPO_VARIANT_CONNECT) = 0, 1, 2, 3, 4
 DGPPO_OBST_FIELDS = 16
 
 c_f32p = ctypes.c_void_p  # device pointers travel as raw addresses
@@ -70,6 +72,23 @@ class EnvCfg(ctypes.Structure):
         ("fov_dmin", ctypes.c_float),
         ("rot_pen", ctypes.c_float),
         ("c_cos_fov", ctypes.c_float),
+        ("variant", ctypes.c_int32),
+        ("n_goals", ctypes.c_int32),
+        ("goals_inner", ctypes.c_int32),
+        ("goal_radius", ctypes.c_float),
+        ("obs_edge_radius", ctypes.c_float),
+        ("connect_radius", ctypes.c_float),
+        ("sample_side_y", ctypes.c_float),
+        ("goal_shift_y", ctypes.c_float),
+        ("line_min_dist", ctypes.c_float),
+        ("c_obs_inflate", ctypes.c_float),
+        ("formation_lo", ctypes.c_float),
+        ("formation_hi", ctypes.c_float),
+        ("c_connect_min", ctypes.c_float),
+        ("line_box_x", ctypes.c_float),
+        ("line_box_y", ctypes.c_float),
+        ("line_off_y", ctypes.c_float),
+        ("obs_x_hi", ctypes.c_float),
     ]
 
 
@@ -279,7 +298,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 5  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 6  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

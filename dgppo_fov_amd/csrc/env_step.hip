@@ -1759,12 +1759,456 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
   }
 }
 
+// ---- reference env variants ------------------------------------------------------------------
+// lidar_line.py, mpe_line.py, mpe_formation.py, mpe_corridor.py, mpe_connect_spread.py: the SPREAD
+// double-integrator envs with `n_goals` goal node rows (2 landmarks / 1 landmark / one per agent),
+// reward goals derived from them (landmark2goal), their own resets and (connect) a connectivity cost.
+// One wave per env, plain loops: these configs are correctness rows, not the benchmarked path.
+// Same fp32 operation order as oracle/env_variants.py (bit-exact, tests/test_env_variants_gpu.py).
+namespace var {
+constexpr int kT = 64;
+constexpr int kLoopCap = 1 << 16;
+
+__device__ __forceinline__ float max_nan(float a, float b) { return (a != a || a >= b) ? a : b; }
+
+// reward goal k of n from the goal node rows (pitch 4): landmark2goal (lidar_line.py:137-142,
+// mpe_line.py:112-121, mpe_formation.py:92-96), or the goal node itself
+__device__ void reward_goal(const dgppo_env_cfg& c, const float* grow, int k, float* gx, float* gy) {
+  const int n = c.n_agents;
+  if (c.variant == DGPPO_VARIANT_LINE) {
+    const float dx = grow[4] - grow[0], dy = grow[5] - grow[1];
+    const float kk = c.goals_inner ? (float)(k + 1) : (float)k;
+    const float m = c.goals_inner ? (float)(n + 1) : (float)(n - 1);
+    *gx = grow[0] + (kk * dx) / m;
+    *gy = grow[1] + (kk * dy) / m;
+  } else if (c.variant == DGPPO_VARIANT_FORMATION) {
+    // th_k = jnp.linspace(0, 2 pi, n + 1)[k] = 0 * (1 - s) + 2pi * s, s = k / n
+    const float sk = (float)k / (float)n;
+    const float th = 0.0f * (1.0f - sk) + 6.28318548202514648438f * sk;
+    float sn, cs;
+    sincos32(th, &sn, &cs);
+    *gx = grow[0] + c.goal_radius * cs;
+    *gy = grow[1] + c.goal_radius * sn;
+  } else {
+    *gx = grow[4 * k];
+    *gy = grow[4 * k + 1];
+  }
+}
+
+// get_graph for the variants: agents | goal rows | hits (Lidar) or obstacles (MPE) | pad
+__device__ void write_graph_var(const dgppo_env_cfg& c, bool mpe, bool lidar, const float* nxt, const float* grow,
+                                const float* third, GraphOut out, int tid, int nthr) {
+  constexpr int SD = 4, ND = 7;
+  const int n = c.n_agents, ng = c.n_goals, O = c.n_obs, k = c.top_k;
+  const int t0 = n + ng;
+  const int n_third = mpe ? O : (lidar ? n * k : 0);
+  const int N = t0 + n_third + 1, pad = N - 1;
+  for (int idx = tid; idx < N * ND; idx += nthr) {
+    const int r = idx / ND, col = idx - r * ND;
+    float v = 0.0f;
+    if (r < n) v = col < SD ? nxt[r * SD + col] : (col == SD + 2 ? 1.0f : 0.0f);
+    else if (r < t0) v = col < SD ? grow[(r - n) * SD + col] : (col == SD + 1 ? 1.0f : 0.0f);
+    else if (r < t0 + n_third) {
+      const int h = r - t0;
+      if (mpe) v = col < SD ? third[h * SD + col] : (col == SD ? 1.0f : 0.0f);
+      else v = col < 2 ? third[h * 2 + col] : (col == SD ? 1.0f : 0.0f);
+    }
+    out.nodes[idx] = v;
+  }
+  for (int idx = tid; idx < N * SD; idx += nthr) {
+    const int r = idx / SD, col = idx - r * SD;
+    float v;
+    if (r < n) v = nxt[r * SD + col];
+    else if (r < t0) v = grow[(r - n) * SD + col];
+    else if (r < t0 + n_third) {
+      const int h = r - t0;
+      v = mpe ? third[h * SD + col] : (col < 2 ? third[h * 2 + col] : 0.0f);
+    } else v = -1.0f;
+    out.states[idx] = v;
+  }
+  const int n_aa = n * n, n_ag = n * ng;
+  const int E = n_aa + n_ag + (mpe ? n * O : n_third);
+  const float robs = c.obs_edge_radius;
+  for (int e = tid; e < E; e += nthr) {
+    float f[4];
+    int rv, sv;
+    if (e < n_aa) {  // agent-agent: s_i - s_j, mask ||p_i - p_j|| (+ comm + 1 on the diagonal) < comm
+      const int i = e / n, j = e - i * n;
+      const float* si = nxt + i * SD;
+      const float* sj = nxt + j * SD;
+      for (int q = 0; q < 4; ++q) f[q] = si[q] - sj[q];
+      float dd = norm2(si[0] - sj[0], si[1] - sj[1]);
+      if (i == j) dd = dd + c.c_self_dist;
+      const bool m = dd < c.comm_radius;
+      rv = m ? i : pad;
+      sv = m ? j : pad;
+    } else if (e < n_aa + n_ag) {  // agent-goal node, all connected
+      const int q = e - n_aa, i = q / ng, j = q - i * ng;
+      const float* si = nxt + i * SD;
+      const float* gj = grow + j * SD;
+      for (int t = 0; t < 4; ++t) f[t] = si[t] - gj[t];
+      rv = i;
+      sv = n + j;
+    } else {
+      const int q = e - n_aa - n_ag;
+      if (mpe) {  // agent-obstacle, mask ||p_i - o|| < obs_edge_radius (comm, or comm * 100)
+        const int i = q / O, o = q - i * O;
+        const float* si = nxt + i * SD;
+        const float* so = third + o * SD;
+        for (int t = 0; t < 4; ++t) f[t] = si[t] - so[t];
+        const bool m = norm2(si[0] - so[0], si[1] - so[1]) < robs;
+        rv = m ? i : pad;
+        sv = m ? t0 + o : pad;
+      } else {  // agent-lidar (1, k) blocks, mask ||p_i - hit|| < comm - 0.1
+        const int i = q / k, h = q - i * k;
+        const float* si = nxt + i * SD;
+        f[0] = si[0] - third[(i * k + h) * 2 + 0];
+        f[1] = si[1] - third[(i * k + h) * 2 + 1];
+        f[2] = 0.0f;
+        f[3] = 0.0f;
+        const bool m = norm2(f[0], f[1]) < c.c_lidar_active;
+        rv = m ? i : pad;
+        sv = m ? t0 + i * k + h : pad;
+      }
+    }
+    for (int t = 0; t < 4; ++t) out.edges[4 * e + t] = f[t];
+    out.recv[e] = rv;
+    out.send[e] = sv;
+  }
+}
+
+// LDS: the base Carve (nxt, obst, evec, lidar tables) + red [8][n] + reward goals [n][2]
+__host__ __device__ inline size_t lds_floats(const dgppo_env_cfg& c) {
+  const Carve cv(c.n_agents, 4, c.n_obs, c.n_rays, c.top_k, c.engine != DGPPO_ENGINE_MPE);
+  return (size_t)cv.total + 10 * (size_t)c.n_agents + 8;
+}
+
+template <int ENGINE>
+__global__ __launch_bounds__(kT) void step_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int SD = 4;
+  constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
+  const Dims<0, -1, 0, 0> d(cfg);
+  const int n = d.n, O = d.O, k = d.k, ng = cfg.n_goals, t0 = n + ng;
+  const bool lidar = !mpe && O > 0;
+  const Carve cv(n, SD, O, d.R, k, !mpe);
+  float* red = lds + cv.total;  // d2goal, far, |a|^2, min agent dist, c0, c1, c2, min obstacle dist
+  float* rg = red + 8 * n;      // reward goals (n, 2)
+  const int tid = threadIdx.x;
+  const int64_t env = blockIdx.x;
+  const float* st = io.states + env * io.states_stride;
+  const int n_cur = (t0 + (mpe ? O : 0)) * SD;  // type_states(0), (1) [, (2) MPE obstacles]
+  for (int idx = tid; idx < n_cur; idx += kT) lds[cv.cur + idx] = st[idx];
+  if (lidar) {
+    for (int idx = tid; idx < n * k * 2; idx += kT) lds[cv.curhit + idx] = st[(t0 + (idx >> 1)) * SD + (idx & 1)];
+    const float* ob = io.obstacles + env * io.obstacles_stride;
+    for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += kT) lds[cv.obst + idx] = ob[idx];
+  }
+  const float* ac = io.action + env * io.action_stride;
+  for (int idx = tid; idx < 2 * n; idx += kT) lds[cv.act + idx] = clampf_nan(ac[idx], -1.0f, 1.0f);
+  __syncthreads();
+  const float* cur = lds + cv.cur;
+  const float* grow = cur + n * SD;
+  const float* obs = cur + t0 * SD;
+  for (int i = tid; i < n; i += kT) {
+    const float* x = cur + i * SD;
+    const float* a = lds + cv.act + 2 * i;
+    const float y[4] = {x[2] * cfg.dt + x[0], x[3] * cfg.dt + x[1], (a[0] * 10.0f) * cfg.dt + x[2],
+                        (a[1] * 10.0f) * cfg.dt + x[3]};
+    for (int q = 0; q < SD; ++q) lds[cv.nxt + i * SD + q] = clampf_nan(y[q], cfg.state_lo[q], cfg.state_hi[q]);
+    const float an = norm2(a[0], a[1]);
+    red[2 * n + i] = an * an;
+    float md = 0.0f;
+    for (int j = 0; j < n; ++j) {
+      float dj = norm2(x[0] - cur[j * SD], x[1] - cur[j * SD + 1]);
+      if (i == j) dj = dj + 1e6f;
+      md = j == 0 ? dj : min_nan(md, dj);
+    }
+    red[3 * n + i] = md;
+    float mo = 0.0f;
+    if (lidar) {
+      const float* hc = lds + cv.curhit + 2 * i * k;
+      for (int h = 0; h < k; ++h) {
+        const float dh = norm2(hc[2 * h] - x[0], hc[2 * h + 1] - x[1]);
+        mo = h == 0 ? dh : min_nan(mo, dh);
+      }
+    } else if (mpe) {
+      for (int o = 0; o < O; ++o) {
+        const float dh = norm2(x[0] - obs[o * SD], x[1] - obs[o * SD + 1]);
+        mo = o == 0 ? dh : min_nan(mo, dh);
+      }
+    }
+    red[7 * n + i] = mo;
+    reward_goal(cfg, grow, i, rg + 2 * i, rg + 2 * i + 1);
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += kT) {  // reward goal i's nearest agent
+    float dg = 0.0f;
+    for (int a = 0; a < n; ++a) {
+      const float da = norm2(rg[2 * i] - cur[a * SD], rg[2 * i + 1] - cur[a * SD + 1]);
+      dg = a == 0 ? da : min_nan(dg, da);
+    }
+    red[i] = dg;
+    red[n + i] = dg > cfg.dist2goal ? 1.0f : 0.0f;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
+    for (int i = 0; i < n; ++i) {
+      sd_ = sd_ + red[i];
+      sf = sf + red[n + i];
+      sa = sa + red[2 * n + i];
+    }
+    const float nn = (float)n;
+    float r = 0.0f - (sd_ / nn) * 0.01f;
+    r = r - (sf / nn) * 0.001f;
+    r = r - (sa / nn) * 0.0001f;
+    io.reward[env * io.reward_stride] = r;
+    const bool connect = cfg.variant == DGPPO_VARIANT_CONNECT;
+    float cm = 0.0f;
+    if (connect) {  // (min_dist - connect_radius).max()
+      for (int i = 0; i < n; ++i) {
+        const float ci = red[3 * n + i] - cfg.connect_radius;
+        cm = i == 0 ? ci : max_nan(cm, ci);
+      }
+    }
+    const bool upper = !mpe || connect;
+    const int nc = connect ? 3 : 2;
+    for (int i = 0; i < n; ++i) {
+      float cs[3];
+      cs[0] = cfg.c_agent_cost - red[3 * n + i];
+      cs[1] = (lidar || (mpe && O > 0)) ? cfg.c_obs_cost - red[7 * n + i] : 0.0f;
+      cs[2] = cm;
+      for (int h = 0; h < nc; ++h) {
+        float v = cs[h] <= 0.0f ? cs[h] - 0.5f : cs[h] + 0.5f;
+        v = upper ? clampf_nan(v, -1.0f, 1.0f) : (v < -1.0f ? -1.0f : v);
+        io.cost[env * io.cost_stride + i * nc + h] = v;
+      }
+    }
+  }
+  if (lidar) {
+    for (int i = tid; i < n; i += kT) agent_is_inside(O, lds, cv, SD, i);
+    stage_edge_vectors(O, lds, cv, tid, kT);
+    __syncthreads();
+    lidar_scan<SD>(d, io.ray_dirs, lds, cv, tid, kT);
+    __syncthreads();
+  }
+  GraphOut out;
+  out.nodes = io.nodes + env * io.nodes_stride;
+  out.edges = io.edges + env * io.edges_stride;
+  out.states = io.out_states + env * io.out_states_stride;
+  out.recv = io.receivers + env * io.edge_index_stride;
+  out.send = io.senders + env * io.edge_index_stride;
+  write_graph_var(cfg, mpe, lidar, lds + cv.nxt, grow, mpe ? obs : lds + cv.hits, out, tid, kT);
+}
+
+// get_node_goal_rng without obstacles, candidates (uniform(0, side), uniform(0, side_y)) (env/utils.py:139-244,
+// oracle/env_variants.py node_goal_rng_y), sequential in one thread
+__device__ void node_goal_rng_seq(Rng& rng, float side, float side_y, int n, float min_dist, float* pos, float* gl) {
+  constexpr int kMaxIter = 1024;
+  for (int i = 0; i < 2 * n; ++i) pos[i] = gl[i] = 0.0f;
+  int agent_id = 0;
+  while (agent_id < n) {
+    float cx = rng.uniform(0.0f, side), cy = rng.uniform(0.0f, side_y);
+    int it = 0;
+    while (true) {
+      float dmin = 0.0f;
+      for (int j = 0; j < n; ++j) {
+        const float dj = norm2(pos[2 * j] - cx, pos[2 * j + 1] - cy);
+        dmin = j == 0 ? dj : min_nan(dmin, dj);
+      }
+      if (!(dmin <= min_dist) || it >= kMaxIter) break;
+      ++it;
+      cx = rng.uniform(0.0f, side);
+      cy = rng.uniform(0.0f, side_y);
+    }
+    const int it_agent = it;
+    pos[2 * agent_id] = cx;
+    pos[2 * agent_id + 1] = cy;
+    float gx = rng.uniform(0.0f, side), gy = rng.uniform(0.0f, side_y);
+    it = 0;
+    while (true) {
+      float dmin = 0.0f;
+      for (int j = 0; j < n; ++j) {
+        const float dj = norm2(gl[2 * j] - gx, gl[2 * j + 1] - gy);
+        dmin = j == 0 ? dj : min_nan(dmin, dj);
+      }
+      const bool outside = gx < 0.0f || gy < 0.0f || gx > side || gy > side;
+      if (!(dmin <= min_dist || outside) || it >= kMaxIter) break;
+      ++it;
+      gx = rng.uniform(0.0f, side);
+      gy = rng.uniform(0.0f, side_y);
+    }
+    gl[2 * agent_id] = gx;
+    gl[2 * agent_id + 1] = gy;
+    ++agent_id;
+    if (it_agent >= kMaxIter || it >= kMaxIter) {
+      agent_id = 0;
+      for (int i = 0; i < 2 * n; ++i) pos[i] = gl[i] = 0.0f;
+    }
+  }
+}
+
+__device__ __forceinline__ float min_dist_row(const float* p, int n, int i) {  // with the eye * 1e6 diagonal
+  float md = 0.0f;
+  for (int j = 0; j < n; ++j) {
+    float dj = norm2(p[2 * i] - p[2 * j], p[2 * i + 1] - p[2 * j + 1]);
+    if (i == j) dj = dj + 1e6f;
+    md = j == 0 ? dj : min_nan(md, dj);
+  }
+  return md;
+}
+
+template <int ENGINE>
+__global__ __launch_bounds__(kT) void reset_kernel(dgppo_env_cfg cfg, dgppo_env_reset_io io) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int SD = 4;
+  constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
+  const Dims<0, -1, 0, 0> d(cfg);
+  const int n = d.n, O = d.O, ng = cfg.n_goals, t0 = n + ng;
+  const bool lidar = !mpe && O > 0;
+  const Carve cv(n, SD, O, d.R, d.k, !mpe);
+  float* grow = lds + cv.cur + n * SD;  // goal node rows
+  float* obs = lds + cv.cur + t0 * SD;  // MPE obstacle rows
+  float* pos = lds + cv.total;          // sampled agents (n, 2) | goals (n, 2) | reward goals (n, 2)
+  float* gl = pos + 2 * n;
+  float* rg = gl + 2 * n;
+  const int tid = threadIdx.x;
+  const int64_t env = blockIdx.x;
+  if (tid == 0) {
+    Rng rng(io.seed_ptr ? *io.seed_ptr : io.seed, (uint32_t)(io.env_offset + env));
+    const float area = cfg.area_size;
+    for (int i = 0; i < t0 * SD + (mpe ? O * SD : 0); ++i) lds[cv.cur + i] = 0.0f;
+    if (cfg.variant == DGPPO_VARIANT_LINE || cfg.variant == DGPPO_VARIANT_FORMATION) {
+      node_goal_rng_seq(rng, area, area, n, cfg.c_agent_cost, pos, gl);
+      if (cfg.variant == DGPPO_VARIANT_LINE) {  // lidar_line.py:53-84, mpe_line.py:47-83
+        float l0x, l0y;
+        if (mpe && cfg.goals_inner) {
+          l0x = rng.uniform(0.0f, area);
+          l0y = rng.uniform(0.0f, area);
+        } else {
+          const float u0 = rng.uniform(0.0f, cfg.line_box_x), u1 = rng.uniform(0.0f, cfg.line_box_y);
+          const float half = area / 2.0f;
+          const float cx = (u0 - half) + 0.0f, cy = (u1 - 0.0f) + cfg.line_off_y;
+          int reg = (int)rng.uniform(0.0f, 4.0f);
+          reg = reg > 3 ? 3 : reg;
+          const float ang = ((float)reg * 3.14159274101257324219f) / 2.0f;
+          float sn, cs;
+          sincos32(ang, &sn, &cs);
+          const float rx = cs * cx + (-sn) * cy, ry = sn * cx + cs * cy;
+          l0x = rx + half;
+          l0y = ry + half;
+        }
+        float l1x = rng.uniform(0.0f, area), l1y = rng.uniform(0.0f, area);
+        for (int it = 0; it < kLoopCap && norm2(l1x - l0x, l1y - l0y) < cfg.line_min_dist; ++it) {
+          l1x = rng.uniform(0.0f, area);
+          l1y = rng.uniform(0.0f, area);
+        }
+        grow[0] = l0x, grow[1] = l0y, grow[SD] = l1x, grow[SD + 1] = l1y;
+      } else {  // mpe_formation.py:47-52
+        grow[0] = rng.uniform(cfg.formation_lo, cfg.formation_hi);
+        grow[1] = rng.uniform(cfg.formation_lo, cfg.formation_hi);
+      }
+      for (int i = 0; i < n; ++i) reward_goal(cfg, grow, i, rg + 2 * i, rg + 2 * i + 1);
+      if (mpe) {  // obstacle rejection against the agents and the reward goals (mpe_line.py:86-112)
+        for (int o = 0; o < O; ++o) {
+          float cx = rng.uniform(0.0f, area), cy = rng.uniform(0.0f, area);
+          for (int it = 0; it < kLoopCap; ++it) {
+            float da = 0.0f, dg = 0.0f;
+            for (int j = 0; j < n; ++j) {
+              const float d1 = norm2(pos[2 * j] - cx, pos[2 * j + 1] - cy);
+              const float d2 = norm2(rg[2 * j] - cx, rg[2 * j + 1] - cy);
+              da = j == 0 ? d1 : min_nan(da, d1);
+              dg = j == 0 ? d2 : min_nan(dg, d2);
+            }
+            const bool bad = da <= cfg.c_mpe_obs_agent || dg <= cfg.c_mpe_obs_goal || cx < cfg.c_mpe_obs_lo ||
+                             cy < cfg.c_mpe_obs_lo || cx > cfg.c_mpe_obs_hi || cy > cfg.c_mpe_obs_hi;
+            if (!bad) break;
+            cx = rng.uniform(cfg.c_mpe_obs_lo, cfg.c_mpe_obs_hi);
+            cy = rng.uniform(cfg.c_mpe_obs_lo, cfg.c_mpe_obs_hi);
+          }
+          obs[o * SD] = cx;
+          obs[o * SD + 1] = cy;
+        }
+      } else if (O > 0) {  // lidar_line.py:86-122: no agent / goal inside an obstacle inflated by 1.1 r
+        float* obst = lds + cv.obst;
+        for (int o = 0; o < O; ++o) {
+          float* rec = obst + o * DGPPO_OBST_FIELDS;
+          for (int it = 0;; ++it) {
+            const float cx = rng.uniform(0.0f, area), cy = rng.uniform(0.0f, area);
+            const float w = rng.uniform(cfg.obs_len_lo, cfg.obs_len_hi), h = rng.uniform(cfg.obs_len_lo, cfg.obs_len_hi);
+            const float th = rng.uniform(0.0f, 3.14159274101257324219f);
+            make_rectangle(rec, cx, cy, w, h, th);
+            bool in = false;
+            for (int j = 0; j < n; ++j)
+              in = in || rect_inside(rec, pos[2 * j], pos[2 * j + 1], cfg.c_obs_inflate) ||
+                   rect_inside(rec, rg[2 * j], rg[2 * j + 1], cfg.c_obs_inflate);
+            if (!in || it >= kLoopCap) break;
+          }
+        }
+      }
+    } else {  // corridor (mpe_corridor.py:40-53) / connect (mpe_connect_spread.py:47-94)
+      const bool connect = cfg.variant == DGPPO_VARIANT_CONNECT;
+      for (int it = 0;; ++it) {
+        node_goal_rng_seq(rng, area, cfg.sample_side_y, n, connect ? cfg.c_connect_min : cfg.c_agent_cost, pos, gl);
+        for (int j = 0; j < n; ++j) gl[2 * j + 1] = gl[2 * j + 1] + cfg.goal_shift_y;
+        if (!connect) break;
+        bool bad = false;
+        for (int i = 0; i < n; ++i) {
+          const float ma = min_dist_row(pos, n, i), mg = min_dist_row(gl, n, i);
+          bad = bad || ma > cfg.connect_radius || ma < cfg.c_agent_cost || mg > cfg.connect_radius;
+        }
+        if (!bad || it + 1 >= kLoopCap) break;
+      }
+      for (int j = 0; j < n; ++j) grow[j * SD] = gl[2 * j], grow[j * SD + 1] = gl[2 * j + 1];
+      if (connect) {
+        obs[0] = rng.uniform(cfg.obs_radius, cfg.obs_x_hi);
+        obs[1] = area / 2.0f;
+      } else {
+        obs[0] = cfg.obs_radius, obs[1] = area / 2.0f;
+        obs[SD] = cfg.obs_x_hi, obs[SD + 1] = area / 2.0f;
+      }
+    }
+    for (int i = 0; i < n; ++i)
+      for (int q = 0; q < SD; ++q) lds[cv.nxt + i * SD + q] = q < 2 ? pos[2 * i + q] : 0.0f;
+  }
+  __syncthreads();
+  if (lidar) {
+    float* ob = io.obstacles + env * io.obstacles_stride;
+    for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += kT) ob[idx] = lds[cv.obst + idx];
+    for (int i = tid; i < n; i += kT) agent_is_inside(O, lds, cv, SD, i);
+    stage_edge_vectors(O, lds, cv, tid, kT);
+    __syncthreads();
+    lidar_scan<SD>(d, io.ray_dirs, lds, cv, tid, kT);
+    __syncthreads();
+  }
+  GraphOut out;
+  out.nodes = io.nodes + env * io.nodes_stride;
+  out.edges = io.edges + env * io.edges_stride;
+  out.states = io.out_states + env * io.out_states_stride;
+  out.recv = io.receivers + env * io.edge_index_stride;
+  out.send = io.senders + env * io.edge_index_stride;
+  write_graph_var(cfg, mpe, lidar, lds + cv.nxt, grow, mpe ? obs : lds + cv.hits, out, tid, kT);
+}
+}  // namespace var
+
 // ---- host dispatch --------------------------------------------------------------------------
 static int validate(const dgppo_env_cfg* c) {
   if (!c) return DGPPO_EINVAL;
   if (c->engine < 0 || c->engine > 3 || c->goal_mode < 0 || c->goal_mode > 1) return DGPPO_EINVAL;
   if (c->n_agents < 1 || c->n_agents > kMaxAgents || c->n_obs < 0 || c->n_obs > kMaxObs) return DGPPO_EINVAL;
   if (c->engine == DGPPO_ENGINE_OMNI && c->goal_mode != DGPPO_GOAL_TARGET) return DGPPO_EINVAL;
+  if (c->variant < DGPPO_VARIANT_NONE || c->variant > DGPPO_VARIANT_CONNECT) return DGPPO_EINVAL;
+  if (c->variant != DGPPO_VARIANT_NONE) {  // variants: SPREAD double integrators; Lidar only for the line
+    if (c->goal_mode != DGPPO_GOAL_SPREAD || (c->engine != DGPPO_ENGINE_MPE && c->engine != DGPPO_ENGINE_LIDAR))
+      return DGPPO_EINVAL;
+    if (c->engine == DGPPO_ENGINE_LIDAR && c->variant != DGPPO_VARIANT_LINE) return DGPPO_EINVAL;
+    if (c->n_goals < 1 || c->n_goals > c->n_agents) return DGPPO_EINVAL;
+    if (c->variant == DGPPO_VARIANT_LINE && c->n_goals != 2) return DGPPO_EINVAL;
+    if (c->variant == DGPPO_VARIANT_FORMATION && c->n_goals != 1) return DGPPO_EINVAL;
+  } else if (c->n_goals != 0 && c->n_goals != c->n_agents) {
+    return DGPPO_EINVAL;
+  }
   const int sd = c->engine == DGPPO_ENGINE_BICYCLE ? 5 : (c->engine == DGPPO_ENGINE_OMNI ? 7 : 4);
   if (c->state_dim != sd || c->node_dim != sd + 3) return DGPPO_EINVAL;
   if (c->engine != DGPPO_ENGINE_MPE && c->n_obs > 0) {
@@ -1885,14 +2329,17 @@ extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
   c->node_dim = c->state_dim + 3;
   c->edge_dim = omni ? kOmniED : 4;
   c->action_dim = omni ? 3 : 2;
-  c->n_cost = omni ? kOmniNC : 2;
-  const int n_ag = c->goal_mode == DGPPO_GOAL_SPREAD ? n * n : n;
+  c->n_cost = omni ? kOmniNC : (c->variant == DGPPO_VARIANT_CONNECT ? 3 : 2);
+  // goal node rows: the variants' landmarks (line 2, formation 1), else one per agent
+  const int ng = (c->variant != DGPPO_VARIANT_NONE && c->n_goals > 0) ? c->n_goals : n;
+  c->n_goals = ng;
+  const int n_ag = c->goal_mode == DGPPO_GOAL_SPREAD ? n * ng : n;
   if (mpe) {
-    c->n_nodes = 2 * n + c->n_obs + 1;
+    c->n_nodes = n + ng + c->n_obs + 1;
     c->n_edges = n * n + n_ag + n * c->n_obs;
   } else {
     const int hits = c->n_obs > 0 ? n * c->top_k : 0;
-    c->n_nodes = 2 * n + hits + 1;
+    c->n_nodes = n + ng + hits + 1;
     c->n_edges = n * n + n_ag + hits;
   }
   const float a = c->area_size;
@@ -1909,9 +2356,12 @@ extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
     for (int i = 0; i < 5; ++i) { c->state_lo[i] = lo[i]; c->state_hi[i] = hi[i]; }
   } else {
     const float v = mpe ? 1.0f : 0.5f;
-    const float lo[5] = {0.f, 0.f, -v, -v, 0.f}, hi[5] = {a, a, v, v, 0.f};
+    // corridor / connect: the goals sit past the obstacles, y up to 2 area (mpe_corridor.py:55-58)
+    const bool tall = c->variant == DGPPO_VARIANT_CORRIDOR || c->variant == DGPPO_VARIANT_CONNECT;
+    const float lo[5] = {0.f, 0.f, -v, -v, 0.f}, hi[5] = {a, tall ? 2.0f * a : a, v, v, 0.f};
     for (int i = 0; i < 5; ++i) { c->state_lo[i] = lo[i]; c->state_hi[i] = hi[i]; }
   }
+  if (c->obs_edge_radius == 0.f) c->obs_edge_radius = c->comm_radius;
   const double r = c->car_radius, orr = c->obs_radius, cr = c->comm_radius;
   if (c->c_agent_cost == 0.f) c->c_agent_cost = (float)(r * 2);
   if (c->c_obs_cost == 0.f) c->c_obs_cost = (float)(mpe ? r + orr : r);
@@ -1966,6 +2416,17 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
     return DGPPO_EINVAL;
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  if (cfg->variant != DGPPO_VARIANT_NONE) {
+    const size_t sh = var::lds_floats(*cfg) * sizeof(float);
+    if (sh > 64 * 1024) return DGPPO_EINVAL;
+    if (cfg->engine == DGPPO_ENGINE_MPE)
+      hipLaunchKernelGGL(var::step_kernel<DGPPO_ENGINE_MPE>, dim3((unsigned)io->n_env), dim3(var::kT), sh,
+                         (hipStream_t)stream, *cfg, *io);
+    else
+      hipLaunchKernelGGL(var::step_kernel<DGPPO_ENGINE_LIDAR>, dim3((unsigned)io->n_env), dim3(var::kT), sh,
+                         (hipStream_t)stream, *cfg, *io);
+    return (int)hipGetLastError();
+  }
   const bool wave_shape = lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK &&
                           cfg->n_obs == 3 && wave_step_enabled();
   if (cfg->engine == DGPPO_ENGINE_OMNI && wave_shape) {
@@ -2005,7 +2466,7 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
 
 static bool wave_config(const dgppo_env_cfg* cfg) {
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
-  return lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
+  return lidar && cfg->variant == DGPPO_VARIANT_NONE && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
          wave_step_enabled();
 }
 
@@ -2071,12 +2532,22 @@ extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_i
   if (!io->nodes || !io->edges || !io->out_states || !io->receivers || !io->senders) return DGPPO_EINVAL;
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io->obstacles || !io->ray_dirs)) return DGPPO_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  if (cfg->variant != DGPPO_VARIANT_NONE) {
+    const size_t sh = var::lds_floats(*cfg) * sizeof(float);
+    if (sh > 64 * 1024) return DGPPO_EINVAL;
+    if (cfg->engine == DGPPO_ENGINE_MPE)
+      hipLaunchKernelGGL(var::reset_kernel<DGPPO_ENGINE_MPE>, dim3((unsigned)io->n_env), dim3(var::kT), sh, s, *cfg,
+                         *io);
+    else
+      hipLaunchKernelGGL(var::reset_kernel<DGPPO_ENGINE_LIDAR>, dim3((unsigned)io->n_env), dim3(var::kT), sh, s,
+                         *cfg, *io);
+    return (int)hipGetLastError();
+  }
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                  cfg->engine != DGPPO_ENGINE_MPE);
   const size_t shmem = ((size_t)cv.total + 2 * kSampTab) * sizeof(float);  // + the sampler's candidate table
-  const hipStream_t s = (hipStream_t)stream;
-  const bool wave = lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK &&
-                    cfg->n_obs == 3 && wave_step_enabled();
+  const bool wave = wave_config(cfg);
   if (!wave) {
     dispatch_reset(*cfg, *io, shmem, s, 0);
     return (int)hipGetLastError();

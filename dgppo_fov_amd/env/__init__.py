@@ -1,25 +1,31 @@
 """Env registry + make_env (dgppo/env/__init__.py:10-55).
 
-The engines BASELINE.json's configs use plus LidarOmniTarget (the FoV env)
-are built; the other reference variants (MPEFormation/Line/Corridor/ConnectSpread, LidarLine, VMAS)
-are listed in DESIGN.md as next rows and raise here."""
+Every Lidar and MPE env of the reference is built (the variants LidarLine, MPELine, MPEFormation,
+MPECorridor and MPEConnectSpread on the variant kernels); VMAS (a separate
+contact-physics engine) is not, and raises here."""
 from typing import Optional
 
 from .base import MultiAgentEnv, StepResult, RolloutResult
-from .lidar_env import LidarSpread, LidarTarget, LidarBicycleTarget, LidarOmniTarget, LidarEnv, LidarEnvState
-from .mpe import MPESpread, MPETarget, MPE, MPEEnvState
+from .lidar_env import (LidarSpread, LidarTarget, LidarBicycleTarget, LidarOmniTarget, LidarLine, LidarEnv,
+                        LidarEnvState)
+from .mpe import (MPESpread, MPETarget, MPELine, MPEFormation, MPECorridor, MPEConnectSpread, MPE,
+                  MPEEnvState)
 
 ENV = {
     "MPETarget": MPETarget,
     "MPESpread": MPESpread,
+    "MPELine": MPELine,
+    "MPEFormation": MPEFormation,
+    "MPECorridor": MPECorridor,
+    "MPEConnectSpread": MPEConnectSpread,
     "LidarSpread": LidarSpread,
     "LidarTarget": LidarTarget,
+    "LidarLine": LidarLine,
     "LidarBicycleTarget": LidarBicycleTarget,
     "LidarOmniTarget": LidarOmniTarget,
 }
 
-NOT_YET_BUILT = ("MPELine", "MPEFormation", "MPECorridor", "MPEConnectSpread", "LidarLine",
-                 "VMASReverseTransport", "VMASWheel")
+NOT_YET_BUILT = ("VMASReverseTransport", "VMASWheel")
 
 DEFAULT_MAX_STEP = 128
 

@@ -61,12 +61,15 @@ class MultiAgentEnv(ABC):
         self._t = 0
         self._max_step = max_step
         self._area_size = area_size
-        self.num_goals = self._num_agents
+        self.num_goals = self._n_goals()  # goal node rows (the line / formation variants: landmarks)
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         self._cfg = self._make_cfg()
         self._cfg_handle = ops.register_env_cfg(self._cfg)  # the torch.ops.dgppo env ops take this handle
         self._dev_cache = {}
+
+    def _n_goals(self) -> int:
+        return self._num_agents
 
     # ---- reference properties --------------------------------------------------------------
     @property
@@ -182,6 +185,7 @@ class MultiAgentEnv(ABC):
         c.c_mpe_obs_goal = r * 2 + orr
         c.c_mpe_obs_lo = r * 3
         c.c_mpe_obs_hi = self._area_size - r * 3
+        c.n_goals = self.num_goals if self.num_goals != self._num_agents else 0
         self._engine_cfg(c)
         _lib.check(_lib.load().dgppo_env_cfg_finalize(ctypes.byref(c)), "dgppo_env_cfg_finalize")
         return c
@@ -211,11 +215,11 @@ class MultiAgentEnv(ABC):
         device = device or self.device
         key = ("node_type", str(device))
         if key not in self._dev_cache:
-            n, N = self._num_agents, self.n_nodes
+            n, ng, N = self._num_agents, self.num_goals, self.n_nodes
             t = -torch.ones(N, dtype=torch.int32)
             t[:n] = self.AGENT
-            t[n:2 * n] = self.GOAL
-            t[2 * n:N - 1] = self.OBS
+            t[n:n + ng] = self.GOAL
+            t[n + ng:N - 1] = self.OBS
             self._dev_cache[key] = t.to(device)
         return self._dev_cache[key]
 
@@ -226,15 +230,15 @@ class MultiAgentEnv(ABC):
         device = device or self.device
         key = ("cand", str(device))
         if key not in self._dev_cache:
-            n = self._num_agents
+            n, ng = self._num_agents, self.num_goals
             spread = self.GOAL_MODE == _lib.DGPPO_GOAL_SPREAD
-            n_ag = n * n if spread else n
+            n_ag = n * ng if spread else n
             mpe = self.ENGINE == _lib.DGPPO_ENGINE_MPE
             k = self.n_obs if mpe else (int(self._params.get("top_k_rays", 0)) if self.n_obs > 0 else 0)
             rows = []
             for i in range(n):
                 r = [i * n + j for j in range(n)]
-                r += [n * n + i * n + j for j in range(n)] if spread else [n * n + i]
+                r += [n * n + i * ng + j for j in range(ng)] if spread else [n * n + i]
                 r += [n * n + n_ag + i * k + h for h in range(k)]
                 rows.append(r)
             self._dev_cache[key] = torch.tensor(rows, dtype=torch.int32).to(device)

@@ -63,7 +63,7 @@ class LidarEnv(MultiAgentEnv):
                 obstacles = obstacles.reshape(obstacles.shape[:1] + (1,) * extra + obstacles.shape[1:]).expand(
                     tuple(states.shape[:-2]) + tuple(obstacles.shape[1:]))
             ob = Rectangle(obstacles)
-        return LidarEnvState(states[..., :n, :], states[..., n:2 * n, :], ob)
+        return LidarEnvState(states[..., :n, :], states[..., n:n + self.num_goals, :], ob)
 
     def _obstacles_of(self, graph):
         if self.n_obs == 0:

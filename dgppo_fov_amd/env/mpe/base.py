@@ -40,5 +40,5 @@ class MPE(MultiAgentEnv):
         return torch.tensor([0.0, 0.0, -1.0, -1.0]), torch.tensor([self.area_size, self.area_size, 1.0, 1.0])
 
     def _env_states(self, states, obstacles):
-        n, O = self.num_agents, self.n_obs
-        return MPEEnvState(states[..., :n, :], states[..., n:2 * n, :], states[..., 2 * n:2 * n + O, :])
+        n, ng, O = self.num_agents, self.num_goals, self.n_obs
+        return MPEEnvState(states[..., :n, :], states[..., n:n + ng, :], states[..., n + ng:n + ng + O, :])

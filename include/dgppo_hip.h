@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 5  /* 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 6  /* 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -33,6 +33,12 @@ extern "C" {
 /* goal wiring */
 #define DGPPO_GOAL_SPREAD 0 /* every agent sees every goal: lidar_spread.py:86-91, mpe_spread.py:64-69 */
 #define DGPPO_GOAL_TARGET 1 /* agent i sees goal i only: lidar_target.py:77-84, mpe_target.py:63-70 */
+/* reference env variants (goal wiring SPREAD, double integrator); reset, reward goals and costs differ */
+#define DGPPO_VARIANT_NONE 0      /* the base envs above */
+#define DGPPO_VARIANT_LINE 1      /* lidar_line.py, mpe_line.py: 2 landmark goal nodes, reward goals on the segment */
+#define DGPPO_VARIANT_FORMATION 2 /* mpe_formation.py: 1 landmark goal node, reward goals on a circle around it */
+#define DGPPO_VARIANT_CORRIDOR 3  /* mpe_corridor.py: 2 fixed wall obstacles, always-connected obstacle edges */
+#define DGPPO_VARIANT_CONNECT 4   /* mpe_connect_spread.py: + connectivity cost (n_cost 3), 1 obstacle */
 
 /* Obstacle record (LidarEnv rectangles), 16 floats = 64 B per obstacle:
  *   [cx, cy, width, height, theta, cos(theta), sin(theta), type, p0x, p0y, p1x, p1y, p2x, p2y, p3x, p3y]
@@ -81,6 +87,22 @@ typedef struct dgppo_env_cfg {
    * fov_angle_deg (FoV half-angle beta), max_sensor_range (r_max), min_safe_distance (D),
    * rotation_penalty; c_cos_fov = cos(deg2rad(fov_angle_deg)) in fp32 (filled by finalize). */
   float omni_max_w, fov_angle_deg, fov_rmax, fov_dmin, rot_pen, c_cos_fov;
+  /* ABI 6: env variants (all zero for the base envs).  Graph layout: agents | n_goals goal rows |
+   * hits or obstacles | pad.  Constants in Python float64 rounded once, like the fields above. */
+  int32_t variant;        /* DGPPO_VARIANT_* */
+  int32_t n_goals;        /* goal node rows (0 -> n_agents; line 2, formation 1) */
+  int32_t goals_inner;    /* line: 1 = the n interior points of the segment (mpe_line.py n <= 3) */
+  float goal_radius;      /* formation: reward goals on this circle (comm_radius, mpe_formation.py:92-96) */
+  float obs_edge_radius;  /* MPE agent-obstacle edge mask radius (0 -> comm_radius; corridor/connect comm*100) */
+  float connect_radius;   /* connect: 0.45 */
+  float sample_side_y;    /* corridor/connect: get_node_goal_rng side_length_y */
+  float goal_shift_y;     /* corridor/connect: goals += [0, goal_shift_y] after sampling */
+  float line_min_dist;    /* line: landmark separation */
+  float c_obs_inflate;    /* lidar_line: obstacle placement radius 1.1 car_radius */
+  float formation_lo, formation_hi; /* formation: landmark coordinate range [R + 2r, area - R - 2r] */
+  float c_connect_min;    /* connect: agent sampling min_dist 2.3 car_radius */
+  float line_box_x, line_box_y, line_off_y; /* line: l0 candidate box [0, area - side] x [0, side], y offset area/2 - side */
+  float obs_x_hi;         /* corridor / connect: area - obs_radius */
 } dgppo_env_cfg;
 
 /* Fills n_nodes / n_edges / node_dim / state_lo/hi and zero derived constants from the other

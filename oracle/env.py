@@ -35,6 +35,16 @@ OMNI_PARAMS = dict(LIDAR_PARAMS, **{  # lidar_omni_target.py:49-68
 
 ENGINE_LIDAR, ENGINE_BICYCLE, ENGINE_MPE, ENGINE_OMNI = 0, 1, 2, 3
 GOAL_SPREAD, GOAL_TARGET = 0, 1
+# reference env variants (oracle/env_variants.py): goal-node layout, reward goals, resets, costs
+VARIANT_NONE, VARIANT_LINE, VARIANT_FORMATION, VARIANT_CORRIDOR, VARIANT_CONNECT = 0, 1, 2, 3, 4
+MPE_CORRIDOR_PARAMS = {  # mpe_corridor.py:14-21 (obs_radius derived in __init__, :37)
+    "car_radius": 0.05, "comm_radius": 0.5, "default_area_size": 1.0, "dist2goal": 0.01, "n_obs": 2,
+    "corridor_width": 0.2,
+}
+MPE_CONNECT_PARAMS = {  # mpe_connect_spread.py:16-24
+    "car_radius": 0.05, "comm_radius": 0.5, "default_area_size": 1.0, "dist2goal": 0.01, "n_obs": 1,
+    "obs_radius": 0.25, "connect_radius": 0.45,
+}
 
 ENVS = {
     "LidarSpread": (ENGINE_LIDAR, GOAL_SPREAD),
@@ -43,7 +53,14 @@ ENVS = {
     "MPESpread": (ENGINE_MPE, GOAL_SPREAD),
     "MPETarget": (ENGINE_MPE, GOAL_TARGET),
     "LidarOmniTarget": (ENGINE_OMNI, GOAL_TARGET),
+    "LidarLine": (ENGINE_LIDAR, GOAL_SPREAD),  # lidar_line.py (LidarSpread params, 2 landmark goal nodes)
+    "MPELine": (ENGINE_MPE, GOAL_SPREAD),  # mpe_line.py (MPESpread params)
+    "MPEFormation": (ENGINE_MPE, GOAL_SPREAD),  # mpe_formation.py
+    "MPECorridor": (ENGINE_MPE, GOAL_SPREAD),  # mpe_corridor.py
+    "MPEConnectSpread": (ENGINE_MPE, GOAL_SPREAD),  # mpe_connect_spread.py
 }
+VARIANTS = {"LidarLine": VARIANT_LINE, "MPELine": VARIANT_LINE, "MPEFormation": VARIANT_FORMATION,
+            "MPECorridor": VARIANT_CORRIDOR, "MPEConnectSpread": VARIANT_CONNECT}
 
 
 @dataclasses.dataclass
@@ -58,7 +75,15 @@ class Spec:
 
     def __post_init__(self):
         self.engine, self.goal_mode = ENVS[self.env_id]
+        self.variant = VARIANTS.get(self.env_id, VARIANT_NONE)
         p = dict(MPE_PARAMS if self.engine == ENGINE_MPE else (OMNI_PARAMS if self.engine == ENGINE_OMNI else LIDAR_PARAMS))
+        if self.variant == VARIANT_CORRIDOR:
+            p = dict(MPE_CORRIDOR_PARAMS)
+            p["obs_radius"] = (p["default_area_size"] - p["corridor_width"]) / 4  # mpe_corridor.py:37
+            self.n_obs = 2  # forced (mpe_corridor.py:33-35)
+        elif self.variant == VARIANT_CONNECT:
+            p = dict(MPE_CONNECT_PARAMS)
+            self.n_obs = 1  # forced (mpe_connect_spread.py:38-40)
         self.params = p
         self.car_r = p["car_radius"]
         self.comm_r = p["comm_radius"]
@@ -73,7 +98,9 @@ class Spec:
         omni = self.engine == ENGINE_OMNI
         self.ed = 10 if omni else 4  # edge_dim (lidar_omni_target.py:136-143)
         self.ad = 3 if omni else 2  # action_dim (ax, ay, alpha)
-        self.n_cost = 5 if omni else 2
+        self.n_cost = 5 if omni else (3 if self.variant == VARIANT_CONNECT else 2)
+        # goal node rows: 2 landmarks (line), 1 landmark (formation), else one per agent
+        self.ng = {VARIANT_LINE: 2, VARIANT_FORMATION: 1}.get(self.variant, self.n)
 
     @property
     def has_lidar(self):
@@ -86,12 +113,12 @@ class Spec:
     @property
     def n_nodes(self):  # graph.py:212-247 (+1 pad node)
         if self.engine == ENGINE_MPE:
-            return 2 * self.n + self.n_obs + 1
-        return 2 * self.n + self.n_hits + 1
+            return self.n + self.ng + self.n_obs + 1
+        return self.n + self.ng + self.n_hits + 1
 
     @property
     def n_ag(self):
-        return self.n * self.n if self.goal_mode == GOAL_SPREAD else self.n
+        return self.n * self.ng if self.goal_mode == GOAL_SPREAD else self.n
 
     @property
     def n_edges(self):
@@ -105,8 +132,9 @@ class Spec:
             return (np.array([0, 0, -1, -1, -2, -2, -w], F), np.array([self.area, self.area, 1, 1, 2, 2, w], F))
         if self.engine == ENGINE_BICYCLE:  # lidar_bicycle_target.py:120-123
             return (np.array([0, 0, -1, -1, -0.5], F), np.array([self.area, self.area, 1, 1, 0.5], F))
-        if self.engine == ENGINE_MPE:  # mpe/base.py:243-246
-            return np.array([0, 0, -1, -1], F), np.array([self.area, self.area, 1, 1], F)
+        if self.engine == ENGINE_MPE:  # mpe/base.py:243-246; corridor / connect: y up to 2 area
+            hy = 2 * self.area if self.variant in (VARIANT_CORRIDOR, VARIANT_CONNECT) else self.area
+            return np.array([0, 0, -1, -1], F), np.array([self.area, hy, 1, 1], F)
         return np.array([0, 0, -0.5, -0.5], F), np.array([self.area, self.area, 0.5, 0.5], F)  # lidar base 273-276
 
 
@@ -435,29 +463,30 @@ def build_graph(spec, agent, goal, third):
     B = agent.shape[0]
     n, sd, nd = spec.n, spec.sd, spec.nd
     N, E = spec.n_nodes, spec.n_edges
+    t0 = n + spec.ng  # first row after the goal node rows
     pad = N - 1
     nodes = np.zeros((B, N, nd), F)
     states = np.zeros((B, N, sd), F)
     nodes[:, :n, :sd] = agent
-    nodes[:, n:2 * n, :sd] = goal
+    nodes[:, n:t0, :sd] = goal
     states[:, :n] = agent
-    states[:, n:2 * n] = goal
+    states[:, n:t0] = goal
     if spec.engine == ENGINE_MPE:
         O = spec.n_obs
         nodes[:, :n, 6] = 1
-        nodes[:, n:2 * n, 5] = 1
+        nodes[:, n:t0, 5] = 1
         if O > 0:
-            nodes[:, 2 * n:2 * n + O, :sd] = third
-            nodes[:, 2 * n:2 * n + O, 4] = 1
-            states[:, 2 * n:2 * n + O] = third
+            nodes[:, t0:t0 + O, :sd] = third
+            nodes[:, t0:t0 + O, 4] = 1
+            states[:, t0:t0 + O] = third
     else:
         nodes[:, :n, sd + 2] = 1
-        nodes[:, n:2 * n, sd + 1] = 1
+        nodes[:, n:t0, sd + 1] = 1
         if spec.has_lidar:
             hits = third.reshape(B, n * spec.top_k, 2)
-            nodes[:, 2 * n:2 * n + spec.n_hits, :2] = hits
-            nodes[:, 2 * n:2 * n + spec.n_hits, sd] = 1
-            states[:, 2 * n:2 * n + spec.n_hits, :2] = hits
+            nodes[:, t0:t0 + spec.n_hits, :2] = hits
+            nodes[:, t0:t0 + spec.n_hits, sd] = 1
+            states[:, t0:t0 + spec.n_hits, :2] = hits
     states[:, pad] = -1
 
     fa = state2feat(spec, agent)
@@ -493,8 +522,8 @@ def build_graph(spec, agent, goal, third):
     dist = dist + (np.eye(n, dtype=F) * F(spec.comm_r + 1))[None]
     block(feats, dist < F(spec.comm_r), ids_a, ids_a)
     # agent-goal
-    if spec.goal_mode == GOAL_SPREAD:
-        block(fa[:, :, None, :] - fg[:, None, :, :], np.ones((B, n, n), bool), ids_a, n + ids_a)
+    if spec.goal_mode == GOAL_SPREAD:  # every agent to every goal node (landmarks for line / formation)
+        block(fa[:, :, None, :] - fg[:, None, :, :], np.ones((B, n, spec.ng), bool), ids_a, n + np.arange(spec.ng))
     else:
         for i in range(n):
             gf = fa[:, i] - fg[:, i]
@@ -507,7 +536,9 @@ def build_graph(spec, agent, goal, third):
         if O > 0:
             op = third[..., :2]
             d = norm2d(ap[:, :, None, 0] - op[:, None, :, 0], ap[:, :, None, 1] - op[:, None, :, 1])
-            block(agent[:, :, None, :] - third[:, None, :, :], d < F(spec.comm_r), ids_a, 2 * n + np.arange(O))
+            # corridor / connect connect every obstacle: jnp.less(dist, comm_radius * 100)
+            r_obs = spec.comm_r * 100 if spec.variant in (VARIANT_CORRIDOR, VARIANT_CONNECT) else spec.comm_r
+            block(agent[:, :, None, :] - third[:, None, :, :], d < F(r_obs), ids_a, t0 + np.arange(O))
     elif spec.has_lidar:
         k = spec.top_k
         for i in range(n):
@@ -517,7 +548,7 @@ def build_graph(spec, agent, goal, third):
             # comm_radius - 0.1 (lidar_spread.py:95)
             active = ld < F(spec.comm_r if omni else spec.comm_r - 1e-1)
             feats = np.concatenate([lf, np.zeros((B, k, spec.ed - 2), F)], -1)
-            block(feats[:, None], active[:, None], [i], 2 * n + i * k + np.arange(k))
+            block(feats[:, None], active[:, None], [i], t0 + i * k + np.arange(k))
     out = dict(
         nodes=nodes,
         edges=np.concatenate(edges, 1).astype(F),
@@ -533,8 +564,8 @@ def node_type(spec):
     n, N = spec.n, spec.n_nodes
     t = -np.ones(N, np.int32)
     t[:n] = 0
-    t[n:2 * n] = 1
-    t[2 * n:N - 1] = 2
+    t[n:n + spec.ng] = 1
+    t[n + spec.ng:N - 1] = 2
     return t
 
 
@@ -546,9 +577,14 @@ def env_step(spec, states, obst, action):
     or None (MPE reads obstacles from graph states); action (B, n, action_dim).
     Returns dict(graph fields of the next graph, reward (B,), cost (B, n, n_cost), next_agent)."""
     n = spec.n
+    t0 = n + spec.ng
     states = np.asarray(states, F)
     agent = states[:, :n]
-    goal = states[:, n:2 * n]
+    goal = states[:, n:t0]
+    if spec.variant != VARIANT_NONE:
+        from .env_variants import variant_step
+
+        return variant_step(spec, states, obst, action)
     if spec.engine == ENGINE_OMNI:  # action_lim: [-1, -1, -1000] .. [1, 1, 1000] (lidar_omni_target.py:511-521)
         a = clip(np.asarray(action, F), np.array([-1, -1, -1000], F), np.array([1, 1, 1000], F))
         nxt = step_omni(spec, agent, a)
@@ -654,7 +690,12 @@ def min_dist_for(spec):
 def env_reset(spec, seed, n_env, env_offset=0):
     """reset (lidar_env/base.py:89-124; lidar_bicycle_target.py:60-90; mpe/base.py:81-127).
 
-    Returns (agent (B,n,sd), goal (B,n,sd), obst (B,O,16) or MPE obstacle states (B,O,4))."""
+    Returns (agent (B,n,sd), goal (B,n,sd), obst (B,O,16) or MPE obstacle states (B,O,4)); the variants
+    (oracle/env_variants.py) return their goal-node rows (B, ng, sd) as `goal`."""
+    if spec.variant != VARIANT_NONE:
+        from .env_variants import variant_reset
+
+        return variant_reset(spec, seed, n_env, env_offset)
     n, sd, O = spec.n, spec.sd, spec.n_obs
     area = spec.area
     md = min_dist_for(spec)

@@ -324,3 +324,21 @@ def test_omni_edge_features_local_frame():
     np.testing.assert_allclose(e[5, 7:], [1.0, 0.4, 0.4], atol=1e-6)  # (1 <- 2): ahead of agent 1 along +x
     assert g["receivers"][0, 2] == 0  # (0, 2): |p| = 0.447 < comm_radius 0.5 -> kept
     assert g["receivers"][0, 0] == spec.n_nodes - 1  # self edge -> pad
+
+
+def test_env_variant_goal_rules_kat():
+    """landmark2goal by hand: LidarLine n=5 on (0,0)-(1,2) -> k/4 steps incl. both ends; MPELine n=3 ->
+    the interior quarter points; MPEFormation n=4, R=0.5 around (1,1) -> (1.5,1), (1,1.5), (0.5,1), (1,0.5)."""
+    from oracle import env_variants as V
+
+    lm = np.array([[[0.0, 0.0], [1.0, 2.0]]], np.float32)
+    g = V.landmark2goal(O.Spec("LidarLine", 5, 0), lm)[0]
+    np.testing.assert_array_equal(g, np.array([[0, 0], [0.25, 0.5], [0.5, 1.0], [0.75, 1.5], [1, 2]], np.float32))
+    g = V.landmark2goal(O.Spec("MPELine", 3, 0), lm)[0]
+    np.testing.assert_array_equal(g, np.array([[0.25, 0.5], [0.5, 1.0], [0.75, 1.5]], np.float32))
+    g = V.landmark2goal(O.Spec("MPEFormation", 4, 0), np.array([[[1.0, 1.0]]], np.float32))[0]
+    np.testing.assert_allclose(g, [[1.5, 1.0], [1.0, 1.5], [0.5, 1.0], [1.0, 0.5]], atol=1e-6)
+    # graph layout of the variants: goal node rows 2 / 1 / n
+    for eid, n, ng in (("LidarLine", 5, 2), ("MPEFormation", 4, 1), ("MPECorridor", 3, 3)):
+        spec = O.Spec(eid, n, 2)
+        assert spec.ng == ng and (O.node_type(spec) == 1).sum() == ng
