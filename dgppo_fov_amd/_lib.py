@@ -168,14 +168,14 @@ class GruSeqArgs(ctypes.Structure):
 
 class GtLayer(ctypes.Structure):
     _fields_ = [("Wq", c_f32p), ("bq", c_f32p), ("Wkt", c_f32p), ("bk", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p),
-                ("bu", c_f32p), ("D", ctypes.c_int32), ("F", ctypes.c_int32)]
+                ("bu", c_f32p), ("D", ctypes.c_int32), ("F", ctypes.c_int32), ("Wex", c_f32p)]
 
 
 class PolicyStepArgs(ctypes.Structure):
     _fields_ = [
         ("G", ctypes.c_int32), ("N", ctypes.c_int32), ("E", ctypes.c_int32), ("n_agents", ctypes.c_int32),
         ("C", ctypes.c_int32), ("D0", ctypes.c_int32), ("A", ctypes.c_int32), ("n_layers", ctypes.c_int32),
-        ("H", ctypes.c_int32), ("mode", ctypes.c_int32),
+        ("H", ctypes.c_int32), ("mode", ctypes.c_int32), ("ED", ctypes.c_int32), ("pad_", ctypes.c_int32),
         ("cand", c_f32p),
         ("nodes", c_f32p), ("nodes_gstride", ctypes.c_int64),
         ("edges", c_f32p), ("edges_gstride", ctypes.c_int64),

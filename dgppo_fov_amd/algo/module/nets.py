@@ -86,15 +86,16 @@ class ActorNet(_Net):
     def _fused_args(self, g: GraphBatch):
         """dgppo_policy_step_args with this net's parameter pointers (None if the fused kernel does not
         cover the configuration)."""
-        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1" or g.ED != 4 or g.nodes.shape[2] > GraphBatch.KD0:
+        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1":
             return None
         a = _lib.PolicyStepArgs()
         a.N, a.E, a.n_agents, a.C, a.D0, a.A = g.N, g.E, self.n, g.C, g.nodes.shape[2], self.A
-        a.n_layers, a.H = len(self.gnn.layers), 3
+        a.n_layers, a.H, a.ED = len(self.gnn.layers), 3, g.ED
         for i, L in enumerate(self.gnn.layers):
             ly = a.layer[i]
             ly.Wq, ly.bq, ly.Wkt, ly.bk = K._p(L.v("Wq")), K._p(L.v("bq")), K._p(L.v("Wkt")), K._p(L.v("bk"))
             ly.Wcat, ly.Wu, ly.bu = K._p(L.v("Wcat")), K._p(L.v("Wu")), K._p(L.v("bu"))
+            ly.Wex = K._p(L.v("Wex")) if getattr(L, "EX", 0) > 0 else None
             ly.D, ly.F = L.D, L.F
         hd = self.head
         a.head_W0, a.head_b0, a.head_W1, a.head_b1 = K._p(hd.d0.W()), K._p(hd.d0.b()), K._p(hd.d1.W()), K._p(hd.d1.b())
@@ -131,7 +132,7 @@ class ActorNet(_Net):
             fa.G, fa.mode = g.G, int(mode)
             fa.cand, fa.receivers, fa.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
             fa.nodes, fa.nodes_gstride = K._p(g.nodes), g.N * g.nodes.shape[2]
-            fa.edges, fa.edges_gstride, fa.idx_gstride = K._p(g.edges), g.E * 4, g.E
+            fa.edges, fa.edges_gstride, fa.idx_gstride = K._p(g.edges), g.E * g.ED, g.E
             fa.h_in, fa.h_out, fa.noise = K._p(h), K._p(h2), K._p(noise)
             fa.action, fa.log_pi = K._p(action), K._p(log_pi)
             K._chk(_lib.load().dgppo_policy_step(ctypes.byref(fa), _lib.stream_handle(dev)), "dgppo_policy_step")

@@ -43,9 +43,12 @@ __device__ __forceinline__ float gsum8(float v) { return lanes::sum8(v); }
 constexpr int kRowsG = 16, kThreads = 256, kHeads = 3, kHid = 64;
 // row tiles of 16, attention sub-rounds (a wave takes two rows per sub-round), pairs per thread
 constexpr int kRT = kRowsG / 16, kSR = kRowsG / 8;
-constexpr int kMaxD0 = 8, kCP = 32;
-// LDS pitches (floats)
-constexpr int kX0P = 9, kQTP = 100, kXCP = 116, kY0P = 36, kYP = 68, kXSP = 40;
+// raw node rows up to 12 wide and edge rows up to 4 + 6 (LidarOmniTarget: 10 / 10); the kernel is
+// instantiated narrow (<= 8, 4: the Lidar / MPE envs, 240 VGPRs = 2 waves per SIMD) and wide
+constexpr int kMaxD0 = 12, kMaxEX = 6, kCP = 32;
+constexpr int kNarrowD0 = 8;
+// LDS pitches (floats); xs rows: x (0..31) | edge head (32..35) | extra edge columns (36..41)
+constexpr int kX0P = 13, kQTP = 100, kXCP = 132, kY0P = 36, kYP = 68, kXSP = 44;
 // work: per layer the (32 + 1) x 100 query-key matrix [QT_0 | QT_1 | QT_2 (32 cols each) | beta_0..2 | 0]
 // (rows 0..D-1) and its bias row (row 32)
 constexpr int kQKRows = 33, kQKCols = kQTP, kQKStride = kQKRows * kQKCols;
@@ -161,19 +164,23 @@ __device__ __forceinline__ void acc_store(const f32x4 (&acc)[CT][kRT], float* ds
   }
 }
 
-// one GraphTransformer layer's operands: [QT | beta] (K = D), Wcat (K = 3 (D + 5)), Wu (K = D)
-template <int KQ, int KC, int KU>
+// one GraphTransformer layer's operands: [QT | beta] (K = D), Wcat (K = 3 (D + 5)), Wex (K = 3 EX, the
+// edge columns past 4; rows read as 0 without them), Wu (K = D)
+template <int KQ, int KC, int KX, int KU>
 struct LayerW {
   Frag<KQ, 2> qk;
   Frag<KC, 1> wc;
+  Frag<KX, 1> wx;
   Frag<KU, 1> wu;
   float bqk[2], bu[1];
 };
 
-template <int KQ, int KC, int KU>
-__device__ __forceinline__ void layer_load(LayerW<KQ, KC, KU>& w, const dgppo_gt_layer& ly, const float* qk) {
+template <int KQ, int KC, int KX, int KU>
+__device__ __forceinline__ void layer_load(LayerW<KQ, KC, KX, KU>& w, const dgppo_gt_layer& ly, const float* qk,
+                                           int EX) {
   frag_load(w.qk, qk, kQKCols, ly.D);
   frag_load(w.wc, ly.Wcat, ly.F, kHeads * (ly.D + 5));
+  frag_load(w.wx, ly.Wex, ly.F, EX > 0 ? kHeads * EX : 0);
   frag_load(w.wu, ly.Wu, ly.F, ly.D);
   bias_load(w.bqk, qk + 32 * kQKCols, kQKCols);
   bias_load(w.bu, ly.bu, ly.F);
@@ -211,26 +218,33 @@ __device__ __forceinline__ Lds carve(float* base) {
 
 // raw sender row and edge features of the pair (row r, candidate c); raw rows are fetched for every
 // sender (layer 0 uses them all, layer 1 those of never-receiving senders)
+template <int MD0, int MEX>
 struct PairG {
-  float xr[kMaxD0];
+  float xr[MD0];
   f32x4 ef;
+  float ex[MEX > 0 ? MEX : 1];  // edge columns 4.. (wide instantiation only)
   int s;
 };
 
 // cur = pg[sr] by selects (a dynamically indexed register array would live in scratch)
-__device__ __forceinline__ void pair_pick(const PairG (&pg)[kSR], int sr, PairG& cur) {
+template <int MD0, int MEX>
+__device__ __forceinline__ void pair_pick(const PairG<MD0, MEX> (&pg)[kSR], int sr, PairG<MD0, MEX>& cur) {
 #pragma unroll
-  for (int k = 0; k < kMaxD0; ++k) cur.xr[k] = pg[0].xr[k];
+  for (int k = 0; k < MD0; ++k) cur.xr[k] = pg[0].xr[k];
 #pragma unroll
   for (int j = 0; j < 4; ++j) cur.ef[j] = pg[0].ef[j];
+#pragma unroll
+  for (int j = 0; j < MEX; ++j) cur.ex[j] = pg[0].ex[j];
   cur.s = pg[0].s;
 #pragma unroll
   for (int q = 1; q < kSR; ++q) {
     const bool tk = sr == q;
 #pragma unroll
-    for (int k = 0; k < kMaxD0; ++k) cur.xr[k] = tk ? pg[q].xr[k] : cur.xr[k];
+    for (int k = 0; k < MD0; ++k) cur.xr[k] = tk ? pg[q].xr[k] : cur.xr[k];
 #pragma unroll
     for (int j = 0; j < 4; ++j) cur.ef[j] = tk ? pg[q].ef[j] : cur.ef[j];
+#pragma unroll
+    for (int j = 0; j < MEX; ++j) cur.ex[j] = tk ? pg[q].ex[j] : cur.ex[j];
     cur.s = tk ? pg[q].s : cur.s;
   }
 }
@@ -238,26 +252,36 @@ __device__ __forceinline__ void pair_pick(const PairG (&pg)[kSR], int sr, PairG&
 // r / n for r < 32, n <= 32: (r * nmag) >> 16 with nmag = 65536 / n + 1 (exact in that range)
 __device__ __forceinline__ int div_n(int r, int nmag) { return (r * nmag) >> 16; }
 
+template <int MD0, int MEX>
 __device__ __forceinline__ void pair_gather(const dgppo_policy_step_args& p, const Lds& L, int r, int c, int64_t g0,
-                                            int nmag, PairG& o) {
+                                            int nmag, PairG<MD0, MEX>& o) {
   const int s = L.psrc[r * kCP + c];
   const int e = L.pedge[r * kCP + c];
   const int64_t g = g0 + div_n(r, nmag);
   const bool ok = s >= 0;
   o.s = s;
-  o.ef = ok ? *(const f32x4*)(p.edges + g * p.edges_gstride + (int64_t)e * 4) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  if (MEX == 0) {
+    o.ef = ok ? *(const f32x4*)(p.edges + g * p.edges_gstride + (int64_t)e * 4) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    o.ex[0] = 0.0f;
+  } else {  // wider edge rows (8-byte aligned at best): scalar loads
+    const float* er = p.edges + g * p.edges_gstride + (int64_t)(ok ? e : 0) * p.ED;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o.ef[j] = ok ? er[j] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < MEX; ++j) o.ex[j] = (ok && 4 + j < p.ED) ? er[4 + j] : 0.0f;
+  }
   const float* xr = p.nodes + g * p.nodes_gstride + (int64_t)(ok ? s : 0) * p.D0;
 #pragma unroll
-  for (int k = 0; k < kMaxD0; ++k) o.xr[k] = (ok && k < p.D0) ? xr[k] : 0.0f;
+  for (int k = 0; k < MD0; ++k) o.xr[k] = (ok && k < p.D0) ? xr[k] : 0.0f;
 }
 
 // One GraphTransformer layer for the group's rows: A (32 x D, LDS) = this layer's agent rows;
 // senders: agents -> A rows of the same graph (layer 1) or their raw rows (layer 0); others -> raw
 // node rows (layer 0) or relu(raw Wu0 + bu0) (layer 1, agent mode).  Output relu(M/H + A Wu + bu)
 // into out (kRowsG x F).  pg[k] = the lane's pair of sub-round k (rows 2 wave + 8 k + (lane >> 5)).
-template <int KQ, int KC, int KU>
+template <int MD0, int MEX, int KQ, int KC, int KX, int KU>
 __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const dgppo_gt_layer& ly,
-                                         const LayerW<KQ, KC, KU>& w, const PairG (&pg)[kSR], const Lds& L,
+                                         const LayerW<KQ, KC, KX, KU>& w, const PairG<MD0, MEX> (&pg)[kSR], const Lds& L,
                                          const float* A, int lda, bool layer0, float* out, int ldo, int nmag,
                                          int pk) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -271,9 +295,11 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
     acc_store(acc, L.qt, kQTP, kQKCols, w.bqk, 1.0f, false);
   }
   // pre-transform operands (layer 1): B[k][d] = Wu0[k][d], k = 4 ks + kq, d = 16 ct + i16
-  float pw[2][2], pb[2];
+  constexpr int kPK = MD0 / 4;
+  const int EX = MEX > 0 ? p.ED - 4 : 0;
+  float pw[kPK][2], pb[2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int ks = 0; ks < kPK; ++ks)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) pw[ks][ct] = layer0 ? 0.0f : L.preW[(4 * ks + kq) * 32 + 16 * ct + i16];
 #pragma unroll
@@ -291,20 +317,20 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
   // rolled loop (keeps the code small); the sub-round's pair is selected out of the registers
 #pragma unroll 1
   for (int sr = 0; sr < kSR; ++sr) {
-    PairG cur;
+    PairG<MD0, MEX> cur;
     pair_pick(pg, sr, cur);
     const int r = 2 * wave + 8 * sr + slot;
     const bool ok = cur.s >= 0;
 #pragma unroll
-    for (int k = 0; k < kMaxD0; ++k) xp[k] = cur.xr[k];
+    for (int k = 0; k < MD0; ++k) xp[k] = cur.xr[k];
     if (!layer0) {
       wave_sync();
       // relu(x_raw Wu0 + bu0) for the wave's 64 pairs: 4 row tiles x 2 column tiles x 2 k-steps
-      float a[4][2];
+      float a[4][kPK];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a[t][ks] = xs[(16 * t + i16) * kXSP + 4 * ks + kq];
+        for (int ks = 0; ks < kPK; ++ks) a[t][ks] = xs[(16 * t + i16) * kXSP + 4 * ks + kq];
       f32x4 pacc[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -312,7 +338,7 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
         for (int ct = 0; ct < 2; ++ct) {
           pacc[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
+          for (int ks = 0; ks < kPK; ++ks)
             pacc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][ks], pw[ks][ct], pacc[t][ct], 0, 0, 0);
         }
       wave_sync();
@@ -333,6 +359,8 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
       }
     }
     *(f32x4*)(xp + 32) = cur.ef;
+#pragma unroll
+    for (int j = 0; j < MEX; ++j) xp[36 + j] = cur.ex[j];
     wave_sync();
     // logits (QT_h . x + beta_h) / sqrt(F) and the softmax over the row's 32 candidates
     const float* qt = L.qt + r * kQTP;
@@ -355,14 +383,21 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
 #pragma unroll
     for (int h = 0; h < kHeads; ++h) aa[pr * 4 + h] = aw[h];
     wave_sync();
-    // xcat row = [xbar_h (D each) | ebar_h (4 each) | sig_h]: lane task (head, float4 column block)
-    if (c < H * Th) {
-      const int h = c / Th, q = c - h * Th;
+    // xcat row = [xbar_h (D each) | ebar_h (4 each) | sig_h | ebar_x_h (EX each)]: lane tasks (head, float4
+    // column block), a second pass when they outnumber the row's 32 lanes (wide edges)
+    const int EXQ = (EX + 3) >> 2, Tw = Th + EXQ;
+    for (int task = c; task < H * Tw; task += 32) {
+      const int h = task / Tw, q = task - h * Tw;
       const float* xb = xs + slot * kCP * kXSP;
       const float* ab = aa + slot * kCP * 4 + h;
       float* o = L.xc + r * kXCP;
-      if (q <= TQ) {
-        const int col = q < TQ ? 4 * q : 32;
+      if (q == TQ + 1) {
+        float acc = 0.0f;
+#pragma unroll 8
+        for (int cc = 0; cc < kCP; ++cc) acc += ab[cc * 4];
+        o[H * D + 4 * H + h] = acc;
+      } else {
+        const int col = q < TQ ? 4 * q : (q == TQ ? 32 : 36 + 4 * (q - TQ - 2));
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 8
         for (int cc = 0; cc < kCP; ++cc) acc += ab[cc * 4] * *(const f32x4*)(xb + cc * kXSP + col);
@@ -370,15 +405,15 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (4 * q + j < D) o[h * D + 4 * q + j] = acc[j];
-        } else {
+        } else if (q == TQ) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[H * D + 4 * h + j] = acc[j];
+        } else {
+          const int j0 = 4 * (q - TQ - 2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j0 + j < EX) o[H * (D + 5) + h * EX + j0 + j] = acc[j];
         }
-      } else {
-        float acc = 0.0f;
-#pragma unroll 8
-        for (int cc = 0; cc < kCP; ++cc) acc += ab[cc * 4];
-        o[H * D + 4 * H + h] = acc;
       }
     }
     wave_sync();
@@ -390,6 +425,7 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
     f32x4 acc[1][kRT];
     acc_zero(acc);
     frag_mma(acc, L.xc, kXCP, H * (D + 5), w.wc);
+    if (EX > 0) frag_mma(acc, L.xc + H * (D + 5), kXCP, H * EX, w.wx);
 #pragma unroll
     for (int rt = 0; rt < kRT; ++rt) acc[0][rt] *= 1.0f / H;
     frag_mma(acc, A, lda, D, w.wu);
@@ -427,6 +463,7 @@ __device__ __forceinline__ void ln_relu64(float* Y, const float* scale, const fl
   }
 }
 
+template <int MD0, int MEX>
 __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Lds L = carve(lds);
@@ -470,8 +507,10 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
     hreg[u] = r < rows ? p.h_in[row0 * kHid + e] : 0.0f;
   }
   if (two) {
-    const int k = threadIdx.x / 32, d = threadIdx.x % 32;  // 256 = kMaxD0 x 32
-    L.preW[threadIdx.x] = (k < p.D0 && d < p.layer[0].F) ? p.layer[0].Wu[k * p.layer[0].F + d] : 0.0f;
+    for (int e = threadIdx.x; e < kMaxD0 * 32; e += kThreads) {
+      const int k = e / 32, d = e % 32;
+      L.preW[e] = (k < p.D0 && d < p.layer[0].F) ? p.layer[0].Wu[k * p.layer[0].F + d] : 0.0f;
+    }
     if (threadIdx.x < 32) L.preb[threadIdx.x] = threadIdx.x < p.layer[0].F ? p.layer[0].bu[threadIdx.x] : 0.0f;
   }
   {
@@ -507,7 +546,7 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
   }
   __syncthreads();
   // ---- level 3: every pair this lane attends over (kSR sub-rounds), kept in registers for both layers
-  PairG pg[kSR];
+  PairG<MD0, MEX> pg[kSR];
   {
     const int slot = lane >> 5, c = lane & 31;
 #pragma unroll
@@ -521,8 +560,8 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
     const bool last = l == p.n_layers - 1;
     const dgppo_gt_layer& ly = l == 0 ? p.layer[0] : p.layer[1];
     // one operand shape for both layers (layer 0's extra k-steps read as zeros): one copy of the code
-    LayerW<8, 28, 8> w;
-    layer_load(w, ly, p.work + l * kQKStride);
+    LayerW<8, 28, (MEX > 0 ? 5 : 1), 8> w;
+    layer_load(w, ly, p.work + l * kQKStride, p.ED - 4);
     gt_layer(p, ly, w, pg, L, l == 0 ? L.x0 : L.y0, l == 0 ? kX0P : kY0P, l == 0, last ? L.yb : L.y0,
              last ? kYP : kY0P, nmag, 2 + 3 * l);
     PROBE(4 + 3 * l);
@@ -687,8 +726,11 @@ size_t lds_bytes() { return lds_floats() * sizeof(float); }
 extern "C" int dgppo_policy_step_supported(const dgppo_policy_step_args* p) {
   if (!p) return 0;
   if (p->n_agents < 1 || p->n_agents > dgppo::kRowsG || p->C < 1 || p->C > dgppo::kCP || p->D0 < 1 ||
-      p->D0 > dgppo::kMaxD0 || p->A < 1 || p->A > 4 || (p->A & (p->A - 1)) != 0 || p->H != dgppo::kHeads)
+      p->D0 > dgppo::kMaxD0 || p->A < 1 || p->A > 4 || p->H != dgppo::kHeads || p->ED < 4 ||
+      p->ED > 4 + dgppo::kMaxEX)
     return 0;
+  for (int l = 0; l < p->n_layers && l < 2; ++l)
+    if (p->ED > 4 && !p->layer[l].Wex) return 0;
   if (p->n_layers == 2)
     return p->layer[0].D == p->D0 && p->layer[0].F == 32 && p->layer[1].D == 32 && p->layer[1].F == 64;
   if (p->n_layers == 1) return p->layer[0].D == p->D0 && p->layer[0].F == 64;
@@ -709,12 +751,19 @@ extern "C" int dgppo_policy_step(const dgppo_policy_step_args* p, void* stream) 
       !p->h_in || !p->h_out || !p->action || (p->mode == 1 && !p->noise) || !p->work || p->G < 0)
     return DGPPO_EINVAL;
   if (p->G == 0) return 0;
-  dgppo::allow_lds((const void*)dgppo::policy_step_kernel);
   const int gpg = dgppo::kRowsG / p->n_agents;
   const int64_t ngroups = (p->G + gpg - 1) / gpg;
   if (ngroups > INT32_MAX) return DGPPO_EINVAL;
   const int64_t grid = ngroups;
-  hipLaunchKernelGGL(dgppo::policy_step_kernel, dim3((unsigned)grid), dim3(dgppo::kThreads), dgppo::lds_bytes(),
-                     (hipStream_t)stream, *p);
+  const bool wide = p->D0 > dgppo::kNarrowD0 || p->ED > 4;
+  const void* fn = wide ? (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX>
+                        : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0>;
+  dgppo::allow_lds(fn);
+  if (wide)
+    hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX>), dim3((unsigned)grid),
+                       dim3(dgppo::kThreads), dgppo::lds_bytes(), (hipStream_t)stream, *p);
+  else
+    hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0>), dim3((unsigned)grid), dim3(dgppo::kThreads),
+                       dgppo::lds_bytes(), (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }

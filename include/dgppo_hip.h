@@ -355,13 +355,15 @@ int dgppo_gru_seq_bwd(const dgppo_gru_seq_args* args, void* stream);
 typedef struct dgppo_gt_layer {
   const float *Wq, *bq, *Wkt, *bk, *Wcat, *Wu, *bu;
   int32_t D, F;
+  const float* Wex; /* (H (ED - 4), F) weights of the edge columns past 4 (LidarOmniTarget), NULL for ED == 4 */
 } dgppo_gt_layer;
 
 typedef struct dgppo_policy_step_args {
   int32_t G, N, E, n_agents, C, D0, A, n_layers, H, mode;
+  int32_t ED, pad_;    /* edge feature width: 4, or up to 10 (LidarOmniTarget) with layer[].Wex */
   const int32_t* cand;
-  const float* nodes; int64_t nodes_gstride;   /* (G, N, D0) */
-  const float* edges; int64_t edges_gstride;   /* (G, E, 4) */
+  const float* nodes; int64_t nodes_gstride;   /* (G, N, D0), D0 <= 12 */
+  const float* edges; int64_t edges_gstride;   /* (G, E, ED) */
   const int32_t* receivers;
   const int32_t* senders; int64_t idx_gstride; /* (G, E) */
   dgppo_gt_layer layer[2];

@@ -132,7 +132,7 @@ def test_env_rollout_lanes_bit_exact(cuda, graph):
 def test_policy_rollout_lanes_bit_exact(cuda, env_id, graph):
     """Policy rollouts (sample and det) stepped as 2 env slices on 2 streams write the same actions,
     log_pi, carries and graphs as one stream, bit for bit, replayed from a hipGraph and eager
-    (LidarOmniTarget: no fused policy step, the engine keeps one stream)."""
+    (LidarOmniTarget through the wide instantiation of the fused policy step: 10-wide nodes / edges, 3 actions)."""
     env = make_env(env_id, 8, num_obs=3, device=cuda)
     B, T = 64, 6
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
@@ -142,7 +142,7 @@ def test_policy_rollout_lanes_bit_exact(cuda, env_id, graph):
         for lanes in (1, 2):
             eng = RolloutEngine(env, B, T, cuda, env_offset=0, actor=algo.actor, mode=mode, lanes=lanes)
             if lanes == 2:
-                assert eng.lanes == (2 if env_id == "LidarSpread" else 1)
+                assert eng.lanes == 2
             if graph:
                 eng.capture()
             eng.run(key=11)
