@@ -193,15 +193,18 @@ def read_pmc_traffic(fn="env_step_pmc.json"):
 def read_mfma_pmc():
     """Executed-MFMA utilisation from the committed PMC profile (scripts/mfma_pmc.sh): SQ_INSTS_VALU_MFMA_MOPS_F32
     x 512 per kernel family over one collect + update, against the fp32 MFMA peak."""
-    fn = os.path.join(ROOT, "profiles", "r01_mfma_util.json")
-    if not os.path.exists(fn):
+    import glob
+
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_util.json")))  # the latest round's profile
+    if not found:
         return None
+    fn = found[-1]
     try:
         d = json.load(open(fn))
         fam = d["families"]
         gemm_t = sum(fam[k]["time_ms"] for k in ("gemm_rows", "gemm_wgrad") if k in fam)
         gemm_f = sum(fam[k]["mfma_tflop"] for k in ("gemm_rows", "gemm_wgrad") if k in fam)
-        return {"source": "profiles/r01_mfma_util.json (rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32)",
+        return {"source": f"profiles/{os.path.basename(fn)} (rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32)",
                 "gnn_gemm_executed_tflops": round(gemm_f / gemm_t * 1e3, 2),
                 "gnn_gemm_frac_of_peak": round(gemm_f / gemm_t * 1e3 / FP32_MFMA_PEAK_TFLOPS, 4),
                 "window_executed_tflops": d["total_mfma_tflops_over_window"],
