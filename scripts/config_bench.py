@@ -1,7 +1,9 @@
 """Per-GPU throughput of every BASELINE.json config on one MI355X (the bench line covers configs[2]).
 
 For each config: the env-step kernel (average launch time from HIP events around 64 back-to-back
-launches captured in a hipGraph, ping-ponging two graph buffers) and, unless --no-ppo, one DGPPO
+launches captured in a hipGraph, ping-ponging two graph buffers), one env-only episode (reset + T = 128
+steps through RolloutEngine, captured: the persistent rollout kernel where the library has it for the
+config, else the step kernel looped inside the call) and, unless --no-ppo, one DGPPO
 collect + update at batch 16384 / rnn_step 16 (second call timed; the first captures graphs and grows
 workspaces).  Multi-GPU configs are measured at their per-GPU share (env-sharded, weak scaling).
 Random-init networks, synthetic resets and uniform random actions."""
@@ -16,6 +18,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dgppo_fov_amd.algo import make_algo  # noqa: E402
 from dgppo_fov_amd.env import make_env  # noqa: E402
+from dgppo_fov_amd.trainer.rollout import RolloutEngine  # noqa: E402
 
 # (label, env, n, obs, envs per GPU)
 CONFIGS = [
@@ -24,6 +27,12 @@ CONFIGS = [
     ("LidarBicycleTarget n8 o3 x4096/GPU (8-GPU config)", "LidarBicycleTarget", 8, 3, 4096),
     ("LidarSpread n32 o8 x1024/GPU (8192 envs over 8 GPUs)", "LidarSpread", 32, 8, 1024),
     ("LidarOmniTarget n8 o3 x4096", "LidarOmniTarget", 8, 3, 4096),
+    # env variants (no BASELINE config names them): same per-GPU shapes as their base envs
+    ("LidarLine n6 o3 x4096 (variant; n = 8 does not fit the landmarks in the default area)", "LidarLine", 6, 3, 4096),
+    ("MPELine n3 o3 x1024 (variant)", "MPELine", 3, 3, 1024),
+    ("MPEFormation n3 o3 x1024 (variant)", "MPEFormation", 3, 3, 1024),
+    ("MPECorridor n3 x1024 (variant, 2 fixed obstacles)", "MPECorridor", 3, 2, 1024),
+    ("MPEConnectSpread n3 x1024 (variant, 1 fixed obstacle)", "MPEConnectSpread", 3, 1, 1024),
 ]
 
 
@@ -57,6 +66,24 @@ def step_us(env, B, dev, m=64):
     return sorted(ts)[len(ts) // 2]
 
 
+def episode_ms(env, B, dev, T=128, reps=10):
+    eng = RolloutEngine(env, B, T, dev, lanes=1)
+    eng.actions.uniform_(-1.0, 1.0)
+    eng.capture()
+    for w in range(3):
+        eng.run(key=w)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for k in range(reps):
+        e0.record()
+        eng.run(key=100 + k)
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return sorted(ts)[len(ts) // 2]
+
+
 def ppo_ms(env, B, dev):
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
                      action_dim=env.action_dim, n_agents=env.num_agents, batch_size=16384, rnn_step=16, seed=0,
@@ -77,13 +104,18 @@ def ppo_ms(env, B, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-ppo", action="store_true")
+    ap.add_argument("--only", default="", help="run only the configs whose label contains this string")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     for label, eid, n, obs, B in CONFIGS:
+        if args.only not in label:
+            continue
         env = make_env(eid, n, num_obs=obs, max_step=128, device=dev)
         us = step_us(env, B, dev)
         row = {"config": label, "env": eid, "n": n, "n_obs": obs, "envs_per_gpu": B, "env_step_us": round(us, 2),
                "env_steps_per_s": round(B / us * 1e6, 1)}
+        ep = episode_ms(env, B, dev)
+        row.update({"episode_ms": round(ep, 3), "episode_env_steps_per_s": round(B * 128 / ep * 1e3, 1)})
         if not args.no_ppo:
             c, u = ppo_ms(env, B, dev)
             row.update({"collect_ms": round(c, 2), "update_ms": round(u, 2),
