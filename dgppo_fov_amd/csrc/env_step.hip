@@ -889,28 +889,18 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   float* eo = io.edges + env * io.edges_stride;
   int32_t* ro = io.receivers + env * io.edge_index_stride;
   int32_t* sno = io.senders + env * io.edge_index_stride;
-  const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
+  // edge rows as vector stores: the launchers send only 16-byte (4-wide) / 8-byte (10-wide) aligned edge
+  // buffers here (wave_edges_aligned); a runtime fallback branch would let the compiler merge both
+  // paths into 4-byte stores
   auto put = [&](int e, float f0, float f1, float f2, float f3, int rv, int sv) {
-    if (vec4) {
-      reinterpret_cast<float4*>(eo)[e] = make_float4(f0, f1, f2, f3);
-    } else {
-      eo[4 * e + 0] = f0;
-      eo[4 * e + 1] = f1;
-      eo[4 * e + 2] = f2;
-      eo[4 * e + 3] = f3;
-    }
+    reinterpret_cast<float4*>(eo)[e] = make_float4(f0, f1, f2, f3);
     ro[e] = rv;
     sno[e] = sv;
   };
-  const bool vec2 = ((io.edges_stride & 1) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 7) == 0);
   auto put_wide = [&](int e, const float (&f)[kOmniED], int rv, int sv) {
-    if (vec2) {
+    float2* row = reinterpret_cast<float2*>(eo + kOmniED * e);
 #pragma unroll
-      for (int q = 0; q < kOmniED / 2; ++q) reinterpret_cast<float2*>(eo + kOmniED * e)[q] = make_float2(f[2 * q], f[2 * q + 1]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < kOmniED; ++c) eo[kOmniED * e + c] = f[c];
-    }
+    for (int q = 0; q < kOmniED / 2; ++q) row[q] = make_float2(f[2 * q], f[2 * q + 1]);
     ro[e] = rv;
     sno[e] = sv;
   };
@@ -2408,6 +2398,8 @@ extern "C" int dgppo_env_set_step_kernel(int mode) {
   return prev;
 }
 
+static bool wave_edges_aligned(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges);
+
 extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
   if (io->n_env == 0) return 0;
@@ -2428,7 +2420,8 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
     return (int)hipGetLastError();
   }
   const bool wave_shape = lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK &&
-                          cfg->n_obs == 3 && wave_step_enabled();
+                          cfg->n_obs == 3 && wave_step_enabled() &&
+                          wave_edges_aligned(cfg, io->edges, io->edges_stride, 0);
   if (cfg->engine == DGPPO_ENGINE_OMNI && wave_shape) {
     const size_t sh = 4 * sizeof(float) * wv::Carve<kOmniSD, 3>::total;
     hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD, 3>),
@@ -2464,15 +2457,50 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
   return (int)hipGetLastError();
 }
 
-static bool wave_config(const dgppo_env_cfg* cfg) {
+// the wave kernels store edge rows as float4 (4-wide) / float2 (LidarOmniTarget's 10-wide): the edge buffer,
+// its per-env stride and (rollouts) its per-step stride must keep that alignment, else the generic kernels run
+static bool wave_edges_aligned(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges) {
+  const int64_t q = cfg->engine == DGPPO_ENGINE_OMNI ? 2 : 4;
+  return (reinterpret_cast<uintptr_t>(edges) % (uintptr_t)(4 * q)) == 0 && edges_stride % q == 0 && t_edges % q == 0;
+}
+
+static bool wave_config(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges) {
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
-  return lidar && cfg->variant == DGPPO_VARIANT_NONE && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK && cfg->n_obs == 3 &&
-         wave_step_enabled();
+  return lidar && cfg->variant == DGPPO_VARIANT_NONE && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR &&
+         cfg->top_k == wv::NK && cfg->n_obs == 3 && wave_step_enabled() &&
+         wave_edges_aligned(cfg, edges, edges_stride, t_edges);
+}
+
+// the initial graph of sampled agent / goal rows and obstacles: the wave step kernel in REBUILD mode, in place
+static void launch_rebuild(const dgppo_env_cfg* cfg, const dgppo_env_step_io& st, hipStream_t s) {
+  const dim3 grid((unsigned)((st.n_env + 3) / 4)), block(256);
+  const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
+  if (cfg->engine == DGPPO_ENGINE_OMNI) {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<kOmniSD, 3>::total;
+    hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD, 3, true>), grid, block,
+                       sh, s, *cfg, st);
+  } else if (cfg->engine == DGPPO_ENGINE_BICYCLE) {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<5, 3>::total;
+    if (spread)
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+    else
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+  } else {
+    const size_t sh = 4 * sizeof(float) * wv::Carve<4, 3>::total;
+    if (spread)
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+    else
+      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4, 3, true>), grid, block,
+                         sh, s, *cfg, st);
+  }
 }
 
 extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
-  if (!wave_config(cfg)) return dgppo_env_reset(cfg, io, stream);
+  if (!wave_config(cfg, io->edges, io->edges_stride, 0)) return dgppo_env_reset(cfg, io, stream);
   if (io->n_env == 0) return 0;
   if (!io->out_states || !io->obstacles) return DGPPO_EINVAL;
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k, true);
@@ -2499,7 +2527,7 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io.obstacles || !io.ray_dirs)) return DGPPO_EINVAL;
   const hipStream_t s = (hipStream_t)stream;
-  if (wave_config(cfg)) {
+  if (wave_config(cfg, io.edges, io.edges_stride, r->t_edges)) {
     const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
     if (cfg->engine == DGPPO_ENGINE_OMNI) launch_rollout<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD>(*cfg, *r, s);
     else if (cfg->engine == DGPPO_ENGINE_BICYCLE && spread) launch_rollout<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(*cfg, *r, s);
@@ -2508,7 +2536,9 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
     else launch_rollout<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(*cfg, *r, s);
     return (int)hipGetLastError();
   }
-  // other configs: the per-step kernel T times (a rebuild_first request got a full reset already)
+  // other configs: the per-step kernel T times.  rebuild_first: a states-only reset (dgppo_env_reset_states)
+  // left graph 0 unbuilt when the wave kernels took it (a misaligned per-step stride sends the rollout here)
+  if (r->rebuild_first && wave_config(cfg, io.edges, io.edges_stride, 0)) launch_rebuild(cfg, io, s);
   for (int t = 0; t < r->T; ++t) {
     dgppo_env_step_io q = io;
     q.states = io.out_states + t * r->t_states;
@@ -2547,7 +2577,7 @@ extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_i
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                  cfg->engine != DGPPO_ENGINE_MPE);
   const size_t shmem = ((size_t)cv.total + 2 * kSampTab) * sizeof(float);  // + the sampler's candidate table
-  const bool wave = wave_config(cfg);
+  const bool wave = wave_config(cfg, io->edges, io->edges_stride, 0);
   if (!wave) {
     dispatch_reset(*cfg, *io, shmem, s, 0);
     return (int)hipGetLastError();
@@ -2573,28 +2603,6 @@ extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_i
   st.senders = io->senders;
   st.edge_index_stride = io->edge_index_stride;
   st.n_env = io->n_env;
-  const dim3 grid((unsigned)((io->n_env + 3) / 4)), block(256);
-  const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
-  if (cfg->engine == DGPPO_ENGINE_OMNI) {
-    const size_t sh = 4 * sizeof(float) * wv::Carve<kOmniSD, 3>::total;
-    hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD, 3, true>), grid, block,
-                       sh, s, *cfg, st);
-  } else if (cfg->engine == DGPPO_ENGINE_BICYCLE) {
-    const size_t sh = 4 * sizeof(float) * wv::Carve<5, 3>::total;
-    if (spread)
-      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5, 3, true>), grid, block,
-                         sh, s, *cfg, st);
-    else
-      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5, 3, true>), grid, block,
-                         sh, s, *cfg, st);
-  } else {
-    const size_t sh = 4 * sizeof(float) * wv::Carve<4, 3>::total;
-    if (spread)
-      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4, 3, true>), grid, block,
-                         sh, s, *cfg, st);
-    else
-      hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4, 3, true>), grid, block,
-                         sh, s, *cfg, st);
-  }
+  launch_rebuild(cfg, st, s);
   return (int)hipGetLastError();
 }

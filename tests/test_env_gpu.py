@@ -164,6 +164,43 @@ def test_step_writes_into_strided_rollout_buffer(cuda):
         ref_g = ref.graph
 
 
+@pytest.mark.parametrize("eid", ["LidarSpread", "LidarOmniTarget"])
+def test_misaligned_edge_buffers_take_the_generic_kernels(cuda, eid):
+    """The wave-per-env kernels store edge rows as float4 / float2; an edge buffer that is only 4-byte
+    aligned must be routed to the workgroup-per-env kernels, with the same results (reset and step)."""
+    n, obs, B = 8, 3, 12
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    spec = O.Spec(eid, n, obs)
+
+    g_ref = env.reset(key=77, n_env=B)
+    ob = torch.empty_like(g_ref.env_states.obstacle.packed)
+
+    def misaligned_graph():
+        g = env.empty_graph((B,), cuda)
+        raw = torch.empty(g.edges.numel() + 1, device=cuda)
+        edges = raw[1:].view(g.edges.shape)
+        assert edges.data_ptr() % 8 == 4
+        return env._assemble(g.nodes, edges, g.states, g.receivers, g.senders, ob)
+
+    out0 = misaligned_graph()
+    g_mis = env.reset(key=77, n_env=B, out=out0, obstacles_out=ob)
+    torch.cuda.synchronize()
+    for f in ("nodes", "edges", "states", "receivers", "senders"):
+        assert torch.equal(getattr(g_mis, f), getattr(g_ref, f)), ("reset", f)
+    a = torch.rand(B, n, spec.ad, device=cuda) * 2 - 1
+    res_ref = env.step(g_ref, a)
+    out1 = misaligned_graph()
+    rew = torch.empty(B, device=cuda)
+    cost = torch.empty(B, n, env.n_cost, device=cuda)
+    g1 = env.step_into(g_mis, a, out1, rew, cost)
+    ref = O.env_step(spec, _np(g_ref.states), _np(g_ref.env_states.obstacle.packed), _np(a))
+    torch.cuda.synchronize()
+    assert_graph_equal(g1, ref, "misaligned step")
+    for f in ("nodes", "edges", "states", "receivers", "senders"):
+        assert torch.equal(getattr(g1, f), getattr(res_ref.graph, f)), ("step", f)
+    assert torch.equal(rew, res_ref.reward) and torch.equal(cost, res_ref.cost)
+
+
 def test_golden_fixtures_on_gpu(cuda):
     import glob
     import os
