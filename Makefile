@@ -21,7 +21,25 @@ $(OUT)/libdgppo_hip.so: $(OBJS)
 	@mkdir -p $(OUT)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
 
+# diagnostic library with the persistent rollout's phase timers (scripts/env_stamps.py; DGPPO_HIP_LIB points at it)
+STAMP_OBJS := $(filter-out $(OBJ)/env_step.o,$(OBJS)) $(OBJ)/env_step_stamps.o
+$(OBJ)/env_step_stamps.o: $(CSRC)/env_step.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DDGPPO_ENV_STAMPS -c $< -o $@
+stamps: $(STAMP_OBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OUT)/libdgppo_hip_stamps.so $(STAMP_OBJS)
+
+# diagnostic library with every env-graph store dropped from the wave kernels (timing experiments only)
+NOSTORE_OBJS := $(filter-out $(OBJ)/env_step.o,$(OBJS)) $(OBJ)/env_step_nostore.o
+$(OBJ)/env_step_nostore.o: $(CSRC)/env_step.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DDGPPO_DIAG_NOSTORE -c $< -o $@
+nostore: $(NOSTORE_OBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OUT)/libdgppo_hip_nostore.so $(NOSTORE_OBJS)
+
 clean:
 	rm -rf $(OBJ) $(OUT)/libdgppo_hip.so
 
-.PHONY: all clean
+.PHONY: all clean stamps nostore

@@ -671,9 +671,91 @@ struct Carve {
 // obstacles and ray table from HBM (io.states / io.obstacles / io.ray_dirs); otherwise they are the
 // LDS state the previous call left (persistent rollout: next agent rows and next hits become current,
 // obstacles and rays stay staged), and only the action comes from HBM.
+// Phase timers of the persistent rollout (diagnostic builds only: -DDGPPO_ENV_STAMPS, `make stamps`):
+// s_memtime deltas per phase summed over the steps of each wave, added into g_env_stamps at the end.
+#ifdef DGPPO_ENV_STAMPS
+struct EnvStamps {
+  uint64_t last, acc[16];
+};
+__device__ unsigned long long g_env_stamps[16];
+#define ENV_STAMP(k)                                             \
+  do {                                                           \
+    if (stamps) {                                                \
+      const uint64_t now_ = __builtin_amdgcn_s_memtime();        \
+      stamps->acc[k] += now_ - stamps->last;                     \
+      stamps->last = now_;                                       \
+    }                                                            \
+  } while (0)
+#else
+struct EnvStamps {};
+#define ENV_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
+// Culling data that depends only on the obstacles and the ray table (constant over an episode): the
+// persistent rollout computes it once, the per-step kernel every call.  Lane l: ray rr = l & 31.
+template <int O>
+struct WaveConst {
+  float rdx, rdy, rlen2, rlen, rho_l;  // ray rr, |ray|^2, |ray| bound, circumradius bound of obstacle l (< O)
+  uint64_t elig_mask;                  // obstacles eligible for culling
+  uint32_t unsafe[O];                  // rays whose determinant against an edge of obstacle o is near 0
+};
+
+template <int O>
+__device__ __forceinline__ WaveConst<O> wave_const(const float* obst, const float* evec, const float* rays, int lane) {
+  WaveConst<O> k;
+  const int rr = lane & 31;
+  k.rdx = rays[2 * rr], k.rdy = rays[2 * rr + 1];
+  k.rlen2 = k.rdx * k.rdx + k.rdy * k.rdy;
+  // obstacle o = lane (< O): circumradius (raw v_sqrt: the culling bounds carry margins) and eligibility
+  {
+    const int o = lane < O ? lane : 0;
+    const float4* rec4 = reinterpret_cast<const float4*>(obst + o * DGPPO_OBST_FIELDS);
+    const float4 c4 = rec4[0], pA = rec4[2], pB = rec4[3];
+    const float pxs[4] = {pA.x, pA.z, pB.x, pB.z}, pys[4] = {pA.y, pA.w, pB.y, pB.w};
+    float r2 = 0.0f;
+    bool elig = (fabsf(c4.x) <= 2.0f) & (fabsf(c4.y) <= 2.0f);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      elig = elig & (fabsf(pxs[p]) <= 2.0f) & (fabsf(pys[p]) <= 2.0f);
+      const float dx = pxs[p] - c4.x, dy = pys[p] - c4.y;
+      r2 = fmaxf(r2, dx * dx + dy * dy);
+    }
+    k.rho_l = __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-6f;
+    elig = elig & (k.rho_l <= 0.5f);
+    k.elig_mask = __ballot(elig & (lane < O));
+  }
+  k.rlen = __builtin_amdgcn_sqrtf(k.rlen2) * 1.0001f;
+#pragma unroll
+  for (int pass = 0; pass < (O + 1) / 2; ++pass) {  // (obstacle 2 pass + half, ray lane & 31)
+    const int o = 2 * pass + (lane >> 5) < O ? 2 * pass + (lane >> 5) : 0;
+    const float4* e4 = reinterpret_cast<const float4*>(evec + o * 8);
+    const float4 eA = e4[0], eB = e4[1];
+    const float exs[4] = {eA.x, eA.z, eB.x, eB.z}, eys[4] = {eA.y, eA.w, eB.y, eB.w};
+    bool safe = (((k.elig_mask >> o) & 1ull) != 0ull) & (k.rlen <= 1.0f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) safe = safe & (fabsf(k.rdy * exs[e] - k.rdx * eys[e]) >= kDetMin);
+    const uint64_t b = __ballot(!safe);
+    k.unsafe[2 * pass] = (uint32_t)b;
+    if (2 * pass + 1 < O) k.unsafe[2 * pass + 1] = (uint32_t)(b >> 32);
+  }
+  return k;
+}
+
+// raw (unclamped) action components of lane gj of this wave's env: (a0, a1, the omni alpha or 0)
+template <int AD>
+__device__ __forceinline__ float3 wave_action(const dgppo_env_step_io& io, int64_t env, int gj) {
+  const float* ac = io.action + env * io.action_stride;
+  return make_float3(ac[AD * gj + 0], ac[AD * gj + 1], AD == 3 ? ac[AD * gj + AD - 1] : 0.0f);
+}
+
+// (pre: LOAD = false only — this step's raw actions, loaded by the caller one step ahead)
 template <int ENGINE, int GOAL, int SD, int O, bool REBUILD, bool LOAD>
 __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_env_step_io& io, float* smem,
-                                          int* wg_items) {
+                                          int* wg_items, float3 pre = make_float3(0.0f, 0.0f, 0.0f),
+                                          EnvStamps* stamps = nullptr, const WaveConst<O>* pc = nullptr) {
+  (void)stamps;
   static_assert(O >= 1 && O <= 4, "obstacle records are staged by one load per lane");
   // LidarOmniTarget (SD 7, own goals): omni dynamics, 5 costs, 10-wide edges; same LiDAR and graph rows
   constexpr bool OMNI = ENGINE == DGPPO_ENGINE_OMNI;
@@ -695,13 +777,18 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   // the two workgroup barriers around the pooled ray cast
   const bool live = env_raw < io.n_env;
   const int64_t env = live ? env_raw : io.n_env - 1;
+#ifdef DGPPO_DIAG_NOSTORE
+  const bool st_live = false;  // diagnostic build: every graph / reward / cost store dropped
+#else
+  const bool st_live = live;
+#endif
   float* lds = smem + wid * C::total;
   const int gi = lane >> 3, gj = lane & 7;
 
   // ---- A: every global load first (unconditional, clamped addresses), then stage in LDS -------
-  const float* ac = io.action + env * io.action_stride;
-  const float a0 = clampf_nan(ac[AD * gj + 0], -1.0f, 1.0f), a1 = clampf_nan(ac[AD * gj + 1], -1.0f, 1.0f);
-  const float aw = OMNI ? clampf_nan(ac[AD * gj + AD - 1], -1000.0f, 1000.0f) : 0.0f;  // omni alpha
+  const float3 araw = LOAD ? wave_action<AD>(io, env, gj) : pre;
+  const float a0 = clampf_nan(araw.x, -1.0f, 1.0f), a1 = clampf_nan(araw.y, -1.0f, 1.0f);
+  const float aw = OMNI ? clampf_nan(araw.z, -1000.0f, 1000.0f) : 0.0f;  // omni alpha
   float hcx, hcy;
   if constexpr (LOAD) {
     const float* st = io.states + env * io.states_stride;
@@ -736,6 +823,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   const float* evec = lds + C::evec;
   const float* rays = lds + C::rays;
 
+  ENV_STAMP(0);
   // ---- B: dynamics of agent j (every lane; lanes 0..7 store it), distances, edge vectors -------
   float x[SD];
 #pragma unroll
@@ -790,7 +878,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
 #pragma unroll
     for (int c = 0; c < SD; ++c) nxt[lane * SD + c] = y[c];
   }
-  if (lane < O * 8) lds[C::evec + lane] = ev;
+  if (!pc && lane < O * 8) lds[C::evec + lane] = ev;  // (persistent: staged once with the constants)
   const float an = norm2(a0, a1);
   const float a2 = an * an;
   float daa = norm2(cix - x[0], ciy - x[1]);
@@ -814,6 +902,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   }
   const float md = min8(daa), dg = min8(dga), mo = min8(dh);
 
+  ENV_STAMP(1);
   // ---- C: cost (lanes j < 2 of group i, 5 for omni), reward (lane 0) -------------------------
   if constexpr (OMNI) {
     float cq[kOmniNC];
@@ -834,7 +923,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     float v = q == 0 ? cq[0] : (q == 1 ? cq[1] : (q == 2 ? cq[2] : (q == 3 ? cq[3] : cq[4])));
     v = v <= 0.0f ? v - 0.1f : v + 0.1f;
     v = clampf_nan(v, -1.0f, 1.0f);
-    if (!REBUILD && live & (gj < kOmniNC)) io.cost[env * io.cost_stride + kOmniNC * gi + gj] = v;
+    if (!REBUILD && st_live & (gj < kOmniNC)) io.cost[env * io.cost_stride + kOmniNC * gi + gj] = v;
     const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
     const float w2 = aw * aw, o2 = x[6] * x[6];
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f, s4 = 0.0f;
@@ -846,7 +935,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       s3 = s3 + rlf(w2, i);
       s4 = s4 + rlf(o2, i);
     }
-    if (!REBUILD && live & (lane == 0)) {  // get_reward (lidar_omni_target.py:295-336)
+    if (!REBUILD && st_live & (lane == 0)) {  // get_reward (lidar_omni_target.py:295-336)
       const float nn = (float)NA;
       float r = 0.0f - (s0 / nn) * 0.01f;
       r = r - (s1 / nn) * 0.001f;
@@ -862,7 +951,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     c1 = c1 <= 0.0f ? c1 - 0.5f : c1 + 0.5f;
     c0 = clampf_nan(c0, -1.0f, 1.0f);
     c1 = clampf_nan(c1, -1.0f, 1.0f);
-    if (!REBUILD && live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = gj == 0 ? c0 : c1;
+    if (!REBUILD && st_live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = gj == 0 ? c0 : c1;
     const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
     float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
 #pragma unroll
@@ -871,7 +960,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       sf = sf + rlf(far, 8 * i);
       sa = sa + rlf(a2, i);  // lane i holds agent j = i
     }
-    if (!REBUILD && live & (lane == 0)) {
+    if (!REBUILD && st_live & (lane == 0)) {
       const float nn = (float)NA;
       float r = 0.0f - (sd_ / nn) * 0.01f;
       r = r - (sf / nn) * 0.001f;
@@ -881,6 +970,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   }
   wave_sync();  // nxt, evec visible
 
+  ENV_STAMP(2);
   // ---- F1: the graph parts that do not depend on the lidar, issued as store packets spread over
   // the compute phases below so the HBM drains them while the ray cast runs (one burst would stall
   // every wave on a full store queue at once)
@@ -907,7 +997,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   float si[SD];
 #pragma unroll
   for (int c = 0; c < SD; ++c) si[c] = nxt[gi * SD + c];
-  if (live) {  // store packet 1: agent-agent edges
+  if (st_live) {  // store packet 1: agent-agent edges
     float sj[SD];
 #pragma unroll
     for (int c = 0; c < SD; ++c) sj[c] = y[c];  // this lane's dynamics result is agent j's next state
@@ -940,50 +1030,20 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     }
   }
 
+  ENV_STAMP(3);
   // ---- D: is-inside at the next state; culling masks; capsule tests -> item list -------------
   const float sxi = si[0], syi = si[1];
   const int oi = gj < O ? gj : 0;
   const bool in_o = (gj < O) & rect_inside0(obst + oi * DGPPO_OBST_FIELDS, sxi, syi);
   const uint64_t in_mask = __ballot(in_o);
   const int rr = lane & 31;
-  const float rdx = rays[2 * rr], rdy = rays[2 * rr + 1];
-  const float rlen2 = rdx * rdx + rdy * rdy;
-  // obstacle o = lane (< O): circumradius (raw v_sqrt: the culling bounds carry margins) and eligibility
-  float rho_l;
-  uint64_t elig_mask;
-  {
-    const int o = lane < O ? lane : 0;
-    const float4* rec4 = reinterpret_cast<const float4*>(obst + o * DGPPO_OBST_FIELDS);
-    const float4 c4 = rec4[0], pA = rec4[2], pB = rec4[3];
-    const float pxs[4] = {pA.x, pA.z, pB.x, pB.z}, pys[4] = {pA.y, pA.w, pB.y, pB.w};
-    float r2 = 0.0f;
-    bool elig = (fabsf(c4.x) <= 2.0f) & (fabsf(c4.y) <= 2.0f);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      elig = elig & (fabsf(pxs[p]) <= 2.0f) & (fabsf(pys[p]) <= 2.0f);
-      const float dx = pxs[p] - c4.x, dy = pys[p] - c4.y;
-      r2 = fmaxf(r2, dx * dx + dy * dy);
-    }
-    rho_l = __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-6f;
-    elig = elig & (rho_l <= 0.5f);
-    elig_mask = __ballot(elig & (lane < O));
-  }
-  const float rlen = __builtin_amdgcn_sqrtf(rlen2) * 1.0001f;
+  const WaveConst<O> kc = pc ? *pc : wave_const<O>(obst, evec, rays, lane);
+  const float rdx = kc.rdx, rdy = kc.rdy, rlen2 = kc.rlen2, rlen = kc.rlen, rho_l = kc.rho_l;
   uint32_t unsafe[O];
 #pragma unroll
-  for (int pass = 0; pass < (O + 1) / 2; ++pass) {  // (obstacle 2 pass + half, ray lane & 31)
-    const int o = 2 * pass + (lane >> 5) < O ? 2 * pass + (lane >> 5) : 0;
-    const float4* e4 = reinterpret_cast<const float4*>(evec + o * 8);
-    const float4 eA = e4[0], eB = e4[1];
-    const float exs[4] = {eA.x, eA.z, eB.x, eB.z}, eys[4] = {eA.y, eA.w, eB.y, eB.w};
-    bool safe = (((elig_mask >> o) & 1ull) != 0ull) & (rlen <= 1.0f);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) safe = safe & (fabsf(rdy * exs[e] - rdx * eys[e]) >= kDetMin);
-    const uint64_t b = __ballot(!safe);
-    unsafe[2 * pass] = (uint32_t)b;
-    if (2 * pass + 1 < O) unsafe[2 * pass + 1] = (uint32_t)(b >> 32);
-  }
-  if (live) {  // store packet 2: agent-goal edges
+  for (int o = 0; o < O; ++o) unsafe[o] = kc.unsafe[o];
+  ENV_STAMP(4);
+  if (st_live) {  // store packet 2: agent-goal edges
     float sj[SD], sg[SD];
 #pragma unroll
     for (int c = 0; c < SD; ++c) {
@@ -1017,6 +1077,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       put(NA * NA + lane, sj[0] - sg[0], sj[1] - sg[1], f2, f3, lane, NA + lane);
     }
   }
+  ENV_STAMP(5);
   // capsule test of every (agent, obstacle, ray) triple: pair p = o * 8 + i, 2 pairs per step (lane
   // halves), o and i = 2 m + half known per step; survivors -> compacted item list
   int n_items = 0;
@@ -1049,7 +1110,8 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       }
     }
   }
-  if (live) {  // store packet 3: node / state rows of agents and goals, pad rows
+  ENV_STAMP(6);
+  if (st_live) {  // store packet 3: node / state rows of agents and goals, pad rows
     // node rows 0..15 (agents, goals) and the pad row; state rows 0..15 and the pad row
 #pragma unroll
     for (int k = 0; k < (16 * ND + 63) / 64; ++k) {
@@ -1075,7 +1137,9 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   uint32_t* alpha = reinterpret_cast<uint32_t*>(lds + C::alpha);
   reinterpret_cast<uint4*>(alpha)[lane] = make_uint4(kEncMiss, kEncMiss, kEncMiss, kEncMiss);
   if (lane == 0) wg_items[wid] = n_items;
+  ENV_STAMP(7);
   __syncthreads();  // item lists of the 4 envs of this workgroup are complete
+  ENV_STAMP(8);
 
   // exact ray cast of the surviving triples, pooled over the workgroup's 4 envs (balances the
   // per-env item counts; each item atomically min-combines into its own env's alpha row)
@@ -1104,17 +1168,10 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       if (act) atomicMin(reinterpret_cast<uint32_t*>(L + C::alpha) + i * NR + r, enc_alpha(a));
     }
   }
-  if (live) {  // store packet 4: constant columns of the hit rows and lidar edges
-    // hit row 16 + lane and agent-lidar edge row n*n + n_ag + lane: every column except the hit
-    // coordinates / edge offsets is a constant ([., ., 0.. | obs 1, goal 0, agent 0], [., ., 0, 0])
-#pragma unroll
-    for (int c = 2; c < ND; ++c) no[(16 + lane) * ND + c] = c == SD ? 1.0f : 0.0f;
-#pragma unroll
-    for (int c = 2; c < SD; ++c) so[(16 + lane) * SD + c] = 0.0f;
-#pragma unroll
-    for (int c = 2; c < ED; ++c) eo[ED * (NA * NA + n_ag + lane) + c] = 0.0f;
-  }
+  ENV_STAMP(9);
+  ENV_STAMP(10);
   __syncthreads();  // every alpha row is final
+  ENV_STAMP(11);
 
   // ---- E: sort keys; misses ranked by popcount, the rest by comparison; top-k hit points ------
   uint64_t* keys = reinterpret_cast<uint64_t*>(lds + C::uni);  // items are dead now
@@ -1161,6 +1218,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     }
   }
   wave_sync();
+  ENV_STAMP(12);
   for (int base = 0; base < n_other; base += 64) {
     const int t = base + lane;
     const int v = olist[t];  // past n_other: stale words (olist is followed by the key region)
@@ -1184,24 +1242,51 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     }
   }
   wave_sync();
+  ENV_STAMP(13);
 
-  // ---- F2: the lidar-dependent columns: hit coordinates, agent-lidar edge offsets and masks -------
-  if (live) {
+  // ---- F2: the hit rows and agent-lidar edges.  Node / state rows of the hits (and Omni's 10-wide edge
+  // rows) are assembled in LDS (olist, keys and items are dead now) and written lane-contiguous: a row per
+  // lane at a 28-40 byte stride would cost a memory request per lane and store instruction
+  {
     const float2 hl = reinterpret_cast<const float2*>(hits)[lane];
     const float f0 = si[0] - hl.x;
     const float f1 = si[1] - hl.y;
     // Lidar: norm < comm_radius - 0.1; omni: norm < comm_radius (lidar_omni_target.py:446-489); on |d|^2
     const bool m = f0 * f0 + f1 * f1 < (OMNI ? cfg.t2_comm : cfg.t2_lidar);
     const int e = NA * NA + n_ag + lane;
-    eo[ED * e + 0] = f0;
-    eo[ED * e + 1] = f1;
-    ro[e] = m ? gi : pad;
-    sno[e] = m ? 2 * NA + lane : pad;
-    no[(16 + lane) * ND + 0] = hl.x;
-    no[(16 + lane) * ND + 1] = hl.y;
-    so[(16 + lane) * SD + 0] = hl.x;
-    so[(16 + lane) * SD + 1] = hl.y;
+    static_assert(64 * (ND + SD) <= C::total - C::olist && 64 * ED <= C::total - C::olist, "F2 staging fits");
+    float* sn = lds + C::olist;  // (64, ND) hit node rows [x, y, 0.. | obstacle 1, goal 0, agent 0]
+    float* ss = sn + 64 * ND;    // (64, SD) hit state rows [x, y, 0..]
+#pragma unroll
+    for (int c = 0; c < ND; ++c) sn[lane * ND + c] = c == 0 ? hl.x : (c == 1 ? hl.y : (c == SD ? 1.0f : 0.0f));
+#pragma unroll
+    for (int c = 0; c < SD; ++c) ss[lane * SD + c] = c == 0 ? hl.x : (c == 1 ? hl.y : 0.0f);
+    wave_sync();
+    if (st_live) {
+      if constexpr (ED == 4) reinterpret_cast<float4*>(eo)[e] = make_float4(f0, f1, 0.0f, 0.0f);
+      ro[e] = m ? gi : pad;
+      sno[e] = m ? 2 * NA + lane : pad;
+      float* nd = no + 16 * ND;
+      float* sdst = so + 16 * SD;
+#pragma unroll
+      for (int k = 0; k < ND; ++k) nd[64 * k + lane] = sn[64 * k + lane];
+#pragma unroll
+      for (int k = 0; k < SD; ++k) sdst[64 * k + lane] = ss[64 * k + lane];
+    }
+    if constexpr (ED != 4) {
+      wave_sync();  // (in-order LDS: the reads above are done before these writes)
+      float* se = lds + C::olist;  // (64, ED) edge rows [f0, f1, 0..]
+#pragma unroll
+      for (int c = 0; c < ED; ++c) se[lane * ED + c] = c == 0 ? f0 : (c == 1 ? f1 : 0.0f);
+      wave_sync();
+      if (st_live) {
+        float* ed = eo + ED * (NA * NA + n_ag);
+#pragma unroll
+        for (int k = 0; k < ED; ++k) ed[64 * k + lane] = se[64 * k + lane];
+      }
+    }
   }
+  ENV_STAMP(14);
 }
 
 // One env step (REBUILD: the graph of the given states) for io.n_env envs, 4 per workgroup.
@@ -1211,6 +1296,8 @@ __global__ __launch_bounds__(256) void lidar_step_wave_kernel(dgppo_env_cfg cfg,
   __shared__ int wg_items[4];
   wave_body<ENGINE, GOAL, SD, O, REBUILD, true>(cfg, io, smem, wg_items);
 }
+
+constexpr int kRolloutActFloats = 16 * NA * 3;  // per wave: a 16-step action chunk (3 action floats max)
 
 // Persistent rollout: T env steps per launch, a wave per env for the whole episode (the reference's
 // lax.scan over env.step, trainer/utils.py:45-55, with the actions given).  Agent rows, hits,
@@ -1254,19 +1341,89 @@ __global__ __launch_bounds__(256) void lidar_rollout_wave_kernel(
     if (XS > 0) lds[C::cur + xsl] = cv1;
     wave_sync();
   }
+  // actions arrive in chunks of KC steps staged in LDS, the next chunk loaded into registers one chunk
+  // ahead: vmcnt counts stores too, so any wait on an action load also waits for the store drain before
+  // it — once per chunk instead of once per step
+  constexpr int AD = ENGINE == DGPPO_ENGINE_OMNI ? 3 : 2;
+  constexpr int APS = NA * AD, KC = 16, PER = KC * APS / 64;  // action floats per step / per lane and chunk
+  static_assert(PER * 64 == KC * APS, "chunk = whole lanes");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gj = lane & 7;
+  const int64_t env_raw = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t env = env_raw < g0.n_env ? env_raw : g0.n_env - 1;
+  float* acts = smem + 4 * wv::Carve<SD, O>::total + wid * (KC * APS);
+  auto load_chunk = [&](int t0, float (&v)[PER]) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = lane * PER + j, st = idx / APS, k = idx - st * APS;
+      const int ts = t0 + st < r.T ? t0 + st : r.T - 1;
+      v[j] = g0.action[ts * r.t_action + env * g0.action_stride + k];
+    }
+  };
+  float cv[PER];
+  if (r.T > 0) load_chunk(0, cv);
+  // episode constants of the culling: the obstacle edge vectors (staged in LDS once; the steps skip
+  // their rewrite) and the per-ray / per-obstacle bounds
+  WaveConst<O> kc;
+  {
+    using Cv = wv::Carve<SD, O>;
+    float* lw = smem + wid * Cv::total;
+    const int o = (lane >> 3) < O ? (lane >> 3) : 0, e = (lane >> 1) & 3, c = lane & 1;
+    const float* rec = lw + Cv::obst + o * DGPPO_OBST_FIELDS;
+    const float ev = rec[8 + 2 * ((e + 3) & 3) + c] - rec[8 + 2 * e + c];
+    wave_sync();
+    if (lane < O * 8) lw[Cv::evec + lane] = ev;
+    wave_sync();
+    kc = wave_const<O>(lw + Cv::obst, lw + Cv::evec, lw + Cv::rays, lane);
+  }
+#ifdef DGPPO_ENV_STAMPS
+  EnvStamps stv{};
+  EnvStamps* stamps = &stv;
+  stv.last = __builtin_amdgcn_s_memtime();
+#else
+  EnvStamps* stamps = nullptr;
+#endif
+  float* const nodes_e = g0.nodes + env * g0.nodes_stride;
+  float* const edges_e = g0.edges + env * g0.edges_stride;
+  float* const states_e = g0.out_states + env * g0.out_states_stride;
+  int32_t* const recv_e = g0.receivers + env * g0.edge_index_stride;
+  int32_t* const send_e = g0.senders + env * g0.edge_index_stride;
+  float* const reward_e = g0.reward + env * g0.reward_stride;
+  float* const cost_e = g0.cost + env * g0.cost_stride;
 #pragma clang loop unroll(disable)
   for (int t = 0; t < r.T; ++t) {
+    const int tc = t % KC;
+    if (tc == 0) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) acts[lane * PER + j] = cv[j];
+      wave_sync();
+      if (t + KC < r.T) load_chunk(t + KC, cv);
+    }
+    const float* ar = acts + tc * APS + AD * gj;
+    const float3 act = make_float3(ar[0], ar[1], AD == 3 ? ar[AD - 1] : 0.0f);
+    // this env's rows of step t: base pointers with the env offset folded in and zero env strides (constants
+    // after inlining), so the step does no 64-bit index arithmetic and keeps fewer values in SGPRs
     dgppo_env_step_io q = g0;
-    q.action = g0.action + t * r.t_action;
-    q.nodes = g0.nodes + (t + 1) * r.t_nodes;
-    q.edges = g0.edges + (t + 1) * r.t_edges;
-    q.out_states = g0.out_states + (t + 1) * r.t_states;
-    q.receivers = g0.receivers + (t + 1) * r.t_index;
-    q.senders = g0.senders + (t + 1) * r.t_index;
-    q.reward = g0.reward + t * r.t_reward;
-    q.cost = g0.cost + t * r.t_cost;
-    wave_body<ENGINE, GOAL, SD, O, false, false>(cfg, q, smem, wg_items);
+    q.nodes = nodes_e + (t + 1) * r.t_nodes;
+    q.nodes_stride = 0;
+    q.edges = edges_e + (t + 1) * r.t_edges;
+    q.edges_stride = 0;
+    q.out_states = states_e + (t + 1) * r.t_states;
+    q.out_states_stride = 0;
+    q.receivers = recv_e + (t + 1) * r.t_index;
+    q.senders = send_e + (t + 1) * r.t_index;
+    q.edge_index_stride = 0;
+    q.reward = reward_e + t * r.t_reward;
+    q.reward_stride = 0;
+    q.cost = cost_e + t * r.t_cost;
+    q.cost_stride = 0;
+    wave_body<ENGINE, GOAL, SD, O, false, false>(cfg, q, smem, wg_items, act, stamps, &kc);
   }
+#ifdef DGPPO_ENV_STAMPS
+  if (lane == 0 && env_raw < g0.n_env)
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_env_stamps[k], (unsigned long long)stv.acc[k]);
+#else
+  (void)stamps;
+#endif
 }
 
 }  // namespace wv
@@ -2511,10 +2668,22 @@ extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_
 
 template <int ENGINE, int GOAL, int SD>
 static void launch_rollout(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, hipStream_t s) {
-  const size_t sh = 4 * sizeof(float) * wv::Carve<SD, 3>::total;
+  const size_t sh = 4 * sizeof(float) * (wv::Carve<SD, 3>::total + wv::kRolloutActFloats);
   hipLaunchKernelGGL((wv::lidar_rollout_wave_kernel<ENGINE, GOAL, SD, 3>), dim3((unsigned)((r.step.n_env + 3) / 4)),
                      dim3(256), sh, s, c, r);
 }
+
+#ifdef DGPPO_ENV_STAMPS
+// diagnostic builds: the phase sums since the last call (16 x u64 s_memtime ticks, summed over waves), then zeroed
+extern "C" int dgppo_env_diag_stamps(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dgppo::wv::g_env_stamps), 16 * sizeof(unsigned long long));
+  if (e == hipSuccess) {
+    static const unsigned long long zero[16] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(dgppo::wv::g_env_stamps), zero, sizeof(zero));
+  }
+  return (int)e;
+}
+#endif
 
 extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollout_io* r, void* stream) {
   if (validate(cfg) || !r || r->T < 0 || r->step.n_env < 0) return DGPPO_EINVAL;
