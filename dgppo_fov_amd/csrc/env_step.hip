@@ -987,12 +987,22 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     ro[e] = rv;
     sno[e] = sv;
   };
-  auto put_wide = [&](int e, const float (&f)[kOmniED], int rv, int sv) {
-    float2* row = reinterpret_cast<float2*>(eo + kOmniED * e);
+  // Omni's 10-wide edge rows: assembled in LDS (olist / items are free until the capsule tests) and stored
+  // lane-contiguous by flush_wide; a 40-byte row per lane would cost a memory request per lane and store
+  float* const wstage = lds + C::olist;
+  static_assert(!OMNI || 64 * kOmniED <= C::total - C::olist, "wide edge staging fits");
+  auto put_wide = [&](int e, int slot, const float (&f)[kOmniED], int rv, int sv) {
 #pragma unroll
-    for (int q = 0; q < kOmniED / 2; ++q) row[q] = make_float2(f[2 * q], f[2 * q + 1]);
+    for (int c = 0; c < kOmniED; ++c) wstage[slot * kOmniED + c] = f[c];
     ro[e] = rv;
     sno[e] = sv;
+  };
+  auto flush_wide = [&](int e0, int rows) {  // every lane; rows e0 .. e0 + rows - 1 from slots 0 .. rows - 1
+    wave_sync();
+    float* dst = eo + kOmniED * e0;
+#pragma unroll
+    for (int k = 0; k < (64 * kOmniED + 63) / 64; ++k)
+      if (64 * k + lane < rows * kOmniED) dst[64 * k + lane] = wstage[64 * k + lane];
   };
   float si[SD];
 #pragma unroll
@@ -1023,7 +1033,8 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
         const float ly = (-si[3]) * gx + si[2] * gy;
         f[8] = norm2(lx, ly);
         f[9] = lx;
-        put_wide(lane, f, m ? gi : pad, m ? gj : pad);
+        put_wide(lane, lane, f, m ? gi : pad, m ? gj : pad);
+        flush_wide(0, NA * NA);
       } else {
         put(lane, dx, dy, f2, f3, m ? gi : pad, m ? gj : pad);
       }
@@ -1064,7 +1075,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       float f[kOmniED];
 #pragma unroll
       for (int c = 0; c < kOmniED; ++c) f[c] = c < SD ? sj[c < SD ? c : 0] - sg[c < SD ? c : 0] : 0.0f;
-      put_wide(NA * NA + lane, f, lane, NA + lane);
+      put_wide(NA * NA + lane, lane, f, lane, NA + lane);
     } else if (lane < NA) {  // agent j -> own goal j
       float f2, f3;
       if (ENGINE == DGPPO_ENGINE_BICYCLE) {
@@ -1076,6 +1087,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       }
       put(NA * NA + lane, sj[0] - sg[0], sj[1] - sg[1], f2, f3, lane, NA + lane);
     }
+    if constexpr (OMNI) flush_wide(NA * NA, NA);
   }
   ENV_STAMP(5);
   // capsule test of every (agent, obstacle, ray) triple: pair p = o * 8 + i, 2 pairs per step (lane
@@ -1310,7 +1322,7 @@ constexpr int kRolloutActFloats = 16 * NA * 3;  // per wave: a 16-step action ch
 // bound the loop's hoisted addressing takes ~150 VGPRs and a quarter of the workgroups would run after
 // the rest had finished their episodes)
 template <int ENGINE, int GOAL, int SD, int O>
-__global__ __launch_bounds__(256) void lidar_rollout_wave_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lidar_rollout_wave_kernel(
     dgppo_env_cfg cfg, dgppo_env_rollout_io r) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int wg_items[4];
