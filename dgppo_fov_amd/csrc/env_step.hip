@@ -1194,17 +1194,25 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   __syncthreads();  // item lists of the 4 envs of this workgroup are complete
   ENV_STAMP(8);
 
-  // exact ray cast of the surviving triples, pooled over the workgroup's 4 envs (balances the
+  // exact ray cast of the surviving triples, pooled over the workgroup's WPG envs (balances the
   // per-env item counts; each item atomically min-combines into its own env's alpha row)
   {
-    const int c0 = wg_items[0], c1 = wg_items[1], c2 = wg_items[2], c3 = wg_items[3];
-    const int s1 = c0, s2 = c0 + c1, s3 = c0 + c1 + c2, tot = s3 + c3;
-    for (int base = wid * 64; base < tot; base += 256) {
+    int starts[WPG], tot = 0;
+#pragma unroll
+    for (int w = 0; w < WPG; ++w) {
+      starts[w] = tot;
+      tot += wg_items[w];
+    }
+    for (int base = wid * 64; base < tot; base += 64 * WPG) {
       const int g = base + lane;
       const bool act = g < tot;
       const int gg = act ? g : 0;
-      const int w2 = gg < s1 ? 0 : (gg < s2 ? 1 : (gg < s3 ? 2 : 3));
-      const int k = gg - (w2 == 0 ? 0 : (w2 == 1 ? s1 : (w2 == 2 ? s2 : s3)));
+      int w2 = 0;
+#pragma unroll
+      for (int w = 1; w < WPG; ++w) w2 = gg >= starts[w] ? w : w2;
+      int k = gg;
+#pragma unroll
+      for (int w = 1; w < WPG; ++w) k = w2 == w ? gg - starts[w] : k;
       float* L = smem + w2 * C::total;
       const int it = reinterpret_cast<const int*>(L + C::uni)[k];
       const int r = it & 31, p = (it >> 5) & 31, o = (p >> 3) < O ? (p >> 3) : 0, i = p & 7;
@@ -1369,7 +1377,7 @@ template <int ENGINE, int GOAL, int SD, int O, int WPG>
 __global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(4))) void lidar_rollout_wave_kernel(
     dgppo_env_cfg cfg, dgppo_env_rollout_io r) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int wg_items[4];
+  __shared__ int wg_items[WPG];
   const dgppo_env_step_io& g0 = r.step;
   if (r.rebuild_first) {
     wave_body<ENGINE, GOAL, SD, O, true, true, WPG>(cfg, g0, smem, wg_items);
@@ -2722,12 +2730,14 @@ extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_
   return (int)hipGetLastError();
 }
 
-// envs per workgroup of the persistent rollout (DGPPO_ROLLOUT_WPG = 1 or 4, A/B knob; default 4: pooling the
-// ray casts of 4 envs measured 1.37 ms per LidarSpread episode against 1.59 ms with one env per workgroup)
+// envs per workgroup of the persistent rollout (DGPPO_ROLLOUT_WPG = 1, 4 or 8, A/B knob; default 8).  Per
+// LidarSpread episode (reset + 128 steps, 4096 envs): 1 env 1.59 ms, 4 envs 1.37, 8 envs 1.34, 16 envs 1.41
+// (register spills); pooling the ray casts of more envs evens out their item counts between the barriers)
 static int rollout_wpg() {
   static const int w = [] {
     const char* e = getenv("DGPPO_ROLLOUT_WPG");
-    return (e && atoi(e) == 1) ? 1 : 4;
+    const int v = e ? atoi(e) : 8;
+    return v == 1 || v == 4 ? v : 8;
   }();
   return w;
 }
@@ -2741,7 +2751,9 @@ static void launch_rollout_w(const dgppo_env_cfg& c, const dgppo_env_rollout_io&
 
 template <int ENGINE, int GOAL, int SD>
 static void launch_rollout(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, hipStream_t s) {
-  if (rollout_wpg() == 4) launch_rollout_w<ENGINE, GOAL, SD, 4>(c, r, s);
+  const int w = rollout_wpg();
+  if (w == 4) launch_rollout_w<ENGINE, GOAL, SD, 4>(c, r, s);
+  else if (w == 8) launch_rollout_w<ENGINE, GOAL, SD, 8>(c, r, s);
   else launch_rollout_w<ENGINE, GOAL, SD, 1>(c, r, s);
 }
 
