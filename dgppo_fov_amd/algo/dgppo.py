@@ -380,6 +380,109 @@ class DGPPO:
             main.wait_stream(st)
         return out
 
+    def _buf(self, name: str, shape) -> torch.Tensor:
+        """Update scratch that keeps its address from update to update (the captured minibatch graph reads it)."""
+        bufs = self.__dict__.setdefault("_bufs", {})
+        t = bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = bufs[name] = torch.empty(shape, device=self.device)
+        return t
+
+    def _mb_graph_ok(self, batches, ph) -> bool:
+        """Replay the minibatch step from a captured hipGraph (DGPPO_UPDATE_GRAPH=1; off by default): one
+        process, no parity trace, no phase timing, equal minibatch sizes, concurrent streams on.  Bit-identical
+        to the eager step; at the bench config it measured 230.3 vs 229.4 ms per update (the update is
+        GPU-bound: the host's launches already run ahead), so it is an option for host-bound setups."""
+        if "_mbg" not in self.__dict__:
+            self._mbg = None
+        return (self.world == 1 and self.trace is None and not ph.on and len({len(b) for b in batches}) == 1
+                and os.environ.get("DGPPO_UPDATE_GRAPH", "0") == "1" and self._aux_streams(2) is not None)
+
+    def _mb_graph_key(self, rollout, det, A, Ql, Qh_det, Bm, T, L):
+        ptr = lambda t: int(t.data_ptr())  # noqa: E731
+        rg, dg = rollout.graph, det.graph
+        fields = (rg.nodes, rg.edges, rg.receivers, rg.senders, rollout.actions, rollout.log_pis, A, Ql,
+                  dg.nodes, dg.edges, dg.receivers, dg.senders, det.rnn_states, Qh_det)
+        return (Bm, T, L) + tuple(ptr(f) for f in fields) + tuple(tuple(f.stride()) for f in fields)
+
+    def _mb_capture(self, gkey, envs, args):
+        """Record the minibatch step (gathers, the three nets' passes on their streams, clip + Adam) into a
+        hipGraph whose env-id input is a static buffer; replays copy each minibatch's ids into it."""
+        static_envs = envs.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self._mb_body(static_envs, *args, _Phases(self.device))
+        self._mbg = (gkey, g, static_envs, out)
+
+    def _mb_body(self, envs, rollout, det, A, Ql, Qh_det, Bm, T, L, ph):
+        """One minibatch (dgppo.py:275-289): gradients of Vl, Vh and the policy on the minibatch's envs, then
+        clip + finite check + Adam per net.  Device work only (capturable)."""
+        env, dev, n = self._env, self.device, self._n_agents
+        S_per_env = T // L
+        if self.trace is not None:
+            self._mb_before = dict(p={k: o.ps.flat.clone() for k, o in self.opt.items()},
+                                   m={k: o.m.clone() for k, o in self.opt.items()},
+                                   v={k: o.v.clone() for k, o in self.opt.items()},
+                                   s={k: o.state.clone() for k, o in self.opt.items()})
+        self.grad_flat.zero_()
+        # the minibatch's rows of both rollouts (x[idx] of dgppo.py:278-279): two gather launches
+        rg = rollout.graph
+        nodes, edges, recv, send, acts, lp_old, adv, tgt = self._gather(
+            envs, rg.nodes, rg.edges, rg.receivers, rg.senders, rollout.actions, rollout.log_pis, A, Ql)
+        g = self._graph_batch(nodes, edges, recv, send).prepare()
+        dg = det.graph
+        dnodes, dedges, drecv, dsend, hd, qhd = self._gather(
+            envs, dg.nodes, dg.edges, dg.receivers, dg.senders, det.rnn_states, Qh_det)
+        gd = self._graph_batch(dnodes, dedges, drecv, dsend).prepare()
+        tgt = tgt.view(Bm * S_per_env, L)
+        acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
+        pending = []
+
+        def vl_job():  # update_Vl (informarl.py:357-385)
+            v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
+            dv = torch.empty_like(v)
+            loss = torch.empty(1, device=dev)
+            K.l2_loss(v, tgt, dv, loss)
+            ph.mark("Vl_fwd")
+            self.Vl.seq_bwd(cache, dv)
+            self._start_reduce(self.Vl, pending)  # the bucket's all-reduce overlaps the other passes
+            ph.mark("Vl_bwd")
+            return loss
+
+        def vh_job():  # update_Vh (dgppo.py:296-321) on the deterministic rollout
+            vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, 64))
+            dvh = torch.empty_like(vh)
+            loss = torch.empty(1, device=dev)
+            K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)
+            ph.mark("Vh_fwd")
+            self.Vh.bwd(cache, dvh)
+            self._start_reduce(self.Vh, pending)
+            ph.mark("Vh_bwd")
+            return loss
+
+        def pi_job():  # update_policy (informarl.py:405-457)
+            lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
+            dlp = torch.empty_like(lp)
+            dent = torch.empty_like(ent)
+            st = torch.empty(4, device=dev)
+            K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, st)
+            ph.mark("pi_fwd")
+            self.actor.eval_seq_bwd(cache, dlp, dent)
+            self._start_reduce(self.actor, pending)
+            ph.mark("pi_bwd")
+            return st
+
+        # the three passes are independent (own parameters and gradient slices): concurrent streams
+        stats, vl_loss, vh_loss = self._parallel([pi_job, vl_job, vh_job])
+        # gradient buckets all-reduced (sum, then / world), clip + finite check + Adam per net
+        self._finish_reduce(pending)
+        if self.trace is not None:
+            self._mb_grad = self.grad_flat.clone()
+        for name in ("Vl", "Vh", "policy"):
+            self.opt[name].step()
+        ph.mark("allreduce_adam")
+        return vl_loss, vh_loss, stats, tgt, lp_old
+
     def update(self, rollout: Rollout, step: int) -> dict:
         env, dev = self._env, self.device
         B, T = rollout.rewards.shape
@@ -409,13 +512,13 @@ class DGPPO:
             costs = rollout.costs.contiguous()
             l = (-rollout.rewards).contiguous()
             Qh = torch.empty((B, T, n, env.n_cost), device=dev)
-            Ql = torch.empty((B, T), device=dev)
+            Ql = self._buf("Ql", (B, T))
             K.gae(costs, l, Vh, Vl, Qh, Ql, self.gamma, self.gae_lambda)
-            Qh_det = torch.empty_like(Qh)
+            Qh_det = self._buf("Qh_det", (B, T, n, env.n_cost))
             Ql_det = torch.empty_like(Ql)
             K.gae(det.costs.contiguous(), (-det.rewards).contiguous(), Vh_det, Vl, Qh_det, Ql_det, self.gamma,
                   self.gae_lambda)
-            A = torch.empty((B, T, n), device=dev)
+            A = self._buf("A", (B, T, n))
             safe_cnt = torch.empty(B, device=dev)
             K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, env.dt, self.alpha, self.cbf_eps, self.cbf_weight_at(step))
             ph.mark("gae_adv")
@@ -427,75 +530,30 @@ class DGPPO:
             batches = minibatch_plan(B, T, self.world, self.batch_size, self.np_rng)
             L = self.rnn_step
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
-            S_per_env = T // L
             env_ids = self._env_ids(batches)
-            for bi in batches:
+            graph_ok = self._mb_graph_ok(batches, ph)
+            for k, bi in enumerate(batches):
                 envs = next(env_ids)
-                Bm = len(bi)
-                self.grad_flat.zero_()
-                # the minibatch's rows of both rollouts (x[idx] of dgppo.py:278-279): two gather launches
-                rg = rollout.graph
-                nodes, edges, recv, send, acts, lp_old, adv, tgt = self._gather(
-                    envs, rg.nodes, rg.edges, rg.receivers, rg.senders, rollout.actions, rollout.log_pis, A, Ql)
-                g = self._graph_batch(nodes, edges, recv, send).prepare()
-                dg = det.graph
-                dnodes, dedges, drecv, dsend, hd, qhd = self._gather(
-                    envs, dg.nodes, dg.edges, dg.receivers, dg.senders, det.rnn_states, Qh_det)
-                gd = self._graph_batch(dnodes, dedges, drecv, dsend).prepare()
-                tgt = tgt.view(Bm * S_per_env, L)
-                acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
-                pending = []
-
-                def vl_job():  # update_Vl (informarl.py:357-385)
-                    v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
-                    dv = torch.empty_like(v)
-                    loss = torch.empty(1, device=dev)
-                    K.l2_loss(v, tgt, dv, loss)
-                    ph.mark("Vl_fwd")
-                    self.Vl.seq_bwd(cache, dv)
-                    self._start_reduce(self.Vl, pending)  # the bucket's all-reduce overlaps the other passes
-                    ph.mark("Vl_bwd")
-                    return loss
-
-                def vh_job():  # update_Vh (dgppo.py:296-321) on the deterministic rollout
-                    vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, 64))
-                    dvh = torch.empty_like(vh)
-                    loss = torch.empty(1, device=dev)
-                    K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)
-                    ph.mark("Vh_fwd")
-                    self.Vh.bwd(cache, dvh)
-                    self._start_reduce(self.Vh, pending)
-                    ph.mark("Vh_bwd")
-                    return loss
-
-                def pi_job():  # update_policy (informarl.py:405-457)
-                    lp, ent, cache = self.actor.eval_seq_fwd(g, Bm * S_per_env, L, acts, self.entropy_eps)
-                    dlp = torch.empty_like(lp)
-                    dent = torch.empty_like(ent)
-                    st = torch.empty(4, device=dev)
-                    K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, st)
-                    ph.mark("pi_fwd")
-                    self.actor.eval_seq_bwd(cache, dlp, dent)
-                    self._start_reduce(self.actor, pending)
-                    ph.mark("pi_bwd")
-                    return st
-
-                # the three passes are independent (own parameters and gradient slices): concurrent streams
-                stats, vl_loss, vh_loss = self._parallel([pi_job, vl_job, vh_job])
-                # gradient buckets all-reduced (sum, then / world), clip + finite check + Adam per net
-                self._finish_reduce(pending)
+                args = (rollout, det, A, Ql, Qh_det, len(bi), T, L)
+                if graph_ok:
+                    gkey = self._mb_graph_key(*args)
+                    if self._mbg is not None and self._mbg[0] == gkey:
+                        self._mbg[2].copy_(envs)
+                        self._mbg[1].replay()
+                        out = self._mbg[3]
+                    else:
+                        out = self._mb_body(envs, *args, ph)  # the first minibatch runs eagerly, then capture
+                        self._mb_capture(gkey, envs, args)
+                else:
+                    out = self._mb_body(envs, *args, ph)
+                vl_loss, vh_loss, stats, tgt, lp_old = out
                 if self.trace is not None:
                     self.trace["mb"].append(dict(
-                        envs=bi.copy(), grad=self.grad_flat.clone(), vl_loss=vl_loss.clone(), vh_loss=vh_loss.clone(),
-                        stats=stats.clone(), before={k: o.ps.flat.clone() for k, o in self.opt.items()},
-                        m_before={k: o.m.clone() for k, o in self.opt.items()},
-                        v_before={k: o.v.clone() for k, o in self.opt.items()},
-                        state_before={k: o.state.clone() for k, o in self.opt.items()}))
-                for name in ("Vl", "Vh", "policy"):
-                    self.opt[name].step()
-                ph.mark("allreduce_adam")
-                info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
-                        "Vh/loss_Vh": vh_loss, "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
+                        envs=bi.copy(), grad=self._mb_grad, vl_loss=vl_loss.clone(), vh_loss=vh_loss.clone(),
+                        stats=stats.clone(), before=self._mb_before["p"], m_before=self._mb_before["m"],
+                        v_before=self._mb_before["v"], state_before=self._mb_before["s"]))
+            info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
+                    "Vh/loss_Vh": vh_loss, "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
             safe = safe_cnt.sum()
             if self.world > 1:
                 dist.all_reduce(safe)
