@@ -49,7 +49,7 @@ __device__ __forceinline__ float norm2(float dx, float dy) { return sqrtf(sq2(dx
 
 // ---- LDS carve (floats) -------------------------------------------------------------------------
 struct Carve {
-  int cur, curhit, obst, evec, act, nxt, alpha, hpt, hits, isin, red, samp, dist, total;
+  int cur, curhit, obst, evec, act, nxt, alpha, hpt, hits, isin, red, samp, dist, dist_n, cull, total;
   __host__ __device__ Carve(int n, int sd, int O, int R, int k, bool lidar) {
     int off = 0;
     auto take = [&](int nf) { int o = off; off += (nf + 3) & ~3; return o; };
@@ -65,7 +65,10 @@ struct Carve {
     isin = take(n);
     red = take(5 * n);  // d2goal, far, |a|^2, cost0, cost1
     samp = take(4 * n);  // reset: sampled positions / goals (n, 2) each
-    dist = take(2 * n * n + n * (k > O ? k : O));  // step: pairwise distance tasks
+    // step: pairwise distance tasks; lidar_scan: the culling's work list (dist is dead by then)
+    dist_n = 2 * n * n + n * (k > O ? k : O) > 256 ? 2 * n * n + n * (k > O ? k : O) : 256;
+    dist = take(dist_n);
+    cull = take(lidar ? 2 * O + 4 + n * R : 0);  // lidar_scan: unsafe ray masks | radii | count | alpha codes
     total = off;
   }
 };
@@ -301,6 +304,104 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
   const float* evec = lds + cv.evec;
   uint64_t* keys = reinterpret_cast<uint64_t*>(lds + cv.alpha);
   float* hpt = lds + cv.hpt;
+  if (R <= 32) {
+    // Exact culling with a compacted work list, the workgroup form of the wave kernel's (proof in the
+    // notes before namespace wv): a (agent, obstacle, ray) triple is left at the reference's 1e6
+    // unless the ray is unsafe for the obstacle (ineligible obstacle, |d| > 1 or a near-parallel edge),
+    // the agent lies outside [-2, 2]^2 or the ray segment meets the disc (c, rho + 0.01).  Survivors
+    // are ray-cast by the whole workgroup, one list-sized round at a time, and min-combined per (agent, ray)
+    // with an LDS atomic on an order-preserving code (NaN wins, as min_nan).  Work list: the dist region.
+    uint32_t* unsafe = reinterpret_cast<uint32_t*>(lds + cv.cull);  // (O) bit r: ray r must be cast
+    float* rho = lds + cv.cull + O;                                    // (O) circumradius bound, -1 ineligible
+    int* cnt = reinterpret_cast<int*>(lds + cv.cull + 2 * O);
+    uint32_t* aenc = reinterpret_cast<uint32_t*>(lds + cv.cull + 2 * O + 4);  // (n R) alpha codes
+    int* items = reinterpret_cast<int*>(lds + cv.dist);  // the step's distance tasks are dead here
+    const int cap = n * R * O < cv.dist_n ? n * R * O : cv.dist_n;
+    auto enc = [](float a) { return a != a ? 0u : __float_as_uint(a) + 1u; };
+    for (int o = tid; o < O; o += nthr) {
+      const float* rec = obst + o * DGPPO_OBST_FIELDS;
+      const float cx = rec[0], cy = rec[1];
+      float r2 = 0.0f;
+      bool elig = (fabsf(cx) <= 2.0f) & (fabsf(cy) <= 2.0f);
+      for (int q = 0; q < 4; ++q) {
+        const float px = rec[8 + 2 * q], py = rec[9 + 2 * q];
+        elig = elig & (fabsf(px) <= 2.0f) & (fabsf(py) <= 2.0f);
+        const float dx = px - cx, dy = py - cy;
+        r2 = fmaxf(r2, dx * dx + dy * dy);
+      }
+      const float rh = __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-6f;
+      rho[o] = elig & (rh <= 0.5f) ? rh : -1.0f;
+      unsafe[o] = 0u;
+    }
+    for (int p = tid; p < n * R; p += nthr) aenc[p] = 0x49742400u + 1u;  // enc(1e6f)
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    for (int q = tid; q < O * R; q += nthr) {
+      const int o = q / R, r = q - (q / R) * R;
+      const float dx = ray_dirs[2 * r], dy = ray_dirs[2 * r + 1];
+      bool safe = (rho[o] >= 0.0f) & (__builtin_amdgcn_sqrtf(dx * dx + dy * dy) * 1.0001f <= 1.0f);
+      for (int e = 0; e < 4; ++e) safe = safe & (fabsf(dy * evec[o * 8 + 2 * e] - dx * evec[o * 8 + 2 * e + 1]) >= 1e-3f);
+      if (!safe) atomicOr(unsafe + o, 1u << r);
+    }
+    __syncthreads();
+    const int tot = n * R * O;
+    const int lane = tid & 63;
+#pragma unroll 1
+    for (int t0 = 0; t0 < tot; t0 += cap) {
+      const int t1 = t0 + cap < tot ? t0 + cap : tot;
+#pragma unroll 1
+      for (int tb = t0; tb < t1; tb += nthr) {  // uniform trip count: every wave joins the ballots
+        const int t = tb + tid;
+        const bool valid = t < t1;
+        const int tt = valid ? t : t0;
+        const int o = tt / (n * R), p = tt - o * (n * R), i = p / R, r = p - (p / R) * R;
+        const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
+        const float dx = ray_dirs[2 * r], dy = ray_dirs[2 * r + 1];
+        const float rlen2 = dx * dx + dy * dy, rlen = __builtin_amdgcn_sqrtf(rlen2) * 1.0001f;
+        const float vx = obst[o * DGPPO_OBST_FIELDS] - sx, vy = obst[o * DGPPO_OBST_FIELDS + 1] - sy;
+        const float perp = vx * dy - vy * dx, proj = vx * dx + vy * dy;
+        const float Rl = (rho[o] + 0.01f) * rlen;
+        const bool qok = (fabsf(sx) <= 2.0f) & (fabsf(sy) <= 2.0f);
+        const bool miss = qok & ((fabsf(perp) > Rl) | (proj < -Rl) | (proj > rlen2 + Rl));
+        const bool keep = valid & (!miss | ((unsafe[o] >> r) & 1u));
+        const uint64_t kb = __ballot(keep);
+        int base = 0;
+        if (lane == 0 && kb) base = atomicAdd(cnt, (int)__popcll(kb));
+        base = __shfl(base, 0);
+        if (keep) {
+          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(kb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)kb, 0u));
+          items[base + below] = (o << 16) | p;
+        }
+      }
+      __syncthreads();
+      const int m = *cnt;
+#pragma unroll 1
+      for (int j = tid; j < m; j += nthr) {
+        const int code = items[j], o = code >> 16, p = code & 0xFFFF, i = p / R, r = p - (p / R) * R;
+        const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
+        const float ex = sx + ray_dirs[2 * r + 0];
+        const float ey = sy + ray_dirs[2 * r + 1];
+        const float a = rect_raytrace(obst + o * DGPPO_OBST_FIELDS, evec + o * 8, sx, sy, sx - ex, sy - ey);
+        atomicMin(aenc + p, enc(a));
+      }
+      __syncthreads();
+      if (tid == 0) *cnt = 0;
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (int p = tid; p < n * R; p += nthr) {
+      const int i = p / R, r = p - (p / R) * R;
+      const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
+      const float ex = sx + ray_dirs[2 * r + 0];
+      const float ey = sy + ray_dirs[2 * r + 1];
+      const uint32_t e = aenc[p];
+      float a = e == 0u ? __builtin_nanf("") : __uint_as_float(e - 1u);
+      a = a * (1.0f - lds[cv.isin + i]);
+      keys[p] = sort_key(a, r);
+      hpt[2 * p + 0] = sx + (ex - sx) * a;
+      hpt[2 * p + 1] = sy + (ey - sy) * a;
+    }
+  } else {
 #pragma unroll 1
   for (int p = tid; p < n * R; p += nthr) {
     asm volatile("" ::: "memory");  // keep obstacle LDS reads inside the loop (no LICM register blow-up)
@@ -318,6 +419,7 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
     keys[p] = sort_key(a, r);
     hpt[2 * p + 0] = sx + (ex - sx) * a;
     hpt[2 * p + 1] = sy + (ey - sy) * a;
+  }
   }
   __syncthreads();
   float* hits = lds + cv.hits;
@@ -354,6 +456,21 @@ __device__ __forceinline__ void agent_is_inside(int O, float* lds, const Carve& 
   lds[cv.isin + i] = in ? 1.0f : 0.0f;
 }
 
+#ifdef DGPPO_ENV_STAMPS
+// diagnostic builds: wave 0's barrier-to-barrier phase times of the workgroup-per-env step kernel
+__device__ unsigned long long g_blk_stamps[8];
+#define BLK_STAMP(k)                                      \
+  do {                                                    \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();   \
+    bst[k] += now_ - blast;                               \
+    blast = now_;                                         \
+  } while (0)
+#else
+#define BLK_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 // ---- the step kernel --------------------------------------------------------------------------
 // Phases (one barrier each), every phase spread over the whole workgroup:
 //   A  stage current rows, obstacles, clipped actions in LDS
@@ -372,6 +489,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
   const Carve cv(n, SD, O, d.R, k, !mpe);
   const int tid = threadIdx.x;
   const int64_t env = blockIdx.x;
+#ifdef DGPPO_ENV_STAMPS
+  uint64_t bst[5] = {0, 0, 0, 0, 0}, blast = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- A ------------------------------------------------------------------------------------
   const float* st = io.states + env * io.states_stride;
@@ -388,6 +508,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
   const float* ac = io.action + env * io.action_stride;
   for (int idx = tid; idx < 2 * n; idx += BLOCK) lds[cv.act + idx] = clampf_nan(ac[idx], -1.0f, 1.0f);
   __syncthreads();
+  BLK_STAMP(0);
 
   // ---- B ------------------------------------------------------------------------------------
   const float* cur = lds + cv.cur;
@@ -461,6 +582,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
   }
   if (lidar) stage_edge_vectors(O, lds, cv, tid, BLOCK);
   __syncthreads();
+  BLK_STAMP(1);
 
   // ---- C ------------------------------------------------------------------------------------
   for (int i = tid; i < n; i += BLOCK) {
@@ -498,6 +620,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
     if (lidar) agent_is_inside(O, lds, cv, SD, i);
   }
   __syncthreads();
+  BLK_STAMP(2);
 
   // ---- D ------------------------------------------------------------------------------------
   if (tid == 0) {
@@ -521,6 +644,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
     lidar_scan<SD>(d, io.ray_dirs, lds, cv, tid, BLOCK);
     __syncthreads();
   }
+  BLK_STAMP(3);
 
   // ---- E ------------------------------------------------------------------------------------
   GraphOut out;
@@ -532,6 +656,11 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
   const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
   const float* third = mpe ? cur + 2 * n * SD : lds + cv.hits;
   write_graph<ENGINE, GOAL, SD>(cfg, d, lds + cv.nxt, goal, third, out, vec4, tid, BLOCK);
+  BLK_STAMP(4);
+#ifdef DGPPO_ENV_STAMPS
+  if (tid == 0)
+    for (int q = 0; q < 5; ++q) atomicAdd(&g_blk_stamps[q], (unsigned long long)bst[q]);
+#endif
 }
 
 // Rectangle.inside with r = 0 (raytracing's is_in): the rounded-corner term sqrt(.) < 0 never holds
@@ -2759,6 +2888,15 @@ static void launch_rollout(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r
 
 #ifdef DGPPO_ENV_STAMPS
 // diagnostic builds: the phase sums since the last call (16 x u64 s_memtime ticks, summed over waves), then zeroed
+extern "C" int dgppo_env_diag_block_stamps(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dgppo::g_blk_stamps), 8 * sizeof(unsigned long long));
+  if (e == hipSuccess) {
+    static const unsigned long long zero[8] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(dgppo::g_blk_stamps), zero, sizeof(zero));
+  }
+  return (int)e;
+}
+
 extern "C" int dgppo_env_diag_stamps(unsigned long long* out) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dgppo::wv::g_env_stamps), 16 * sizeof(unsigned long long));
   if (e == hipSuccess) {
