@@ -68,7 +68,8 @@ struct Carve {
     // step: pairwise distance tasks; lidar_scan: the culling's work list (dist is dead by then)
     dist_n = 2 * n * n + n * (k > O ? k : O) > 256 ? 2 * n * n + n * (k > O ? k : O) : 256;
     dist = take(dist_n);
-    cull = take(lidar ? 2 * O + 4 + n * R : 0);  // lidar_scan: unsafe ray masks | radii | count | alpha codes
+    // lidar_scan: unsafe masks | radii | count | alpha codes | (16-byte aligned) ray table
+    cull = take(lidar ? ((2 * O + 4 + n * R + 3) & ~3) + 4 * R : 0);
     total = off;
   }
 };
@@ -217,9 +218,10 @@ __device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d
         f2 = si[2] - sj[2];
         f3 = si[3] - sj[3];
       }
-      float d = norm2(si[0] - sj[0], si[1] - sj[1]);
-      if (i == j) d = d + cfg.c_self_dist;
-      const bool m = d < comm;
+      // norm + (c_self_dist on the diagonal) < comm_radius on the squared norm: sqrtf is correctly
+      // rounded and monotone, so sqrtf(x) < r <=> x < t2_comm; the diagonal's difference is exactly 0 or NaN
+      const float d2 = sq2(si[0] - sj[0], si[1] - sj[1]);
+      const bool m = i == j ? ((d2 == 0.0f) & (cfg.c_self_dist < comm)) : (d2 < cfg.t2_comm);
       rv = m ? i : pad;
       sv = m ? j : pad;
     } else if (e < n_aa + n_ag) {
@@ -257,7 +259,7 @@ __device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d
         f1 = si[1] - so[1];
         f2 = si[2] - so[2];
         f3 = si[3] - so[3];
-        const bool m = norm2(si[0] - so[0], si[1] - so[1]) < comm;
+        const bool m = sq2(si[0] - so[0], si[1] - so[1]) < cfg.t2_comm;
         rv = m ? i : pad;
         sv = m ? 2 * n + o : pad;
       } else {  // agent-lidar blocks (1, k) per agent, mask ||p_i - hit|| < comm_radius - 0.1
@@ -267,7 +269,7 @@ __device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d
         f1 = si[1] - third[(i * k + h) * 2 + 1];
         f2 = 0.0f;
         f3 = 0.0f;
-        const bool m = norm2(f0, f1) < cfg.c_lidar_active;
+        const bool m = sq2(f0, f1) < cfg.t2_lidar;
         rv = m ? i : pad;
         sv = m ? 2 * n + i * k + h : pad;
       }
@@ -315,6 +317,7 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
     float* rho = lds + cv.cull + O;                                    // (O) circumradius bound, -1 ineligible
     int* cnt = reinterpret_cast<int*>(lds + cv.cull + 2 * O);
     uint32_t* aenc = reinterpret_cast<uint32_t*>(lds + cv.cull + 2 * O + 4);  // (n R) alpha codes
+    float4* rayc = reinterpret_cast<float4*>(lds + cv.cull + ((2 * O + 4 + n * R + 3) & ~3));  // (R) [dx, dy, |d|^2, |d| bound]
     int* items = reinterpret_cast<int*>(lds + cv.dist);  // the step's distance tasks are dead here
     const int cap = n * R * O < cv.dist_n ? n * R * O : cv.dist_n;
     auto enc = [](float a) { return a != a ? 0u : __float_as_uint(a) + 1u; };
@@ -334,12 +337,17 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
       unsafe[o] = 0u;
     }
     for (int p = tid; p < n * R; p += nthr) aenc[p] = 0x49742400u + 1u;  // enc(1e6f)
+    for (int r = tid; r < R; r += nthr) {
+      const float dx = ray_dirs[2 * r], dy = ray_dirs[2 * r + 1], l2 = dx * dx + dy * dy;
+      rayc[r] = make_float4(dx, dy, l2, __builtin_amdgcn_sqrtf(l2) * 1.0001f);
+    }
     if (tid == 0) *cnt = 0;
     __syncthreads();
     for (int q = tid; q < O * R; q += nthr) {
       const int o = q / R, r = q - (q / R) * R;
-      const float dx = ray_dirs[2 * r], dy = ray_dirs[2 * r + 1];
-      bool safe = (rho[o] >= 0.0f) & (__builtin_amdgcn_sqrtf(dx * dx + dy * dy) * 1.0001f <= 1.0f);
+      const float4 rc = rayc[r];
+      const float dx = rc.x, dy = rc.y;
+      bool safe = (rho[o] >= 0.0f) & (rc.w <= 1.0f);
       for (int e = 0; e < 4; ++e) safe = safe & (fabsf(dy * evec[o * 8 + 2 * e] - dx * evec[o * 8 + 2 * e + 1]) >= 1e-3f);
       if (!safe) atomicOr(unsafe + o, 1u << r);
     }
@@ -356,8 +364,8 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
         const int tt = valid ? t : t0;
         const int o = tt / (n * R), p = tt - o * (n * R), i = p / R, r = p - (p / R) * R;
         const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
-        const float dx = ray_dirs[2 * r], dy = ray_dirs[2 * r + 1];
-        const float rlen2 = dx * dx + dy * dy, rlen = __builtin_amdgcn_sqrtf(rlen2) * 1.0001f;
+        const float4 rc = rayc[r];
+        const float dx = rc.x, dy = rc.y, rlen2 = rc.z, rlen = rc.w;
         const float vx = obst[o * DGPPO_OBST_FIELDS] - sx, vy = obst[o * DGPPO_OBST_FIELDS + 1] - sy;
         const float perp = vx * dy - vy * dx, proj = vx * dx + vy * dy;
         const float Rl = (rho[o] + 0.01f) * rlen;
@@ -379,8 +387,9 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
       for (int j = tid; j < m; j += nthr) {
         const int code = items[j], o = code >> 16, p = code & 0xFFFF, i = p / R, r = p - (p / R) * R;
         const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
-        const float ex = sx + ray_dirs[2 * r + 0];
-        const float ey = sy + ray_dirs[2 * r + 1];
+        const float4 rc = rayc[r];
+        const float ex = sx + rc.x;
+        const float ey = sy + rc.y;
         const float a = rect_raytrace(obst + o * DGPPO_OBST_FIELDS, evec + o * 8, sx, sy, sx - ex, sy - ey);
         atomicMin(aenc + p, enc(a));
       }
@@ -392,8 +401,9 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
     for (int p = tid; p < n * R; p += nthr) {
       const int i = p / R, r = p - (p / R) * R;
       const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
-      const float ex = sx + ray_dirs[2 * r + 0];
-      const float ey = sy + ray_dirs[2 * r + 1];
+      const float4 rc = rayc[r];
+      const float ex = sx + rc.x;
+      const float ey = sy + rc.y;
       const uint32_t e = aenc[p];
       float a = e == 0u ? __builtin_nanf("") : __uint_as_float(e - 1u);
       a = a * (1.0f - lds[cv.isin + i]);
