@@ -86,8 +86,8 @@ class ActorNet(_Net):
     def _fused_args(self, g: GraphBatch):
         """dgppo_policy_step_args with this net's parameter pointers (None if the fused kernel does not
         cover the configuration)."""
-        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1":
-            return None
+        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1" or len(self.gnn.layers) > 2:
+            return None  # (the fused kernel holds at most 2 GNN layers; deeper stacks run the layer chain)
         a = _lib.PolicyStepArgs()
         a.N, a.E, a.n_agents, a.C, a.D0, a.A = g.N, g.E, self.n, g.C, g.nodes.shape[2], self.A
         a.n_layers, a.H, a.ED = len(self.gnn.layers), 3, g.ED

@@ -373,12 +373,15 @@ class GraphTransformer:
              "Dense_4": {"kernel": orthogonal(rng, (D, F)), "bias": np.zeros(F, np.float32)}}
         self.load_flax(d)
 
-    def _attn_args(self, g: "GraphBatch", QB, xa=None, pre=None) -> dict:
+    def _attn_args(self, g: "GraphBatch", QB, xa=None, pre=None, xfull=None) -> dict:
         """Inputs of torch.ops.dgppo.gnn_attn_fwd / _bwd for this layer on graph batch g, Q-free form:
-        QB (R, H*D + H) = [qt | beta] rows (see qb_weights)."""
+        QB (R, H*D + H) = [qt | beta] rows (see qb_weights).  xfull (G, N, D): every node's input row
+        (layers past the second of a deeper GNN), else the raw nodes (first layer) or agent mode."""
         D0 = 0
         pre_W = pre_b = None
-        if xa is None:
+        if xfull is not None:
+            x, x_gs = xfull, g.N * self.D
+        elif xa is None:
             x, x_gs = g.nodes, g.N * g.nodes.shape[2]
         else:  # agent mode: agents from xa, other senders = pre's Dense_4 + ReLU of raw rows
             raw, cols = g.sender_raw
@@ -415,24 +418,25 @@ class GraphTransformer:
         K.gemm(Waug, self.v("bk"), QBW, D + 1, 1, F, lda=H * F, sa=F, ldb=1, sb=F, ldc=W, sc=1, c_off=H * D, batch=H)
         return QBW
 
-    def fwd(self, g: "GraphBatch", xa=None, pre=None):
+    def fwd(self, g: "GraphBatch", xa=None, pre=None, xfull=None):
         """One layer on the graph batch.  xa None: senders read the raw nodes (G, N, D) (first layer);
         else xa (G*n, D) holds the agents' rows and the never-receiving nodes are `pre`'s
-        Dense_4 + ReLU of their raw rows (agent mode).  Returns Y (G*n, F) = the agents' outputs
-        (only agents receive, so only their rows feed the next layer's queries) and the cache.
+        Dense_4 + ReLU of their raw rows (agent mode); xfull (G, N, D): every node's row given
+        (GNN layers past the second).  Returns Y (G*n, F) = the agents' outputs (only agents
+        receive, so only their rows feed the next layer's queries) and the cache.
         Edge columns past the first 4 add (sum_c attn * efx) @ Wex to the messages (edge_wsum)."""
         G, N, n = g.G, g.N, g.n
         D, F, H, C = self.D, self.F, self.H, g.C
         dev = g.nodes.device
         R = G * n
-        A, akw = (g.nodes, dict(lda=D, a_grp=n, a_gs=N * D)) if xa is None else (xa, dict(lda=D))
+        A, akw = self._rows_in(g, xa, xfull)
         QBW = self.qb_weights()
         W = H * D + H
         QB = torch.empty((R, W), device=dev)  # [qt | beta] per receiving agent: one GEMM, q never stored
         K.gemm(A, QBW, QB, R, W, D, bias=QBW[D], **akw)
         attn = torch.empty((R, H, C), device=dev)
         xcat = torch.empty((R, H * (D + 5)), device=dev)
-        torch.ops.dgppo.gnn_attn_fwd(**self._attn_args(g, QB, xa, pre), attn=attn, xcat=xcat)
+        torch.ops.dgppo.gnn_attn_fwd(**self._attn_args(g, QB, xa, pre, xfull), attn=attn, xcat=xcat)
         M = torch.empty((R, F), device=dev)
         K.gemm(xcat, self.v("Wcat"), M, R, F, H * (D + 5), alpha=1.0 / H)
         xcx = None
@@ -442,20 +446,27 @@ class GraphTransformer:
             K.gemm(xcx, self.v("Wex"), M, R, F, H * self.EX, alpha=1.0 / H, beta=1.0)
         Y = torch.empty((R, F), device=dev)
         K.gemm(A, self.v("Wu"), Y, R, F, D, bias=self.v("bu"), addend=M, relu=True, **akw)
-        return Y, (xa, pre, QBW, QB, attn, xcat, xcx, Y)
+        return Y, (xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull)
+
+    def _rows_in(self, g: "GraphBatch", xa, xfull):
+        """The receiving agents' input rows as a GEMM operand: (tensor, row-grouping kwargs)."""
+        if xa is not None:
+            return xa, dict(lda=self.D)
+        x = xfull if xfull is not None else g.nodes
+        return x, dict(lda=self.D, a_grp=g.n, a_gs=g.N * self.D)
 
     def bwd(self, cache, dY, g: "GraphBatch"):
-        """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, else None;
-        accumulates this layer's grads and, in agent mode with `pre`, pre's Dense_4 grads from the
-        transformed senders."""
-        xa, pre, QBW, QB, attn, xcat, xcx, Y = cache
+        """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, d xfull (G, N, D)
+        when every node's row was given, else None; accumulates this layer's grads and, in agent mode
+        with `pre`, pre's Dense_4 grads from the transformed senders."""
+        xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull = cache
         G, N, n = g.G, g.N, g.n
         D, F, H, C = self.D, self.F, self.H, g.C
         R = G * n
         W = H * (D + 5)
         HD, WQ = H * D, H * D + H
         dev = dY.device
-        A, akw = (g.nodes, dict(lda=D, a_grp=n, a_gs=N * D)) if xa is None else (xa, dict(lda=D))
+        A, akw = self._rows_in(g, xa, xfull)
         K.relu_bwd_(dY, Y)  # dY := dZ
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
@@ -470,7 +481,8 @@ class GraphTransformer:
             K.edge_da(G, n, C, H, self.EX, g.E, dxx, g.cand, g.sidx, g.edges_x, da_add)
         dQB = torch.empty((R, WQ), device=dev)  # [dqt | dbeta]
         dXa = torch.zeros((R, D), device=dev) if xa is not None else None
-        args = self._attn_args(g, QB, xa, pre)
+        dXf = torch.zeros((G, N, D), device=dev) if xfull is not None else None  # every sender's gradient
+        args = self._attn_args(g, QB, xa, pre, xfull)
         part = None
         if xa is not None and pre is not None:
             nb = ops.gnn_attn_partial_blocks(**args)
@@ -478,7 +490,7 @@ class GraphTransformer:
             part = K.workspace(nb * PK, dev, "attn_pre")
         torch.ops.dgppo.gnn_attn_bwd(**args, attn=attn, dxcat=dxcat, da_add=da_add, dqt=dQB, dq=None,
                                      dbeta=dQB[:, HD:], dxa=dXa, dxa_gstride=n * D, dpre_part=part, dqt_ld=WQ,
-                                     dbeta_ld=WQ)
+                                     dbeta_ld=WQ, dx=dXf, dx_gstride=N * D)
         if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre (Wu rows = the raw columns used)
             cols = g.sender_raw[1]
             ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
@@ -513,7 +525,13 @@ class GraphTransformer:
         if dXa is not None:
             K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
             K.gemm(dQB, QBW, dXa, R, D, WQ, tb=True, ldb=WQ, beta=1.0)  # d[qt | beta] / dx = QBW[:D]^T
-        return dXa
+            return dXa
+        if dXf is not None:  # the agents' rows also fed Dense_4 and the queries: added in place (row-grouped C)
+            cg = dict(c_grp=n, c_gs=N * D, ldc=D, beta=1.0)
+            K.gemm(dY, self.v("Wu"), dXf, R, D, F, tb=True, ldb=F, **cg)
+            K.gemm(dQB, QBW, dXf, R, D, WQ, tb=True, ldb=WQ, **cg)
+            return dXf
+        return None
 
 
 _COLS = {}
@@ -610,9 +628,8 @@ class GNN:
     type_nodes(agent): returns the agent rows of the last layer, (G*n, out_dim)."""
 
     def __init__(self, ps, name, node_dim, n_layers, msg_dim=32, out_dim=64, n_heads=3, edge_dim=4):
-        if not 1 <= n_layers <= 2:
-            raise NotImplementedError("GNN depth 1 or 2 (the reference's actor/Vl/Vh configs): deeper stacks need "
-                                      "the never-receiving nodes' hidden features materialised")
+        if n_layers < 1:
+            raise ValueError(f"GNN depth {n_layers} < 1")
         self.layers = []
         d = node_dim
         for i in range(n_layers):
@@ -631,15 +648,63 @@ class GNN:
         for L, d in zip(self.layers, layers):
             L.load_flax(d)
 
+    def _lift(self, Z, i, rows):
+        """Z_{i+1} = relu(Z_i Wu_i + bu_i) over every node row: the layer-(i+1) input of a node that never
+        receives (goals, hits, obstacles: empty aggregation, gnn.py:110-117)."""
+        L = self.layers[i]
+        out = torch.empty((rows, L.F), device=Z.device)
+        K.gemm(Z, L.v("Wu"), out, rows, L.F, L.D, bias=L.v("bu"), relu=True)
+        return out
+
     def fwd(self, g: GraphBatch):
+        """Layer 0 reads the raw nodes, layer 1 runs in agent mode (never-receivers' layer-1 rows recomputed
+        from the raw rows in the kernel).  Layers l >= 2 (deeper stacks than the reference's defaults) read
+        materialised rows X_l (G, N, D): the agents' rows are the previous layer's outputs, every other
+        node's row is Z_l = relu(Z_{l-1} Wu_{l-1} + bu_{l-1}) from Z_0 = the raw nodes."""
         caches = []
         Y = None
+        G, N, n = g.G, g.N, g.n
+        Zs = [g.nodes.reshape(G * N, g.nodes.shape[2])] if len(self.layers) > 2 else None
         for i, L in enumerate(self.layers):
-            Y, c = L.fwd(g) if i == 0 else L.fwd(g, xa=Y, pre=self.layers[0])
+            if i == 0:
+                Y, c = L.fwd(g)
+            elif i == 1:
+                Y, c = L.fwd(g, xa=Y, pre=self.layers[0])
+            else:
+                while len(Zs) <= i:
+                    Zs.append(self._lift(Zs[-1], len(Zs) - 1, G * N))
+                X = Zs[i].view(G, N, L.D).clone()
+                X[:, :n] = Y.view(G, n, L.D)
+                Y, c = L.fwd(g, xfull=X)
             caches.append(c)
-        return Y, caches
+        return Y, (caches, Zs)
 
     def bwd(self, caches, dZ, g: GraphBatch):
+        caches, Zs = caches
+        G, N, n = g.G, g.N, g.n
+        rows = G * N
         d = dZ
+        acc = None  # gradient of the never-receivers' lifted rows Z_i (rows, D_i), deep stacks only
         for i in range(len(self.layers) - 1, -1, -1):
-            d = self.layers[i].bwd(caches[i], d, g)
+            L = self.layers[i]
+            if i >= 2:
+                dX = L.bwd(caches[i], d, g)  # (G, N, D_i): every sender's row
+                d = dX[:, :n].reshape(G * n, L.D).contiguous()
+                dX[:, :n] = 0.0  # agents' rows came from the previous layer, not from the lift
+                dz = dX.view(rows, L.D)
+                if acc is not None:
+                    dz.add_(acc)
+                P = self.layers[i - 1]  # Z_i = relu(Z_{i-1} Wu_{i-1} + bu_{i-1})
+                K.relu_bwd_(dz, Zs[i])
+                K.gemm(Zs[i - 1], dz, P.v("Wu", True), P.D, P.F, rows, ta=True, beta=1.0, bias_grad=P.v("bu", True))
+                acc = None
+                if i - 1 >= 1:
+                    acc = torch.empty((rows, P.D), device=dz.device)
+                    K.gemm(dz, P.v("Wu"), acc, rows, P.D, P.F, tb=True, ldb=P.F)
+                continue
+            if i == 1 and acc is not None:  # Z_1 = relu(Z_0 Wu_0 + bu_0) of the raw rows Z_0
+                P = self.layers[0]
+                K.relu_bwd_(acc, Zs[1])
+                K.gemm(Zs[0], acc, P.v("Wu", True), P.D, P.F, rows, ta=True, beta=1.0, bias_grad=P.v("bu", True))
+                acc = None
+            d = L.bwd(caches[i], d, g)

@@ -240,18 +240,20 @@ def _gnn_attn_fwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, e
     return None
 
 
-@torch.library.custom_op("dgppo::gnn_attn_bwd", mutates_args=("dqt", "dq", "dbeta", "dxa", "dpre_part"))
+@torch.library.custom_op("dgppo::gnn_attn_bwd", mutates_args=("dqt", "dq", "dbeta", "dxa", "dpre_part", "dx"))
 def gnn_attn_bwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
                  x_gstride: int, ef: Tensor, ef_gstride: int, q: Optional[Tensor], qt: Tensor, bk: Tensor,
                  scale: float, xa: Optional[Tensor], xa_gstride: int, pre_W: Optional[Tensor],
                  pre_b: Optional[Tensor], attn: Tensor, dxcat: Tensor, da_add: Optional[Tensor], dqt: Tensor,
                  dq: Optional[Tensor], dbeta: Tensor, dxa: Optional[Tensor], dxa_gstride: int,
                  dpre_part: Optional[Tensor], beta: Optional[Tensor] = None, beta_ld: int = 0, qt_ld: int = 0,
-                 dqt_ld: int = 0, dbeta_ld: int = 0) -> None:
+                 dqt_ld: int = 0, dbeta_ld: int = 0, dx: Optional[Tensor] = None, dx_gstride: int = 0) -> None:
     """Backward of gnn_attn_fwd given dL/dxcat (+ da_add, extra dL/dattn of edge columns past 4): dqt, dq,
     dbeta (dL/d(q . bk)); in agent mode dxa (accumulated, agent senders) and the partial Dense_4
-    gradients of the recomputed never-receiving senders (dpre_part, one row per workgroup).  Q-free form:
-    dq None (not written), dqt / dbeta row strides dqt_ld / dbeta_ld (e.g. one [dqt | dbeta] buffer)."""
+    gradients of the recomputed never-receiving senders (dpre_part, one row per workgroup); otherwise,
+    if dx is given, the sender gradient of every node row of x (accumulated, graph stride dx_gstride).
+    Q-free form: dq None (not written), dqt / dbeta row strides dqt_ld / dbeta_ld (e.g. one [dqt | dbeta]
+    buffer)."""
     _lib.require_gpu(qt.device, "dgppo::gnn_attn_bwd")
     a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
                      xa_gstride, pre_W, pre_b, beta, beta_ld, qt_ld)
@@ -259,13 +261,14 @@ def gnn_attn_bwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tens
     a.attn, a.dxcat, a.da_add = _p(attn), _p(dxcat), _p(da_add)
     a.dqt, a.dq, a.dbeta = _p(dqt), _p(dq), _p(dbeta)
     a.dxa, a.dxa_gstride, a.dpre_part = _p(dxa), int(dxa_gstride), _p(dpre_part)
+    a.dx, a.dx_gstride = _p(dx), int(dx_gstride)
     _lib.check(_lib.load().dgppo_gnn_attn_bwd(ctypes.byref(a), _stream(qt)), "dgppo_gnn_attn_bwd")
 
 
 @gnn_attn_bwd.register_fake
 def _gnn_attn_bwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, q, qt, bk, scale, xa,
                        xa_gstride, pre_W, pre_b, attn, dxcat, da_add, dqt, dq, dbeta, dxa, dxa_gstride, dpre_part,
-                       beta=None, beta_ld=0, qt_ld=0, dqt_ld=0, dbeta_ld=0) -> None:
+                       beta=None, beta_ld=0, qt_ld=0, dqt_ld=0, dbeta_ld=0, dx=None, dx_gstride=0) -> None:
     return None
 
 

@@ -263,18 +263,19 @@ def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
 
 
 # ---- known-answer test on the attention kernels ----------------------------------
-@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("MPESpread", 3, 3), ("LidarSpread", 32, 8)])
-def test_attention_uniform_logits_give_inverse_in_degree(cuda, eid, n, obs):
+@pytest.mark.parametrize("eid,n,obs,layers", [("LidarSpread", 8, 3, 2), ("MPESpread", 3, 3, 2), ("LidarSpread", 32, 8, 2),
+                                              ("LidarSpread", 8, 3, 3)])
+def test_attention_uniform_logits_give_inverse_in_degree(cuda, eid, n, obs, layers):
     """Wq = 0, bq = 0 makes every logit q.k/sqrt(F) zero, so jraph.segment_softmax gives each of a
-    receiver's in-edges weight exactly 1 / in-degree (masked candidates 0), in both layers (the
-    first reads raw sender rows, the second is the agent-mode kernel)."""
+    receiver's in-edges weight exactly 1 / in-degree (masked candidates 0), in every layer (the
+    first reads raw sender rows, the second is the agent-mode kernel, a third reads materialised rows)."""
     S, L = 2, 3
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=9)
-    net = ActorNet(env.node_dim, n, cuda, seed=1, action_dim=env.action_dim, **_nets_kw(env))
+    net = ActorNet(env.node_dim, n, cuda, seed=1, gnn_layers=layers, action_dim=env.action_dim, **_nets_kw(env))
     for layer in net.gnn.layers:
         layer.v("Wq").zero_()
         layer.v("bq").zero_()
-    _, caches = net.gnn.fwd(gb)
+    _, (caches, _) = net.gnn.fwd(gb)
     torch.cuda.synchronize()
     recv = host["receivers"]
     deg = np.stack([(recv == i).sum(1) for i in range(n)], 1).reshape(-1)  # (G*n,) in-degree of agent rows
@@ -299,3 +300,62 @@ def test_vl_long_scan_matches_oracle(cuda, S, L):
     torch.cuda.synchronize()
     _close(v.cpu().numpy(), rv.detach().numpy(), what="Vl over a long scan")
     _close(hT.cpu().numpy(), rh.detach().numpy(), what="final carry")
+
+
+# GNN stacks deeper than the reference's defaults (--actor-gnn-layers / --Vl-gnn-layers / --Vh-gnn-layers > 2,
+# train.py): layers past the second read materialised node rows (agents: the previous layer's outputs; every other
+# node: its lifted Dense_4 + ReLU chain, nn/layers.py GNN.fwd) and their backward returns every sender's gradient
+DEEP = [("LidarSpread", 8, 3, 3), ("LidarOmniTarget", 3, 2, 3), ("MPESpread", 3, 3, 4)]
+
+
+@pytest.mark.parametrize("eid,n,obs,layers", DEEP)
+def test_deep_gnn_nets_fwd_bwd(cuda, eid, n, obs, layers):
+    S, L = 2, 3
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=8)
+    A = env.action_dim
+    rng = np.random.default_rng(11)
+    # actor: eval_action over the sequences (log pi, entropy and every gradient)
+    net = ActorNet(env.node_dim, n, cuda, seed=9, gnn_layers=layers, action_dim=A, **_nets_kw(env))
+    assert len(net.gnn.layers) == layers and net._fused_args(gb) is None
+    actions = rng.uniform(-0.99, 0.99, (S * L * n, A)).astype(np.float32)
+    eps = rng.standard_normal((n, A)).astype(np.float32)
+    lp, ent, cache = net.eval_seq_fwd(gb, S, L, torch.from_numpy(actions).to(cuda), torch.from_numpy(eps).to(cuda))
+    p = R.to_t(net.flax(), requires_grad=True)
+    rlp, rent = R.actor_eval_seq(p, host, S, L, n, actions, eps)
+    torch.cuda.synchronize()
+    _close(lp.cpu().numpy(), rlp.detach().numpy().reshape(-1), what="log_pi")
+    _close(ent.cpu().numpy(), rent.detach().numpy().reshape(-1), what="entropy")
+    w1, w2 = rng.standard_normal(S * L * n), rng.standard_normal(S * L * n)
+    (rlp.reshape(-1) * torch.tensor(w1) + rent.reshape(-1) * torch.tensor(w2)).sum().backward()
+    net.ps.zero_grad()
+    net.eval_seq_bwd(cache, torch.tensor(w1, dtype=torch.float32, device=cuda),
+                     torch.tensor(w2, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    net.ps.swap_views()
+    g = net.flax()
+    net.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(p)):
+        _grad_close(a, b, f"deep actor grad {path}")
+    # one policy step (the rollout's unfused path) with non-zero carries
+    h = torch.from_numpy(rng.standard_normal((S * L * n, 64)).astype(np.float32) * 0.5).to(cuda)
+    _, _, h2 = net.act(gb, h, 0)
+    h2_ref = R.actor_carry(R.to_t(net.flax()), host, h.cpu().double().reshape(S * L, n, 64), n)
+    torch.cuda.synchronize()
+    _close(h2.cpu().numpy(), h2_ref.numpy().reshape(-1, 64), what="carry")
+    # Vl: values and gradients over the sequences
+    vl = VlNet(env.node_dim, n, cuda, seed=10, gnn_layers=layers, **_nets_kw(env))
+    v, _, vc = vl.seq_fwd(gb, S, L)
+    pv = R.to_t(vl.flax(), requires_grad=True)
+    rv = R.vl_seq(pv, host, S, L, n)
+    torch.cuda.synchronize()
+    _close(v.cpu().numpy(), rv.detach().numpy(), what="Vl")
+    w = rng.standard_normal((S, L))
+    (rv * torch.tensor(w)).sum().backward()
+    vl.ps.zero_grad()
+    vl.seq_bwd(vc, torch.tensor(w, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    vl.ps.swap_views()
+    g = vl.flax()
+    vl.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(pv)):
+        _grad_close(a, b, f"deep Vl grad {path}")
