@@ -258,6 +258,8 @@ SIGNATURES = {
     "dgppo_gnn_attn_fwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
     "dgppo_gnn_attn_bwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
     "dgppo_relu_bwd": (ctypes.c_int, [_V, _V, _I64, _V]),
+    "dgppo_lstm_cell_fwd": (ctypes.c_int, [_I64, ctypes.c_int32, _V, _V, _V, _V, _V]),
+    "dgppo_lstm_cell_bwd": (ctypes.c_int, [_I64, ctypes.c_int32, _V, _V, _V, _V, _V, _V, _V, _V]),
     "dgppo_layernorm_fwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _I64, _I32, _I32, _F32, _V]),
     "dgppo_layernorm_bwd_workspace_floats": (ctypes.c_int64, [_I64, _I32]),
     "dgppo_layernorm_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _I32, _V, _V]),
@@ -298,7 +300,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 6  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 7  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

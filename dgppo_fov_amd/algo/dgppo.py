@@ -105,8 +105,8 @@ class DGPPO:
                  rnn_layers: int = 1, rnn_step: int = 16, use_lstm: bool = False, alpha: float = 10.0,
                  cbf_eps: float = 1e-2, cbf_weight: float = 1.0, train_steps: int = int(1e5),
                  cbf_schedule: bool = True, device=None, **kwargs):
-        if not use_rnn or use_lstm or rnn_layers != 1:
-            raise NotImplementedError("the MI355X path implements the reference default: 1-layer GRU policy/critics")
+        if rnn_layers < 1:
+            raise ValueError(f"rnn_layers {rnn_layers} < 1")
         self._env = env
         self.device = torch.device(device) if device is not None else env.device
         self._node_dim, self._edge_dim, self._action_dim, self._n_agents = node_dim, edge_dim, action_dim, n_agents
@@ -121,11 +121,14 @@ class DGPPO:
         self.rank = dist.get_rank() if self.world > 1 else 0
 
         dev = self.device
+        # RNN(GRUCell | LSTMCell, rnn_layers) or none (--no-rnn / --use-lstm / --rnn-layers, nn/rnn.py:10-30)
+        rk = dict(rnn="none" if not use_rnn else ("lstm" if use_lstm else "gru"), rnn_layers=rnn_layers)
         self.actor = ActorNet(node_dim, n_agents, dev, seed=seed * 3 + 0, gnn_layers=actor_gnn_layers,
-                              action_dim=action_dim, edge_dim=edge_dim)
-        self.Vl = VlNet(node_dim, n_agents, dev, seed=seed * 3 + 1, gnn_layers=Vl_gnn_layers, edge_dim=edge_dim)
+                              action_dim=action_dim, edge_dim=edge_dim, **rk)
+        self.Vl = VlNet(node_dim, n_agents, dev, seed=seed * 3 + 1, gnn_layers=Vl_gnn_layers, edge_dim=edge_dim, **rk)
         self.Vh = self.VH_NET(node_dim, n_agents, env.n_cost, dev, seed=seed * 3 + 2, gnn_layers=Vh_gnn_layers,
-                              edge_dim=edge_dim)
+                              edge_dim=edge_dim, **rk)
+        self.n_carries = self.actor.gru.carries
         # one flat gradient buffer for the three nets (one all-reduce per minibatch)
         sizes = [self.Vl.ps.size, self.Vh.ps.size, self.actor.ps.size]
         self.grad_flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
@@ -140,8 +143,8 @@ class DGPPO:
         # identical for every vmapped env/step (distribution.py:37-43); here: a fixed (n, A) draw
         self.entropy_eps = torch.from_numpy(
             np.random.default_rng(10_000 + seed).standard_normal((n_agents, action_dim)).astype(np.float32)).to(dev)
-        self.init_rnn_state = torch.zeros((rnn_layers, n_agents, 1, 64), device=dev)
-        self.init_Vl_rnn_state = torch.zeros((rnn_layers, 1, 1, 64), device=dev)
+        self.init_rnn_state = torch.zeros((rnn_layers, n_agents, self.n_carries, 64), device=dev)
+        self.init_Vl_rnn_state = torch.zeros((rnn_layers, 1, self.n_carries, 64), device=dev)
         self._engines = {}
         self.trace: Optional[dict] = None  # set to {} to record update intermediates (parity tests)
         self.key = np.random.default_rng(seed)
@@ -204,14 +207,24 @@ class DGPPO:
     def _gb(self, graph) -> GraphBatch:
         return GraphBatch.from_graph(graph, self._env)
 
+    @staticmethod
+    def _rows(rs: torch.Tensor) -> torch.Tensor:
+        """Reference carry layout (..., rnn_layers, n, carries, 64) -> the kernels' agent-major rows (..., n, W)
+        (a view of the rollout engine's (T+1, B, n, W) buffer)."""
+        return rs.movedim(-3, -4).flatten(-3)
+
+    def _unrows(self, h: torch.Tensor) -> torch.Tensor:
+        """(..., n, W) carry rows -> the reference layout (..., rnn_layers, n, carries, 64)."""
+        return h.unflatten(-1, (self.rnn_layers, self.n_carries, 64)).movedim(-4, -3)
+
     def act(self, graph, rnn_state: torch.Tensor, params=None):
-        """get_action for a batch of graphs: rnn_state (B, 1, n, 1, 64) -> (action (B, n, A), rnn)."""
+        """get_action for a batch of graphs: rnn_state (B, rnn_layers, n, carries, 64) -> (action (B, n, A), rnn)."""
         self._check_params(params)
         g = self._gb(graph)
         B, n = g.G, self._n_agents
-        h = rnn_state.reshape(B * n, 64).contiguous()
+        h = self._rows(rnn_state).reshape(B * n, -1).contiguous()
         a, _, h2 = self.actor.act(g, h, 0)
-        return a.view(B, n, -1), h2.view(B, 1, n, 1, 64)
+        return a.view(B, n, -1), self._unrows(h2.view(B, n, -1))
 
     def step(self, graph, rnn_state: torch.Tensor, key: int, params=None):
         """sample_action: (action, log_pi (B, n), rnn)."""
@@ -219,8 +232,8 @@ class DGPPO:
         B, n = g.G, self._n_agents
         noise = torch.empty((B * n, self._action_dim), device=self.device)
         K.normal_(noise, seed=int(key))
-        a, lp, h2 = self.actor.act(g, rnn_state.reshape(B * n, 64).contiguous(), 1, noise=noise)
-        return a.view(B, n, -1), lp.view(B, n), h2.view(B, 1, n, 1, 64)
+        a, lp, h2 = self.actor.act(g, self._rows(rnn_state).reshape(B * n, -1).contiguous(), 1, noise=noise)
+        return a.view(B, n, -1), lp.view(B, n), self._unrows(h2.view(B, n, -1))
 
     def _rollout_lanes(self, n_env: int) -> int:
         """Env slices on separate streams (RolloutEngine lanes): DGPPO_ROLLOUT_LANES when the slices are
@@ -320,12 +333,12 @@ class DGPPO:
         for e0 in range(0, B, chunk):
             e1 = min(B, e0 + chunk)
             g = self._graphs(rollout.graph, slice(e0, e1))
-            h = rollout.rnn_states[e0:e1].reshape((e1 - e0) * T * n, 64).contiguous()
+            h = self._rows(rollout.rnn_states[e0:e1]).reshape((e1 - e0) * T * n, -1).contiguous()
             v, _ = self.Vh.fwd(g, h, keep_cache=False)
             out[e0:e1, :T].copy_(v.view(e1 - e0, T, n, -1))
             # final: act on next_graph[-1] from rnn_states[-1], then Vh with that carry
             gl = self._last_graph(rollout.next_graph, slice(e0, e1))
-            h_last = rollout.rnn_states[e0:e1, -1].reshape((e1 - e0) * n, 64).contiguous()
+            h_last = self._rows(rollout.rnn_states[e0:e1, -1]).reshape((e1 - e0) * n, -1).contiguous()
             _, _, h2 = self.actor.act(gl, h_last, 0)
             vf, _ = self.Vh.fwd(gl, h2, keep_cache=False)
             out[e0:e1, T].copy_(vf.view(e1 - e0, n, -1))
@@ -432,7 +445,7 @@ class DGPPO:
         g = self._graph_batch(nodes, edges, recv, send).prepare()
         dg = det.graph
         dnodes, dedges, drecv, dsend, hd, qhd = self._gather(
-            envs, dg.nodes, dg.edges, dg.receivers, dg.senders, det.rnn_states, Qh_det)
+            envs, dg.nodes, dg.edges, dg.receivers, dg.senders, self._rows(det.rnn_states), Qh_det)
         gd = self._graph_batch(dnodes, dedges, drecv, dsend).prepare()
         tgt = tgt.view(Bm * S_per_env, L)
         acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
@@ -450,7 +463,7 @@ class DGPPO:
             return loss
 
         def vh_job():  # update_Vh (dgppo.py:296-321) on the deterministic rollout
-            vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, 64))
+            vh, cache = self.Vh.fwd(gd, hd.view(Bm * T * n, -1))
             dvh = torch.empty_like(vh)
             loss = torch.empty(1, device=dev)
             K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)

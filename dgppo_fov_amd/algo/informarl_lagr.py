@@ -28,7 +28,7 @@ class InforMARLLagr(InforMARL):
         super().__init__(*args, cost_weight=0.0, **kwargs)
         self.lagr_init, self.lr_lagr = float(lagr_init), float(lr_lagr)
         self.ah_lagr = torch.full((self._n_agents, self._env.n_cost), self.lagr_init, device=self.device)
-        self.init_Vh_rnn_state = torch.zeros((self.rnn_layers, self._n_agents, 1, 64), device=self.device)
+        self.init_Vh_rnn_state = torch.zeros((self.rnn_layers, self._n_agents, self.n_carries, 64), device=self.device)
 
     @property
     def config(self) -> dict:
@@ -169,4 +169,8 @@ class InforMARLLagr(InforMARL):
         super().load(load_dir, step)
         fn = os.path.join(load_dir, str(step), "lagr.pt")
         if os.path.exists(fn):
-            self.ah_lagr.copy_(torch.load(fn, weights_only=True)["ah_lagr"])
+            lagr = torch.load(fn, weights_only=True)["ah_lagr"]
+            # per-(agent, cost) multipliers of the training agent count: an eval on another -n (test.py) does not
+            # use them, and the reference's checkpoint holds the networks only (informarl_lagr.py:311-327)
+            if lagr.shape == self.ah_lagr.shape:
+                self.ah_lagr.copy_(lagr)

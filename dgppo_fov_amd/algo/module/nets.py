@@ -24,7 +24,7 @@ import torch
 
 from ... import _lib
 from ...nn import kernels as K
-from ...nn.layers import GNN, Dense, GraphBatch, GRUCell, MLPHead, ParamSpace
+from ...nn.layers import GNN, Dense, GraphBatch, MLPHead, ParamSpace, RNNStack
 
 STD_DEV_INIT_INV = math.log(math.exp(0.5) - 1.0)  # TanhNormal.std_dev_init_inv (policy.py:54-59)
 STD_DEV_MIN = 1e-5
@@ -42,16 +42,21 @@ class _Net:
     def n_params(self):
         return self.ps.size
 
+    @property
+    def carry_width(self) -> int:
+        """floats per agent carry row: (rnn_layers, carries, 64) flattened (64 for the 1-layer GRU default)."""
+        return self.gru.W
+
 
 class ActorNet(_Net):
     def __init__(self, node_dim: int, n_agents: int, device, seed: int = 0, gnn_layers: int = 2, action_dim: int = 2,
-                 edge_dim: int = 4):
+                 edge_dim: int = 4, rnn: str = "gru", rnn_layers: int = 1):
         self.n, self.A = n_agents, action_dim
         self.node_dim, self.edge_dim = node_dim, edge_dim
         ps = self.ps = ParamSpace()
         self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head")
-        self.gru = GRUCell(ps, "gru")
+        self.gru = RNNStack(ps, "gru", rnn, rnn_layers)  # RNN(GRUCell | LSTMCell, layers) or none
         self.scale_hid = Dense(ps, "ScaleHid", 64, 64, scale=0.01)
         self.mean = Dense(ps, "OutputDenseMean", 64, action_dim)
         self.std = Dense(ps, "OutputDenseStdTrans", 64, action_dim)
@@ -86,8 +91,8 @@ class ActorNet(_Net):
     def _fused_args(self, g: GraphBatch):
         """dgppo_policy_step_args with this net's parameter pointers (None if the fused kernel does not
         cover the configuration)."""
-        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1" or len(self.gnn.layers) > 2:
-            return None  # (the fused kernel holds at most 2 GNN layers; deeper stacks run the layer chain)
+        if os.environ.get("DGPPO_FUSED_POLICY", "1") != "1" or len(self.gnn.layers) > 2 or not self.gru.simple:
+            return None  # (the fused kernel holds at most 2 GNN layers and one GRU layer; else the layer chain)
         a = _lib.PolicyStepArgs()
         a.N, a.E, a.n_agents, a.C, a.D0, a.A = g.N, g.E, self.n, g.C, g.nodes.shape[2], self.A
         a.n_layers, a.H, a.ED = len(self.gnn.layers), 3, g.ED
@@ -101,8 +106,9 @@ class ActorNet(_Net):
         a.head_W0, a.head_b0, a.head_W1, a.head_b1 = K._p(hd.d0.W()), K._p(hd.d0.b()), K._p(hd.d1.W()), K._p(hd.d1.b())
         a.ln0_s, a.ln0_b = K._p(self.ps.view(hd.ln0.name + ".scale")), K._p(self.ps.view(hd.ln0.name + ".bias"))
         a.ln1_s, a.ln1_b = K._p(self.ps.view(hd.ln1.name + ".scale")), K._p(self.ps.view(hd.ln1.name + ".bias"))
-        a.gru_Wi, a.gru_bi = K._p(self.gru.v("Wi")), K._p(self.gru.v("bi"))
-        a.gru_Wh, a.gru_bhn = K._p(self.gru.v("Wh")), K._p(self.gru.v("bhn"))
+        gru = self.gru.cells[0]
+        a.gru_Wi, a.gru_bi = K._p(gru.v("Wi")), K._p(gru.v("bi"))
+        a.gru_Wh, a.gru_bhn = K._p(gru.v("Wh")), K._p(gru.v("bhn"))
         a.Ws, a.bs = K._p(self.scale_hid.W()), K._p(self.scale_hid.b())
         a.Wm, a.bm, a.Wsd, a.bsd = K._p(self.mean.W()), K._p(self.mean.b()), K._p(self.std.W()), K._p(self.std.b())
         a.std_shift, a.std_min = STD_DEV_INIT_INV, STD_DEV_MIN
@@ -138,8 +144,8 @@ class ActorNet(_Net):
             K._chk(_lib.load().dgppo_policy_step(ctypes.byref(fa), _lib.stream_handle(dev)), "dgppo_policy_step")
             return action, log_pi, h2
         y, _ = self._trunk(g)
-        h2, _ = self.gru.fwd(y, h, h_out=h_out)
-        _, mu, sr = self._outputs(h2)
+        feat, h2, _ = self.gru.fwd(y, h, h_out=h_out)
+        _, mu, sr = self._outputs(feat)
         action = action_out if action_out is not None else torch.empty((rows, self.A), device=h.device)
         log_pi = log_pi_out if log_pi_out is not None else torch.empty(rows, device=h.device)
         a = _lib.TanhNormalArgs()
@@ -196,12 +202,13 @@ class ActorNet(_Net):
 
 
 class VlNet(_Net):
-    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 1, gnn_layers: int = 2, edge_dim: int = 4):
+    def __init__(self, node_dim: int, n_agents: int, device, seed: int = 1, gnn_layers: int = 2, edge_dim: int = 4,
+                 rnn: str = "gru", rnn_layers: int = 1):
         self.n = n_agents
         ps = self.ps = ParamSpace()
         self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head")
-        self.gru = GRUCell(ps, "gru")
+        self.gru = RNNStack(ps, "gru", rnn, rnn_layers)  # RNN(GRUCell | LSTMCell, layers) or none
         self.out = Dense(ps, "out", 64, 1)
         self.modules = [self.gnn, self.head, self.gru, self.out]
         ps.build(device)
@@ -224,7 +231,7 @@ class VlNet(_Net):
         zm = torch.empty((G, 64), device=dev)
         K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
         y, hc = self.head.fwd(zm)
-        hT = torch.empty((S, 64), device=dev)
+        hT = torch.empty((S, self.gru.W), device=dev)
         Hs, gcs = self.gru.seq_fwd(y, S, L, 1, h0=h0, hT_out=hT)
         v = self.out.fwd(Hs, G)
         cache = (g, S, L, gc, z, hc, gcs, Hs) if keep_cache else None
@@ -244,12 +251,12 @@ class VlNet(_Net):
 
 class VhNet(_Net):
     def __init__(self, node_dim: int, n_agents: int, n_cost: int, device, seed: int = 2, gnn_layers: int = 1,
-                 edge_dim: int = 4):
+                 edge_dim: int = 4, rnn: str = "gru", rnn_layers: int = 1):
         self.n, self.n_cost = n_agents, n_cost
         ps = self.ps = ParamSpace()
         self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head")
-        self.gru = GRUCell(ps, "gru")
+        self.gru = RNNStack(ps, "gru", rnn, rnn_layers)  # RNN(GRUCell | LSTMCell, layers) or none
         self.out = Dense(ps, "out", 64, n_cost)
         self.modules = [self.gnn, self.head, self.gru, self.out]
         ps.build(device)
@@ -264,11 +271,11 @@ class VhNet(_Net):
         self.out.load_flax(d["out"])
 
     def fwd(self, g: GraphBatch, h: torch.Tensor, keep_cache=True):
-        """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, 64): (G*n, n_cost)."""
+        """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, W): (G*n, n_cost)."""
         rows = g.G * self.n
         z, gc = self.gnn.fwd(g)
         y, hc = self.head.fwd(z)
-        h2, rc = self.gru.fwd(y, h)
+        h2, _, rc = self.gru.fwd(y, h)
         out = self.out.fwd(h2, rows)
         return out, ((g, gc, hc, rc, h2) if keep_cache else None)
 
@@ -289,12 +296,12 @@ class VhGlobalNet(_Net):
     (one GEMM of the agent-mean rows, added per graph through the GEMM addend's row grouping)."""
 
     def __init__(self, node_dim: int, n_agents: int, n_cost: int, device, seed: int = 2, gnn_layers: int = 1,
-                 edge_dim: int = 4):
+                 edge_dim: int = 4, rnn: str = "gru", rnn_layers: int = 1):
         self.n, self.n_cost = n_agents, n_cost
         ps = self.ps = ParamSpace()
         self.gnn = GNN(ps, "gnn", node_dim, gnn_layers, edge_dim=edge_dim)
         self.head = MLPHead(ps, "head", d_in=128)
-        self.gru = GRUCell(ps, "gru")
+        self.gru = RNNStack(ps, "gru", rnn, rnn_layers)  # RNN(GRUCell | LSTMCell, layers) or none
         self.out = Dense(ps, "out", 64, n_cost)
         self.modules = [self.gnn, self.head, self.gru, self.out]
         ps.build(device)
@@ -326,7 +333,7 @@ class VhGlobalNet(_Net):
         y0, c0 = hd.ln0.fwd(h0pre)
         h1 = hd.d1.fwd(y0, rows)
         y1, c1 = hd.ln1.fwd(h1)
-        hT = torch.empty((S * n, 64), device=dev)
+        hT = torch.empty((S * n, self.gru.W), device=dev)
         Hs, gcs = self.gru.seq_fwd(y1, S * n, L, n, h0=h0, hT_out=hT)
         out = self.out.fwd(Hs, rows)
         cache = (g, S, L, gc, z, zm, y0, c0, c1, gcs, Hs) if keep_cache else None

@@ -716,6 +716,52 @@ static int grid_for(int64_t n) {
   return (int)(b < 8192 ? (b < 1 ? 1 : b) : 8192);
 }
 
+// flax.linen.LSTMCell gate math for one step of `rows` carries (the --use-lstm option, dgppo/nn/rnn.py:15-30):
+// g (rows, 4H) = [i | f | g | o] pre-activations (x W_i + h W_h + b, from the GEMMs) -> activated in place;
+// c' = f c + i g, h' = o tanh(c').  A thread per (row, column); the gate columns of a row are H apart.
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(int64_t rows, int H, float* __restrict__ g,
+                                                            const float* __restrict__ c_prev, float* __restrict__ c_out,
+                                                            float* __restrict__ h_out) {
+  const int64_t total = rows * H;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / H;
+    const int j = (int)(t - r * H);
+    float* gr = g + r * 4 * H + j;
+    const float i = sigm(gr[0]), f = sigm(gr[H]), gg = tanhf(gr[2 * H]), o = sigm(gr[3 * H]);
+    const float c = f * (c_prev ? c_prev[t] : 0.0f) + i * gg;
+    gr[0] = i, gr[H] = f, gr[2 * H] = gg, gr[3 * H] = o;
+    c_out[t] = c;
+    h_out[t] = o * tanhf(c);
+  }
+}
+
+// backward of one step: g = the activated gates, c = c', dh = dL/dh' (incl. the recurrent part), dc = dL/dc' from
+// the next step (null: 0) -> dg (rows, 4H) pre-activation gradients, dc_prev = dL/dc (null: not wanted)
+__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int64_t rows, int H, const float* __restrict__ g,
+                                                            const float* __restrict__ c_prev,
+                                                            const float* __restrict__ c, const float* __restrict__ dh,
+                                                            const float* __restrict__ dc, float* __restrict__ dg,
+                                                            float* __restrict__ dc_prev) {
+  const int64_t total = rows * H;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / H;
+    const int j = (int)(t - r * H);
+    const float* gr = g + r * 4 * H + j;
+    const float i = gr[0], f = gr[H], gg = gr[2 * H], o = gr[3 * H];
+    const float tc = tanhf(c[t]);
+    const float cp = c_prev ? c_prev[t] : 0.0f;
+    const float dcc = dh[t] * o * (1.0f - tc * tc) + (dc ? dc[t] : 0.0f);
+    float* dr = dg + r * 4 * H + j;
+    dr[0] = dcc * gg * i * (1.0f - i);
+    dr[H] = dcc * cp * f * (1.0f - f);
+    dr[2 * H] = dcc * i * (1.0f - gg * gg);
+    dr[3 * H] = dh[t] * tc * o * (1.0f - o);
+    if (dc_prev) dc_prev[t] = dcc * f;
+  }
+}
+
 }  // namespace dgppo
 
 using namespace dgppo;
@@ -726,6 +772,24 @@ extern "C" int dgppo_relu_bwd(float* dy, const float* y, int64_t n, void* stream
   if (n < 0 || !dy || !y) return DGPPO_EINVAL;
   if (n == 0) return 0;
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), dy, y, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_lstm_cell_fwd(int64_t rows, int32_t H, float* g, const float* c_prev, float* c_out, float* h_out,
+                                   void* stream) {
+  if (rows < 0 || H < 1 || !g || !c_out || !h_out) return DGPPO_EINVAL;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(grid_for(rows * H)), dim3(256), 0, DG_STREAM(stream), rows, H, g,
+                     c_prev, c_out, h_out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_lstm_cell_bwd(int64_t rows, int32_t H, const float* g, const float* c_prev, const float* c,
+                                   const float* dh, const float* dc, float* dg, float* dc_prev, void* stream) {
+  if (rows < 0 || H < 1 || !g || !c || !dh || !dg) return DGPPO_EINVAL;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(grid_for(rows * H)), dim3(256), 0, DG_STREAM(stream), rows, H, g,
+                     c_prev, c, dh, dc, dg, dc_prev);
   return (int)hipGetLastError();
 }
 

@@ -84,6 +84,16 @@ def relu_bwd_(dy, y):
     _chk(_lib.load().dgppo_relu_bwd(_p(dy), _p(y), int(dy.numel()), _stream(dy)), "dgppo_relu_bwd")
 
 
+def lstm_cell_fwd(rows, H, g, c_prev, c_out, h_out):
+    _chk(_lib.load().dgppo_lstm_cell_fwd(int(rows), int(H), _p(g), _p(c_prev), _p(c_out), _p(h_out), _stream(g)),
+         "dgppo_lstm_cell_fwd")
+
+
+def lstm_cell_bwd(rows, H, g, c_prev, c, dh, dc, dg, dc_prev):
+    _chk(_lib.load().dgppo_lstm_cell_bwd(int(rows), int(H), _p(g), _p(c_prev), _p(c), _p(dh), _p(dc), _p(dg),
+                                         _p(dc_prev), _stream(g)), "dgppo_lstm_cell_bwd")
+
+
 def layernorm_fwd(x, scale, bias, y, mean, rstd, relu=True, eps=1e-6):
     rows, F = x.shape
     _chk(_lib.load().dgppo_layernorm_fwd(_p(x), _p(scale), _p(bias), _p(y), _p(mean), _p(rstd), int(rows), int(F),

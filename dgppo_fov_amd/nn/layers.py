@@ -307,6 +307,204 @@ class GRUCell:
         return self.seq_bwd(cache, dhn, need_dx=need_dx, need_dh0=True)
 
 
+class LSTMCell:
+    """flax.linen.LSTMCell(features=64) (the --use-lstm option of dgppo/nn/rnn.py:21-23): gates
+    [i | f | g | o] = x Wi + h Wh + b (the input Denses ii/if/ig/io have no bias, the hidden ones hi/hf/hg/ho
+    do), c' = f c + i g, h' = o tanh(c').  Carry rows [c | h] (2 H floats), the reference's stacked (c, h).
+    Sequences run time-major inside: one GEMM of every step's input projection, then per step one GEMM of
+    the recurrent projection and one gate kernel (dgppo_lstm_cell_fwd / _bwd)."""
+
+    carries = 2
+
+    def __init__(self, ps, name, d_in=64, H=64):
+        self.ps, self.name, self.d_in, self.H = ps, name, d_in, H
+        ps.add(name + ".Wi", (d_in, 4 * H), "lecun")
+        ps.add(name + ".Wh", (H, 4 * H), "orthogonal")
+        ps.add(name + ".b", (4 * H,), "zeros")
+
+    def v(self, k, g=False):
+        return self.ps.view(self.name + "." + k, g)
+
+    def init_host(self, rng):
+        H = self.H
+        wi = np.concatenate([lecun_normal(rng, (self.d_in, H)) for _ in range(4)], axis=1)
+        wh = np.concatenate([orthogonal(rng, (H, H)) for _ in range(4)], axis=1)
+        self.v("Wi").copy_(torch.from_numpy(wi))
+        self.v("Wh").copy_(torch.from_numpy(wh))
+
+    _GATES = ("i", "f", "g", "o")
+
+    def flax(self):
+        H = self.H
+        wi, wh, b = (self.v(k).cpu().numpy() for k in ("Wi", "Wh", "b"))
+        d = {}
+        for k, gate in enumerate(self._GATES):
+            d["i" + gate] = {"kernel": wi[:, k * H:(k + 1) * H]}
+            d["h" + gate] = {"kernel": wh[:, k * H:(k + 1) * H], "bias": b[k * H:(k + 1) * H]}
+        return d
+
+    def load_flax(self, d):
+        f32 = lambda a: np.asarray(a, np.float32)  # noqa: E731
+        self.v("Wi").copy_(torch.from_numpy(np.concatenate([f32(d["i" + g]["kernel"]) for g in self._GATES], 1)))
+        self.v("Wh").copy_(torch.from_numpy(np.concatenate([f32(d["h" + g]["kernel"]) for g in self._GATES], 1)))
+        self.v("b").copy_(torch.from_numpy(np.concatenate([f32(d["h" + g]["bias"]) for g in self._GATES])))
+
+    def seq_fwd(self, x, Q, L, n, h0=None, hs_out=None, hT_out=None):
+        """Same contract as GRUCell.seq_fwd, carries (Q, 2H) = [c | h]: returns (hs (Q*L, H), cache)."""
+        H, dev = self.H, x.device
+        S = Q // n
+        xt = x.view(S, L, n, self.d_in).transpose(0, 1).reshape(L * Q, self.d_in)  # rows (t, s, agent)
+        G = torch.empty((L, Q, 4 * H), device=dev)
+        K.gemm(xt, self.v("Wi"), G.view(L * Q, 4 * H), L * Q, 4 * H, self.d_in)
+        cs = torch.empty((L, Q, H), device=dev)
+        hst = torch.empty((L, Q, H), device=dev)
+        c0 = h0[:, :H].contiguous() if h0 is not None else None
+        hh0 = h0[:, H:].contiguous() if h0 is not None else torch.zeros((Q, H), device=dev)
+        c_prev, h_prev = c0, hh0
+        for t in range(L):
+            K.gemm(h_prev, self.v("Wh"), G[t], Q, 4 * H, H, bias=self.v("b"), beta=1.0)
+            K.lstm_cell_fwd(Q, H, G[t], c_prev, cs[t], hst[t])
+            c_prev, h_prev = cs[t], hst[t]
+        hs = hs_out if hs_out is not None else torch.empty((Q * L, H), device=dev)
+        hs.view(S, L, n, H).copy_(hst.view(L, S, n, H).transpose(0, 1))
+        if hT_out is not None:
+            hT_out[:, :H] = cs[L - 1]
+            hT_out[:, H:] = hst[L - 1]
+        return hs, (xt, G, cs, hst, c0, hh0, Q, L, n)
+
+    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False):
+        """Backward of seq_fwd: accumulates dWi, dWh, db; returns (dx, dh0 (Q, 2H) = [dc0 | dh0])."""
+        xt, G, cs, hst, c0, hh0, Q, L, n = cache
+        H, dev = self.H, dhs.device
+        S = Q // n
+        dht = dhs.view(S, L, n, H).transpose(0, 1).contiguous()  # (L, S, n, H): accumulates the recurrent part
+        dht = dht.view(L, Q, H)
+        dG = torch.empty((L, Q, 4 * H), device=dev)
+        dh0 = torch.empty((Q, 2 * H), device=dev) if need_dh0 else None
+        dc = None
+        for t in range(L - 1, -1, -1):
+            c_prev = cs[t - 1] if t > 0 else c0
+            dcp = torch.empty((Q, H), device=dev) if (t > 0 or need_dh0) else None
+            K.lstm_cell_bwd(Q, H, G[t], c_prev, cs[t], dht[t], dc, dG[t], dcp)
+            if t > 0:
+                K.gemm(dG[t], self.v("Wh"), dht[t - 1], Q, H, 4 * H, tb=True, ldb=4 * H, beta=1.0)
+            elif need_dh0:
+                dh0[:, :H] = dcp
+                hpart = torch.empty((Q, H), device=dev)
+                K.gemm(dG[0], self.v("Wh"), hpart, Q, H, 4 * H, tb=True, ldb=4 * H)
+                dh0[:, H:] = hpart
+            dc = dcp
+        hprev = torch.cat([hh0.unsqueeze(0), hst[:L - 1]], 0).view(L * Q, H)
+        dGf = dG.view(L * Q, 4 * H)
+        dWh, db = self.v("Wh", True), self.v("b", True)
+        for j in (0, 2 * H):  # two 2H-column halves: the weight-gradient kernel (fused bias colsum) takes N <= 192
+            K.gemm(hprev, dGf, dWh, H, 2 * H, L * Q, ta=True, ldb=4 * H, b_off=j, ldc=4 * H, c_off=j, beta=1.0,
+                   bias_grad=db[j:j + 2 * H])
+        K.gemm(xt, dGf, self.v("Wi", True), self.d_in, 4 * H, L * Q, ta=True, beta=1.0)
+        dx = None
+        if need_dx:
+            dxt = torch.empty((L * Q, self.d_in), device=dev)
+            K.gemm(dGf, self.v("Wi"), dxt, L * Q, self.d_in, 4 * H, tb=True, ldb=4 * H)
+            dx = dxt.view(L, S, n, self.d_in).transpose(0, 1).reshape(Q * L, self.d_in)
+        return dx, dh0
+
+
+class RNNStack:
+    """RNN(rnn_cls, rnn_layers) of dgppo/nn/rnn.py:10-30: `layers` GRUCell / LSTMCell(64) applied in turn (each
+    layer's output is the next one's input), or kind "none" (use_rnn=False: the features pass through and the
+    carry is kept, policy.py:174-181 / value.py:142-150).  Carry rows hold the reference's (layers, carries, 64)
+    flattened: W = layers * carries * 64 floats.  The default (one GRU layer) is exactly GRUCell, same parameter
+    names; its carry is the output."""
+
+    def __init__(self, ps, name, kind="gru", layers=1, d_in=64, H=64):
+        if kind not in ("gru", "lstm", "none") or layers < 1:
+            raise ValueError(f"RNN kind {kind!r}, layers {layers}")
+        self.kind, self.H, self.layers = kind, H, layers
+        self.carries = 2 if kind == "lstm" else 1
+        self.simple = kind == "gru" and layers == 1
+        if kind == "none":
+            self.cells = []
+        elif self.simple:
+            self.cells = [GRUCell(ps, name, d_in, H)]
+        else:
+            cls = GRUCell if kind == "gru" else LSTMCell
+            self.cells = [cls(ps, f"{name}.{cls.__name__}_{k}", d_in if k == 0 else H, H) for k in range(layers)]
+        self.widths = [getattr(c, "carries", 1) * H for c in self.cells]
+        self.W = sum(self.widths) if self.cells else layers * H  # (no RNN: the reference's unused zero carry)
+
+    def init_host(self, rng):
+        for c in self.cells:
+            c.init_host(rng)
+
+    def flax(self):
+        """One GRUCell tree for the default; else the list of cell trees ([] without an RNN)."""
+        return self.cells[0].flax() if self.simple else [c.flax() for c in self.cells]
+
+    def load_flax(self, d):
+        if self.simple:
+            self.cells[0].load_flax(d)
+        else:
+            for c, dc in zip(self.cells, d):
+                c.load_flax(dc)
+
+    def seq_fwd(self, x, Q, L, n, h0=None, hs_out=None, hT_out=None):
+        """Scan over L steps of Q carries (GRUCell.seq_fwd's row order); h0 / hT_out (Q, W).  Returns the last
+        layer's outputs (Q*L, 64) and the cache."""
+        if self.simple:
+            return self.cells[0].seq_fwd(x, Q, L, n, h0=h0, hs_out=hs_out, hT_out=hT_out)
+        if not self.cells:
+            if hT_out is not None:
+                if h0 is None:
+                    hT_out.zero_()
+                else:
+                    hT_out.copy_(h0)
+            if hs_out is not None:
+                hs_out.copy_(x)
+                return hs_out, None
+            return x, None
+        caches, off = [], 0
+        for k, (c, w) in enumerate(zip(self.cells, self.widths)):
+            h0k = h0[:, off:off + w].contiguous() if h0 is not None else None
+            hTk = torch.empty((Q, w), device=x.device) if hT_out is not None else None
+            last = k == len(self.cells) - 1
+            x, ck = c.seq_fwd(x, Q, L, n, h0=h0k, hT_out=hTk, hs_out=hs_out if last else None)
+            if hT_out is not None:
+                hT_out[:, off:off + w] = hTk
+            caches.append(ck)
+            off += w
+        return x, caches
+
+    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False):
+        """Backward of seq_fwd: returns (dx, dh0 (Q, W))."""
+        if self.simple:
+            return self.cells[0].seq_bwd(cache, dhs, need_dx=need_dx, need_dh0=need_dh0)
+        if not self.cells:
+            return (dhs if need_dx else None), (torch.zeros((dhs.shape[0], self.W), device=dhs.device)
+                                                if need_dh0 else None)
+        dh0s = []
+        d = dhs
+        for k in range(len(self.cells) - 1, -1, -1):
+            d, dh0k = self.cells[k].seq_bwd(cache[k], d, need_dx=need_dx or k > 0, need_dh0=need_dh0)
+            dh0s.append(dh0k)
+        dh0 = torch.cat(dh0s[::-1], 1) if need_dh0 else None
+        return d, dh0
+
+    def fwd(self, x, h, h_out=None):
+        """One step for `rows` independent carries h (rows, W) (act / get_Vh): (output (rows, 64), new carries
+        (rows, W), cache)."""
+        rows = h.shape[0]
+        if self.simple:
+            h2, c = self.cells[0].fwd(x, h, h_out=h_out)
+            return h2, h2, c
+        h2 = h_out if h_out is not None else torch.empty((rows, self.W), device=h.device)
+        y, c = self.seq_fwd(x, rows, 1, 1, h0=h, hT_out=h2)
+        return y, h2, c
+
+    def bwd(self, cache, dy, need_dx=True):
+        """returns (dx, dh)"""
+        return self.seq_bwd(cache, dy, need_dx=need_dx, need_dh0=True)
+
+
 class GraphTransformer:
     """GraphTransformer layer (dgppo/nn/gnn.py:78-117) in the per-receiving-agent form."""
 

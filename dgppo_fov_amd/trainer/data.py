@@ -12,7 +12,7 @@ from ..utils.graph import GraphsTuple
 class Rollout(NamedTuple):
     graph: GraphsTuple
     actions: torch.Tensor  # (B, T, n, 2)
-    rnn_states: Optional[torch.Tensor]  # (B, T, L, n, 1, 64) actor carries
+    rnn_states: Optional[torch.Tensor]  # (B, T, rnn_layers, n, carries, 64) actor carries
     rewards: torch.Tensor  # (B, T)
     costs: torch.Tensor  # (B, T, n, n_cost)
     dones: torch.Tensor  # (B, T) bool

@@ -58,7 +58,8 @@ class RolloutEngine:
         self.dones = torch.zeros((T, B), dtype=torch.bool, device=dev)
         self.key = torch.zeros(1, dtype=torch.int64, device=dev)
         if actor is not None:
-            self.rnn = torch.zeros((T + 1, B, n, 64), dtype=torch.float32, device=dev)
+            self.W = actor.carry_width  # carry floats per agent: (rnn_layers, carries, 64) flattened
+            self.rnn = torch.zeros((T + 1, B, n, self.W), dtype=torch.float32, device=dev)
             self.log_pis = torch.zeros((T, B, n), dtype=torch.float32, device=dev)
             self.noise = torch.empty((B * n, env.action_dim), dtype=torch.float32, device=dev)
         self._hip_graph = None
@@ -84,8 +85,8 @@ class RolloutEngine:
 
     def _act_slice(self, t: int, sl: slice, k: int):
         n, A, w = self.env.num_agents, self.env.action_dim, sl.stop - sl.start
-        h = self.rnn[t][sl].view(w * n, 64)
-        kw = dict(action_out=self.actions[t][sl].view(-1, A), h_out=self.rnn[t + 1][sl].view(w * n, 64), prepare=False)
+        h = self.rnn[t][sl].view(w * n, self.W)
+        kw = dict(action_out=self.actions[t][sl].view(-1, A), h_out=self.rnn[t + 1][sl].view(w * n, self.W), prepare=False)
         if self.mode == self.MODE_SAMPLE:
             self.actor.act(self._batch(t, sl), h, 1, noise=self.noise_all[t][k * w * n:(k + 1) * w * n],
                            log_pi_out=self.log_pis[t][sl].view(-1), **kw)
@@ -96,16 +97,16 @@ class RolloutEngine:
         env = self.env
         g = self._batch(t)
         n = env.num_agents
-        h = self.rnn[t].view(self.B * n, 64)
+        h = self.rnn[t].view(self.B * n, self.W)
         if self.mode == self.MODE_SAMPLE:
             # per-step, per-shard Philox stream: (env_offset, t) -> disjoint noise across ranks
             K.normal_(self.noise, stream_id=(self.env_offset << 32) | t, seed_tensor=self.key)
             self.actor.act(g, h, 1, noise=self.noise, action_out=self.actions[t].view(-1, env.action_dim),
-                           log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, 64),
+                           log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, self.W),
                            prepare=t == 0)
         else:
             self.actor.act(g, h, 0, action_out=self.actions[t].view(-1, env.action_dim),
-                           h_out=self.rnn[t + 1].view(self.B * n, 64), prepare=t == 0)
+                           h_out=self.rnn[t + 1].view(self.B * n, self.W), prepare=t == 0)
 
     def _run(self):
         env = self.env
@@ -181,9 +182,11 @@ class RolloutEngine:
         rnn = None
         log_pis = None
         if self.actor is not None:
-            # (B, T, 1, n, 1, 64): rnn_states[t] = carry before (stochastic) / after (deterministic) step t
+            # (B, T, rnn_layers, n, carries, 64): rnn_states[t] = carry before (stochastic) / after (deterministic)
+            # step t; a view of the (T+1, B, n, W) buffer
             sl = slice(0, T) if self.mode == self.MODE_SAMPLE else slice(1, T + 1)
-            rnn = self.rnn[sl].transpose(0, 1).unsqueeze(2).unsqueeze(4)
+            rs = self.actor.gru
+            rnn = self.rnn[sl].transpose(0, 1).unflatten(-1, (rs.layers, rs.carries, 64)).movedim(-4, -3)
             log_pis = self.log_pis.transpose(0, 1) if self.mode == self.MODE_SAMPLE else None
         return Rollout(view(slice(0, T)), self.actions.transpose(0, 1), rnn, self.rewards.transpose(0, 1),
                        self.costs.transpose(0, 1), self.dones.transpose(0, 1), log_pis, view(slice(1, T + 1)))

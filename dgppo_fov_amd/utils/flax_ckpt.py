@@ -24,6 +24,7 @@ import os
 import numpy as np
 
 GRU_KEYS = {"ir", "iz", "in", "hr", "hz", "hn"}
+LSTM_KEYS = {"ii", "if", "ig", "io", "hi", "hf", "hg", "ho"}
 HEAD_KEYS = {"Dense_0", "LayerNorm_0", "Dense_1", "LayerNorm_1"}
 
 
@@ -74,7 +75,22 @@ def _gnn_layers(tree):
 
 
 def _gru(tree):
-    return _find(tree, lambda p, t: GRU_KEYS <= set(t), "GRUCell")[1]
+    """The RNN cells (nn/rnn.py:10-30) in the layout RNNStack.load_flax takes: one GRUCell tree (the 1-layer GRU
+    default), else the list of GRUCell / LSTMCell trees ordered by their autoname index ([] without an RNN)."""
+    cells = [(p, t) for p, t in _subtrees(tree) if GRU_KEYS <= set(t) or LSTM_KEYS <= set(t)]
+    if len({p[:-1] for p, _ in cells}) > 1:
+        raise ValueError(f"reference tree: RNN cells under more than one parent ({['/'.join(p) for p, _ in cells]})")
+    cells.sort(key=lambda pt: int(pt[0][-1].rsplit("_", 1)[-1]) if pt[0] and pt[0][-1].rsplit("_", 1)[-1].isdigit()
+               else 0)
+    if len(cells) == 1 and GRU_KEYS <= set(cells[0][1]):
+        return cells[0][1]
+    return [t for _, t in cells]
+
+
+def _rnn_ref(d):
+    """RNNStack.flax() -> the reference's RNN_0 subtree (cells under their autonames), or {} without an RNN."""
+    cells = [d] if isinstance(d, dict) else d
+    return {"RNN_0": {f"{'LSTMCell' if 'ii' in c else 'GRUCell'}_{k}": c for k, c in enumerate(cells)}} if cells else {}
 
 
 def _head(tree, name):
@@ -100,7 +116,7 @@ def actor_reference_tree(net) -> dict:
     """ActorNet -> the reference's actor tree (inverse of actor_tree; GRU under the autonames RNN_0/GRUCell_0)."""
     d = net.flax()
     base = {"GraphTransformerGNN_0": {f"GraphTransformer_{i}": L for i, L in enumerate(d["gnn"])},
-            "PolicyGNNHead": d["head"], "RNN_0": {"GRUCell_0": d["gru"]}}
+            "PolicyGNNHead": d["head"], **_rnn_ref(d["gru"])}
     return {"params": {"PolicyNet_0": base, "ScaleHid": d["ScaleHid"], "OutputDenseMean": d["OutputDenseMean"],
                        "OutputDenseStdTrans": d["OutputDenseStdTrans"]}}
 
@@ -108,7 +124,7 @@ def actor_reference_tree(net) -> dict:
 def value_reference_tree(net) -> dict:
     d = net.flax()
     return {"params": {"GraphTransformerGNN_0": {f"GraphTransformer_{i}": L for i, L in enumerate(d["gnn"])},
-                       "ValueGNNHead": d["head"], "RNN_0": {"GRUCell_0": d["gru"]}, "Dense_0": d["out"]}}
+                       "ValueGNNHead": d["head"], **_rnn_ref(d["gru"]), "Dense_0": d["out"]}}
 
 
 def load_reference_npz(algo, model_dir: str) -> None:

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 6  /* 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 7  /* 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -302,6 +302,16 @@ int dgppo_layernorm_bwd(const float* x, const float* y, const float* dy, const f
 
 /* dy *= (y > 0) in place (ReLU backward) */
 int dgppo_relu_bwd(float* dy, const float* y, int64_t n, void* stream);
+
+/* flax.linen.LSTMCell, one step of `rows` contiguous carries (the --use-lstm option; replaces the LSTMCell
+ * branch of RNN.__call__, dgppo/nn/rnn.py:21-23).  fwd: g (rows, 4H) = [i | f | g | o] pre-activations
+ * (x W_i + h W_h + b) are activated in place, c_out = f c_prev + i g, h_out = o tanh(c_out); c_prev may be NULL
+ * (zero carry).  bwd: g = the activated gates, c = c_out, dh = dL/dh_out, dc = dL/dc_out from the next step
+ * (NULL: 0) -> dg (rows, 4H) pre-activation gradients and dc_prev = dL/dc_prev (NULL: not written). */
+int dgppo_lstm_cell_fwd(int64_t rows, int32_t H, float* g, const float* c_prev, float* c_out, float* h_out,
+                        void* stream);
+int dgppo_lstm_cell_bwd(int64_t rows, int32_t H, const float* g, const float* c_prev, const float* c, const float* dh,
+                        const float* dc, float* dg, float* dc_prev, void* stream);
 
 /* out = alpha * column_sums(x) + beta * out (deterministic; bias gradients) */
 int64_t dgppo_colsum_workspace_floats(int64_t rows, int32_t cols);

@@ -50,6 +50,49 @@ def gru_cell(p, h, x):
     return (1.0 - z) * n + z * h
 
 
+def lstm_cell(p, c, h, x):
+    """flax.linen.LSTMCell: input Denses ii/if/ig/io without bias, hidden Denses hi/hf/hg/ho with bias;
+    i, f, o sigmoid, g tanh; c' = f c + i g, h' = o tanh(c').  Returns (c', h')."""
+    i = torch.sigmoid(dense(x, p["ii"]) + dense(h, p["hi"]))
+    f = torch.sigmoid(dense(x, p["if"]) + dense(h, p["hf"]))
+    g = torch.tanh(dense(x, p["ig"]) + dense(h, p["hg"]))
+    o = torch.sigmoid(dense(x, p["io"]) + dense(h, p["ho"]))
+    c2 = f * c + i * g
+    return c2, o * torch.tanh(c2)
+
+
+def rnn(p, h, x):
+    """RNN(rnn_cls, rnn_layers) (dgppo/nn/rnn.py:15-30) on carries h (..., layers * carries * 64), the reference's
+    (layers, carries, 64) per agent flattened: returns (the last layer's output, new carries).  p: one GRUCell
+    tree (the 1-layer GRU default), a list of GRUCell / LSTMCell trees (carry [c, h] per LSTM layer, the
+    reference's jnp.stack((c, h), axis=1)), or [] (use_rnn=False: x passes through, the carry is kept)."""
+    if isinstance(p, dict):
+        h2 = gru_cell(p, h, x)
+        return h2, h2
+    if len(p) == 0:
+        return x, h
+    outs, off = [], 0
+    for cell in p:
+        if "ii" in cell:
+            c2, x = lstm_cell(cell, h[..., off:off + 64], h[..., off + 64:off + 128], x)
+            outs += [c2, x]
+            off += 128
+        else:
+            x = gru_cell(cell, h[..., off:off + 64], x)
+            outs.append(x)
+            off += 64
+    return x, torch.cat(outs, -1)
+
+
+def rnn_width(p, layers=1):
+    """carry floats per row for the RNN tree p (no RNN: the reference's unused (layers, 1, 64) zero carry)."""
+    if isinstance(p, dict):
+        return 64
+    if len(p) == 0:
+        return 64 * layers
+    return sum(128 if "ii" in c else 64 for c in p)
+
+
 def segment_softmax(logits, seg, num):
     idx = seg[:, None].expand_as(logits)
     mx = torch.full((num,) + logits.shape[1:], -math.inf, dtype=logits.dtype).scatter_reduce(
@@ -129,11 +172,11 @@ def actor_eval_seq(p, graph, S, L, n, actions, eps_fixed):
     """scan_eval_action over S sequences of L graphs (zero carries); graph batch ordered (s, t).
     Returns log_pi, entropy (S, L, n)."""
     y = mlp_head(gnn(p["gnn"], graph, n), p["head"]).reshape(S, L, n, 64)
-    h = torch.zeros((S, n, 64), dtype=T64)
+    h = torch.zeros((S, n, rnn_width(p["gru"])), dtype=T64)
     hs = []
     for t in range(L):
-        h = gru_cell(p["gru"], h, y[:, t])
-        hs.append(h)
+        o, h = rnn(p["gru"], h, y[:, t])
+        hs.append(o)
     H = torch.stack(hs, 1)
     mu, sd = policy_dist(p, H)
     act = torch.as_tensor(actions, dtype=T64).reshape(S, L, n, -1)
@@ -143,11 +186,11 @@ def actor_eval_seq(p, graph, S, L, n, actions, eps_fixed):
 def vl_seq(p, graph, S, L, n, h0=None, return_h=False):
     """scan_Vl over S sequences of L graphs (zero carries unless h0 (S, 64)): values (S, L)."""
     y = mlp_head(gnn(p["gnn"], graph, n).mean(1), p["head"]).reshape(S, L, 64)
-    h = torch.zeros((S, 64), dtype=T64) if h0 is None else torch.as_tensor(h0, dtype=T64)
+    h = torch.zeros((S, rnn_width(p["gru"])), dtype=T64) if h0 is None else torch.as_tensor(h0, dtype=T64)
     vs = []
     for t in range(L):
-        h = gru_cell(p["gru"], h, y[:, t])
-        vs.append(dense(h, p["out"])[:, 0])
+        o, h = rnn(p["gru"], h, y[:, t])
+        vs.append(dense(o, p["out"])[:, 0])
     v = torch.stack(vs, 1)
     return (v, h) if return_h else v
 
@@ -158,24 +201,24 @@ def vh_global_seq(p, graph, S, L, n, h0=None, return_h=False):
     x = gnn(p["gnn"], graph, n)  # (G, n, 64)
     x = torch.cat([x, x.mean(1, keepdim=True).expand(-1, n, -1)], -1)
     y = mlp_head(x, p["head"]).reshape(S, L, n, 64)
-    h = torch.zeros((S, n, 64), dtype=T64) if h0 is None else torch.as_tensor(h0, dtype=T64)
+    h = torch.zeros((S, n, rnn_width(p["gru"])), dtype=T64) if h0 is None else torch.as_tensor(h0, dtype=T64)
     vs = []
     for t in range(L):
-        h = gru_cell(p["gru"], h, y[:, t])
-        vs.append(dense(h, p["out"]))
+        o, h = rnn(p["gru"], h, y[:, t])
+        vs.append(dense(o, p["out"]))
     v = torch.stack(vs, 1)
     return (v, h) if return_h else v
 
 
 def actor_carry(p, graph, h, n):
-    """act(): the policy GRU carry after one graph (policy.py:61-74), h (G, n, 64)."""
+    """act(): the policy RNN carry after one graph (policy.py:61-74), h (G, n, W)."""
     y = mlp_head(gnn(p["gnn"], graph, n), p["head"])
-    return gru_cell(p["gru"], torch.as_tensor(h, dtype=T64), y)
+    return rnn(p["gru"], torch.as_tensor(h, dtype=T64), y)[1]
 
 
 def vh(p, graph, h, n):
     y = mlp_head(gnn(p["gnn"], graph, n), p["head"])
-    return dense(gru_cell(p["gru"], torch.as_tensor(h, dtype=T64), y), p["out"])
+    return dense(rnn(p["gru"], torch.as_tensor(h, dtype=T64), y)[0], p["out"])
 
 
 def ppo_loss(log_pis, log_pis_old, A, entropy, clip_eps=0.25, coef_ent=1e-2):
@@ -219,7 +262,7 @@ def dgppo_prepass(pa, pl, ph, roll, det, n, dt, gamma, lam, alpha, cbf_eps, cbf_
 
         def vh_all(r):
             nh = r["costs"].shape[-1]
-            vhs = vh(ph, _flat(r["graph"]), np.asarray(r["rnn"]).reshape(B * T, n, 64), n).reshape(B, T, n, nh)
+            vhs = vh(ph, _flat(r["graph"]), np.asarray(r["rnn"]).reshape(B * T, n, -1), n).reshape(B, T, n, nh)
             h2 = actor_carry(pa, _flat({k: x[:, None] for k, x in r["last"].items()}), r["rnn"][:, -1], n)
             vfin = vh(ph, _flat({k: x[:, None] for k, x in r["last"].items()}), h2.numpy(), n)
             return torch.cat([vhs, vfin.reshape(B, 1, n, nh)], 1).numpy()
@@ -257,7 +300,7 @@ def dgppo_minibatch_grads(pa, pl, ph, roll, det, envs, Ql, Qh_det, A, n, L, eps_
     loss_vl.backward()
     gd = _flat(det["graph"], envs)
     nh = Qh_det.shape[-1]
-    out = vh(ph, gd, np.asarray(det["rnn"])[envs].reshape(Bm * T, n, 64), n)
+    out = vh(ph, gd, np.asarray(det["rnn"])[envs].reshape(Bm * T, n, -1), n)
     loss_vh = (0.5 * (out - torch.as_tensor(Qh_det[envs].reshape(Bm * T, n, nh), dtype=T64)) ** 2).mean()
     loss_vh.backward()
     acts = np.asarray(roll["actions"])[envs].reshape(S * L * n, -1)

@@ -11,11 +11,11 @@ from dgppo_fov_amd.algo.module.nets import ActorNet, VhNet, VlNet
 from dgppo_fov_amd.utils import flax_ckpt as FC
 
 
-def _nets(seed, edge_dim=4, node_dim=7, A=2, n_cost=2):
+def _nets(seed, edge_dim=4, node_dim=7, A=2, n_cost=2, **rk):
     return types.SimpleNamespace(
-        actor=ActorNet(node_dim, 3, "cpu", seed=seed, action_dim=A, edge_dim=edge_dim),
-        Vl=VlNet(node_dim, 3, "cpu", seed=seed + 1, edge_dim=edge_dim),
-        Vh=VhNet(node_dim, 3, n_cost, "cpu", seed=seed + 2, edge_dim=edge_dim))
+        actor=ActorNet(node_dim, 3, "cpu", seed=seed, action_dim=A, edge_dim=edge_dim, **rk),
+        Vl=VlNet(node_dim, 3, "cpu", seed=seed + 1, edge_dim=edge_dim, **rk),
+        Vh=VhNet(node_dim, 3, n_cost, "cpu", seed=seed + 2, edge_dim=edge_dim, **rk))
 
 
 @pytest.mark.parametrize("edge_dim,node_dim,A,n_cost", [(4, 7, 2, 2), (10, 10, 3, 5)])
@@ -23,6 +23,24 @@ def test_reference_npz_round_trip(tmp_path, edge_dim, node_dim, A, n_cost):
     a = _nets(1, edge_dim, node_dim, A, n_cost)
     b = _nets(7, edge_dim, node_dim, A, n_cost)
     FC.save_reference_npz(a, str(tmp_path))
+    FC.load_reference_npz(b, str(tmp_path))
+    for k in ("actor", "Vl", "Vh"):
+        assert np.array_equal(getattr(a, k).ps.flat.numpy(), getattr(b, k).ps.flat.numpy()), k
+
+
+@pytest.mark.parametrize("rnn,layers", [("gru", 2), ("lstm", 1), ("lstm", 3), ("none", 1)])
+def test_reference_npz_round_trip_rnn_options(tmp_path, rnn, layers):
+    """--rnn-layers / --use-lstm / --no-rnn: the cells sit under RNN_0 as GRUCell_k / LSTMCell_k (ii..ho)."""
+    a = _nets(1, rnn=rnn, rnn_layers=layers)
+    b = _nets(5, rnn=rnn, rnn_layers=layers)
+    FC.save_reference_npz(a, str(tmp_path))
+    flat = FC.flatten(FC.actor_reference_tree(a.actor))
+    cell = "LSTMCell" if rnn == "lstm" else "GRUCell"
+    names = {k.split("/")[3] for k in flat if "/RNN_0/" in k}
+    assert names == ({f"{cell}_{k}" for k in range(layers)} if rnn != "none" else set())
+    if rnn == "lstm":
+        assert flat["params/PolicyNet_0/RNN_0/LSTMCell_0/hf/bias"].shape == (64,)
+        assert "params/PolicyNet_0/RNN_0/LSTMCell_0/if/bias" not in flat
     FC.load_reference_npz(b, str(tmp_path))
     for k in ("actor", "Vl", "Vh"):
         assert np.array_equal(getattr(a, k).ps.flat.numpy(), getattr(b, k).ps.flat.numpy()), k

@@ -359,3 +359,87 @@ def test_deep_gnn_nets_fwd_bwd(cuda, eid, n, obs, layers):
     vl.ps.swap_views()
     for path, a, b in _walk(g, R.grads(pv)):
         _grad_close(a, b, f"deep Vl grad {path}")
+
+
+# the reference CLI's RNN options (--rnn-layers, --use-lstm, --no-rnn; dgppo/nn/rnn.py:10-30): RNN(GRUCell |
+# LSTMCell, layers) with (layers, carries, 64) carries per agent, or no RNN (features pass through)
+RNNS = [("gru", 2), ("lstm", 1), ("lstm", 2), ("none", 1)]
+
+
+@pytest.mark.parametrize("kind,layers", RNNS)
+def test_rnn_options_nets_fwd_bwd(cuda, kind, layers):
+    eid, n, obs = "LidarSpread", 4, 2
+    S, L = 2, 4
+    env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=12)
+    A, rows = env.action_dim, S * L * n
+    rng = np.random.default_rng(13)
+    rk = dict(rnn=kind, rnn_layers=layers)
+    net = ActorNet(env.node_dim, n, cuda, seed=14, action_dim=A, **_nets_kw(env), **rk)
+    W = net.carry_width
+    assert W == (128 if kind == "lstm" else 64) * layers and net._fused_args(gb) is None
+    actions = rng.uniform(-0.99, 0.99, (rows, A)).astype(np.float32)
+    eps = rng.standard_normal((n, A)).astype(np.float32)
+    lp, ent, cache = net.eval_seq_fwd(gb, S, L, torch.from_numpy(actions).to(cuda), torch.from_numpy(eps).to(cuda))
+    p = R.to_t(net.flax(), requires_grad=True)
+    rlp, rent = R.actor_eval_seq(p, host, S, L, n, actions, eps)
+    torch.cuda.synchronize()
+    _close(lp.cpu().numpy(), rlp.detach().numpy().reshape(-1), what="log_pi")
+    _close(ent.cpu().numpy(), rent.detach().numpy().reshape(-1), what="entropy")
+    w1, w2 = rng.standard_normal(rows), rng.standard_normal(rows)
+    (rlp.reshape(-1) * torch.tensor(w1) + rent.reshape(-1) * torch.tensor(w2)).sum().backward()
+    net.ps.zero_grad()
+    net.eval_seq_bwd(cache, torch.tensor(w1, dtype=torch.float32, device=cuda),
+                     torch.tensor(w2, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    net.ps.swap_views()
+    g = net.flax()
+    net.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(p)):
+        _grad_close(a, b, f"{kind}{layers} actor grad {path}")
+    # one policy step from non-zero carries (the rollout's act): the new carries and the action
+    h = rng.standard_normal((rows, W)).astype(np.float32) * 0.5
+    a, _, h2 = net.act(gb, torch.from_numpy(h).to(cuda), 0)
+    pq = R.to_t(net.flax())
+    hh = torch.as_tensor(h, dtype=torch.float64).reshape(S * L, n, W)
+    h2_ref = R.actor_carry(pq, host, hh, n)
+    feat, _ = R.rnn(pq["gru"], hh, R.mlp_head(R.gnn(pq["gnn"], host, n), pq["head"]))
+    mu, _ = R.policy_dist(pq, feat)
+    torch.cuda.synchronize()
+    _close(h2.cpu().numpy(), h2_ref.numpy().reshape(rows, W), what="carry")
+    _close(a.cpu().numpy(), torch.tanh(mu).numpy().reshape(rows, A), what="action")
+    # Vl from given initial carries: values, final carries, gradients
+    vl = VlNet(env.node_dim, n, cuda, seed=15, **_nets_kw(env), **rk)
+    h0 = rng.standard_normal((S, W)).astype(np.float32) * 0.5
+    v, hT, vc = vl.seq_fwd(gb, S, L, h0=torch.from_numpy(h0).to(cuda))
+    pv = R.to_t(vl.flax(), requires_grad=True)
+    rv, rhT = R.vl_seq(pv, host, S, L, n, h0=h0.astype(np.float64), return_h=True)
+    torch.cuda.synchronize()
+    _close(v.cpu().numpy(), rv.detach().numpy(), what="Vl")
+    _close(hT.cpu().numpy(), rhT.detach().numpy(), what="Vl final carry")
+    w = rng.standard_normal((S, L))
+    (rv * torch.tensor(w)).sum().backward()
+    vl.ps.zero_grad()
+    vl.seq_bwd(vc, torch.tensor(w, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    vl.ps.swap_views()
+    g = vl.flax()
+    vl.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(pv)):
+        _grad_close(a, b, f"{kind}{layers} Vl grad {path}")
+    # Vh on the actor's carries
+    vh = VhNet(env.node_dim, n, 2, cuda, seed=16, **_nets_kw(env), **rk)
+    out, hc = vh.fwd(gb, torch.from_numpy(h).to(cuda))
+    ph = R.to_t(vh.flax(), requires_grad=True)
+    rout = R.vh(ph, host, hh, n)
+    torch.cuda.synchronize()
+    _close(out.cpu().numpy(), rout.detach().numpy().reshape(-1, 2), what="Vh")
+    wv = rng.standard_normal(rout.shape)
+    (rout * torch.tensor(wv)).sum().backward()
+    vh.ps.zero_grad()
+    vh.bwd(hc, torch.tensor(wv.reshape(-1, 2), dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    vh.ps.swap_views()
+    g = vh.flax()
+    vh.ps.swap_views()
+    for path, a, b in _walk(g, R.grads(ph)):
+        _grad_close(a, b, f"{kind}{layers} Vh grad {path}")

@@ -86,6 +86,44 @@ def test_grucell_zero_weights_halves_carry():
     np.testing.assert_array_equal(O.gru_cell(p, h, np.array([[3.0, 4.0]])), 0.5 * h)  # r = z = 0.5, n = 0
 
 
+def test_lstmcell_hand_values():
+    """flax LSTMCell (--use-lstm): i/f/o = sigmoid, g = tanh of (x W_i* + h W_h* + b_h*), the input Denses have
+    no bias; c' = f c + i g, h' = o tanh(c')."""
+    x, c, h = 0.5, -0.3, 0.25
+    w = dict(ii=1.0, hi=0.5, bi=0.1, if_=-1.0, hf=2.0, bf=0.3, ig=2.0, hg=-1.5, bg=-0.2, io=0.7, ho=1.1, bo=0.0)
+    i = _sig(w["ii"] * x + w["hi"] * h + w["bi"])
+    f = _sig(w["if_"] * x + w["hf"] * h + w["bf"])
+    g = math.tanh(w["ig"] * x + w["hg"] * h + w["bg"])
+    o = _sig(w["io"] * x + w["ho"] * h + w["bo"])
+    c_want = f * c + i * g
+    h_want = o * math.tanh(c_want)
+    k = lambda v: torch.tensor([[v]], dtype=torch.float64)  # noqa: E731
+    b = lambda v: torch.tensor([v], dtype=torch.float64)  # noqa: E731
+    p = {"ii": {"kernel": k(w["ii"])}, "if": {"kernel": k(w["if_"])}, "ig": {"kernel": k(w["ig"])},
+         "io": {"kernel": k(w["io"])}, "hi": {"kernel": k(w["hi"]), "bias": b(w["bi"])},
+         "hf": {"kernel": k(w["hf"]), "bias": b(w["bf"])}, "hg": {"kernel": k(w["hg"]), "bias": b(w["bg"])},
+         "ho": {"kernel": k(w["ho"]), "bias": b(w["bo"])}}
+    c2, h2 = R.lstm_cell(p, k(c), k(h), k(x))
+    assert abs(c2.item() - c_want) < 1e-15 and abs(h2.item() - h_want) < 1e-15
+    # the stacked form: carry rows [c | h] (64 wide per carry), two layers, the second fed the first's h'
+    H = 64
+    z = lambda *sh: torch.zeros(sh, dtype=torch.float64)  # noqa: E731
+    cell = {key: ({"kernel": z(H, H)} if key[0] == "i" else {"kernel": z(H, H), "bias": z(H)})
+            for key in ("ii", "if", "ig", "io", "hi", "hf", "hg", "ho")}
+    carry = torch.cat([torch.full((1, H), 2.0, dtype=torch.float64), z(1, H), torch.full((1, H), -4.0, dtype=torch.float64),
+                       z(1, H)], 1)
+    out, new = R.rnn([cell, cell], carry, z(1, H))
+    # zero weights: i = f = o = 1/2, g = 0 -> c' = c / 2, h' = tanh(c') / 2 per layer
+    assert R.rnn_width([cell, cell]) == 4 * H and new.shape == (1, 4 * H)
+    np.testing.assert_allclose(new[0, :H].numpy(), 1.0)
+    np.testing.assert_allclose(new[0, H:2 * H].numpy(), 0.5 * math.tanh(1.0))
+    np.testing.assert_allclose(new[0, 2 * H:3 * H].numpy(), -2.0)
+    np.testing.assert_allclose(out[0].numpy(), 0.5 * math.tanh(-2.0))
+    # no RNN: features pass through, the carry is kept
+    o2, c2n = R.rnn([], carry, torch.ones((1, H), dtype=torch.float64))
+    assert torch.equal(o2, torch.ones((1, H), dtype=torch.float64)) and torch.equal(c2n, carry)
+
+
 # ---- jraph.segment_softmax / GraphTransformer (gnn.py:99-117) ----------------------------------------
 def test_segment_softmax_uniform_logits_give_inverse_in_degree():
     seg = np.array([0, 0, 0, 2, 2, 1])  # in-degrees 3, 1, 2

@@ -23,14 +23,18 @@ def _entry(name):  # the repo-root scripts by path (`test` would also name the s
     return mod
 
 
-@pytest.mark.parametrize("eid,n,obs,algo", [("LidarSpread", 3, 2, "dgppo"), ("LidarOmniTarget", 3, 2, "dgppo"),
-                                            ("LidarSpread", 3, 2, "informarl"), ("LidarSpread", 3, 2, "hcbfcrpo")])
-def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, n, obs, algo):
+@pytest.mark.parametrize("eid,n,obs,algo,extra", [
+    ("LidarSpread", 3, 2, "dgppo", []), ("LidarOmniTarget", 3, 2, "dgppo", []), ("LidarSpread", 3, 2, "informarl", []),
+    ("LidarSpread", 3, 2, "hcbfcrpo", []),
+    # the network options of the reference CLI: 2-layer LSTM, a 3-layer actor GNN; no RNN with InforMARL-Lagr
+    ("LidarSpread", 3, 2, "dgppo", ["--use-lstm", "--rnn-layers", "2", "--actor-gnn-layers", "3"]),
+    ("LidarSpread", 3, 2, "informarl_lagr", ["--no-rnn"])], ids=lambda v: "-".join(v) if isinstance(v, list) else None)
+def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, n, obs, algo, extra):
     test_py, train_py = _entry("test"), _entry("train")
 
     argv = ["train.py", "--env", eid, "-n", str(n), "--algo", algo, "--obs", str(obs), "--steps", "2",
             "--n-env-train", "8", "--batch-size", "256", "--n-env-test", "4", "--eval-interval", "1",
-            "--save-interval", "2", "--log-dir", str(tmp_path)]
+            "--save-interval", "2", "--log-dir", str(tmp_path)] + extra
     monkeypatch.setattr(sys, "argv", argv)
     train_py.main()
     runs = glob.glob(os.path.join(str(tmp_path), eid, algo, "seed0_*"))

@@ -16,6 +16,7 @@ import pytest
 import torch
 
 from dgppo_fov_amd.algo import make_algo
+from dgppo_fov_amd.algo.dgppo import DGPPO
 from dgppo_fov_amd.env import make_env
 from dgppo_fov_amd.nn import kernels as K
 from oracle import nets as O
@@ -164,7 +165,7 @@ def _host(r, n):
     f = lambda G, sl: {k: getattr(G, k)[sl].cpu().numpy() for k in ("nodes", "edges", "receivers", "senders")}  # noqa
     return dict(graph=f(r.graph, slice(None)), last=f(r.next_graph, (slice(None), -1)),
                 rewards=r.rewards.cpu().numpy(), costs=r.costs.cpu().numpy(),
-                rnn=r.rnn_states.reshape(B, T, n, 64).cpu().numpy(), actions=r.actions.cpu().numpy(),
+                rnn=DGPPO._rows(r.rnn_states).reshape(B, T, n, -1).cpu().numpy(), actions=r.actions.cpu().numpy(),
                 log_pis=None if r.log_pis is None else r.log_pis.cpu().numpy())
 
 
@@ -184,12 +185,25 @@ def _net_trees(algo, grad=False):
                                          # the BASELINE bench shape and the bicycle config at n = 8, obs = 3
                                          ("LidarSpread", 8, 3, 8), ("LidarBicycleTarget", 8, 3, 8)])
 def test_dgppo_update_matches_oracle(cuda, eid, n, obs, B):
+    _update_parity(cuda, eid, n, obs, B)
+
+
+# the reference CLI's RNN options (--rnn-layers, --use-lstm, --no-rnn): RNN(GRUCell | LSTMCell, layers) or none
+@pytest.mark.parametrize("rk", [dict(rnn_layers=2), dict(use_lstm=True), dict(use_lstm=True, rnn_layers=2),
+                                dict(use_rnn=False)], ids=["gru2", "lstm1", "lstm2", "no_rnn"])
+def test_dgppo_update_rnn_options_match_oracle(cuda, rk):
+    _update_parity(cuda, "LidarSpread", 3, 2, 4, **rk)
+
+
+def _update_parity(cuda, eid, n, obs, B, **rk):
     T, L = 32, 16
     env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
                      action_dim=env.action_dim, n_agents=n, batch_size=B * T, rnn_step=L, train_steps=100,
-                     seed=1, device=cuda)
+                     seed=1, device=cuda, **rk)
     roll = algo.collect(algo.params, 7, n_env=B)
+    lay, car = rk.get("rnn_layers", 1), 2 if rk.get("use_lstm") and rk.get("use_rnn", True) else 1
+    assert roll.rnn_states.shape == (B, T, lay, n, car, 64)
     pa, pl, ph = _net_trees(algo)
     algo.trace = {}
     info = algo.update(roll, 60)  # past 50% of train_steps: cbf weight doubled
