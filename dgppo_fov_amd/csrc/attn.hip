@@ -1017,7 +1017,10 @@ constexpr int kRows = 16, kSR = 2, kQP = 100;
 // xs row pitch: x (DM floats; the pre-transform writes 32) then the edge features at column EC
 template <int DM>
 struct Pitch {
-  static constexpr int EC = DM <= 8 ? 8 : (DM <= 16 ? 16 : 32), XSP = EC + (DM <= 16 ? 4 : 8), AW = 64 * (XSP + 4);
+  // XSP = EC + 4 (12 / 20 / 36 floats): every 16 consecutive lanes' row starts fall on distinct 4-bank groups,
+  // so the per-lane float4 row reads and the pre-transform's strided accesses are bank-conflict free (a 40-float
+  // pitch put lanes L and L + 8 on the same banks)
+  static constexpr int EC = DM <= 8 ? 8 : (DM <= 16 ? 16 : 32), XSP = EC + 4, AW = 64 * (XSP + 4);
 };
 template <int DM>
 constexpr size_t lds_floats() {
@@ -1474,11 +1477,17 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
       }
       if (want_dxa && ok && s < n) {
         float* dst = cbi + (rl * n + s) * D;
+        if ((D & 3) == 0) {  // float4 rows (D-float stride): one wide store per column block
 #pragma unroll
-        for (int q = 0; q < DM / 4; ++q)
+          for (int q = 0; q < DM / 4; ++q)
+            if (q < TQ) ((f32x4*)dst)[q] = cq[q];
+        } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * q + j < D) dst[4 * q + j] = cq[q][j];
+          for (int q = 0; q < DM / 4; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (4 * q + j < D) dst[4 * q + j] = cq[q][j];
+        }
       }
       if (want_pre) {
         wave_sync();  // the dqt readers of xs are done: x -> dz
