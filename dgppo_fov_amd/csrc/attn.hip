@@ -1559,9 +1559,13 @@ bool bwd2_ok(const dgppo_gnn_attn_args* p) {
 }
 
 int64_t bwd2_grid(const dgppo_gnn_attn_args* p, int64_t* nblk) {
+  static const int64_t cap = [] {
+    const char* e = getenv("DGPPO_BWD2_BLOCKS");  // persistent-grid cap (A/B knob)
+    return e ? (int64_t)atoi(e) : (int64_t)bwd2::kMaxBlocks;
+  }();
   const int gpb = bwd2::kRows / p->n_agents;
   *nblk = (p->G + gpb - 1) / gpb;
-  return *nblk < bwd2::kMaxBlocks ? *nblk : bwd2::kMaxBlocks;
+  return *nblk < cap ? *nblk : cap;
 }
 
 void bwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
