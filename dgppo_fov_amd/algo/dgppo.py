@@ -54,6 +54,10 @@ def allreduce_mean_(t: torch.Tensor, world: int):
     return t
 
 
+# graphs per prepass chunk (the Vl scan / Vh passes over the whole rollout run env chunks of this many graphs)
+PREPASS_GRAPHS = int(os.environ.get("DGPPO_PREPASS_GRAPHS", 65536))
+
+
 class _Phases:
     """Host wall-clock per update phase (synchronising) when DGPPO_PROFILE=1; no-op otherwise."""
 
@@ -316,14 +320,16 @@ class DGPPO:
         from the scan's last carry (final_Vl_fn_, dgppo.py:203-216): (B, T+1)."""
         B, T = rollout.rewards.shape
         Vl = torch.empty((B, T + 1), device=self.device)
+        hT_all = torch.empty((B, self.Vl.carry_width), device=self.device)
         for e0 in range(0, B, chunk):
             e1 = min(B, e0 + chunk)
             g = self._graphs(rollout.graph, slice(e0, e1))
             v, hT, _ = self.Vl.seq_fwd(g, e1 - e0, T, keep_cache=False)
             Vl[e0:e1, :T].copy_(v)
-            vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph, slice(e0, e1)), e1 - e0, 1, h0=hT,
-                                       keep_cache=False)
-            Vl[e0:e1, T].copy_(vf[:, 0])
+            hT_all[e0:e1].copy_(hT)
+        # the final values of every env in one pass (rows are independent: identical to per-chunk passes)
+        vf, _, _ = self.Vl.seq_fwd(self._last_graph(rollout.next_graph), B, 1, h0=hT_all, keep_cache=False)
+        Vl[:, T].copy_(vf[:, 0])
         return Vl
 
     def _vh_all(self, rollout: Rollout, chunk: int):
@@ -336,12 +342,12 @@ class DGPPO:
             h = self._rows(rollout.rnn_states[e0:e1]).reshape((e1 - e0) * T * n, -1).contiguous()
             v, _ = self.Vh.fwd(g, h, keep_cache=False)
             out[e0:e1, :T].copy_(v.view(e1 - e0, T, n, -1))
-            # final: act on next_graph[-1] from rnn_states[-1], then Vh with that carry
-            gl = self._last_graph(rollout.next_graph, slice(e0, e1))
-            h_last = self._rows(rollout.rnn_states[e0:e1, -1]).reshape((e1 - e0) * n, -1).contiguous()
-            _, _, h2 = self.actor.act(gl, h_last, 0)
-            vf, _ = self.Vh.fwd(gl, h2, keep_cache=False)
-            out[e0:e1, T].copy_(vf.view(e1 - e0, n, -1))
+        # final, every env in one pass: act on next_graph[-1] from rnn_states[-1], then Vh with that carry
+        gl = self._last_graph(rollout.next_graph)
+        h_last = self._rows(rollout.rnn_states[:, -1]).reshape(B * n, -1).contiguous()
+        _, _, h2 = self.actor.act(gl, h_last, 0)
+        vf, _ = self.Vh.fwd(gl, h2, keep_cache=False)
+        out[:, T].copy_(vf.view(B, n, -1))
         return out
 
     def _allreduce_grads(self):
@@ -504,7 +510,7 @@ class DGPPO:
         ph.mark()
         det_key = int(self.key.integers(0, 2 ** 62))
         assert B * T * self.world >= self.batch_size
-        chunk = max(1, min(B, 65536 // T))
+        chunk = max(1, min(B, PREPASS_GRAPHS // T))
         info = {}
         det = None
         for _ in range(self.epoch_ppo):

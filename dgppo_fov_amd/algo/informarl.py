@@ -16,7 +16,7 @@ import torch
 
 from ..nn import kernels as K
 from ..trainer.rollout import Rollout
-from .dgppo import DGPPO, minibatch_plan
+from .dgppo import PREPASS_GRAPHS, DGPPO, minibatch_plan
 
 
 class InforMARL(DGPPO):
@@ -64,7 +64,7 @@ class InforMARL(DGPPO):
     def update(self, rollout: Rollout, step: int) -> dict:
         dev = self.device
         B, T = rollout.rewards.shape
-        chunk = max(1, min(B, 65536 // T))
+        chunk = max(1, min(B, PREPASS_GRAPHS // T))
         info, extra = {}, {}
         for _ in range(self.epoch_ppo):
             # Vl scan over the whole episode + final Vl (informarl.py:310-322)
