@@ -1700,12 +1700,16 @@ constexpr int kMaxC = 128;
 // per-wave buffers: 4 x kMaxC x (kH + 1 + 4) floats, reused for the pre-mode staging (N D0 + D0 D + D)
 template <int DM>
 size_t wave_floats(int N) {
-  const size_t w = 4 * (size_t)kMaxC * (kH + 1 + 4), st = (size_t)N * kD0 + kD0 * DM + DM;
+  const size_t w = 4 * (size_t)kMaxC * (kH + 1 + 4), st = (((size_t)N * kD0 + 3) & ~(size_t)3) + kD0 * DM + DM;
   return w > st ? w : st;
 }
+// sender-row pitch: DM + 1 for the 8-wide first layers (scalar reads); 36 for DM = 32 (float4 row reads,
+// 16-byte aligned, bank-conflict free across 16 lanes)
+template <int DM>
+constexpr int row_pitch() { return DM == 32 ? 36 : DM + 1; }
 template <int DM>
 size_t lds_floats(int N, int n) {
-  return (size_t)N * (DM + 1) + (size_t)n * (kH * DM + 4) + wave_floats<DM>(N);
+  return (size_t)N * row_pitch<DM>() + (size_t)n * (kH * DM + 4) + wave_floats<DM>(N);
 }
 }  // namespace gfwd
 
@@ -1713,7 +1717,8 @@ template <int DM>
 __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args p) {
   using lanes::f32x4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int XP = DM + 1, QP = kH * DM + 4;
+  constexpr int XP = gfwd::row_pitch<DM>(), QP = kH * DM + 4;
+  constexpr bool V4 = DM == 32;  // float4 logits / weighted sums (rows zero-padded to DM)
   const int n = p.n_agents, N = p.N, D = p.D, F = p.F, C = p.C, H = kH;
   const int64_t g = blockIdx.x;
   float* X = lds;                         // [N][XP] sender rows
@@ -1725,18 +1730,57 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
   // per-wave buffers that are free until the row loop)
   const bool pre = agent && p.pre_W != nullptr;
   const int D0 = p.D0;
-  float* R0 = Wb;                      // [N][D0] raw rows
-  float* PW = R0 + (size_t)N * D0;     // [D0][D] | b [D]
+  float* R0 = Wb;                                     // [N][D0] raw rows
+  float* PW = R0 + (((size_t)N * D0 + 3) & ~(size_t)3);  // [D0][D] | b [D] (16-byte aligned)
   if (pre) {
     for (int e = threadIdx.x; e < N * D0; e += 256) R0[e] = p.x[g * p.x_gstride + e];
     for (int e = threadIdx.x; e < D0 * D; e += 256) PW[e] = p.pre_W[e];
     for (int e = threadIdx.x; e < D; e += 256) PW[D0 * D + e] = p.pre_b[e];
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < N * D; e += 256) {
-    const int r = e / D, d = e - r * D;
+  if constexpr (V4) {  // a column quad per thread and step (float4 LDS / global accesses where aligned)
+    const bool q4ok = (D & 3) == 0;
+    for (int e = threadIdx.x; e < N * (DM / 4); e += 256) {
+      const int r = e / (DM / 4), c = 4 * (e - r * (DM / 4));
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (c < D) {
+        if (agent && r >= n && pre && q4ok) {
+          v = *reinterpret_cast<const f32x4*>(PW + D0 * D + c);
+          for (int k = 0; k < D0; ++k) v += R0[r * D0 + k] * *reinterpret_cast<const f32x4*>(PW + k * D + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.0f ? v[j] : 0.0f;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int d = c + j;
+            float x = 0.0f;
+            if (d < D) {
+              if (!agent) {
+                x = p.x[g * p.x_gstride + (int64_t)r * D + d];
+              } else if (r < n) {
+                x = p.xa[g * p.xa_gstride + (int64_t)r * D + d];
+              } else if (pre) {
+                float acc = PW[D0 * D + d];
+                for (int k = 0; k < D0; ++k) acc += R0[r * D0 + k] * PW[k * D + d];
+                x = acc > 0.0f ? acc : 0.0f;
+              } else {
+                x = p.x[g * p.x_gstride + (int64_t)r * D0 + d];
+              }
+            }
+            v[j] = x;
+          }
+        }
+      }
+      *reinterpret_cast<f32x4*>(X + r * XP + c) = v;
+    }
+  }
+  const int DS = V4 ? 0 : D;  // staged columns of the scalar path
+  for (int e = threadIdx.x; e < N * DS; e += 256) {
+    const int r = e / DS, d = e - r * DS;
     float v;
-    if (!agent) {
+    if (d >= D) {
+      v = 0.0f;
+    } else if (!agent) {
       v = p.x[g * p.x_gstride + (int64_t)r * D + d];
     } else if (r < n) {
       v = p.xa[g * p.xa_gstride + (int64_t)r * D + d];
@@ -1749,9 +1793,9 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
     }
     X[r * XP + d] = v;
   }
-  for (int e = threadIdx.x; e < n * H * D; e += 256) {
-    const int i = e / (H * D), k = e - i * (H * D), h = k / D, d = k - h * D;
-    Q[i * QP + h * DM + d] = p.qt[(g * n + i) * qt_ld(p) + k];
+  for (int e = threadIdx.x; e < n * H * DM; e += 256) {
+    const int i = e / (H * DM), k = e - i * (H * DM), h = k / DM, d = k - h * DM;
+    if (V4 || d < D) Q[i * QP + h * DM + d] = d < D ? p.qt[(g * n + i) * qt_ld(p) + h * D + d] : 0.0f;
   }
   for (int e = threadIdx.x; e < n * H; e += 256) {  // beta_h = q_h . bk_h
     const int i = e / H, h = e - i * H;
@@ -1792,14 +1836,31 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
       const int sd = sv[u];
       const bool ok = sd >= 0;
       const float* xr = X + (ok ? sd : 0) * XP;
+      if constexpr (V4) {
+        f32x4 xv[DM / 4];
 #pragma unroll
-      for (int h = 0; h < kH; ++h) {
-        const float* qt = Q + i * QP + h * DM;
-        float acc = 0.0f;
+        for (int q = 0; q < DM / 4; ++q) xv[q] = reinterpret_cast<const f32x4*>(xr)[q];
 #pragma unroll
-        for (int d = 0; d < DM; ++d)
-          if (d < D) acc += qt[d] * xr[d];
-        lg[u][h] = ok ? (acc + Q[i * QP + kH * DM + h]) * p.scale : -INFINITY;
+        for (int h = 0; h < kH; ++h) {
+          const f32x4* qt4 = reinterpret_cast<const f32x4*>(Q + i * QP + h * DM);
+          float acc = 0.0f;
+#pragma unroll
+          for (int q = 0; q < DM / 4; ++q) {
+            const f32x4 qq = qt4[q];
+            acc += qq[0] * xv[q][0] + qq[1] * xv[q][1] + qq[2] * xv[q][2] + qq[3] * xv[q][3];
+          }
+          lg[u][h] = ok ? (acc + Q[i * QP + kH * DM + h]) * p.scale : -INFINITY;
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < kH; ++h) {
+          const float* qt = Q + i * QP + h * DM;
+          float acc = 0.0f;
+#pragma unroll
+          for (int d = 0; d < DM; ++d)
+            if (d < D) acc += qt[d] * xr[d];
+          lg[u][h] = ok ? (acc + Q[i * QP + kH * DM + h]) * p.scale : -INFINITY;
+        }
       }
       if (c < C) {
         *reinterpret_cast<f32x4*>(E + c * 4) = ev[u];
@@ -1829,6 +1890,52 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (V4) {
+      // weighted sums as float4 tasks: lane t = lane & 31 owns column quad (head, q) of xbar, or head h's
+      // edge quad, or the three sigmas; the two lane halves take the two halves of the candidates and are
+      // combined by one shuffle (masked candidates have weight 0 and read row 0)
+      const int TQ = (D + 3) >> 2, t = lane & 31, half = lane >> 5;
+      const int kind = t < H * TQ ? 0 : (t < H * TQ + H ? 1 : (t == H * TQ + H ? 2 : 3));
+      const int h = kind == 0 ? t / TQ : (kind == 1 ? t - H * TQ : 0), q = kind == 0 ? t - h * TQ : 0;
+      const int Ch = (C + 1) >> 1, c0 = half * Ch, c1 = half ? C : Ch;
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f}, acc2 = acc;
+      // one candidate's term (the S -> X reads of four candidates are issued before their FMAs)
+      auto term = [&](int c) -> f32x4 {
+        const int sd = S[c];
+        const float* ar = A + c * kH;
+        if (kind == 2) return f32x4{ar[0], ar[1], ar[2], 0.0f};
+        const float a = sd >= 0 ? ar[h] : 0.0f;
+        const f32x4 v = kind == 0 ? reinterpret_cast<const f32x4*>(X + (sd >= 0 ? sd : 0) * XP)[q]
+                                  : reinterpret_cast<const f32x4*>(E)[c];
+        return a * v;
+      };
+      if (kind < 3) {
+        int c = c0;
+        for (; c + 4 <= c1; c += 4) {
+          const f32x4 t0 = term(c), t1 = term(c + 1), t2 = term(c + 2), t3 = term(c + 3);
+          acc += t0 + t1;
+          acc2 += t2 + t3;
+        }
+        for (; c < c1; ++c) acc += term(c);
+        acc += acc2;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += __shfl_xor(acc[j], 32, 64);
+      if (half == 0) {
+        float* o = p.xcat + row * W;
+        if (kind == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * q + j < D) o[h * D + 4 * q + j] = acc[j];
+        } else if (kind == 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[H * D + 4 * h + j] = acc[j];
+        } else if (kind == 2) {
+#pragma unroll
+          for (int j = 0; j < kH; ++j) o[H * D + 4 * H + j] = acc[j];
+        }
+      }
+    } else
     // weighted sums, 8 candidates per step with independent partial sums (the per-candidate LDS reads
     // of one step do not wait on each other); masked candidates have weight 0 and read row 0
     for (int o = lane; o < W; o += 64) {
@@ -1981,9 +2088,14 @@ bool gfwd_ok(const dgppo_gnn_attn_args* p) {
     const char* e = getenv("DGPPO_ATTN_GRAPH");
     return e && atoi(e) == 0;
   }();
-  // measured (LidarSpread n = 32): 1.6 ms vs 3.1 ms for the block kernel at D <= 8; at D = 32 the LDS
-  // footprint (2 workgroups per CU) leaves it latency-bound and the block kernel is faster (5.3 vs 7.2 ms)
-  if (off || p->H != kH || p->C <= 32 || p->C > gfwd::kMaxC || p->D > 8 || !p->sidx) return false;
+  // measured (LidarSpread n = 32): 1.6 ms vs 3.1 ms for the block kernel at D <= 8; at D = 32 the float4 form
+  // (DGPPO_ATTN_GRAPH32=0 keeps the block kernel there)
+  static const bool off32 = [] {
+    const char* e = getenv("DGPPO_ATTN_GRAPH32");
+    return e && atoi(e) == 0;
+  }();
+  if (off || p->H != kH || p->C <= 32 || p->C > gfwd::kMaxC || p->D > 32 || !p->sidx) return false;
+  if (p->D > 8 && off32) return false;
   if (p->xa && p->D0 > kD0) return false;
   const size_t bytes = (p->D <= 8 ? gfwd::lds_floats<8>(p->N, p->n_agents) : gfwd::lds_floats<32>(p->N, p->n_agents)) *
                        sizeof(float);
