@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec + PPO-updates/sec, LidarSpread n=8 ×4096 envs, 1/2/4/8 GPU"
 ENV_ID, N_AGENTS, N_OBS, B_PER_GPU, T = "LidarSpread", 8, 3, 4096, 128
+B_TOTAL_STRONG = 4096  # --strong: the whole job's envs (BASELINE.md strong-scaling variant)
 BYTES_PER_ENV_STEP = 8856  # SURVEY.md §8(d), LidarSpread n8 O3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -171,6 +172,54 @@ def cpu_baseline_update():
                       f"(prepass and deterministic rollout not counted)"}
 
 
+def cpu_baseline_rollout():
+    """The policy rollout on the host ("full rollouts with policy inference"): oracle/env.py
+    NumPy fp32 env steps + the torch-CPU fp32 actor (oracle/nets_t.py: per-edge GraphTransformer GNN, MLP
+    head, GRU, TanhNormal sample) on a bounded sample of ROLL_ENVS envs x ROLL_STEPS steps,
+    torch.set_num_threads(host cores), warm-up 1 + median of 3 episodes-fragments.  env-steps/s."""
+    import torch as th
+
+    from oracle import env as O
+    from oracle import nets_t as R
+
+    P = _cpu_workers()
+    th.set_num_threads(P)
+    ROLL_ENVS, ROLL_STEPS = 256, 16
+    spec = O.Spec(ENV_ID, N_AGENTS, N_OBS)
+    ag, gl, third = O.env_reset(spec, 5, ROLL_ENVS)
+    g0 = O.initial_graph(spec, ag, gl, third)
+    rng = np.random.default_rng(3)
+    R.T64 = th.float32
+    try:
+        pa = R.to_t(_random_flax_trees(spec)[0])
+
+        def fragment():
+            g, h = g0, np.zeros((ROLL_ENVS, N_AGENTS, 64), np.float32)
+            for t in range(ROLL_STEPS):
+                with th.no_grad():
+                    h2 = R.actor_carry(pa, g, h, N_AGENTS)
+                    mu, sd = R.policy_dist(pa, h2)
+                    eps = th.as_tensor(rng.standard_normal(mu.shape), dtype=th.float32)
+                    a = th.tanh(mu + sd * eps)
+                    R.tanh_normal_log_prob(a, mu, sd)
+                h = h2.numpy()
+                g = O.env_step(spec, g["states"], third, a.numpy())
+        times = []
+        for it in range(1 + 3):
+            t0 = time.perf_counter()
+            fragment()
+            if it >= 1:
+                times.append(time.perf_counter() - t0)
+    finally:
+        R.T64 = th.float64
+    t = float(np.median(times))
+    return {"value": round(ROLL_ENVS * ROLL_STEPS / t, 1), "unit": "env-steps/s", "cores": P, "kind": "port",
+            "cpu": _cpu_model(),
+            "sample": f"oracle/env.py NumPy fp32 env steps + oracle/nets_t.py torch-CPU fp32 actor sample_action "
+                      f"({P} threads) on {ROLL_ENVS} LidarSpread n=8 o=3 envs x {ROLL_STEPS} steps, warm-up 1, "
+                      f"median of 3 = {t:.2f} s"}
+
+
 def _random_flax_trees(spec):
     """Random-init actor / Vl / Vh parameter trees in the reference's flax layout (built on the host)."""
     from dgppo_fov_amd.algo.module.nets import ActorNet, VhNet, VlNet
@@ -208,7 +257,9 @@ def read_mfma_pmc():
                 "gnn_gemm_executed_tflops": round(gemm_f / gemm_t * 1e3, 2),
                 "gnn_gemm_frac_of_peak": round(gemm_f / gemm_t * 1e3 / FP32_MFMA_PEAK_TFLOPS, 4),
                 "window_executed_tflops": d["total_mfma_tflops_over_window"],
-                "window_frac_of_peak": round(d["total_mfma_tflops_over_window"] / FP32_MFMA_PEAK_TFLOPS, 4)}
+                "window_frac_of_peak": round(d["total_mfma_tflops_over_window"] / FP32_MFMA_PEAK_TFLOPS, 4),
+                "update_window_ms": None if "update_window_s" not in d else round(d["update_window_s"] * 1e3, 2),
+                "update_mfma_tflop": d.get("update_mfma_tflop")}
     except Exception:
         return None
 
@@ -221,7 +272,7 @@ UPDATE_TFLOP_PER_4096_ENVS, ROLLOUT_TFLOP_PER_4096_ENVS = 22.1, 5.3
 FP32_MFMA_PEAK_TFLOPS = 157.3
 
 
-def ppo_bench(env, dev, world, rank, iters):
+def ppo_bench(env, dev, world, rank, iters, strong=False):
     """DGPPO training iterations at the bench config: collect (policy rollout, 4096 envs x T=128 in
     one hipGraph) + update (det rollout, Vl/Vh prepass, GAE, advantages, 32 minibatches x
     [Vl, Vh, policy fwd+bwd, one grad all-reduce, clip + Adam]).  Random-init nets, synthetic envs.
@@ -229,8 +280,9 @@ def ppo_bench(env, dev, world, rank, iters):
     from dgppo_fov_amd.algo import make_algo
     from dgppo_fov_amd.nn import kernels as K
 
+    batch = PPO_BATCH if strong else PPO_BATCH * world  # strong: the global minibatch stays 16,384 samples
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
-                     action_dim=env.action_dim, n_agents=N_AGENTS, batch_size=PPO_BATCH * world, rnn_step=RNN_STEP,
+                     action_dim=env.action_dim, n_agents=N_AGENTS, batch_size=batch, rnn_step=RNN_STEP,
                      seed=0, device=dev, train_steps=1000)
     r = algo.collect(algo.params, 0, n_env=B_PER_GPU)
     algo.update(r, 0)  # warm-up: captures the deterministic-rollout graph, grows workspaces
@@ -259,6 +311,19 @@ def ppo_bench(env, dev, world, rank, iters):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # per iteration, the slowest rank
     t_col, t_upd = (float(x) for x in t.median(dim=1).values.tolist())
     t_upd_mean = float(t[1].mean())
+    pmc = read_mfma_pmc()
+    executed = None
+    if pmc is not None and pmc.get("update_window_ms") and pmc.get("update_mfma_tflop") is not None:
+        # the hardware's executed fp32 MFMA flops of one update (PMC profile of the same config) over THIS run's
+        # measured update time; quoted only when the profiled update window matches the measured one (10 %)
+        dev_rel = abs(pmc["update_window_ms"] - t_upd * 1e3) / (t_upd * 1e3)
+        if dev_rel <= 0.10 and world == 1 and not strong:
+            ach = pmc["update_mfma_tflop"] / t_upd
+            executed = {"achieved": round(ach, 2), "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                        "tflop_per_update": pmc["update_mfma_tflop"], "profile_update_ms": pmc["update_window_ms"]}
+        else:
+            executed = {"status": f"not quoted: the PMC profile's update window ({pmc['update_window_ms']} ms) is not "
+                                  f"this run's update ({t_upd * 1e3:.1f} ms, world {world}) within 10 %"}
     upd_tf = UPDATE_TFLOP_PER_4096_ENVS * (B_PER_GPU / 4096) * world + ROLLOUT_TFLOP_PER_4096_ENVS / 2 * (
         B_PER_GPU / 4096) * world  # the update runs the deterministic rollout too
     return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),
@@ -266,32 +331,89 @@ def ppo_bench(env, dev, world, rank, iters):
             "update_roofline": {"bound": "mfma", "algorithmic_tflop": round(upd_tf, 2),
                                 "achieved": round(upd_tf / t_upd, 2), "peak": FP32_MFMA_PEAK_TFLOPS * world,
                                 "unit": "TFLOP/s", "frac": round(upd_tf / t_upd / (FP32_MFMA_PEAK_TFLOPS * world), 4),
-                                "flops_source": "SURVEY.md 8(d): 22.1 TF per update + 2.65 TF det-rollout inference"},
+                                "flops_source": "SURVEY.md 8(d): 22.1 TF per update + 2.65 TF det-rollout inference",
+                                "executed_mfma": executed},
             "collect_ms": round(t_col * 1e3, 2),
             "collect_env_steps_per_s": round(B_PER_GPU * T * world / t_col, 1),
-            "iters": iters, "batch_size": PPO_BATCH * world, "rnn_step": RNN_STEP, "epoch_ppo": 1,
-            "minibatches": B_PER_GPU * T * world // (PPO_BATCH * world),
+            "iters": iters, "batch_size": batch, "rnn_step": RNN_STEP, "epoch_ppo": 1,
+            "minibatches": B_PER_GPU * T * world // batch,
             "gemm_tflop_per_update": round(gemm_flops / 1e12, 3),
             "gemm_tflops_over_update": round(gemm_flops / t_upd / 1e12, 3), "fp32_mfma_peak_tflops": 157.3,
-            "mfma_pmc": read_mfma_pmc()}
+            "mfma_pmc": pmc}
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly (no torchrun): start N fresh child processes of this script, one per
+    GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, exactly as
+    `torch.distributed.run --nproc-per-node N` would; rank 0 prints the JSON line.  This parent never
+    touches the GPU (no HIP call before or after the children), and if a rank fails the others are
+    terminated.  Returns the first non-zero exit code (0 when every rank succeeded)."""
+    import subprocess
+
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main():
+    global B_PER_GPU
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)  # SURVEY.md 8(d): warm-up 10, median of 50
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: 4096 envs (and the 16,384-sample PPO batch) in total, split over the ranks")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppo-iters", type=int, default=10, help="timed DGPPO collect+update iterations (0: skip)")
+    ap.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)  # launcher test (CPU only)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                 f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop WORLD_SIZE")
     rank = int(os.environ.get("RANK", "0"))
+    if args.print_rank_env:  # tests/test_bench_cpu.py: what each launched rank sees, before any GPU use
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT")}), flush=True)
+        return
+    if args.strong:
+        if B_TOTAL_STRONG % world:
+            sys.exit(f"bench.py --strong: {B_TOTAL_STRONG} envs do not split over {world} ranks")
+        B_PER_GPU = B_TOTAL_STRONG // world
     # CPU baselines first: forked workers must never inherit an initialised GPU context
-    cpu_env = cpu_upd = None
+    cpu_env = cpu_upd = cpu_roll = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_env = cpu_baseline()
+        cpu_roll = cpu_baseline_rollout()
         cpu_upd = cpu_baseline_update() if args.ppo_iters > 0 else None
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -402,7 +524,7 @@ def main():
     traffic = read_pmc_traffic("r02_env_rollout_pmc.json" if roll_ms is not None else "env_step_pmc.json")
     fused = eng.fused and lanes == 1
     del eng, outs, cur, g_step
-    ppo = ppo_bench(env, dev, world, rank, args.ppo_iters) if args.ppo_iters > 0 else None
+    ppo = ppo_bench(env, dev, world, rank, args.ppo_iters, strong=args.strong) if args.ppo_iters > 0 else None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -414,12 +536,13 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "ms_per_step_median": round(step_ms_median, 4),  # HIP events around each step, rank 0
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (Philox-sampled resets, uniform random actions in HBM)",
             "config": {
-                "workload": f"{ENV_ID} n={N_AGENTS} obs={N_OBS} rays=32 top_k=8, {B_PER_GPU} envs/GPU, "
+                "workload": f"{ENV_ID} n={N_AGENTS} obs={N_OBS} rays=32 top_k=8, {B_PER_GPU} envs/GPU"
+                            f"{f' ({B_PER_GPU * world} in total, strong scaling)' if args.strong else ''}, "
                             f"1 step = reset + T={T} fused env steps into the (B,T+1) rollout buffer",
                 "env": ENV_ID, "num_agents": N_AGENTS, "n_obs": N_OBS, "n_env_per_gpu": B_PER_GPU, "T": T,
                 "hip_graph": use_graph, "stream_lanes": lanes, "persistent_rollout": fused,
@@ -444,6 +567,7 @@ def main():
             },
             "cpu_baseline": cpu_env,
             "cpu_baseline_update": cpu_upd,
+            "cpu_baseline_rollout": cpu_roll,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

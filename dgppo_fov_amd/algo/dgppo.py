@@ -16,6 +16,7 @@ and are all-reduced (mean) once per minibatch before clip + Adam, so replicas st
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Optional
 
@@ -56,6 +57,11 @@ def allreduce_mean_(t: torch.Tensor, world: int):
 
 # graphs per prepass chunk (the Vl scan / Vh passes over the whole rollout run env chunks of this many graphs)
 PREPASS_GRAPHS = int(os.environ.get("DGPPO_PREPASS_GRAPHS", 65536))
+
+
+def FORCE_SAFE() -> bool:
+    """Learning-dynamics ablation (scripts/learn_ablate.sh): treat every sample as inside the safe set."""
+    return os.environ.get("DGPPO_DEBUG_FORCE_SAFE", "0") == "1"
 
 
 class _Phases:
@@ -539,7 +545,10 @@ class DGPPO:
                   self.gae_lambda)
             A = self._buf("A", (B, T, n))
             safe_cnt = torch.empty(B, device=dev)
-            K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, env.dt, self.alpha, self.cbf_eps, self.cbf_weight_at(step))
+            # DGPPO_DEBUG_FORCE_SAFE=1 (ablation knob, not a reference option): dt = inf and alpha = 0 make
+            # the CBF derivative exactly 0, so every sample counts as safe and A = -(Al + cbf_eps * w)
+            dt, alpha = (math.inf, 0.0) if FORCE_SAFE() else (env.dt, self.alpha)
+            K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, dt, alpha, self.cbf_eps, self.cbf_weight_at(step))
             ph.mark("gae_adv")
             if self.trace is not None:
                 self.trace.update(det=det, Vl=Vl.clone(), Vh=Vh.clone(), Vh_det=Vh_det.clone(), Ql=Ql.clone(),

@@ -11,11 +11,13 @@ per-(agent, cost) Lagrange multipliers.
 Kernels: the DGPPO networks, dgppo_clip_min0, dgppo_lagr_advantages, dgppo_lagr_update."""
 from __future__ import annotations
 
+import warnings
+
 import torch
 
 from ..nn import kernels as K
 from ..trainer.rollout import Rollout
-from .dgppo import DGPPO, minibatch_plan
+from .dgppo import PREPASS_GRAPHS, DGPPO, minibatch_plan
 from .informarl import InforMARL
 from .module.nets import VhGlobalNet
 
@@ -56,11 +58,12 @@ class InforMARLLagr(InforMARL):
         env, dev = self._env, self.device
         B, T = rollout.rewards.shape
         n, nh = self._n_agents, env.n_cost
-        chunk = max(1, min(B, 65536 // T))
+        chunk = max(1, min(B, PREPASS_GRAPHS // T))
         info = {}
         for _ in range(self.epoch_ppo):
-            Vl = self._vl_all(rollout, chunk)  # (B, T+1)
-            Vh = self._vh_scan_all(rollout, chunk)  # (B, T+1, n, nh)
+            # the Vl and Vh scans are independent: two streams, as DGPPO's prepass
+            Vl, Vh = self._parallel([lambda: self._vl_all(rollout, chunk),  # (B, T+1)
+                                     lambda: self._vh_scan_all(rollout, chunk)])  # (B, T+1, n, nh)
             hs = torch.empty(rollout.costs.shape, device=dev)  # max(costs, 0) (informarl_lagr.py:197)
             K.clip_min0(rollout.costs.contiguous(), hs)
             Qh = torch.empty((B, T, n, nh), device=dev)
@@ -174,3 +177,9 @@ class InforMARLLagr(InforMARL):
             # use them, and the reference's checkpoint holds the networks only (informarl_lagr.py:311-327)
             if lagr.shape == self.ah_lagr.shape:
                 self.ah_lagr.copy_(lagr)
+                return
+            warnings.warn(f"{fn}: multipliers of shape {tuple(lagr.shape)} do not fit this algorithm's "
+                          f"{tuple(self.ah_lagr.shape)}; keeping lagr_init (fine for evaluation, not for resuming)")
+        else:
+            warnings.warn(f"{fn} missing (network-only or reference checkpoint): the Lagrange multipliers keep "
+                          "lagr_init (fine for evaluation, not for resuming training)")

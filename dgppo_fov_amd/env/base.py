@@ -65,7 +65,7 @@ class MultiAgentEnv(ABC):
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         self._cfg = self._make_cfg()
-        self._cfg_handle = ops.register_env_cfg(self._cfg)  # the torch.ops.dgppo env ops take this handle
+        self._cfg_handle = ops.register_env_cfg(self._cfg, owner=self)  # the torch.ops.dgppo env ops take this handle
         self._dev_cache = {}
 
     def _n_goals(self) -> int:

@@ -24,6 +24,8 @@ registered once per env instance and the ops take its integer handle.
 from __future__ import annotations
 
 import ctypes
+import itertools
+import weakref
 from typing import List, Optional
 
 import torch
@@ -32,12 +34,17 @@ from torch import Tensor
 from . import _lib
 
 _CFGS: dict = {}
+_NEXT_HANDLE = itertools.count(1)
 
 
-def register_env_cfg(cfg: _lib.EnvCfg) -> int:
-    """Keep `cfg` alive for the process and return the handle the env ops take."""
-    h = len(_CFGS) + 1
+def register_env_cfg(cfg: _lib.EnvCfg, owner=None) -> int:
+    """Keep `cfg` alive and return the handle the env ops take (handles are never reused).  With an
+    `owner` the entry is released when the owner is garbage-collected, so per-test / per-config envs
+    do not accumulate for the life of the process."""
+    h = next(_NEXT_HANDLE)
     _CFGS[h] = cfg
+    if owner is not None:
+        weakref.finalize(owner, _CFGS.pop, h, None)
     return h
 
 

@@ -80,8 +80,24 @@ class Trainer:
                 self.algo.save(self.model_dir, step)
             key = int(self.rng.integers(0, 2 ** 62))
             rollouts = self.algo.collect(self.algo.params, key, n_env=self.n_env_train)
-            train_info = {k.replace("eval/", "train/"): v for k, v in eval_info(rollouts.rewards, rollouts.costs).items()
-                          if k in ("eval/reward", "eval/unsafe_frac")}  # the stochastic rollouts' own metrics
+            train_stats = self._train_stats(rollouts)  # device scalars: no host sync before the update
             update_info = self.algo.update(rollouts, step)
-            self._log({"step": self.update_steps, **update_info, **train_info})
+            self._log({"step": self.update_steps, **update_info, **self._read_stats(train_stats)})
             self.update_steps += 1
+
+    def _train_stats(self, rollouts):
+        """The stochastic rollouts' own metrics as ONE device vector, enqueued right after collect (the next
+        collect overwrites the rollout buffers): [episode return, unsafe_frac (eval_info's definitions),
+        mean |E_(env,t)[action]| over (agent, dim) -- a policy-mean drift indicator]."""
+        import torch
+
+        r, c, a = rollouts.rewards, rollouts.costs, rollouts.actions
+        return torch.stack([r.sum(-1).mean(), (c.amax(-1).amax(-2) >= 1e-6).float().mean(),
+                            a.mean((0, 1)).abs().mean()])
+
+    def _read_stats(self, v) -> dict:
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(v)
+            v = v / dist.get_world_size()
+        s = v.tolist()
+        return {"train/reward": s[0], "train/unsafe_frac": s[1], "train/act_drift": s[2]}

@@ -51,17 +51,23 @@ def main():
     for step in (0, a.steps):
         res[step] = test.test(argparse.Namespace(**{**vars(_test_args(test)), "path": run, "epi": a.epi, "step": step,
                                                     "log": True}))
-    out = {"env": a.env, "n": a.n, "obs": a.obs, "algo": a.algo, "steps": a.steps, "train_args": extra, "train_wall_s": round(t_train, 1),
+    out = {"env": a.env, "n": a.n, "obs": a.obs, "algo": a.algo, "steps": a.steps, "train_args": extra,
+           "env_vars": {k: v for k, v in os.environ.items() if k.startswith("DGPPO_")}, "train_wall_s": round(t_train, 1),
            "s_per_iteration": round(t_train / (a.steps + 1), 4),
            "eval_curve": [{k: r[k] for k in ("step", "eval/reward", "eval/cost", "eval/unsafe_frac")} for r in evals],
            "test_untrained_step0": res[0], f"test_step{a.steps}": res[a.steps], "test_epi": a.epi,
-           "train_curve": [(r["step"], round(r["train/reward"], 4), round(r["train/unsafe_frac"], 3)) for r in rows
-                           if "train/reward" in r][::max(1, a.steps // 20)],
            "update_tail": [{k: v for k, v in r.items() if not k.startswith("eval/")} for r in rows
-                           if "Vl/loss" in r][-3:]}
+                           if "Vl/loss" in r][-3:],
+           "update_curve": [[r["step"]] + [round(float(r.get(k, float("nan"))), 4) for k in CURVE_KEYS]
+                            for r in rows if "Vl/loss" in r][::max(1, a.steps // 30)],
+           "update_curve_keys": ["step"] + list(CURVE_KEYS)}
     with open(os.path.join(a.out, "learning_run.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ("train_wall_s", "test_untrained_step0", f"test_step{a.steps}")}))
+
+
+CURVE_KEYS = ("train/reward", "train/unsafe_frac", "train/act_drift", "eval/safe_data", "Vl/loss", "Vh/loss_Vh",
+              "policy/clip_frac", "policy/entropy", "policy/total_variation_dist")
 
 
 def _test_args(test):

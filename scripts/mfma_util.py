@@ -54,5 +54,20 @@ for fam in sorted(set(pmc) | set(dur), key=lambda f: -dur.get(f, 0)):
                             "mfma_busy_frac": round(busy / (g / 8 * 1024), 4) if g else None}
 out["total_mfma_tflop"] = round(tot_f / 1e12, 4)
 out["total_mfma_tflops_over_window"] = round(tot_f / span / 1e12, 2)
+# the update alone: every dispatch after the last `spin_kernel` marker update_smoke.py launches between the
+# second collect and its update (the counter pass and the trace pass run the same dispatch sequence)
+marks = [r for r in trows if "spin_kernel" in r["Kernel_Name"]]
+pmarks = sorted(int(r["Dispatch_Id"]) for r in prow if "spin_kernel" in r["Kernel_Name"])
+if marks:
+    t_mark = max(int(r["End_Timestamp"]) for r in marks)
+    upd = [r for r in trows if int(r["Start_Timestamp"]) >= t_mark]
+    d_mark = pmarks[-1] if pmarks else None
+    uf = sum(float(r["Counter_Value"]) * 512 for r in prow if r["Counter_Name"] == "SQ_INSTS_VALU_MFMA_MOPS_F32"
+             and d_mark is not None and int(r["Dispatch_Id"]) > d_mark)
+    uspan = (max(int(r["End_Timestamp"]) for r in upd) - min(int(r["Start_Timestamp"]) for r in upd)) * 1e-9
+    out["update_window_s"] = round(uspan, 4)
+    out["update_mfma_tflop"] = round(uf / 1e12, 4)
+    out["update_executed_tflops"] = round(uf / uspan / 1e12, 2)
+    out["update_frac_of_peak"] = round(uf / uspan / PEAK, 4)
 print(json.dumps(out, indent=1))
 json.dump(out, open(os.path.join(root, "mfma_util.json"), "w"), indent=1)

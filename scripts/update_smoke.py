@@ -16,6 +16,7 @@ B = int(os.environ.get("N_ENV", "16"))
 T = int(os.environ.get("T", "32"))
 bs = int(os.environ.get("BATCH", str(B * T // 2)))
 iters = int(os.environ.get("ITERS", "2"))
+MARK = os.environ.get("MARK_UPDATE", "1") == "1"
 dev = torch.device("cuda:0")
 env = make_env(env_id, n, num_obs=obs, max_step=T, device=dev)
 algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
@@ -25,6 +26,8 @@ for it in range(iters):
     r = algo.collect(algo.params, it, n_env=B)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if MARK:
+        torch.cuda._sleep(1000)  # a `spin_kernel` dispatch marks where the update starts (scripts/mfma_util.py)
     info = algo.update(r, it)
     torch.cuda.synchronize()
     t2 = time.perf_counter()

@@ -1,0 +1,184 @@
+"""Multi-update / multi-minibatch checks of the DGPPO update driver (dgppo.py:136-321,
+informarl.py:258-457) -- the orchestration the single-minibatch parity tests in test_update_gpu.py
+cannot see: which env rows minibatch k gathers, that each minibatch's gradient is taken at the
+parameters the previous minibatch's Adam step left, that Adam's moments and step count carry across
+minibatches and updates, that the concurrent-stream schedule is bit-identical to the serial one, and
+that DGPPO without its safety terms is InforMARL.
+
+* `test_trajectory_matches_oracle_loop`: K = 5 updates x 4 minibatches, teacher-forced: at every
+  update the float64 oracle recomputes the prepass (values, GAE targets, merged advantages) from the
+  GPU's parameters at the start of that update, and at every minibatch it recomputes the gradient at
+  the GPU's parameters before that minibatch, then clip + Adam with the GPU's carried moments; the
+  result must equal the parameters the GPU starts the NEXT minibatch (or update) from.  Tolerances as
+  in test_update_gpu.py (1e-5 relative + 8x the float32 noise floor of the same oracle; Adam results
+  1e-6 absolute).  Teacher forcing keeps the check exact over many steps: an untethered float64 loop
+  drifts from any fp32 run within a few Adam steps (sign(g) steps of size lr on near-zero gradients).
+* `test_streams_bit_identical`: DGPPO_STREAMS=1 (policy / Vl / Vh passes on three HIP streams) vs 0
+  (serial), 3 updates x 8 minibatches: parameters, Adam state and every info entry bit-identical.
+* `test_force_safe_dgppo_is_informarl`: DGPPO with cbf_weight 0 and every sample forced safe
+  (DGPPO_DEBUG_FORCE_SAFE=1: A = -normalised Al exactly) runs the same policy / Vl update as
+  InforMARL with cost_weight 0; 3 updates x 4 minibatches from the same seed, each algorithm
+  collecting its own rollouts: policy and Vl parameters agree to 1e-5 (the two advantage kernels
+  reduce in different orders, so not bit for bit).
+"""
+import numpy as np
+import pytest
+import torch
+
+from dgppo_fov_amd.algo import make_algo
+from dgppo_fov_amd.env import make_env
+from oracle import nets as O
+from oracle import nets_t as R
+
+from test_update_gpu import _close_floor, _host, _net_trees, _walk
+
+pytestmark = pytest.mark.gpu
+
+
+def _algo(cuda, eid, n, obs, T, batch, L=16, algo="dgppo", seed=3, **kw):
+    env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
+    return make_algo(algo, env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=n, batch_size=batch, rnn_step=L, train_steps=100, seed=seed,
+                     device=cuda, **kw), env
+
+
+def _trees_at(algo, flats):
+    """flax trees of (actor, Vl, Vh) at the given flat parameter vectors (the live buffers are restored)."""
+    nets = (("policy", algo.actor), ("Vl", algo.Vl), ("Vh", algo.Vh))
+    keep = {k: net.ps.flat.clone() for k, net in nets}
+    try:
+        for k, net in nets:
+            net.ps.flat.copy_(flats[k])
+        return _net_trees(algo)
+    finally:
+        for k, net in nets:
+            net.ps.flat.copy_(keep[k])
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("MPETarget", 2, 0)])
+def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
+    B, T, L, K_UPD = 8, 32, 16, 5
+    algo, env = _algo(cuda, eid, n, obs, T, batch=2 * T, L=L)  # 2 envs per minibatch -> 4 minibatches
+    nets = (("Vl", algo.Vl), ("Vh", algo.Vh), ("policy", algo.actor))
+    for it in range(K_UPD):
+        roll = algo.collect(algo.params, 100 + it, n_env=B)
+        start = {k: net.ps.flat.clone() for k, net in nets}
+        algo.trace = {}
+        step = 20 * it  # crosses the CBF schedule's 50% boundary (train_steps 100) at it = 3
+        info = algo.update(roll, step)
+        torch.cuda.synchronize()
+        tr = algo.trace
+        assert len(tr["mb"]) == 4
+        hr, hd = _host(roll, n), _host(tr["det"], n)
+        cw = algo.cbf_weight_at(step)
+        pa, pl, ph = _trees_at(algo, start)
+        # prepass at the update-start parameters
+        refs = {}
+        try:
+            for dt in (torch.float64, torch.float32):
+                R.T64 = dt
+                refs[dt] = R.dgppo_prepass(R.to_t(pa), R.to_t(pl), R.to_t(ph), hr, hd, n, env.dt, algo.gamma,
+                                           algo.gae_lambda, algo.alpha, algo.cbf_eps, cw)
+        finally:
+            R.T64 = torch.float64
+        ref, ref32 = refs[torch.float64], refs[torch.float32]
+        for k in ("Vl", "Vh", "Ql", "Qh_det"):
+            _close_floor(tr[k].cpu().numpy(), ref[k], ref32[k], f"update {it} {k}")
+        robust = np.abs(ref["deriv"]).min(-1) > 1e-3
+        env_floor = np.broadcast_to(np.abs(ref32["A"] - ref["A"]).max(axis=(1, 2), keepdims=True), ref["A"].shape)
+        _close_floor(tr["A"].cpu().numpy()[robust], ref["A"][robust], ref32["A"][robust], f"update {it} A",
+                     floor=env_floor[robust])
+        # the minibatches partition the envs
+        seen = np.sort(np.concatenate([mb["envs"] for mb in tr["mb"]]))
+        assert np.array_equal(seen, np.arange(B))
+        Ql, Qh_det, A = (tr[k].double().cpu().numpy() for k in ("Ql", "Qh_det", "A"))
+        for k, mb in enumerate(tr["mb"]):
+            # parameters before minibatch k = start of the update, or Adam after minibatch k - 1
+            if k == 0:
+                for name, _ in nets:
+                    assert torch.equal(mb["before"][name], start[name]), (it, name)
+            pa, pl, ph = _trees_at(algo, mb["before"])
+            rg = {}
+            try:
+                for dt in (torch.float64, torch.float32):
+                    R.T64 = dt
+                    ts = [R.to_t(x, requires_grad=True) for x in (pa, pl, ph)]
+                    R.dgppo_minibatch_grads(*ts, hr, hd, np.asarray(mb["envs"]), Ql, Qh_det, A, n, L,
+                                            algo.entropy_eps.cpu().numpy(), algo.clip_eps, algo.coef_ent)
+                    rg[dt] = [R.grads(t) for t in ts]
+            finally:
+                R.T64 = torch.float64
+            keep = algo.grad_flat.clone()
+            algo.grad_flat.copy_(mb["grad"])
+            gpu = _net_trees(algo, grad=True)
+            algo.grad_flat.copy_(keep)
+            for tag, g, r64, r32 in zip(("actor", "Vl", "Vh"), gpu, rg[torch.float64], rg[torch.float32]):
+                for (path, a, b), (_, c, _) in zip(_walk(g, r64), _walk(r32, r64)):
+                    b = np.asarray(b, np.float64)
+                    err = np.abs(np.asarray(a, np.float64) - b).max()
+                    floor = np.abs(np.asarray(c, np.float64) - b).max()
+                    assert err <= 2e-5 * np.abs(b).max() + 1e-6 + 8 * floor, \
+                        f"update {it} mb {k} {tag} grad {path}: {err:.3e} (fp32 floor {floor:.3e})"
+            # clip + Adam with the carried moments -> the parameters the next minibatch starts from
+            nxt = tr["mb"][k + 1]["before"] if k + 1 < len(tr["mb"]) else {nm: net.ps.flat for nm, net in nets}
+            off = 0
+            for name, net in nets:
+                sz = net.ps.size
+                g = mb["grad"][off:off + sz].double().cpu().numpy()
+                off += sz
+                (gc,), _ = O.clip_by_global_norm_ref([g], algo.max_grad_norm)
+                count = int(mb["state_before"][name][2].item())
+                assert count == it * 4 + k, (it, k, name, count)  # every step so far was finite
+                (rp,), _, _ = O.adam_step([mb["before"][name].double().cpu().numpy()], [gc],
+                                          [mb["m_before"][name].double().cpu().numpy()],
+                                          [mb["v_before"][name].double().cpu().numpy()], count, algo.opt[name].lr)
+                err = np.abs(nxt[name].double().cpu().numpy() - rp).max()
+                assert err <= 1e-6, f"update {it} mb {k} {name} Adam: {err:.3e}"
+        assert np.isfinite(info["policy/loss"])
+
+
+def test_streams_bit_identical(cuda, monkeypatch):
+    eid, n, obs, B, T = "LidarSpread", 3, 2, 8, 32
+
+    def run(flag):
+        monkeypatch.setenv("DGPPO_STREAMS", flag)
+        algo, _ = _algo(cuda, eid, n, obs, T, batch=T)  # 1 env per minibatch -> 8 minibatches
+        infos = []
+        for it in range(3):
+            infos.append(algo.update(algo.collect(algo.params, 21 + it, n_env=B), it))
+        torch.cuda.synchronize()
+        return algo, infos
+
+    a1, i1 = run("1")
+    assert a1._aux_streams(2) is not None
+    a0, i0 = run("0")
+    assert a0._aux_streams(2) is None
+    for name in ("Vl", "Vh", "policy"):
+        o0, o1 = a0.opt[name], a1.opt[name]
+        assert torch.equal(o0.ps.flat, o1.ps.flat), name
+        assert torch.equal(o0.m, o1.m) and torch.equal(o0.v, o1.v) and torch.equal(o0.state, o1.state), name
+    for d0, d1 in zip(i0, i1):
+        assert d0.keys() == d1.keys()
+        for k in d0:
+            assert d0[k] == d1[k] or (np.isnan(d0[k]) and np.isnan(d1[k])), k
+
+
+def test_force_safe_dgppo_is_informarl(cuda, monkeypatch):
+    eid, n, obs, B, T = "LidarTarget", 2, 1, 8, 32
+    monkeypatch.setenv("DGPPO_DEBUG_FORCE_SAFE", "1")
+    dg, _ = _algo(cuda, eid, n, obs, T, batch=2 * T, cbf_weight=0.0)
+    inf, _ = _algo(cuda, eid, n, obs, T, batch=2 * T, algo="informarl", cost_weight=0.0)
+    for name in ("policy", "Vl"):
+        assert torch.equal(dg.params[name], inf.params[name])
+    for it in range(3):
+        rd = dg.collect(dg.params, 40 + it, n_env=B)
+        ri = inf.collect(inf.params, 40 + it, n_env=B)
+        assert (rd.actions - ri.actions).abs().max().item() <= 1e-5, it
+        idg = dg.update(rd, it)
+        iinf = inf.update(ri, it)
+        assert idg["eval/safe_data"] == 1.0
+        for name in ("policy", "Vl"):
+            err = (dg.params[name] - inf.params[name]).abs().max().item()
+            assert err <= 1e-5, f"update {it} {name}: {err:.3e}"
+        for k in ("Vl/loss", "policy/loss", "policy/entropy", "policy/clip_frac"):
+            assert abs(idg[k] - iinf[k]) <= 1e-5 * (1 + abs(iinf[k])), (it, k, idg[k], iinf[k])
