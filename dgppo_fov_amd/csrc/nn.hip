@@ -691,15 +691,17 @@ __device__ __forceinline__ uint32_t philox_w(uint32_t c0, uint32_t c1, uint32_t 
   return word == 0 ? c0 : (word == 1 ? c1 : (word == 2 ? c2 : c3));
 }
 
+// Counter (element lo, element hi, stream lo, stream hi | kNoiseDomain): the domain bit keeps every noise word
+// disjoint from the env-reset draws, whose counters are (draw, env, purpose, 0) under the same key (math32.h Rng)
+constexpr uint32_t kNoiseDomain = 0x80000000u;
 __global__ __launch_bounds__(256) void normal_kernel(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed,
                                                      uint64_t stream_id) {
   const uint64_t sd = seed_ptr ? *seed_ptr : seed;
+  const uint32_t c2 = (uint32_t)stream_id, c3 = (uint32_t)(stream_id >> 32) | kNoiseDomain;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
     const uint32_t c0 = (uint32_t)t, c1 = (uint32_t)(t >> 32);
-    const uint32_t a = philox_w(c0, c1, (uint32_t)stream_id, (uint32_t)(stream_id >> 32), (uint32_t)sd,
-                                (uint32_t)(sd >> 32), 0);
-    const uint32_t b = philox_w(c0, c1, (uint32_t)stream_id, (uint32_t)(stream_id >> 32), (uint32_t)sd,
-                                (uint32_t)(sd >> 32), 1);
+    const uint32_t a = philox_w(c0, c1, c2, c3, (uint32_t)sd, (uint32_t)(sd >> 32), 0);
+    const uint32_t b = philox_w(c0, c1, c2, c3, (uint32_t)sd, (uint32_t)(sd >> 32), 1);
     const float u1 = ((a >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
     const float u2 = (b >> 8) * (1.0f / 16777216.0f);
     out[t] = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958648f * u2);

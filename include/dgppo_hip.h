@@ -504,7 +504,10 @@ typedef struct dgppo_gather_field {
 int dgppo_gather_env_steps(const dgppo_gather_field* fields, int32_t n_fields, const int64_t* envs, int32_t n_sel,
                            int32_t T, void* stream);
 
-/* standard normal noise from Philox4x32-10 (Box-Muller); seed from *seed_ptr when non-NULL */
+/* standard normal noise from Philox4x32-10 (Box-Muller); seed from *seed_ptr when non-NULL.  Element t uses
+   counter (t lo, t hi, stream_id lo, stream_id hi | 0x80000000): the top bit is the noise domain, disjoint from
+   the env-reset draws (counter (draw, env, purpose, 0)) under the same key.  Replaces the threefry draws of
+   sample_action (policy.py:196-203, jax.random.normal inside tfd.Normal.sample). */
 int dgppo_normal(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed, uint64_t stream_id, void* stream);
 
 /* Library / device introspection */

@@ -14,7 +14,7 @@ run() {  # name, env vars..., -- , learning_run args...
   local envs=()
   while [ "$1" != "--" ]; do envs+=("$1"); shift; done
   shift
-  env "${envs[@]}" timeout -k 10 400 python -u scripts/learning_run.py --out gpurun_out/abl_$name --steps $STEPS \
+  env "${envs[@]}" timeout -k 10 600 python -u scripts/learning_run.py --out gpurun_out/abl_$name --steps $STEPS \
     --eval-interval 50 --epi 32 "$@" > gpurun_out/abl_$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
@@ -41,5 +41,11 @@ case $group in
     run lt16_inf_ent0 X=0 -- --env LidarTarget -n 2 --obs 0 --algo informarl --coef-ent 0
     run lt_dg_ent0 X=0 -- "${LT[@]}" --algo dgppo --coef-ent 0
     run mp_dg_ent0 X=0 -- "${MP[@]}" --algo dgppo --coef-ent 0
+    ;;
+  seeds)
+    for sd in 1 2 3; do run lt_dg_seed$sd X=0 -- "${LT[@]}" --algo dgppo --seed $sd; done
+    ;;
+  quickstart)  # the reference README's quickstart: python train.py --env LidarSpread --algo dgppo -n 3 --obs 3
+    for sd in 0 1; do STEPS=2000 run qs_dg_seed$sd X=0 -- --env LidarSpread -n 3 --obs 3 --algo dgppo --seed $sd; done
     ;;
 esac
