@@ -43,3 +43,12 @@ clean:
 	rm -rf $(OBJ) $(OUT)/libdgppo_hip.so
 
 .PHONY: all clean stamps nostore
+
+# diagnostic library with the fused policy step's phase timestamps (scripts/policy_probe.py; DGPPO_HIP_LIB points at it)
+PROBE_OBJS := $(filter-out $(OBJ)/policy.o,$(OBJS)) $(OBJ)/policy_probe.o
+$(OBJ)/policy_probe.o: $(CSRC)/policy.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DPOLICY_PROBE -c $< -o $@
+probe: $(PROBE_OBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OUT)/libdgppo_hip_probe.so $(PROBE_OBJS)

@@ -197,7 +197,60 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(dgppo_gemm_args p) {
 constexpr int kRowsMaxK = 256;
 constexpr int kRowsLdsFloats = 12800;  // 50 KB: K16 * (N + 1) must fit
 
-template <int NTW, bool VEC>
+// Epilogue operands of one 32-row unit (rows m0 + (r & 3) + 8 (r >> 2) + 4 h, columns col0 + 32 t + i): the
+// bias and, when EXTRA, beta * C + addend, requested as straight-line loads BEFORE the next unit's A
+// prefetch and consumed after the MFMAs.  A load issued after the prefetch (or guarded by a branch) makes its
+// in-order vmcnt wait cover the whole prefetch -- one HBM round trip per epilogue element when guarded.
+// EXTRA bit 0: addend, bit 1: beta * C (only the operands a call has are loaded)
+template <int NTW, int EXTRA>
+__device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* C, const float* Dd, int m0, int col0,
+                                         int i, int h, float (&bv)[NTW], float (&xv)[NTW][16]) {
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int col = col0 + 32 * t + i;
+    const bool cok = col < p.N;
+    bv[t] = (p.bias && cok) ? p.bias[col] : 0.0f;
+    if (EXTRA) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool ok = cok && row < p.M;
+        float x = 0.0f;
+        if (EXTRA & 2) {
+          const float* cs = ok ? C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col : (const float*)g_zero_row;
+          x = p.beta * *cs;
+        }
+        if (EXTRA & 1) {
+          const float* ds = ok ? Dd + row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col : (const float*)g_zero_row;
+          x += *ds;
+        }
+        xv[t][r] = x;
+      }
+    }
+  }
+}
+
+template <int NTW, int EXTRA>
+__device__ __forceinline__ void epi_store(const dgppo_gemm_args& p, float* C, const f32x16 (&acc)[NTW], int m0,
+                                          int col0, int i, int h, const float (&bv)[NTW], const float (&xv)[NTW][16]) {
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int col = col0 + 32 * t + i;
+    if (col >= p.N) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row < p.M) {
+        float v = p.alpha * acc[t][r] + bv[t];
+        if (EXTRA) v += xv[t][r];
+        if (p.relu) v = v > 0.0f ? v : 0.0f;
+        C[row_off(row, p.ldc, p.c_grp, p.c_gstride) + col] = v;
+      }
+    }
+  }
+}
+
+template <int NTW, bool VEC, int EXTRA>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int ncg) {
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
   const int NC = 32 * NTW * ncg, NP = NC + 1;
@@ -282,6 +335,8 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
     const float* bcol = Bs + 8 * h * NP + cg * 32 * NTW + i;
+    float bv[NTW], xv[NTW][16];
+    epi_load<NTW, EXTRA>(p, C, Dd, m0, cg * NTW * 32, i, h, bv, xv);
     bool rokn = false;
     const float* Arn = Ar;
     for (int c = 0; c < nch; ++c) {
@@ -304,25 +359,113 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
     Ar = Arn;
     rok = rokn;
     // epilogue: lane holds column (cg NTW + t) 32 + i, rows (r&3) + 8 (r>>2) + 4 h of the panel
+    epi_store<NTW, EXTRA>(p, C, acc, m0, cg * NTW * 32, i, h, bv, xv);
+  }
+}
+
+// ================================================================================================
+// rows, whole-unit prefetch form (K <= 16 NCH <= 64, 16-byte A rows): the same unit walk and LDS-staged B as
+// gemm_rows_kernel, but a wave requests ALL of a unit's A bytes at once (NCH chunks, 32 B x NCH per lane) and
+// the next unit's while the current one's MFMAs and stores issue.  At the update's shapes (131072 rows,
+// K = 64) a wave owns one or two units, so the chunk-at-a-time pipeline above serialised NCH HBM round trips
+// per unit; here one round trip covers the unit and every wave's bytes are in flight together.
+// ================================================================================================
+template <int NTW, int NCH, int EXTRA>
+__global__ __launch_bounds__(256) void gemm_rows_pf_kernel(dgppo_gemm_args p, int ncg) {
+  extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
+  const int NC = 32 * NTW * ncg, NP = NC + 1;
+  constexpr int K16 = 16 * NCH;
+  const int K = p.K, N = p.N, M = p.M;
+  const int b = blockIdx.z;
+  const float* A = p.A + (int64_t)b * p.stride_a;
+  const float* B = p.B + (int64_t)b * p.stride_b;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int panels = (M + 31) / 32;
+  const int64_t nunits = (int64_t)panels * ncg;
+  const int64_t ustep = (int64_t)gridDim.x * 4;
+  auto row_ptr = [&](int64_t uu, bool& rok) -> const float* {
+    const int row = (int)(uu / ncg) * 32 + i;
+    rok = uu < nunits && row < M;
+    return A + (rok ? row_off(row, p.lda, p.a_grp, p.a_gstride) : 0) + 8 * h;
+  };
+  auto load_unit = [&](const float* Ar, bool rok, float (&a)[NCH][8]) {  // branch-free, as gemm_rows_kernel
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      const int col = (cg * NTW + t) * 32 + i;
-      if (col >= N) continue;
-      const float bv = p.bias ? p.bias[col] : 0.0f;
+    for (int c = 0; c < NCH; ++c) {
+      const bool ok = rok && 16 * c + 8 * h < K;
+      const float* src = ok ? Ar + 16 * c : (const float*)g_zero_row;
+      const float4 v0 = *(const float4*)src, v1 = *(const float4*)(src + 4);
+      a[c][0] = v0.x; a[c][1] = v0.y; a[c][2] = v0.z; a[c][3] = v0.w;
+      a[c][4] = v1.x; a[c][5] = v1.y; a[c][6] = v1.z; a[c][7] = v1.w;
+    }
+  };
+  int64_t u = (int64_t)blockIdx.x * 4 + wave;
+  bool rok;
+  const float* Ar = row_ptr(u, rok);
+  float a0[NCH][8], a1[NCH][8];
+  load_unit(Ar, rok, a0);  // the first unit is requested before B is staged
+  {
+    const int total = K16 * NC;
+    const int dv = p.trans_b ? K16 : NC;
+    const float inv = 1.0f / (float)dv;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * 16) {
+      float v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < M) {
-          float* cp = C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
-          float v = p.alpha * acc[t][r];
-          if (p.beta != 0.0f) v += p.beta * *cp;
-          v += bv;
-          if (Dd) v += Dd[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
-          if (p.relu) v = v > 0.0f ? v : 0.0f;
-          *cp = v;
+      for (int uu = 0; uu < 16; ++uu) {
+        const int e = e0 + uu * 256;
+        const int mj = (int)(((float)e + 0.5f) * inv), mn = e - mj * dv;
+        const int k = p.trans_b ? mn : mj, n = p.trans_b ? mj : mn;
+        v[uu] = (e < total && k < K && n < N)
+                    ? (p.trans_b ? B[row_off(n, p.ldb, p.b_grp, p.b_gstride) + k]
+                                 : B[row_off(k, p.ldb, p.b_grp, p.b_gstride) + n])
+                    : 0.0f;
+      }
+#pragma unroll
+      for (int uu = 0; uu < 16; ++uu) {
+        const int e = e0 + uu * 256;
+        if (e < total) {
+          const int mj = (int)(((float)e + 0.5f) * inv), mn = e - mj * dv;
+          const int k = p.trans_b ? mn : mj, n = p.trans_b ? mj : mn;
+          Bs[k * NP + n] = v[uu];
         }
       }
     }
+  }
+  __syncthreads();
+  float* C = p.C + (int64_t)b * p.stride_c;
+  const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  for (; u < nunits; u += ustep) {
+    const int panel = (int)(u / ncg), cg = (int)(u - (int64_t)panel * ncg);
+    const int m0 = panel * 32;
+    // this unit's epilogue operands are requested before the next unit's prefetch (epi_load)
+    float bv[NTW], xv[NTW][16];
+    epi_load<NTW, EXTRA>(p, C, Dd, m0, cg * NTW * 32, i, h, bv, xv);
+    bool rokn;
+    const float* Arn = row_ptr(u + ustep, rokn);
+    load_unit(Arn, rokn, a1);  // the next unit's bytes are in flight during this unit's MFMAs and stores
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const float* bcol = Bs + 8 * h * NP + cg * 32 * NTW + i;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const float* brow = bcol + 16 * c * NP;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c][q], brow[q * NP + 32 * t], acc[t], 0, 0, 0);
+    }
+    epi_store<NTW, EXTRA>(p, C, acc, m0, cg * NTW * 32, i, h, bv, xv);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a0[c][q] = a1[c][q];
+    Ar = Arn;
+    rok = rokn;
   }
 }
 
@@ -332,7 +475,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
 // registers, so the main loop issues MFMAs fed by the streamed A chunks and registers only (no LDS
 // read per MFMA).  Same unit walk, A chunk pipeline and epilogue as gemm_rows_kernel.
 // ================================================================================================
-template <int NTW, int NCH>
+template <int NTW, int NCH, int EXTRA>
 __global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) {
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
   constexpr int NC = 32 * NTW, NP = NC + 1, K16 = 16 * NCH;
@@ -398,11 +541,10 @@ __global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) 
       for (int t = 0; t < NTW; ++t) bf[c][q][t] = Bs[(16 * c + 8 * h + q) * NP + 32 * t + i];
   float* C = p.C + (int64_t)b * p.stride_c;
   const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
-  float bv[NTW];
-#pragma unroll
-  for (int t = 0; t < NTW; ++t) bv[t] = (p.bias && 32 * t + i < N) ? p.bias[32 * t + i] : 0.0f;
   for (; u < nunits; u += ustep) {
     const int m0 = (int)u * 32;
+    float bv[NTW], xv[NTW][16];
+    epi_load<NTW, EXTRA>(p, C, Dd, m0, 0, i, h, bv, xv);
     f32x16 acc[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
@@ -429,24 +571,7 @@ __global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) 
     }
     Ar = Arn;
     rok = rokn;
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      const int col = t * 32 + i;
-      if (col >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < M) {
-          float* cp = C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
-          float v = p.alpha * acc[t][r];
-          if (p.beta != 0.0f) v += p.beta * *cp;
-          v += bv[t];
-          if (Dd) v += Dd[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
-          if (p.relu) v = v > 0.0f ? v : 0.0f;
-          *cp = v;
-        }
-      }
-    }
+    epi_store<NTW, EXTRA>(p, C, acc, m0, 0, i, h, bv, xv);
   }
 }
 
@@ -707,25 +832,54 @@ void launch_rows_t(const dgppo_gemm_args* p, int ncg, hipStream_t s) {
     const char* v = getenv("DGPPO_ROWS_WG_PER_CU");
     knob = v ? atoi(v) : -1;
   }
+  const bool vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
+                   (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
+  // kernel choice and workgroups per CU, measured on the update's shapes (scripts/ab_gemm_pf.sh,
+  // profiles/r03_gemm_rows_ab.txt, 131072 rows): the whole-unit prefetch form wins for K <= 32 and for N > 64
+  // (N99 K32 35.7 -> 27.8 us, N64 K32 + addend 39.8 -> 22.4, N192 K32 52.4 -> 41.3, N192 K64 68.8 -> 63.9) at 3
+  // workgroups per CU; the B-in-registers form stays best for N <= 64, K = 64 at 2 (28.0 -> 24.4-24.8 us)
+  static const int pf = env_knob("DGPPO_ROWS_PF", 1);
+  static const int breg = env_knob("DGPPO_ROWS_BREG", 1);
+  const bool use_pf = vec && pf && K16 <= 64 && (K16 <= 32 || ncg > 1 || !breg);
+  const bool use_breg = !use_pf && vec && breg && ncg == 1 && K16 <= 64;
+  if (use_pf && per_cu > 3) per_cu = 3;
+  if (use_breg && per_cu > 2) per_cu = 2;
   if (knob > 0 && knob < per_cu) per_cu = knob;
   const int64_t want = (units + 3) / 4, cap = 256LL * per_cu;
   const int grid = (int)(want < cap ? want : cap);
-  const bool vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
-                   (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
-  static const int breg = env_knob("DGPPO_ROWS_BREG", 1);
-  if (vec && breg && ncg == 1 && K16 <= 64) {
+  const int extra = (p->addend != nullptr ? 1 : 0) | (p->beta != 0.0f ? 2 : 0);
+  if (use_pf) {
+#define DG_PF(c)                                                                                               \
+  if (K16 == 16 * c) {                                                                                         \
+    switch (extra) {                                                                                           \
+      case 0: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 0>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); break; \
+      case 1: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 1>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); break; \
+      case 2: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 2>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); break; \
+      default: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 3>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); \
+    }                                                                                                          \
+    return;                                                                                                    \
+  }
+    DG_PF(1) DG_PF(2) DG_PF(3) DG_PF(4)
+#undef DG_PF
+  }
+  if (use_breg) {
 #define DG_RB(c)                                                                                              \
   if (K16 == 16 * c) {                                                                                        \
-    hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); \
+    switch (extra) {                                                                                          \
+      case 0: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 0>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); break; \
+      case 1: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 1>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); break; \
+      case 2: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 2>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); break; \
+      default: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 3>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); \
+    }                                                                                                         \
     return;                                                                                                   \
   }
     DG_RB(1) DG_RB(2) DG_RB(3) DG_RB(4)
 #undef DG_RB
   }
-  if (vec)
-    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, true>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
-  else
-    hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, false>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
+#define DG_R(v, x) \
+  if (vec == v && extra == x) hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, v, x>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
+  DG_R(true, 0) DG_R(true, 1) DG_R(true, 2) DG_R(true, 3) DG_R(false, 0) DG_R(false, 1) DG_R(false, 2) DG_R(false, 3)
+#undef DG_R
 }
 
 int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {

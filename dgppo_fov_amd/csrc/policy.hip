@@ -53,7 +53,7 @@ constexpr int kX0P = 13, kQTP = 100, kXCP = 132, kY0P = 36, kYP = 68, kXSP = 44;
 // (rows 0..D-1) and its bias row (row 32)
 constexpr int kQKRows = 33, kQKCols = kQTP, kQKStride = kQKRows * kQKCols;
 
-// phase timestamps for tuning (scripts/policy_probe.py builds this file with -DPOLICY_PROBE): thread 0
+// phase timestamps for tuning (`make probe` builds this file with -DPOLICY_PROBE, scripts/policy_probe.py reads them): thread 0
 // of each workgroup writes s_memrealtime (100 MHz) at phase k into p.h_out viewed as uint64[grid][32]
 #ifdef POLICY_PROBE
 #define PROBE(k)                                                                                      \
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
   bias_load(bi, p.gru_bi, 3 * kHid);
   bias_load(bhn, p.gru_bhn, kHid);
   bias_load(bs, p.bs, kHid);
-  PROBE(7);
+  PROBE(12);
   // ---- MLP head: two Dense(64) + LN + ReLU, in place in L.yb
   {
     f32x4 acc[1][kRT];

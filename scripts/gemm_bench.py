@@ -20,6 +20,8 @@ SHAPES = [
     ("fwd N64 K111", M, 64, 111, 0, 0, 1, False, 0.0),
     ("dx N111 K64 tb", M, 111, 64, 0, 1, 1, False, 0.0),
     ("fwd N192 K32 +b", M, 192, 32, 0, 0, 1, True, 0.0),
+    ("fwd N99 K32 +b", M, 99, 32, 0, 0, 1, True, 0.0),
+    ("fwd N64 K32 +b +add relu", M, 64, 32, 0, 0, 1, True, 0.0),
     ("dx N32 K192 tb", M, 32, 192, 0, 1, 1, False, 0.0),
     ("wgrad M64 N192", 64, 192, M, 1, 0, 1, False, 1.0),
     ("wgrad M64 N64", 64, 64, M, 1, 0, 1, False, 1.0),
@@ -51,8 +53,11 @@ for (lab, m, n, k, ta, tb, batch, bias, beta) in SHAPES:
     bv = torch.randn(n, device=dev) if bias else None
     bg = torch.zeros(n, device=dev) if ta else None
 
+    add = torch.randn((m, n), device=dev) if "+add" in lab else None
+
     def run():
-        K.gemm(A, B, C, m, n, k, ta=bool(ta), tb=bool(tb), bias=bv, beta=beta, bias_grad=bg)
+        K.gemm(A, B, C, m, n, k, ta=bool(ta), tb=bool(tb), bias=bv, beta=beta, bias_grad=bg, addend=add,
+               relu="relu" in lab)
 
     for _ in range(3):
         run()
