@@ -489,34 +489,40 @@ __device__ unsigned long long g_blk_stamps[8];
 //   C  per-agent row minima -> cost and reward terms; is-inside on the next state
 //   D  reward/cost stores, ray cast of the next state (keys + hit points), stable rank -> top-k
 //   E  stream the next graph out
-template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
-__global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+// One env step of one workgroup's env.  LOAD: the current graph's rows come from io.states (and the
+// obstacles from io.obstacles); otherwise they are already in LDS (the persistent rollout below carries the
+// previous step's next rows over, bit-identical to re-reading what that step wrote).
+template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK, bool LOAD, bool ACT_LDS = false>
+__device__ __forceinline__ void block_step(const dgppo_env_cfg& cfg, const dgppo_env_step_io& io, float* lds,
+                                           int64_t env) {
   constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
   const Dims<NA, NO, NR, NK> d(cfg);
   const int n = d.n, O = d.O, k = d.k;
   const bool lidar = !mpe && O > 0;
   const Carve cv(n, SD, O, d.R, k, !mpe);
   const int tid = threadIdx.x;
-  const int64_t env = blockIdx.x;
 #ifdef DGPPO_ENV_STAMPS
   uint64_t bst[5] = {0, 0, 0, 0, 0}, blast = __builtin_amdgcn_s_memtime();
 #endif
 
   // ---- A ------------------------------------------------------------------------------------
-  const float* st = io.states + env * io.states_stride;
-  const int n_cur = (2 * n + (mpe ? O : 0)) * SD;  // type_states(0), (1) [, (2) for MPE]
-  for (int idx = tid; idx < n_cur; idx += BLOCK) lds[cv.cur + idx] = st[idx];
-  if (lidar) {
-    for (int idx = tid; idx < n * k * 2; idx += BLOCK) {  // type_states(2)[:, :2] = current hits
-      const int h = idx >> 1, c = idx & 1;
-      lds[cv.curhit + idx] = st[(2 * n + h) * SD + c];
+  if (LOAD) {
+    const float* st = io.states + env * io.states_stride;
+    const int n_cur = (2 * n + (mpe ? O : 0)) * SD;  // type_states(0), (1) [, (2) for MPE]
+    for (int idx = tid; idx < n_cur; idx += BLOCK) lds[cv.cur + idx] = st[idx];
+    if (lidar) {
+      for (int idx = tid; idx < n * k * 2; idx += BLOCK) {  // type_states(2)[:, :2] = current hits
+        const int h = idx >> 1, c = idx & 1;
+        lds[cv.curhit + idx] = st[(2 * n + h) * SD + c];
+      }
+      const float* ob = io.obstacles + env * io.obstacles_stride;
+      for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) lds[cv.obst + idx] = ob[idx];
     }
-    const float* ob = io.obstacles + env * io.obstacles_stride;
-    for (int idx = tid; idx < O * DGPPO_OBST_FIELDS; idx += BLOCK) lds[cv.obst + idx] = ob[idx];
   }
-  const float* ac = io.action + env * io.action_stride;
-  for (int idx = tid; idx < 2 * n; idx += BLOCK) lds[cv.act + idx] = clampf_nan(ac[idx], -1.0f, 1.0f);
+  if (!ACT_LDS) {  // (ACT_LDS: the caller staged the clipped actions in LDS)
+    const float* ac = io.action + env * io.action_stride;
+    for (int idx = tid; idx < 2 * n; idx += BLOCK) lds[cv.act + idx] = clampf_nan(ac[idx], -1.0f, 1.0f);
+  }
   __syncthreads();
   BLK_STAMP(0);
 
@@ -671,6 +677,57 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
   if (tid == 0)
     for (int q = 0; q < 5; ++q) atomicAdd(&g_blk_stamps[q], (unsigned long long)bst[q]);
 #endif
+}
+
+template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
+__global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgppo_env_step_io io) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  block_step<ENGINE, GOAL, SD, BLOCK, NA, NO, NR, NK, true>(cfg, io, lds, blockIdx.x);
+}
+
+// Persistent rollout of the workgroup-per-env kernel (dgppo_env_rollout for every shape the wave kernels do
+// not take: MPE, Lidar n = 32 / 8 obstacles, other sizes): one launch runs all T steps of one env per
+// workgroup, step t reading graph t's rows from LDS (graph 0 from HBM) and writing graph t + 1 into the
+// time-major (T + 1) buffers, reward[t], cost[t] -- the same arithmetic as T per-step launches, without their
+// launch floor and their re-reads of every graph.
+template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
+__global__ __launch_bounds__(BLOCK) void env_rollout_block_kernel(dgppo_env_cfg cfg, dgppo_env_rollout_io r) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
+  const Dims<NA, NO, NR, NK> d(cfg);
+  const int n = d.n, O = d.O, k = d.k;
+  const bool lidar = !mpe && O > 0;
+  const Carve cv(n, SD, O, d.R, k, !mpe);
+  const int64_t env = blockIdx.x;
+  // step t + 1's actions are requested before step t's graph stores: vmcnt counts stores too, so a load
+  // issued after them would wait for the whole store drain of the previous step (one HBM round trip per step)
+  static_assert(BLOCK >= 64, "2 n <= 64 actions per step, one per thread");
+  const int na = 2 * n;
+  const float* act0 = r.step.action + env * r.step.action_stride;
+  float a_nxt = threadIdx.x < na ? act0[threadIdx.x] : 0.0f;
+#pragma unroll 1
+  for (int t = 0; t < r.T; ++t) {
+    if (threadIdx.x < na) lds[cv.act + threadIdx.x] = clampf_nan(a_nxt, -1.0f, 1.0f);
+    if (t + 1 < r.T && threadIdx.x < na) a_nxt = act0[(t + 1) * r.t_action + threadIdx.x];
+    dgppo_env_step_io q = r.step;
+    q.states = r.step.out_states + t * r.t_states;
+    q.action = r.step.action + t * r.t_action;
+    q.nodes = r.step.nodes + (t + 1) * r.t_nodes;
+    q.edges = r.step.edges + (t + 1) * r.t_edges;
+    q.out_states = r.step.out_states + (t + 1) * r.t_states;
+    q.receivers = r.step.receivers + (t + 1) * r.t_index;
+    q.senders = r.step.senders + (t + 1) * r.t_index;
+    q.reward = r.step.reward + t * r.t_reward;
+    q.cost = r.step.cost + t * r.t_cost;
+    if (t == 0) block_step<ENGINE, GOAL, SD, BLOCK, NA, NO, NR, NK, true, true>(cfg, q, lds, env);
+    else block_step<ENGINE, GOAL, SD, BLOCK, NA, NO, NR, NK, false, true>(cfg, q, lds, env);
+    __syncthreads();
+    // graph t + 1 becomes the current graph: agent rows <- next rows, current hits <- next hits
+    for (int idx = threadIdx.x; idx < n * SD; idx += BLOCK) lds[cv.cur + idx] = lds[cv.nxt + idx];
+    if (lidar)
+      for (int idx = threadIdx.x; idx < n * k * 2; idx += BLOCK) lds[cv.curhit + idx] = lds[cv.hits + idx];
+    __syncthreads();
+  }
 }
 
 // Rectangle.inside with r = 0 (raytracing's is_in): the rounded-corner term sqrt(.) < 0 never holds
@@ -2586,6 +2643,45 @@ static void launch_step(const dgppo_env_cfg& c, const dgppo_env_step_io& io, siz
                      dim3(BLOCK), shmem, s, c, io);
 }
 
+template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
+static void launch_rollout_block(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem, hipStream_t s) {
+  hipLaunchKernelGGL((env_rollout_block_kernel<ENGINE, GOAL, SD, BLOCK, NA, NO, NR, NK>), dim3((unsigned)r.step.n_env),
+                     dim3(BLOCK), shmem, s, c, r);
+}
+
+// the same compile-time size selection as dispatch_step_sized
+template <int ENGINE, int GOAL, int SD>
+static void dispatch_rollout_block_sized(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem,
+                                         hipStream_t s) {
+  const int n = c.n_agents, O = c.n_obs, R = c.n_rays, k = c.top_k;
+  if (ENGINE == DGPPO_ENGINE_MPE) {
+    if (n == 3 && O == 3) return launch_rollout_block<ENGINE, GOAL, SD, 64, 3, 3, 0, 0>(c, r, shmem, s);
+    if (n == 3 && O == 0) return launch_rollout_block<ENGINE, GOAL, SD, 64, 3, 0, 0, 0>(c, r, shmem, s);
+    return launch_rollout_block<ENGINE, GOAL, SD, 64, 0, -1, 0, 0>(c, r, shmem, s);
+  }
+  if (R == 32 && k == 8) {
+    if (n == 8 && O == 3) return launch_rollout_block<ENGINE, GOAL, SD, 256, 8, 3, 32, 8>(c, r, shmem, s);
+    if (n == 32 && O == 8) return launch_rollout_block<ENGINE, GOAL, SD, 256, 32, 8, 32, 8>(c, r, shmem, s);
+  }
+  if (n * R >= 256) return launch_rollout_block<ENGINE, GOAL, SD, 256, 0, -1, 0, 0>(c, r, shmem, s);
+  return launch_rollout_block<ENGINE, GOAL, SD, 128, 0, -1, 0, 0>(c, r, shmem, s);
+}
+
+static void dispatch_rollout_block(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem, hipStream_t s) {
+  const bool spread = c.goal_mode == DGPPO_GOAL_SPREAD;
+  switch (c.engine) {
+    case DGPPO_ENGINE_MPE:
+      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, r, shmem, s)
+                    : dispatch_rollout_block_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, r, shmem, s);
+    case DGPPO_ENGINE_BICYCLE:
+      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, r, shmem, s)
+                    : dispatch_rollout_block_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, r, shmem, s);
+    default:
+      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, r, shmem, s)
+                    : dispatch_rollout_block_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, r, shmem, s);
+  }
+}
+
 template <int ENGINE, int GOAL, int SD>
 static void dispatch_step_sized(const dgppo_env_cfg& c, const dgppo_env_step_io& io, size_t shmem, hipStream_t s) {
   const int n = c.n_agents, O = c.n_obs, R = c.n_rays, k = c.top_k;
@@ -2937,9 +3033,21 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
     else launch_rollout<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(*cfg, *r, s);
     return (int)hipGetLastError();
   }
-  // other configs: the per-step kernel T times.  rebuild_first: a states-only reset (dgppo_env_reset_states)
-  // left graph 0 unbuilt when the wave kernels took it (a misaligned per-step stride sends the rollout here)
+  // other configs: rebuild_first: a states-only reset (dgppo_env_reset_states) left graph 0 unbuilt when the
+  // wave kernels took it (a misaligned per-step stride sends the rollout here)
   if (r->rebuild_first && wave_config(cfg, io.edges, io.edges_stride, 0)) launch_rebuild(cfg, io, s);
+  // the workgroup-per-env shapes: one persistent launch for all T steps (DGPPO_ENV_BLOCK_ROLLOUT=0: T launches)
+  static const bool block_rollout = [] {
+    const char* e = getenv("DGPPO_ENV_BLOCK_ROLLOUT");
+    return !(e && atoi(e) == 0);
+  }();
+  if (block_rollout && r->T > 0 && cfg->variant == DGPPO_VARIANT_NONE && cfg->engine != DGPPO_ENGINE_OMNI &&
+      cfg->n_agents <= 32) {  // (2 n actions per step staged one per thread of a >= 64-thread workgroup)
+    const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
+                   cfg->engine != DGPPO_ENGINE_MPE);
+    dispatch_rollout_block(*cfg, *r, (size_t)cv.total * sizeof(float), s);
+    return (int)hipGetLastError();
+  }
   for (int t = 0; t < r->T; ++t) {
     dgppo_env_step_io q = io;
     q.states = io.out_states + t * r->t_states;

@@ -155,7 +155,10 @@ def test_policy_rollout_lanes_bit_exact(cuda, env_id, graph):
 
 @pytest.mark.parametrize("eid,n,obs,B", [("LidarSpread", 8, 3, 255), ("LidarTarget", 8, 3, 64),
                                          ("LidarBicycleTarget", 8, 3, 130), ("LidarOmniTarget", 8, 3, 97),
-                                         ("MPESpread", 3, 3, 33), ("LidarSpread", 4, 2, 20)])
+                                         ("MPESpread", 3, 3, 33), ("LidarSpread", 4, 2, 20),
+                                         # the workgroup-per-env persistent kernel (env_rollout_block_kernel)
+                                         ("MPETarget", 3, 0, 17), ("LidarTarget", 2, 0, 11),
+                                         ("LidarBicycleTarget", 2, 1, 7), ("LidarSpread", 32, 8, 5)])
 @pytest.mark.parametrize("graph", [False, True])
 def test_persistent_env_rollout_bit_exact(cuda, eid, n, obs, B, graph):
     """The env-only rollout as ONE persistent launch (states-only reset + dgppo_env_rollout, a wave per
@@ -177,6 +180,32 @@ def test_persistent_env_rollout_bit_exact(cuda, eid, n, obs, B, graph):
         b = eng.buf
         outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders, eng.rewards,
                                               eng.costs)])
+    for k, (x, y) in enumerate(zip(*outs)):
+        assert np.array_equal(x, y), k
+
+
+def test_block_persistent_rollout_matches_wave_steps(cuda):
+    """With the workgroup-per-env kernels forced (dgppo_env_set_step_kernel(1)), the n = 8 Lidar configs take the
+    block persistent rollout; it matches the default path (wave kernels) bit for bit."""
+    from dgppo_fov_amd import _lib
+    lib = _lib.load()
+    env = make_env("LidarSpread", 8, num_obs=3, device=cuda)
+    B, T = 37, 16
+    outs = []
+    for mode in (0, 1):
+        prev = lib.dgppo_env_set_step_kernel(mode)
+        try:
+            eng = RolloutEngine(env, B, T, cuda, fused=True)
+            gen = torch.Generator(device=cuda)
+            gen.manual_seed(3)
+            eng.actions.uniform_(-1.0, 1.0, generator=gen)
+            eng.run(key=8)
+            torch.cuda.synchronize(cuda)
+            b = eng.buf
+            outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders, eng.rewards,
+                                                  eng.costs)])
+        finally:
+            lib.dgppo_env_set_step_kernel(prev)
     for k, (x, y) in enumerate(zip(*outs)):
         assert np.array_equal(x, y), k
 
