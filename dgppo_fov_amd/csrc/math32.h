@@ -71,6 +71,74 @@ __host__ __device__ inline float atan2_32(float y, float x) {
   return signbit(y) ? -a : a;
 }
 
+// ---- exp / log1p / logaddexp(0, x) ---------------------------------------------------------
+// The VMAS contact force (env/vmas/physax/world.py `_get_constraint_forces`) evaluates
+// jnp.logaddexp(0, (d_min - d) / k); these restate it as max(0, x) + log1p(exp(-|x|)) on a
+// cephes expf (Cody-Waite ln2 split, degree-6 minimax) and logf (frexp + degree-9 minimax), with
+// log1p from Goldberg's correction log(u) * y / (u - 1), u = 1 + y.
+constexpr float kLog2e = 1.44269504088896341f;
+constexpr float kLn2Hi = 0.693359375f, kLn2Lo = -2.12194440e-4f;
+constexpr float kSqrtHalf = 0.707106781186547524f;
+
+__host__ __device__ inline float exp32_nonpos(float x) {  // x <= 0; 0 below -87 (no subnormals)
+  if (!(x >= -87.0f)) return 0.0f;
+  const float n = rintf(x * kLog2e);
+  float r = x - n * kLn2Hi;
+  r = r - n * kLn2Lo;
+  float p = 1.9875691500e-4f;
+  p = p * r + 1.3981999507e-3f;
+  p = p * r + 8.3334519073e-3f;
+  p = p * r + 4.1665795894e-2f;
+  p = p * r + 1.6666665459e-1f;
+  p = p * r + 5.0000001201e-1f;
+  p = ((p * r) * r + r) + 1.0f;
+  const uint32_t eb = (uint32_t)((int)n + 127) << 23;  // 2^n, n in [-126, 0]
+  float two_n;
+  __builtin_memcpy(&two_n, &eb, 4);
+  return p * two_n;
+}
+
+__host__ __device__ inline float log32_pos(float x) {  // x normal, > 0
+  uint32_t b;
+  __builtin_memcpy(&b, &x, 4);
+  int e = (int)((b >> 23) & 0xFFu) - 126;
+  b = (b & 0x807FFFFFu) | 0x3F000000u;  // mantissa in [0.5, 1)
+  float m;
+  __builtin_memcpy(&m, &b, 4);
+  if (m < kSqrtHalf) {
+    e -= 1;
+    m = (m + m) - 1.0f;
+  } else {
+    m = m - 1.0f;
+  }
+  const float z = m * m;
+  float p = 7.0376836292e-2f;
+  p = p * m - 1.1514610310e-1f;
+  p = p * m + 1.1676998740e-1f;
+  p = p * m - 1.2420140846e-1f;
+  p = p * m + 1.4249322787e-1f;
+  p = p * m - 1.6668057665e-1f;
+  p = p * m + 2.0000714765e-1f;
+  p = p * m - 2.4999993993e-1f;
+  p = p * m + 3.3333331174e-1f;
+  const float fe = (float)e;
+  float y = (p * m) * z;
+  y = y + fe * kLn2Lo;
+  y = y - 0.5f * z;
+  return (m + y) + fe * kLn2Hi;
+}
+
+__host__ __device__ inline float log1p32(float y) {  // y in [0, 1]
+  const float u = 1.0f + y;
+  if (u == 1.0f) return y;
+  return log32_pos(u) * (y / (u - 1.0f));
+}
+
+__host__ __device__ inline float logaddexp0_32(float x) {  // jnp.logaddexp(0, x), finite x
+  const float amax = x > 0.0f ? x : 0.0f;
+  return amax + log1p32(exp32_nonpos(-fabsf(x)));
+}
+
 // ---- Philox4x32-10 -------------------------------------------------------------------------
 __host__ __device__ inline uint32_t philox4x32_w0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                   uint32_t k0, uint32_t k1) {

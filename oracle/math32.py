@@ -95,6 +95,74 @@ def atan2(y, x):
 
 
 # --------------------------------------------------------------------------------------------
+# exp / log1p / logaddexp(0, x): twins of exp32_nonpos / log32_pos / log1p32 / logaddexp0_32 in
+# csrc/math32.h, restating jnp.logaddexp(0, .) of env/vmas/physax/world.py `_get_constraint_forces`.
+# --------------------------------------------------------------------------------------------
+LOG2E = F(1.44269504088896341)
+LN2_HI, LN2_LO = F(0.693359375), F(-2.12194440e-4)
+SQRT_HALF = F(0.707106781186547524)
+EXP_P = [F(v) for v in (1.9875691500e-4, 1.3981999507e-3, 8.3334519073e-3, 4.1665795894e-2,
+                        1.6666665459e-1, 5.0000001201e-1)]
+LOG_P = [F(v) for v in (7.0376836292e-2, -1.1514610310e-1, 1.1676998740e-1, -1.2420140846e-1,
+                        1.4249322787e-1, -1.6668057665e-1, 2.0000714765e-1, -2.4999993993e-1,
+                        3.3333331174e-1)]
+
+
+def exp_nonpos(x):
+    """exp(x) for x <= 0 (0 below -87)."""
+    x = _f(x)
+    with np.errstate(all="ignore"):
+        n = np.rint(x * LOG2E).astype(F)
+        r = x - n * LN2_HI
+        r = r - n * LN2_LO
+        p = EXP_P[0]
+        for c in EXP_P[1:]:
+            p = p * r + c
+        p = ((p * r) * r + r) + F(1.0)
+        ni = np.clip(n, -126, 0).astype(np.int64)
+        two_n = ((ni + 127).astype(U32) << U32(23)).view(F)
+        out = (p * two_n).astype(F)
+    return np.where(x >= F(-87.0), out, F(0.0)).astype(F)
+
+
+def log_pos(x):
+    """log(x) for normal x > 0."""
+    x = _f(x)
+    b = np.ascontiguousarray(x).view(U32)
+    e = ((b >> U32(23)) & U32(0xFF)).astype(np.int64) - 126
+    m = ((b & U32(0x807FFFFF)) | U32(0x3F000000)).view(F)
+    with np.errstate(all="ignore"):
+        low = m < SQRT_HALF
+        e = np.where(low, e - 1, e)
+        m = np.where(low, (m + m) - F(1.0), m - F(1.0)).astype(F)
+        z = m * m
+        p = LOG_P[0]
+        for c in LOG_P[1:]:
+            p = p * m + c
+        fe = e.astype(F)
+        y = (p * m) * z
+        y = y + fe * LN2_LO
+        y = y - F(0.5) * z
+        return ((m + y) + fe * LN2_HI).astype(F)
+
+
+def log1p(y):
+    """log(1 + y) for y in [0, 1]."""
+    y = _f(y)
+    u = F(1.0) + y
+    with np.errstate(all="ignore"):
+        v = log_pos(np.where(u == F(1.0), F(2.0), u)) * (y / (u - F(1.0)))
+    return np.where(u == F(1.0), y, v).astype(F)
+
+
+def logaddexp0(x):
+    """jnp.logaddexp(0, x) for finite x."""
+    x = _f(x)
+    amax = np.where(x > F(0.0), x, F(0.0)).astype(F)
+    return (amax + log1p(exp_nonpos(-np.abs(x)))).astype(F)
+
+
+# --------------------------------------------------------------------------------------------
 # Philox4x32-10
 # --------------------------------------------------------------------------------------------
 PHILOX_M0 = np.uint64(0xD2511F53)
