@@ -15,6 +15,8 @@ LIB_PATH = pathlib.Path(os.environ.get("DGPPO_HIP_LIB", PKG_DIR / "lib" / "libdg
 
 DGPPO_EINVAL = -22
 DGPPO_ENGINE_LIDAR, DGPPO_ENGINE_BICYCLE, DGPPO_ENGINE_MPE, DGPPO_ENGINE_OMNI = 0, 1, 2, 3
+DGPPO_ENGINE_VMAS_WHEEL, DGPPO_ENGINE_VMAS_TRANSPORT = 4, 5
+DGPPO_VMAS_FIELDS = 8
 DGPPO_GOAL_SPREAD, DGPPO_GOAL_TARGET = 0, 1
 (DGPPO_VARIANT_NONE, DGPPO_VARIANT_LINE, DGPPO_VARIANT_FORMATION, DGPPO_VARIANT_CORRIDOR,
  DGPPO_VARIANT_CONNECT) = 0, 1, 2, 3, 4
@@ -300,7 +302,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 7  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 8  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

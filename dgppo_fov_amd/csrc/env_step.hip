@@ -26,6 +26,7 @@
 
 #include "../../include/dgppo_hip.h"
 #include "math32.h"
+#include "vmas.h"
 
 #pragma clang fp contract(off)
 
@@ -2602,6 +2603,7 @@ __global__ __launch_bounds__(kT) void reset_kernel(dgppo_env_cfg cfg, dgppo_env_
 // ---- host dispatch --------------------------------------------------------------------------
 static int validate(const dgppo_env_cfg* c) {
   if (!c) return DGPPO_EINVAL;
+  if (vmas::is_vmas(c)) return vmas::validate(c);
   if (c->engine < 0 || c->engine > 3 || c->goal_mode < 0 || c->goal_mode > 1) return DGPPO_EINVAL;
   if (c->n_agents < 1 || c->n_agents > kMaxAgents || c->n_obs < 0 || c->n_obs > kMaxObs) return DGPPO_EINVAL;
   if (c->engine == DGPPO_ENGINE_OMNI && c->goal_mode != DGPPO_GOAL_TARGET) return DGPPO_EINVAL;
@@ -2768,6 +2770,7 @@ static float sq_threshold(float r) {
 
 extern "C" int dgppo_env_cfg_finalize(dgppo_env_cfg* c) {
   if (!c) return DGPPO_EINVAL;
+  if (vmas::is_vmas(c)) return vmas::finalize(c);
   const bool mpe = c->engine == DGPPO_ENGINE_MPE;
   const int n = c->n_agents;
   const bool omni = c->engine == DGPPO_ENGINE_OMNI;
@@ -2858,6 +2861,7 @@ static bool wave_edges_aligned(const dgppo_env_cfg* cfg, const float* edges, int
 
 extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
+  if (vmas::is_vmas(cfg)) return vmas::step(cfg, io, stream);
   if (io->n_env == 0) return 0;
   if (!io->states || !io->action || !io->nodes || !io->edges || !io->out_states || !io->receivers ||
       !io->senders || !io->reward || !io->cost)
@@ -2956,6 +2960,7 @@ static void launch_rebuild(const dgppo_env_cfg* cfg, const dgppo_env_step_io& st
 
 extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
+  if (vmas::is_vmas(cfg)) return vmas::reset(cfg, io, stream);  // the full reset (graph 0 included)
   if (!wave_config(cfg, io->edges, io->edges_stride, 0)) return dgppo_env_reset(cfg, io, stream);
   if (io->n_env == 0) return 0;
   if (!io->out_states || !io->obstacles) return DGPPO_EINVAL;
@@ -3015,6 +3020,7 @@ extern "C" int dgppo_env_diag_stamps(unsigned long long* out) {
 
 extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollout_io* r, void* stream) {
   if (validate(cfg) || !r || r->T < 0 || r->step.n_env < 0) return DGPPO_EINVAL;
+  if (vmas::is_vmas(cfg)) return vmas::rollout(cfg, r, stream);
   const dgppo_env_step_io& io = r->step;
   if (r->T == 0 && !r->rebuild_first) return 0;
   if (io.n_env == 0) return 0;
@@ -3067,6 +3073,7 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
 
 extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
+  if (vmas::is_vmas(cfg)) return vmas::reset(cfg, io, stream);
   if (io->n_env == 0) return 0;
   if (!io->nodes || !io->edges || !io->out_states || !io->receivers || !io->senders) return DGPPO_EINVAL;
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;

@@ -1,8 +1,8 @@
 """Env registry + make_env (dgppo/env/__init__.py:10-55).
 
-Every Lidar and MPE env of the reference is built (the variants LidarLine, MPELine, MPEFormation,
-MPECorridor and MPEConnectSpread on the variant kernels); VMAS (a separate
-contact-physics engine) is not, and raises here."""
+Every env of the reference is built: Lidar and MPE (the variants LidarLine, MPELine, MPEFormation,
+MPECorridor and MPEConnectSpread on the variant kernels) and the two VMAS contact-physics envs
+(csrc/vmas.hip), SURVEY.md §8f rank 4."""
 from typing import Optional
 
 from .base import MultiAgentEnv, StepResult, RolloutResult
@@ -10,6 +10,7 @@ from .lidar_env import (LidarSpread, LidarTarget, LidarBicycleTarget, LidarOmniT
                         LidarEnvState)
 from .mpe import (MPESpread, MPETarget, MPELine, MPEFormation, MPECorridor, MPEConnectSpread, MPE,
                   MPEEnvState)
+from .vmas import VMASWheel, VMASReverseTransport, VMASEnv
 
 ENV = {
     "MPETarget": MPETarget,
@@ -23,17 +24,15 @@ ENV = {
     "LidarLine": LidarLine,
     "LidarBicycleTarget": LidarBicycleTarget,
     "LidarOmniTarget": LidarOmniTarget,
+    "VMASReverseTransport": VMASReverseTransport,
+    "VMASWheel": VMASWheel,
 }
-
-NOT_YET_BUILT = ("VMASReverseTransport", "VMASWheel")
 
 DEFAULT_MAX_STEP = 128
 
 
 def make_env(env_id: str, num_agents: int, max_step: int = None, full_observation: bool = False,
              num_obs: Optional[int] = None, n_rays: Optional[int] = None, device=None) -> MultiAgentEnv:
-    if env_id in NOT_YET_BUILT:
-        raise NotImplementedError(f"Environment {env_id} is not built yet (see DESIGN.md, next rows)")
     assert env_id in ENV, f"Environment {env_id} not implemented."
     params = dict(ENV[env_id].PARAMS)  # copied: the reference mutates the class dict (env/__init__.py:40-46)
     max_step = DEFAULT_MAX_STEP if max_step is None else max_step

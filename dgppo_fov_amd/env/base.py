@@ -150,6 +150,10 @@ class MultiAgentEnv(ABC):
     def _obstacle_fields(self) -> int:
         return 0
 
+    def _obstacle_rows(self) -> int:
+        """Rows of the per-env obstacle buffer (env_states records the step kernels read)."""
+        return max(self.n_obs, 1)
+
     def _make_cfg(self) -> _lib.EnvCfg:
         p = self._params
         c = _lib.EnvCfg()
@@ -293,7 +297,7 @@ class MultiAgentEnv(ABC):
         g = self.empty_graph((n_env,), dev) if out is None else out
         ob = obstacles_out
         if ob is None and self._obstacle_fields() > 0:
-            ob = torch.empty((n_env, max(self.n_obs, 1), self._obstacle_fields()), dtype=torch.float32, device=dev)
+            ob = torch.empty((n_env, self._obstacle_rows(), self._obstacle_fields()), dtype=torch.float32, device=dev)
         tkey = key if isinstance(key, torch.Tensor) else None
         seed = 0 if tkey is not None else int(key) & 0xFFFFFFFFFFFFFFFF
         torch.ops.dgppo.env_reset(self._cfg_handle, tkey, seed if seed < 2 ** 63 else seed - 2 ** 64,
@@ -311,7 +315,7 @@ class MultiAgentEnv(ABC):
         g = self.empty_graph((n_env,), dev) if out is None else out
         ob = obstacles_out
         if ob is None and self._obstacle_fields() > 0:
-            ob = torch.empty((n_env, max(self.n_obs, 1), self._obstacle_fields()), dtype=torch.float32, device=dev)
+            ob = torch.empty((n_env, self._obstacle_rows(), self._obstacle_fields()), dtype=torch.float32, device=dev)
         tkey = key if isinstance(key, torch.Tensor) else None
         seed = 0 if tkey is not None else int(key) & 0xFFFFFFFFFFFFFFFF
         torch.ops.dgppo.env_reset_states(self._cfg_handle, tkey, seed if seed < 2 ** 63 else seed - 2 ** 64,

@@ -51,7 +51,7 @@ class RolloutEngine:
         B, T, n, dev = self.B, self.T, env.num_agents, self.device
         self.buf = env.empty_graph((T + 1, B), dev)
         nf = env._obstacle_fields()
-        self.obstacles = (torch.empty((B, max(env.n_obs, 1), nf), dtype=torch.float32, device=dev) if nf else None)
+        self.obstacles = (torch.empty((B, env._obstacle_rows(), nf), dtype=torch.float32, device=dev) if nf else None)
         self.actions = torch.zeros((T, B, n, env.action_dim), dtype=torch.float32, device=dev)
         self.rewards = torch.empty((T, B), dtype=torch.float32, device=dev)
         self.costs = torch.empty((T, B, n, env.n_cost), dtype=torch.float32, device=dev)

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 7  /* 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 8  /* 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -30,6 +30,8 @@ extern "C" {
 #define DGPPO_ENGINE_BICYCLE 1 /* LidarBicycleTarget: dgppo/env/lidar_env/lidar_bicycle_target.py */
 #define DGPPO_ENGINE_MPE 2     /* MPE double integrator: dgppo/env/mpe/base.py */
 #define DGPPO_ENGINE_OMNI 3    /* LidarOmniTarget omni-wheel + FoV costs: dgppo/env/lidar_env/lidar_omni_target.py */
+#define DGPPO_ENGINE_VMAS_WHEEL 4     /* VMASWheel contact physics: dgppo/env/vmas/vmas_wheel.py */
+#define DGPPO_ENGINE_VMAS_TRANSPORT 5 /* VMASReverseTransport contact physics: dgppo/env/vmas/vmas_reverse_transport.py */
 /* goal wiring */
 #define DGPPO_GOAL_SPREAD 0 /* every agent sees every goal: lidar_spread.py:86-91, mpe_spread.py:64-69 */
 #define DGPPO_GOAL_TARGET 1 /* agent i sees goal i only: lidar_target.py:77-84, mpe_target.py:63-70 */
@@ -44,6 +46,15 @@ extern "C" {
  *   [cx, cy, width, height, theta, cos(theta), sin(theta), type, p0x, p0y, p1x, p1y, p2x, p2y, p3x, p3y]
  * = Rectangle(type, center, width, height, theta, points) of env/obstacle.py:30-56 plus a cached cos/sin. */
 #define DGPPO_OBST_FIELDS 16
+
+/* VMAS engines (n_agents 3): graph of 4 nodes (3 agents + pad) and 9 agent-agent edges, node_dim 13 (Wheel)
+ * / 20 (Transport), state_dim 4.  `states` rows 0..2 are the agents [x, y, vx, vy]; row 3 (the pad row,
+ * 0-wide in the reference) carries the moving body: Wheel [line_angle, line_angvel, 0, 0], Transport
+ * [box_x, box_y, box_vx, box_vy].  The `obstacles` buffer holds one record of DGPPO_VMAS_FIELDS floats per
+ * env (written by reset, read by step / rollout): Wheel [goal_angle, avoid_angle, 0 x 6], Transport
+ * [goal_x, goal_y, o0x, o0y, o1x, o1y, o2x, o2y].  All sizes / radii are fixed by the reference classes;
+ * dgppo_env_cfg_finalize fills the layout fields from `engine`. */
+#define DGPPO_VMAS_FIELDS 8
 
 /* Static description of one environment family + size (the reference's env PARAMS,
  * env/__init__.py:31-55 make_env, and the graph layout of utils/graph.py:212-247). */

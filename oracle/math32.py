@@ -128,7 +128,7 @@ def exp_nonpos(x):
 def log_pos(x):
     """log(x) for normal x > 0."""
     x = _f(x)
-    b = np.ascontiguousarray(x).view(U32)
+    b = np.ascontiguousarray(x).view(U32).reshape(x.shape)
     e = ((b >> U32(23)) & U32(0xFF)).astype(np.int64) - 126
     m = ((b & U32(0x807FFFFF)) | U32(0x3F000000)).view(F)
     with np.errstate(all="ignore"):

@@ -136,13 +136,15 @@ CASES = [("LidarSpread", 8, 3), ("MPETarget", 3, 0), ("MPESpread", 3, 3), ("Lida
 OMNI = [("LidarOmniTarget", 3, 2), ("LidarOmniTarget", 8, 3)]
 # BASELINE's dense-graph config: 72 candidate edges per agent (past the row-block kernels' 32)
 DENSE = [("LidarSpread", 32, 8)]
+# VMAS: 13 / 20-wide nodes (raw-row columns), agent-only graphs (3 candidate edges per agent)
+VMAS = [("VMASWheel", 3, 0), ("VMASReverseTransport", 3, 0)]
 
 
 def _nets_kw(env):
     return dict(edge_dim=env.edge_dim)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES + OMNI + DENSE)
+@pytest.mark.parametrize("eid,n,obs", CASES + OMNI + DENSE + VMAS)
 def test_actor_eval_seq_fwd_bwd(cuda, eid, n, obs):
     S, L = 3, 4
     env, gb, host = _graphs(cuda, eid, n, obs, S, L)
@@ -173,7 +175,7 @@ def test_actor_eval_seq_fwd_bwd(cuda, eid, n, obs):
         _grad_close(a, b, "actor grad " + path)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES[:2] + CASES[4:] + OMNI[:1])
+@pytest.mark.parametrize("eid,n,obs", CASES[:2] + CASES[4:] + OMNI[:1] + VMAS)
 def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
     S, L = 3, 5
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=4)
@@ -195,7 +197,7 @@ def test_vl_seq_fwd_bwd(cuda, eid, n, obs):
         _grad_close(a, b, "Vl grad " + path)
 
 
-@pytest.mark.parametrize("eid,n,obs", CASES[:3] + CASES[4:] + OMNI[:1] + DENSE)
+@pytest.mark.parametrize("eid,n,obs", CASES[:3] + CASES[4:] + OMNI[:1] + DENSE + VMAS)
 def test_vh_fwd_bwd(cuda, eid, n, obs):
     S, L = 2, 3
     env, gb, host = _graphs(cuda, eid, n, obs, S, L, seed=6)
@@ -220,7 +222,7 @@ def test_vh_fwd_bwd(cuda, eid, n, obs):
 
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("layers", [2, 1])
-@pytest.mark.parametrize("eid,n,obs", CASES + OMNI[:1] + DENSE)
+@pytest.mark.parametrize("eid,n,obs", CASES + OMNI[:1] + DENSE + VMAS)
 def test_actor_act_step(cuda, monkeypatch, eid, n, obs, layers, fused):
     """ActorNet.act (PPOPolicy.get_action / sample_action, policy.py:191-212) for one graph batch with
     non-zero carries, through the fused dgppo_policy_step kernel ("1") and the unfused layer chain
