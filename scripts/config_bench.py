@@ -33,14 +33,18 @@ CONFIGS = [
     ("MPEFormation n3 o3 x1024 (variant)", "MPEFormation", 3, 3, 1024),
     ("MPECorridor n3 x1024 (variant, 2 fixed obstacles)", "MPECorridor", 3, 2, 1024),
     ("MPEConnectSpread n3 x1024 (variant, 1 fixed obstacle)", "MPEConnectSpread", 3, 1, 1024),
+    # VMAS contact physics (no BASELINE config names them): the MPE-sized batch and a 4x larger one
+    ("VMASWheel n3 x1024", "VMASWheel", 3, 0, 1024),
+    ("VMASWheel n3 x4096", "VMASWheel", 3, 0, 4096),
+    ("VMASReverseTransport n3 x1024", "VMASReverseTransport", 3, 0, 1024),
+    ("VMASReverseTransport n3 x4096", "VMASReverseTransport", 3, 0, 4096),
 ]
 
 
 def step_us(env, B, dev, m=64):
     g = env.reset(key=1, n_env=B)
     a = torch.rand(B, env.num_agents, env.action_dim, device=dev) * 2 - 1
-    obst = getattr(g.env_states, "obstacle", None)  # Lidar: Rectangle records; MPE: obstacles live in the states
-    ob = obst.packed if obst is not None and hasattr(obst, "packed") else None
+    ob = env._obstacles_of(g)  # Lidar: rectangle records; VMAS: per-env records; MPE: None (in the states)
     outs = [env.empty_graph((B,), dev) for _ in range(2)]
     outs = [env._assemble(o.nodes, o.edges, o.states, o.receivers, o.senders, ob) for o in outs]
     rew = torch.empty(B, device=dev)
