@@ -52,3 +52,12 @@ $(OBJ)/policy_probe.o: $(CSRC)/policy.hip $(HDRS)
 probe: $(PROBE_OBJS)
 	@mkdir -p $(OUT)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OUT)/libdgppo_hip_probe.so $(PROBE_OBJS)
+
+# register-form policy step at 4 waves per SIMD instead of the default 3 (A/B: DGPPO_HIP_LIB=dgppo_fov_amd/lib/libdgppo_hip_w4.so)
+W4_OBJS := $(filter-out $(OBJ)/policy.o,$(OBJS)) $(OBJ)/policy_w4.o
+$(OBJ)/policy_w4.o: $(CSRC)/policy.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DPOLICY_REG_WAVES=4 -c $< -o $@
+w4: $(W4_OBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OUT)/libdgppo_hip_w4.so $(W4_OBJS)

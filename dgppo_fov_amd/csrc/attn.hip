@@ -23,6 +23,7 @@
 #include "lds_attr.h"
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/dgppo_hip.h"
 #include "lanes.h"
@@ -1221,6 +1222,166 @@ __global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
   }
 }
 
+// Register form of the row-block forward (the default; DGPPO_ATTN_FWD2=lds keeps the LDS-staged
+// kernel above): each lane's pair row x stays in registers (pre mode: relu(x_raw pre_W + pre_b) by VALU
+// FMAs against the LDS-resident pre_W), and the attention-weighted sums over the row's 32 candidates --
+// xbar_h per head, [ebar_h | sig_h] of all heads -- are transposed DPP reductions (lanes::treduce32)
+// whose totals each lane stores to its row of xcat.  LDS holds only the block's qt / beta rows and
+// pre_W (7.5 KB instead of 56 KB), so occupancy is set by registers.
+template <int DM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void attn_fwd2r_kernel(
+    dgppo_gnn_attn_args p) {
+  using lanes::f32x4;
+  constexpr int kRows = fwd2::kRows, kSR = fwd2::kSR, kQP = fwd2::kQP;
+  static_assert(DM == 8 || DM == 16 || DM == 32, "fwd2r instantiations");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* qts = lds;                 // [16][100]: qt_h (32-float stride per head) | beta_h at 96 + h
+  float* preW = qts + kRows * kQP;  // [8][32]
+  float* preb = preW + kD0 * 32;    // [32]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane >> 5, c = lane & 31;
+  const int n = p.n_agents, D = p.D, C = p.C, H = kH;
+  const int nrows = p.G * n;
+  const int row0 = blockIdx.x * kRows;
+  const bool agent = p.xa != nullptr;
+  const bool pre = DM == 32 && agent && p.pre_W != nullptr;
+  // ---- stage qt (zero padded per head), beta_h = q_h . bk_h, pre weights
+  for (int e = threadIdx.x; e < kRows * 96; e += 256) {
+    const int r = e / 96, k = e - r * 96, h = k >> 5, d = k & 31;
+    qts[r * kQP + k] = (row0 + r < nrows && d < D) ? p.qt[(int64_t)(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
+  }
+  {
+    const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const bool act = row0 + r < nrows;
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float acc = 0.0f;
+      if (act) acc = q_dot_bk(p, (int64_t)(row0 + r), h, j, 16);
+      acc = lanes::sum16(acc);
+      if (j == 0) qts[r * kQP + 96 + h] = acc;
+    }
+  }
+  if (pre) {
+    const int k = threadIdx.x >> 5, d = threadIdx.x & 31;
+    preW[threadIdx.x] = (k < p.D0 && d < D) ? p.pre_W[k * D + d] : 0.0f;
+    if (threadIdx.x < 32) preb[threadIdx.x] = threadIdx.x < D ? p.pre_b[threadIdx.x] : 0.0f;
+  }
+  __syncthreads();
+  const int TQ = (D + 3) >> 2, W = H * (D + 5);
+  constexpr int NEV = kH * 5;
+  // one sub-round at a time, gathers included: at 4 waves per SIMD the other waves hide the gather latency,
+  // and a prefetch of the next sub-round's 32-float rows would not fit the register budget
+#pragma unroll 1
+  for (int sr = 0; sr < kSR; ++sr) {
+    const int rl = 2 * wave + 8 * sr + slot;
+    const int row = row0 + rl;
+    const bool active = row < nrows;
+    float x[DM];
+    f32x4 ef;
+    int s = -1;
+    {
+      const int g = active ? row / n : 0;
+      const int i = active ? row - g * n : 0;
+      int e = 0;
+      if (active && c < C) {
+        e = p.cand[i * C + c];
+        s = p.sidx[(int64_t)row * C + c];
+      }
+      const bool okg = s >= 0;
+      const float* er = p.ef + (int64_t)g * p.ef_gstride + (int64_t)(okg ? e : 0) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ef[j] = okg ? er[j] : 0.0f;
+      if (!agent) {
+        load_row<DM>(p.x + (int64_t)g * p.x_gstride + (int64_t)(okg ? s : 0) * D, D, okg, x);
+      } else if (!okg || s < n) {
+        load_row<DM>(p.xa + (int64_t)g * p.xa_gstride + (int64_t)(okg ? s : 0) * D, D, okg, x);
+      } else {
+        const float* xr = p.x + (int64_t)g * p.x_gstride + (int64_t)s * p.D0;
+#pragma unroll
+        for (int kk = 0; kk < DM; ++kk) x[kk] = (kk < kD0 && kk < p.D0) ? xr[kk < kD0 ? kk : 0] : 0.0f;
+      }
+    }
+    const bool ok = s >= 0;
+    if (pre && ok && s >= n) {  // never-receiving sender: relu(x_raw pre_W + pre_b) in place
+      float xr[kD0];
+#pragma unroll
+      for (int k = 0; k < kD0; ++k) xr[k] = x[k];
+#pragma unroll
+      for (int q = 0; q < DM / 4; ++q) {
+        const f32x4 b = *(const f32x4*)(preb + 4 * q);
+        x[4 * q] = b[0];
+        x[4 * q + 1] = b[1];
+        x[4 * q + 2] = b[2];
+        x[4 * q + 3] = b[3];
+      }
+#pragma unroll
+      for (int k = 0; k < kD0; ++k)
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q) {
+          const f32x4 w = *(const f32x4*)(preW + k * 32 + 4 * q);
+          x[4 * q] += xr[k] * w[0];
+          x[4 * q + 1] += xr[k] * w[1];
+          x[4 * q + 2] += xr[k] * w[2];
+          x[4 * q + 3] += xr[k] * w[3];
+        }
+#pragma unroll
+      for (int d = 0; d < DM; ++d) x[d] = x[d] > 0.0f ? x[d] : 0.0f;
+    }
+    // logits, softmax over the row's candidates, attention weights out
+    const float* qt = qts + rl * kQP;
+    float aw[kH];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int q = 0; q < DM / 4; ++q)
+        if (q < TQ) {
+          const f32x4 qq = ((const f32x4*)(qt + 32 * h))[q];
+          acc += x[4 * q] * qq[0] + x[4 * q + 1] * qq[1] + x[4 * q + 2] * qq[2] + x[4 * q + 3] * qq[3];
+        }
+      const float lg = ok ? (acc + qt[96 + h]) * p.scale : -INFINITY;
+      const float mx = lanes::max32(lg);
+      const float ex = ok ? expf(lg - mx) : 0.0f;
+      const float sm = lanes::sum32(ex);
+      aw[h] = ok ? ex / sm : 0.0f;
+      if (active && c < C && p.attn) p.attn[((int64_t)row * H + h) * C + c] = aw[h];
+    }
+    float* o = p.xcat + (int64_t)row * W;
+    // xbar_h = sum_c a_h x_c
+#pragma unroll
+    for (int h = 0; h < kH; ++h) {
+      float v[DM];
+#pragma unroll
+      for (int d = 0; d < DM; ++d) v[d] = aw[h] * x[d];
+      int cnt;
+      const int base = lanes::treduce32(v, cnt);
+#pragma unroll
+      for (int j = 0; j < lanes::tr_final<DM>(); ++j) {
+        const int q = base + j;
+        if (active && j < cnt && q < D) o[h * D + q] = v[j];
+      }
+    }
+    // [ebar_h (4) | sig_h] of the three heads
+    {
+      float v[NEV];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[h * 5 + j] = aw[h] * ef[j];
+        v[h * 5 + 4] = aw[h];
+      }
+      int cnt;
+      const int base = lanes::treduce32(v, cnt);
+#pragma unroll
+      for (int j = 0; j < lanes::tr_final<NEV>(); ++j) {
+        const int q = base + j;
+        const int h = q / 5, k = q - h * 5;
+        if (active && j < cnt) o[k < 4 ? H * D + 4 * h + k : H * D + 4 * H + h] = v[j];
+      }
+    }
+  }
+}
+
 bool fwd2_ok(const dgppo_gnn_attn_args* p) {
   static const bool off = [] {
     const char* e = getenv("DGPPO_ATTN_FWD1");
@@ -1234,6 +1395,17 @@ void fwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const int64_t rows = (int64_t)p->G * p->n_agents;
   const unsigned grid = (unsigned)((rows + fwd2::kRows - 1) / fwd2::kRows);
   const bool no_pre = !(p->xa && p->pre_W);
+  static const bool reg = [] {
+    const char* e = getenv("DGPPO_ATTN_FWD2");
+    return !(e && strcmp(e, "lds") == 0);
+  }();
+  if (reg) {
+    const size_t bytes = ((size_t)fwd2::kRows * fwd2::kQP + kD0 * 32 + 32) * sizeof(float);
+    if (p->D <= 8 && no_pre) hipLaunchKernelGGL(attn_fwd2r_kernel<8>, dim3(grid), dim3(256), bytes, s, *p);
+    else if (p->D <= 16 && no_pre) hipLaunchKernelGGL(attn_fwd2r_kernel<16>, dim3(grid), dim3(256), bytes, s, *p);
+    else hipLaunchKernelGGL(attn_fwd2r_kernel<32>, dim3(grid), dim3(256), bytes, s, *p);
+    return;
+  }
   if (p->D <= 8 && no_pre)
     hipLaunchKernelGGL(attn_fwd2_kernel<8>, dim3(grid), dim3(256), fwd2::lds_floats<8>() * sizeof(float), s, *p);
   else if (p->D <= 16 && no_pre)  // e.g. LidarOmniTarget's 10-wide first layer

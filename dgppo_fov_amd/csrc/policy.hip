@@ -27,6 +27,8 @@
 
 #include "lds_attr.h"
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "../../include/dgppo_hip.h"
 #include "lanes.h"
@@ -47,6 +49,11 @@ constexpr int kRT = kRowsG / 16, kSR = kRowsG / 8;
 // instantiated narrow (<= 8, 4: the Lidar / MPE envs, 240 VGPRs = 2 waves per SIMD) and wide
 constexpr int kMaxD0 = 12, kMaxEX = 6, kCP = 32;
 constexpr int kNarrowD0 = 8;
+// register form: waves per SIMD the compiler must fit (VGPR budget 512 / kRegWaves)
+#ifndef POLICY_REG_WAVES
+#define POLICY_REG_WAVES 3
+#endif
+constexpr int kRegWaves = POLICY_REG_WAVES;
 // LDS pitches (floats); xs rows: x (0..31) | edge head (32..35) | extra edge columns (36..41)
 constexpr int kX0P = 13, kQTP = 100, kXCP = 132, kY0P = 36, kYP = 68, kXSP = 44;
 // work: per layer the (32 + 1) x 100 query-key matrix [QT_0 | QT_1 | QT_2 (32 cols each) | beta_0..2 | 0]
@@ -193,9 +200,11 @@ struct Lds {
 };
 
 constexpr int kAttPerWave = 2 * kCP * (kXSP + 4);
-constexpr size_t lds_floats() {
+// the register form's att region only hosts the pair tables (before the GNN) and the carries (after it)
+constexpr int kAttReg = kRowsG * kYP > 2 * kRowsG * kCP ? kRowsG * kYP : 2 * kRowsG * kCP;
+constexpr size_t lds_floats(bool reg) {
   return (size_t)kRowsG * (kX0P + kQTP + kXCP + kY0P + kYP) + kMaxD0 * 32 + 32 + 4 * kHid + 2 * kHid * 4 + 8 +
-         4 * kAttPerWave;
+         (reg ? kAttReg : 4 * kAttPerWave);
 }
 
 __device__ __forceinline__ Lds carve(float* base) {
@@ -434,6 +443,166 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
   __syncthreads();
 }
 
+// Register form of the same layer (the default): a lane's pair keeps its sender row x in registers
+// (layer 0: the raw row; layer 1: relu(x_raw Wu0 + bu0) by VALU FMAs against the LDS-resident Wu0, or
+// the agent's layer-0 output row from LDS), the logits are lane-local dots against the row's QT_h, and
+// the attention-weighted sums over the row's 32 candidates -- [xbar_h | ebar_h | sig_h | ebar_x_h] --
+// are one transposed DPP reduction per head (lanes::treduce32), whose totals each lane writes to the
+// row's xcat.  No per-pair LDS staging: the workgroup's LDS is its row activations only, so more
+// workgroups are resident per CU, and the weighted sums need no LDS round trips.
+template <int DX, bool layer0, int MD0, int MEX, int KQ, int KC, int KX, int KU>
+__device__ __forceinline__ void gt_layer_reg(const dgppo_policy_step_args& p, const dgppo_gt_layer& ly,
+                                             const PairG<MD0, MEX> (&pg)[kSR], const Lds& L, const float* qk,
+                                             const float* A, int lda, float* out, int ldo, int nmag, int pk) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = p.n_agents, D = ly.D, F = ly.F, H = kHeads;
+  const int EX = MEX > 0 ? p.ED - 4 : 0;
+  // [QT_h | beta_h] = A QK + qk_bias (kRowsG x 100)
+  {
+    Frag<KQ, 2> fq;
+    float bq[2];
+    frag_load(fq, qk, kQKCols, D);
+    bias_load(bq, qk + 32 * kQKCols, kQKCols);
+    f32x4 acc[2][kRT];
+    acc_zero(acc);
+    frag_mma(acc, A, lda, D, fq);
+    acc_store(acc, L.qt, kQTP, kQKCols, bq, 1.0f, false);
+  }
+  __syncthreads();
+  PROBE(pk);
+  const int slot = lane >> 5, c = lane & 31;
+  const float scale = rsqrtf((float)F);
+  // x width DX: layer 0 the raw row (MD0), layer 1 the 32-wide hidden row.  Per head the DX weighted x
+  // sums are one transposed reduction; the edge / sig sums of all heads ([ebar_h (4) | sig_h | ebar_x_h
+  // (EX)] x 3) a second one, so at most DX + DX values are live
+  constexpr int NE = 5 + MEX, NEV = kHeads * NE;
+#pragma unroll
+  for (int sr = 0; sr < kSR; ++sr) {  // unrolled: pg[sr] read directly, pg[0] dies after the first sub-round
+    const PairG<MD0, MEX>& cur = pg[sr];
+    const int r = 2 * wave + 8 * sr + slot;
+    const bool ok = cur.s >= 0;
+    float x[DX];
+    if (layer0) {
+#pragma unroll
+      for (int d = 0; d < DX; ++d) x[d] = d < MD0 ? cur.xr[d] : 0.0f;
+    } else if (ok && cur.s < n) {  // agent sender: the layer input row of the same graph
+      const f32x4* src = (const f32x4*)(A + (div_n(r, nmag) * n + cur.s) * lda);
+#pragma unroll
+      for (int q = 0; q < DX / 4; ++q) {
+        const f32x4 v = src[q];
+        x[4 * q] = v[0];
+        x[4 * q + 1] = v[1];
+        x[4 * q + 2] = v[2];
+        x[4 * q + 3] = v[3];
+      }
+    } else {  // never-receiving sender: relu(x_raw Wu0 + bu0) (masked pairs too; their weights are 0)
+#pragma unroll
+      for (int q = 0; q < DX / 4; ++q) {
+        const f32x4 b = *(const f32x4*)(L.preb + 4 * q);
+        x[4 * q] = b[0];
+        x[4 * q + 1] = b[1];
+        x[4 * q + 2] = b[2];
+        x[4 * q + 3] = b[3];
+      }
+#pragma unroll
+      for (int k = 0; k < MD0; ++k) {
+        const float xk = cur.xr[k];
+#pragma unroll
+        for (int q = 0; q < DX / 4; ++q) {
+          const f32x4 w = *(const f32x4*)(L.preW + k * 32 + 4 * q);
+          x[4 * q] += xk * w[0];
+          x[4 * q + 1] += xk * w[1];
+          x[4 * q + 2] += xk * w[2];
+          x[4 * q + 3] += xk * w[3];
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < DX; ++d) x[d] = x[d] > 0.0f ? x[d] : 0.0f;
+    }
+    // logits (QT_h . x + beta_h) / sqrt(F) and the softmax over the row's 32 candidates
+    const float* qt = L.qt + r * kQTP;
+    float* o = L.xc + r * kXCP;
+    float aw[kHeads];
+#pragma unroll
+    for (int h = 0; h < kHeads; ++h) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int q = 0; q < DX / 4; ++q) {
+        const f32x4 qv = *(const f32x4*)(qt + 32 * h + 4 * q);
+        acc += x[4 * q] * qv[0] + x[4 * q + 1] * qv[1] + x[4 * q + 2] * qv[2] + x[4 * q + 3] * qv[3];
+      }
+      const float lg = ok ? (acc + qt[96 + h]) * scale : -INFINITY;
+      const float mx = gmax32(lg);
+      const float ex = ok ? expf(lg - mx) : 0.0f;
+      const float sm = gsum32(ex);
+      aw[h] = ok ? ex / sm : 0.0f;
+    }
+    // xbar_h = sum_c a_h x_c
+#pragma unroll
+    for (int h = 0; h < kHeads; ++h) {
+      float v[DX];
+#pragma unroll
+      for (int d = 0; d < DX; ++d) v[d] = aw[h] * x[d];
+      int cnt;
+      const int base = lanes::treduce32(v, cnt);
+#pragma unroll
+      for (int j = 0; j < lanes::tr_final<DX>(); ++j) {
+        const int q = base + j;
+        if (j < cnt && q < D) o[h * D + q] = v[j];
+      }
+    }
+    // [ebar_h | sig_h | ebar_x_h] of the three heads
+    {
+      float v[NEV];
+#pragma unroll
+      for (int h = 0; h < kHeads; ++h) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[h * NE + j] = aw[h] * cur.ef[j];
+        v[h * NE + 4] = aw[h];
+#pragma unroll
+        for (int j = 0; j < MEX; ++j) v[h * NE + 5 + j] = aw[h] * cur.ex[j];
+      }
+      int cnt;
+      const int base = lanes::treduce32(v, cnt);
+#pragma unroll
+      for (int j = 0; j < lanes::tr_final<NEV>(); ++j) {
+        const int q = base + j;
+        const int h = q / NE, k = q - h * NE;
+        int col = -1;
+        if (j < cnt) {
+          if (k < 4) col = H * D + 4 * h + k;
+          else if (k == 4) col = H * D + 4 * H + h;
+          else if (k - 5 < EX) col = H * (D + 5) + h * EX + (k - 5);
+        }
+        if (col >= 0) o[col] = v[j];
+      }
+    }
+  }
+  // message + update operands (after the barrier: loads hoisted into the attention would raise its
+  // register pressure), then out = relu(xcat Wcat / H + A Wu + bu)
+  __syncthreads();
+  PROBE(pk + 1);
+  Frag<KC, 1> fc;
+  Frag<KX, 1> fx;
+  Frag<KU, 1> fu;
+  float bu[1];
+  frag_load(fc, ly.Wcat, ly.F, kHeads * (ly.D + 5));
+  frag_load(fx, ly.Wex, ly.F, EX > 0 ? kHeads * EX : 0);
+  frag_load(fu, ly.Wu, ly.F, ly.D);
+  bias_load(bu, ly.bu, ly.F);
+  {
+    f32x4 acc[1][kRT];
+    acc_zero(acc);
+    frag_mma(acc, L.xc, kXCP, H * (D + 5), fc);
+    if (EX > 0) frag_mma(acc, L.xc + H * (D + 5), kXCP, H * EX, fx);
+#pragma unroll
+    for (int rt = 0; rt < kRT; ++rt) acc[0][rt] *= 1.0f / H;
+    frag_mma(acc, A, lda, D, fu);
+    acc_store(acc, out, ldo, F, bu, 1.0f, true);
+  }
+  __syncthreads();
+}
+
 // in-place LayerNorm (eps 1e-6) + ReLU over 64 columns of the kRowsG rows: 8 lanes per row
 __device__ __forceinline__ void ln_relu64(float* Y, const float* scale, const float* bias) {
   if (threadIdx.x >= kRowsG * 8) return;  // whole waves
@@ -463,8 +632,8 @@ __device__ __forceinline__ void ln_relu64(float* Y, const float* scale, const fl
   }
 }
 
-template <int MD0, int MEX>
-__global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step_args p) {
+template <int MD0, int MEX, bool REG>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG && MD0 <= kNarrowD0 ? kRegWaves : 1, 8))) void policy_step_kernel(dgppo_policy_step_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Lds L = carve(lds);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -555,8 +724,19 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
   __syncthreads();  // the pair tables alias the attention scratch
   PROBE(1);
   // ---- GNN
+  if (REG) {
+    constexpr int KX = MEX > 0 ? (kHeads * MEX + 3) / 4 : 1;
+    gt_layer_reg<MD0, true, MD0, MEX, (MD0 + 3) / 4, (kHeads * (MD0 + 5) + 3) / 4, KX, (MD0 + 3) / 4>(
+        p, p.layer[0], pg, L, p.work, L.x0, kX0P, two ? L.y0 : L.yb, two ? kY0P : kYP, nmag, 2);
+    PROBE(4);
+    if (two) {
+      gt_layer_reg<32, false, MD0, MEX, 8, 28, KX, 8>(p, p.layer[1], pg, L, p.work + kQKStride, L.y0, kY0P, L.yb, kYP,
+                                                     nmag, 5);
+      PROBE(7);
+    }
+  }
 #pragma unroll 1
-  for (int l = 0; l < p.n_layers; ++l) {
+  for (int l = 0; l < (REG ? 0 : p.n_layers); ++l) {
     const bool last = l == p.n_layers - 1;
     const dgppo_gt_layer& ly = l == 0 ? p.layer[0] : p.layer[1];
     // one operand shape for both layers (layer 0's extra k-steps read as zeros): one copy of the code
@@ -572,15 +752,19 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
     L.hb[(e / kHid) * kYP + e % kHid] = hreg[u];
   }
   // head / GRU / ScaleHid operands: loaded after the GNN (holding them through the attention would
-  // spill), all in flight at once
+  // spill).  LDS form: all in flight at once; register form: each loaded one phase ahead of its GEMM
+  // (fi during the second head layer, fh after gi, fs during the gate math) so that at most ~100
+  // registers of fragments are live and the kernel fits 3-4 waves per SIMD
   Frag<16, 1> fh0, fh1, fs;
   Frag<16, 3> fi, fh;
   float bh0[1], bh1[1], bs[1], bi[3], bhn[1];
   frag_load(fh0, p.head_W0, kHid, kHid);
   frag_load(fh1, p.head_W1, kHid, kHid);
-  frag_load(fi, p.gru_Wi, 3 * kHid, kHid);
-  frag_load(fh, p.gru_Wh, 3 * kHid, kHid);
-  frag_load(fs, p.Ws, kHid, kHid);
+  if (!REG) {
+    frag_load(fi, p.gru_Wi, 3 * kHid, kHid);
+    frag_load(fh, p.gru_Wh, 3 * kHid, kHid);
+    frag_load(fs, p.Ws, kHid, kHid);
+  }
   bias_load(bh0, p.head_b0, kHid);
   bias_load(bh1, p.head_b1, kHid);
   bias_load(bi, p.gru_bi, 3 * kHid);
@@ -597,6 +781,7 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
     __syncthreads();
     ln_relu64(L.yb, L.lnp, L.lnp + kHid);
     __syncthreads();
+    if (REG) frag_load(fi, p.gru_Wi, 3 * kHid, kHid);
     acc_zero(acc);
     frag_mma(acc, L.yb, kYP, kHid, fh1);
     __syncthreads();
@@ -612,7 +797,9 @@ __global__ __launch_bounds__(kThreads) void policy_step_kernel(dgppo_policy_step
     acc_zero(gi);
     acc_zero(gh);
     frag_mma(gi, L.yb, kYP, kHid, fi);
+    if (REG) frag_load(fh, p.gru_Wh, 3 * kHid, kHid);
     frag_mma(gh, L.hb, kYP, kHid, fh);
+    if (REG) frag_load(fs, p.Ws, kHid, kHid);
     const int col = wave * 16 + i16;
     float hn[kRT][4];
 #pragma unroll
@@ -718,7 +905,7 @@ __global__ __launch_bounds__(256) void policy_prepare_kernel(dgppo_policy_step_a
   p.work[(int64_t)l * kQKStride + idx] = v;
 }
 
-size_t lds_bytes() { return lds_floats() * sizeof(float); }
+size_t lds_bytes(bool reg) { return lds_floats(reg) * sizeof(float); }
 
 }  // namespace
 }  // namespace dgppo
@@ -756,14 +943,22 @@ extern "C" int dgppo_policy_step(const dgppo_policy_step_args* p, void* stream) 
   if (ngroups > INT32_MAX) return DGPPO_EINVAL;
   const int64_t grid = ngroups;
   const bool wide = p->D0 > dgppo::kNarrowD0 || p->ED > 4;
-  const void* fn = wide ? (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX>
-                        : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0>;
-  dgppo::allow_lds(fn);
-  if (wide)
-    hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX>), dim3((unsigned)grid),
-                       dim3(dgppo::kThreads), dgppo::lds_bytes(), (hipStream_t)stream, *p);
-  else
-    hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0>), dim3((unsigned)grid), dim3(dgppo::kThreads),
-                       dgppo::lds_bytes(), (hipStream_t)stream, *p);
+  // DGPPO_POLICY_ATTN=lds selects the LDS-staged attention (A/B); default: the register form
+  static const bool reg = [] {
+    const char* e = getenv("DGPPO_POLICY_ATTN");
+    return !(e && strcmp(e, "lds") == 0);
+  }();
+  const void* fn = wide ? (reg ? (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, true>
+                               : (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, false>)
+                        : (reg ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>
+                               : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>);
+  const size_t bytes = dgppo::lds_bytes(reg);
+  if (bytes > 64 * 1024) dgppo::allow_lds(fn);
+  const dim3 g((unsigned)grid), b(dgppo::kThreads);
+  const hipStream_t s = (hipStream_t)stream;
+  if (wide && reg) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, true>), g, b, bytes, s, *p);
+  else if (wide) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, false>), g, b, bytes, s, *p);
+  else if (reg) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>), g, b, bytes, s, *p);
+  else hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>), g, b, bytes, s, *p);
   return (int)hipGetLastError();
 }
