@@ -1718,6 +1718,268 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
   }
 }
 
+// Register form of the row-block backward (the default; DGPPO_ATTN_BWD2=lds keeps the kernel above): a
+// lane's pair row x stays in registers (pre mode: relu(x_raw pre_W + pre_b) by VALU FMAs against the
+// LDS-resident pre_W), da / dl / dbeta and the sender gradient are lane-local math against the row's
+// LDS-staged dxbar / qt, dqt_h = sum_c dl_h x_c is one transposed DPP reduction per head, and the pre
+// layer's gradient [x_raw | 1]^T dz goes through the MFMA in four 16-pair chunks staged in a 2.8 KB
+// per-wave area (instead of a 64-pair image).  The agent-sender image and its fixed-order sums are the
+// same as the LDS form.
+namespace bwd2r {
+constexpr int kPS = 44;  // chunk staging row: dz (0..31) | x_raw (32..39) | 1 (40)
+template <int DM>
+size_t lds_floats(int n, int D) {
+  using L = bwd2::Lay<DM>;
+  return (size_t)bwd2::kRows * (L::QP + L::GP) + kD0 * 32 + 32 + 4 * 16 * kPS + (size_t)bwd2::kRows * n * D;
+}
+}  // namespace bwd2r
+
+template <int DM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void attn_bwd2r_kernel(
+    dgppo_gnn_attn_args p, int64_t nblk) {
+  using lanes::f32x4;
+  using lanes::wave_sync;
+  using LY = bwd2::Lay<DM>;
+  constexpr int kRows = bwd2::kRows, kSR = bwd2::kSR, HS = LY::HS, kQP = LY::QP, kGP = LY::GP;
+  constexpr int kPS = bwd2r::kPS;
+  static_assert(DM == 8 || DM == 16 || DM == 32, "bwd2r instantiations");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* qts = lds;                 // [16][QP]: qt_h (HS stride per head)
+  float* gs = qts + kRows * kQP;    // [16][GP]: dxbar_h (HS stride) | debar (3HS..+12) | dsig (3HS+12..+3)
+  float* preW = gs + kRows * kGP;   // [8][32]
+  float* preb = preW + kD0 * 32;    // [32]
+  float* stg = preb + 32;           // per wave [16][kPS]: pre-gradient chunk staging
+  float* cbi = stg + 4 * 16 * kPS;  // [rows][n][D] agent-sender contributions
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int slot = lane >> 5, c = lane & 31;
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = kH;
+  const int gpb = kRows / n;
+  const bool agent = p.xa != nullptr;
+  const bool pre = DM == 32 && agent && p.pre_W != nullptr;
+  const bool want_dxa = agent && p.dxa != nullptr;
+  const bool want_pre = pre && p.dpre_part != nullptr;
+  if (pre) {
+    const int k = threadIdx.x >> 5, d = threadIdx.x & 31;
+    preW[threadIdx.x] = (k < p.D0 && d < D) ? p.pre_W[k * D + d] : 0.0f;
+    if (threadIdx.x < 32) preb[threadIdx.x] = threadIdx.x < D ? p.pre_b[threadIdx.x] : 0.0f;
+  }
+  __syncthreads();
+  f32x4 gacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // [x_raw | 1]^T dz
+  float* ws = stg + wave * 16 * kPS;
+  const int TQ = (D + 3) >> 2, W = H * (D + 5);
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t g0 = blk * gpb;
+    const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
+    const int nrec = ng * n;
+    const int64_t row0 = g0 * n;
+    // ---- block staging: qt rows, dxcat rows (split at aligned offsets), agent image cleared
+    for (int e = threadIdx.x; e < kRows * 3 * HS; e += 256) {
+      const int r = e / (3 * HS), k = e - r * (3 * HS), h = k / HS, d = k - h * HS;
+      qts[r * kQP + k] = (r < nrec && d < D) ? p.qt[(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
+    }
+    for (int e = threadIdx.x; e < kRows * kGP; e += 256) {
+      const int r = e / kGP, k = e - r * kGP;
+      int src = -1;
+      if (k < 3 * HS) src = (k % HS) < D ? (k / HS) * D + (k % HS) : -1;
+      else if (k < 3 * HS + 12) src = H * D + (k - 3 * HS);
+      else if (k < 3 * HS + 15) src = H * D + 4 * H + (k - 3 * HS - 12);
+      gs[e] = (r < nrec && src >= 0) ? p.dxcat[(row0 + r) * W + src] : 0.0f;
+    }
+    if (want_dxa)
+      for (int e = threadIdx.x; e < kRows * n * D; e += 256) cbi[e] = 0.0f;
+    __syncthreads();
+#pragma unroll 1
+    for (int sr = 0; sr < kSR; ++sr) {
+      const int rl = 2 * wave + 8 * sr + slot;
+      const bool active = rl < nrec;
+      const int64_t row = row0 + rl;
+      // ---- the pair: sender, edge, attention, sender row
+      const int gl = active ? rl / n : 0;
+      const int i = active ? rl - gl * n : 0;
+      const int64_t g = g0 + gl;
+      int s = -1, e = 0;
+      if (active && c < C) {
+        e = p.cand[i * C + c];
+        s = p.sidx[row * C + c];
+      }
+      const bool ok = s >= 0;
+      float av[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) av[h] = ok ? p.attn[(row * H + h) * C + c] : 0.0f;
+      f32x4 ef;
+      const float* er = p.ef + g * p.ef_gstride + (int64_t)(ok ? e : 0) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ef[j] = ok ? er[j] : 0.0f;
+      float x[DM];
+      if (!agent) {
+        load_row<DM>(p.x + g * p.x_gstride + (int64_t)(ok ? s : 0) * D, D, ok, x);
+      } else if (!ok || s < n) {
+        load_row<DM>(p.xa + g * p.xa_gstride + (int64_t)(ok ? s : 0) * D, D, ok, x);
+      } else {
+        const float* xr = p.x + g * p.x_gstride + (int64_t)s * p.D0;
+#pragma unroll
+        for (int k = 0; k < DM; ++k) x[k] = (k < kD0 && k < p.D0) ? xr[k < kD0 ? k : 0] : 0.0f;
+      }
+      const bool viapre = pre && ok && s >= n;
+      float xraw[kD0];
+#pragma unroll
+      for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? x[k < DM ? k : 0] : 0.0f;
+      if (viapre) {  // relu(x_raw pre_W + pre_b)
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q) {
+          const f32x4 b = *(const f32x4*)(preb + 4 * q);
+          x[4 * q] = b[0];
+          x[4 * q + 1] = b[1];
+          x[4 * q + 2] = b[2];
+          x[4 * q + 3] = b[3];
+        }
+#pragma unroll
+        for (int k = 0; k < kD0; ++k)
+#pragma unroll
+          for (int q = 0; q < DM / 4; ++q) {
+            const f32x4 w = *(const f32x4*)(preW + k * 32 + 4 * q);
+            x[4 * q] += xraw[k] * w[0];
+            x[4 * q + 1] += xraw[k] * w[1];
+            x[4 * q + 2] += xraw[k] * w[2];
+            x[4 * q + 3] += xraw[k] * w[3];
+          }
+#pragma unroll
+        for (int d = 0; d < DM; ++d) x[d] = x[d] > 0.0f ? x[d] : 0.0f;
+      }
+      // ---- softmax backward
+      const float* gv = gs + rl * kGP;
+      float dl[kH], dbeta[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float da = 0.0f;
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q)
+          if (q < TQ) {
+            const f32x4 gq = ((const f32x4*)(gv + HS * h))[q];
+            da += x[4 * q] * gq[0] + x[4 * q + 1] * gq[1] + x[4 * q + 2] * gq[2] + x[4 * q + 3] * gq[3];
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) da += gv[3 * HS + 4 * h + j] * ef[j];
+        da += gv[3 * HS + 12 + h];
+        if (p.da_add && ok) da += p.da_add[(row * H + h) * C + c];
+        da = ok ? da : 0.0f;
+        const float dot = lanes::sum32(av[h] * da);
+        dl[h] = ok ? av[h] * (da - dot) * p.scale : 0.0f;
+        dbeta[h] = lanes::sum32(dl[h]);
+      }
+      if (active) {
+        if (c < kH) p.dbeta[row * dbeta_ld(p) + c] = c == 0 ? dbeta[0] : c == 1 ? dbeta[1] : dbeta[2];
+        for (int kk = c; kk < H * F; kk += 32) {
+          const int h = kk / F;
+          if (p.dq) p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+        }
+      }
+      // ---- dqt_h = sum_c dl_h x_c (transposed reduction per head)
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float v[DM];
+#pragma unroll
+        for (int d = 0; d < DM; ++d) v[d] = dl[h] * x[d];
+        int cnt;
+        const int base = lanes::treduce32(v, cnt);
+        float* o = p.dqt + row * dqt_ld(p) + h * D;
+#pragma unroll
+        for (int j = 0; j < lanes::tr_final<DM>(); ++j) {
+          const int q = base + j;
+          if (active && j < cnt && q < D) o[q] = v[j];
+        }
+      }
+      // ---- sender gradient of this pair: sum_h a_h dxbar_h + dl_h qt_h
+      f32x4 cq[DM / 4];
+      const float* qt = qts + rl * kQP;
+#pragma unroll
+      for (int q = 0; q < DM / 4; ++q) {
+        cq[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (q < TQ)
+#pragma unroll
+          for (int h = 0; h < kH; ++h)
+            cq[q] += av[h] * ((const f32x4*)(gv + HS * h))[q] + dl[h] * ((const f32x4*)(qt + HS * h))[q];
+      }
+      if (want_dxa && ok && s < n) {
+        float* dst = cbi + (rl * n + s) * D;
+        if ((D & 3) == 0) {
+#pragma unroll
+          for (int q = 0; q < DM / 4; ++q)
+            if (q < TQ) ((f32x4*)dst)[q] = cq[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < DM / 4; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (4 * q + j < D) dst[4 * q + j] = cq[q][j];
+        }
+      }
+      // ---- pre layer gradient: gacc[ct] += [x_raw | 1]^T dz over the wave's pairs, 16-pair chunks (one DPP
+      // row of lanes each) staged in the wave's area
+      if (want_pre) {
+#pragma unroll 1
+        for (int ch = 0; ch < 4; ++ch) {
+          if (kq == ch) {
+            float* sp = ws + i16 * kPS;
+#pragma unroll
+            for (int q = 0; q < DM / 4; ++q) {
+              f32x4 dz;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) dz[j] = (viapre && x[4 * q + j] > 0.0f) ? cq[q][j] : 0.0f;
+              ((f32x4*)sp)[q] = dz;
+            }
+            ((f32x4*)(sp + 32))[0] = f32x4{xraw[0], xraw[1], xraw[2], xraw[3]};
+            ((f32x4*)(sp + 32))[1] = f32x4{xraw[4], xraw[5], xraw[6], xraw[7]};
+            sp[40] = viapre ? 1.0f : 0.0f;
+          }
+          wave_sync();
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const int pp = 4 * ks + kq;
+            const float a = i16 <= kD0 ? ws[pp * kPS + 32 + i16] : 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              gacc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ws[pp * kPS + 16 * ct + i16], gacc[ct], 0, 0, 0);
+          }
+          wave_sync();
+        }
+      }
+    }
+    __syncthreads();
+    if (want_dxa) {  // agent j of graph gl: sum over its receivers i in order
+      for (int e = threadIdx.x; e < nrec * D; e += 256) {
+        const int gl = e / (n * D), jd = e - gl * (n * D), j = jd / D, d = jd - j * D;
+        float acc = 0.0f;
+        for (int i = 0; i < n; ++i) acc += cbi[((gl * n + i) * n + j) * D + d];
+        p.dxa[(g0 + gl) * p.dxa_gstride + j * D + d] += acc;
+      }
+      __syncthreads();
+    }
+  }
+  if (want_pre) {  // fixed-order combine of the 4 waves' accumulators -> this workgroup's partial row
+    float* red = stg;  // [16][33] (the staging area is free now)
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float* dst = red + (4 * kq + i) * 33 + 16 * ct + i16;
+            *dst = (w == 0 ? 0.0f : *dst) + gacc[ct][i];
+          }
+      }
+      __syncthreads();
+    }
+    const int PK = p.D0 * D + D;
+    for (int o = threadIdx.x; o < PK; o += 256) {
+      const int m = o < p.D0 * D ? o / D : kD0;
+      const int d = o < p.D0 * D ? o - m * D : o - p.D0 * D;
+      p.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * 33 + d];
+    }
+  }
+}
+
 bool bwd2_ok(const dgppo_gnn_attn_args* p) {
   static const bool off = [] {
     const char* e = getenv("DGPPO_ATTN_BWD1");
@@ -1730,11 +1992,24 @@ bool bwd2_ok(const dgppo_gnn_attn_args* p) {
   return bwd2::lds_floats<32>(p->n_agents, p->D) * sizeof(float) <= 160 * 1024;
 }
 
-int64_t bwd2_grid(const dgppo_gnn_attn_args* p, int64_t* nblk) {
-  static const int64_t cap = [] {
-    const char* e = getenv("DGPPO_BWD2_BLOCKS");  // persistent-grid cap (A/B knob)
-    return e ? (int64_t)atoi(e) : (int64_t)bwd2::kMaxBlocks;
+// the register form (default) or the LDS-staged kernel (DGPPO_ATTN_BWD2=lds)
+static bool bwd2_reg() {
+  static const bool reg = [] {
+    const char* e = getenv("DGPPO_ATTN_BWD2");
+    return !(e && strcmp(e, "lds") == 0);
   }();
+  return reg;
+}
+
+int64_t bwd2_grid(const dgppo_gnn_attn_args* p, int64_t* nblk) {
+  // persistent-grid cap (A/B knob DGPPO_BWD2_BLOCKS): the resident workgroups of the chosen kernel, 3 per CU
+  // for the register form (42 KB of LDS, 3 waves per SIMD), 4 per CU for the LDS form
+  static const int64_t knob = [] {
+    const char* e = getenv("DGPPO_BWD2_BLOCKS");
+    return e ? (int64_t)atoi(e) : (int64_t)0;
+  }();
+  const bool wide = p->D > 16 || (p->xa && p->pre_W);  // the DM = 32 instantiation
+  const int64_t cap = knob > 0 ? knob : (bwd2_reg() ? (wide ? 768 : 1536) : (int64_t)bwd2::kMaxBlocks);
   const int gpb = bwd2::kRows / p->n_agents;
   *nblk = (p->G + gpb - 1) / gpb;
   return *nblk < cap ? *nblk : cap;
@@ -1745,6 +2020,19 @@ void bwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const unsigned grid = (unsigned)bwd2_grid(p, &nblk);
   const bool no_pre = !(p->xa && p->pre_W);
   const int v = p->D <= 8 && no_pre ? 0 : (p->D <= 16 && no_pre ? 1 : 2);  // DM 8 / 16 / 32
+  if (bwd2_reg()) {
+    const size_t bytes = (v == 0   ? bwd2r::lds_floats<8>(p->n_agents, p->D)
+                          : v == 1 ? bwd2r::lds_floats<16>(p->n_agents, p->D)
+                                   : bwd2r::lds_floats<32>(p->n_agents, p->D)) *
+                         sizeof(float);
+    const void* fn = v == 0 ? (const void*)attn_bwd2r_kernel<8>
+                            : (v == 1 ? (const void*)attn_bwd2r_kernel<16> : (const void*)attn_bwd2r_kernel<32>);
+    if (bytes > 64 * 1024) allow_lds(fn);
+    if (v == 0) hipLaunchKernelGGL(attn_bwd2r_kernel<8>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+    else if (v == 1) hipLaunchKernelGGL(attn_bwd2r_kernel<16>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+    else hipLaunchKernelGGL(attn_bwd2r_kernel<32>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+    return;
+  }
   const size_t bytes = (v == 0   ? bwd2::lds_floats<8>(p->n_agents, p->D)
                         : v == 1 ? bwd2::lds_floats<16>(p->n_agents, p->D)
                                  : bwd2::lds_floats<32>(p->n_agents, p->D)) *
