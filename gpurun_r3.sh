@@ -1,5 +1,12 @@
-timeout -k 10 400 python -u -m pytest tests/test_rollout_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r3_tests.log; [ $rc -eq 0 ] || exit $rc
-bash gpurun_mpeprof.sh > gpurun_out/mpeprof.txt 2>&1 || exit 1
-f=$(find gpurun_out/mpe_prof -name "*kernel_stats.csv" | head -1); cut -d, -f1-4 "$f" | head -4 | cut -c1-60,130-200
-timeout -k 10 200 python -u scripts/config_bench.py --no-ppo --only "MPE" || exit 1
+#!/bin/bash
+# round-3 re-entry check: the trajectory test under both attention-backward forms, the default bench line, then
+# this round's profiles
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+mkdir -p gpurun_out
+T=tests/test_update_dynamics_gpu.py::test_trajectory_matches_oracle_loop
+timeout -k 10 300 python -u -m pytest "$T" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_traj_reg.log 2>&1; echo "reg rc=$?"
+DGPPO_ATTN_BWD2=lds timeout -k 10 300 python -u -m pytest "$T" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_traj_lds.log 2>&1; echo "lds rc=$?"
+grep -h 'AssertionError' gpurun_out/r3_traj_*.log
+timeout -k 10 400 python3 bench.py > gpurun_out/r3_bench.json 2> gpurun_out/r3_bench.err || { tail -20 gpurun_out/r3_bench.err; exit 1; }
+cat gpurun_out/r3_bench.json | cut -c1-600
+bash scripts/round_profiles.sh > gpurun_out/r3_round_profiles.txt 2>&1; rc=$?; tail -40 gpurun_out/r3_round_profiles.txt; exit $rc

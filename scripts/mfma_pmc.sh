@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/mfma
 mkdir -p $OUT
-export TMPDIR=/tmp ENV_ID=LidarSpread N_AGENTS=8 N_OBS=3 N_ENV=4096 T=128 BATCH=16384 ITERS=2
+export TMPDIR=/tmp ENV_ID=LidarSpread N_AGENTS=8 N_OBS=3 N_ENV=4096 T=128 BATCH=16384 ITERS=3
 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
   -d $OUT/pmc -o run --output-format csv -- python3 scripts/update_smoke.py > $OUT/pmc.log 2>&1
 rc=$?; echo "pmc rc=$rc"; [ $rc -ne 0 ] && exit $rc
