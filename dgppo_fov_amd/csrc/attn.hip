@@ -2524,6 +2524,286 @@ __global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args
   }
 }
 
+// Backward, graph form, agent mode at D = 32 (the dense graphs' second layer, e.g. LidarSpread n = 32: 72
+// candidates per agent, 289 never-receiving senders per graph).  A persistent 512-thread workgroup takes one
+// graph at a time: the graph's raw rows, agent rows, qt and dxbar rows are staged once in LDS and every
+// never-receiver's relu(x_raw pre_W + pre_b) is computed ONCE per node (the forward's order of operations, so
+// the ReLU gates agree bit for bit), instead of once per (receiver, candidate) pair.  A wave takes a receiver
+// row at a time, candidates c = lane and lane + 64: the pair rows x come from LDS into registers, da / dl /
+// dbeta are lane-local math with 64-lane DPP sums, dqt_h = sum_c dl_h x_c is a transposed DPP reduction per
+// head, and the sender gradient contrib = sum_h a_h dxbar_h + dl_h qt_h goes (agent senders) into the wave's
+// private LDS image of the graph's agent rows -- a receiver's candidates have distinct senders, so the lanes
+// never collide -- or (never-receivers) through the ReLU gate into the pre layer's [x_raw | 1]^T dz, MFMA
+// 16x16x4 over 16-pair chunks.  The wave images are summed in fixed wave order per graph and the MFMA
+// accumulators in fixed wave order per workgroup: bitwise deterministic, no atomics.
+namespace gbwd32 {
+constexpr int kWaves = 8, kXP = 36, kQP = 96, kGP = 112, kPS = 44;
+inline size_t lds_floats(int N, int n) {
+  return (size_t)N * kXP + (size_t)N * kD0 + kD0 * 32 + 32 + (size_t)n * (kQP + kGP) +
+         (size_t)kWaves * ((size_t)n * 32 + 16 * kPS);
+}
+}  // namespace gbwd32
+
+__device__ __forceinline__ float sum64(float v) {
+  v = lanes::sum16(v);
+  return (lanes::rlane(v, 0) + lanes::rlane(v, 16)) + (lanes::rlane(v, 32) + lanes::rlane(v, 48));
+}
+
+__global__ __launch_bounds__(512) void attn_bwd_graph32_kernel(dgppo_gnn_attn_args p) {
+  using lanes::f32x4;
+  using lanes::wave_sync;
+  using namespace gbwd32;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int n = p.n_agents, N = p.N, D = p.D, D0 = p.D0, F = p.F, C = p.C, H = kH;
+  float* X = lds;                      // [N][36] sender rows (agents: xa; the rest: relu(x_raw W + b))
+  float* R0 = X + (size_t)N * kXP;     // [N][8] raw rows, zero padded
+  float* PW = R0 + (size_t)N * kD0;    // [8][32] pre_W | [32] pre_b
+  float* Pb = PW + kD0 * 32;
+  float* QT = Pb + 32;                 // [n][96] qt_h (32-float stride per head)
+  float* GS = QT + (size_t)n * kQP;    // [n][112] dxbar_h (32 stride) | debar (96..107) | dsig (108..110)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  float* dxw = GS + (size_t)n * kGP + (size_t)wave * (n * 32 + 16 * kPS);  // this wave's [n][32] agent image
+  float* stg = dxw + n * 32;                                                // [16][44] MFMA chunk staging
+  const bool want_pre = p.dpre_part != nullptr;
+  const bool want_dxa = p.dxa != nullptr;
+  {
+    const int k = threadIdx.x >> 5, d = threadIdx.x & 31;
+    if (threadIdx.x < kD0 * 32) PW[threadIdx.x] = (k < D0 && d < D) ? p.pre_W[k * D + d] : 0.0f;
+    if (threadIdx.x < 32) Pb[threadIdx.x] = threadIdx.x < D ? p.pre_b[threadIdx.x] : 0.0f;
+  }
+  f32x4 gacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // [x_raw | 1]^T dz
+  const int W = H * (D + 5);
+  for (int64_t g = blockIdx.x; g < p.G; g += gridDim.x) {
+    __syncthreads();  // the previous graph's readers are done
+    for (int e = threadIdx.x; e < N * kD0; e += 512) {
+      const int r = e >> 3, k = e & 7;
+      R0[e] = k < D0 ? p.x[g * p.x_gstride + (int64_t)r * D0 + k] : 0.0f;
+    }
+    for (int e = threadIdx.x; e < n * 32; e += 512) {
+      const int i = e >> 5, d = e & 31;
+      X[i * kXP + d] = d < D ? p.xa[g * p.xa_gstride + (int64_t)i * D + d] : 0.0f;
+    }
+    for (int e = threadIdx.x; e < n * kQP; e += 512) {
+      const int i = e / kQP, k = e - i * kQP, h = k >> 5, d = k & 31;
+      QT[e] = d < D ? p.qt[(g * n + i) * qt_ld(p) + h * D + d] : 0.0f;
+    }
+    for (int e = threadIdx.x; e < n * kGP; e += 512) {
+      const int i = e / kGP, k = e - i * kGP;
+      int src = -1;
+      if (k < 96) src = (k & 31) < D ? (k >> 5) * D + (k & 31) : -1;
+      else if (k < 108) src = H * D + (k - 96);
+      else if (k < 111) src = H * D + 4 * H + (k - 108);
+      GS[e] = src >= 0 ? p.dxcat[(g * n + i) * W + src] : 0.0f;
+    }
+    if (want_dxa)
+      for (int e = lane; e < n * 32; e += 64) dxw[e] = 0.0f;
+    __syncthreads();
+    // never-receivers' rows, in attn_fwd_graph_kernel's order of operations (bias, then k ascending)
+    for (int e = threadIdx.x; e < (N - n) * 8; e += 512) {
+      const int r = n + (e >> 3), c4 = 4 * (e & 7);
+      f32x4 v = *reinterpret_cast<const f32x4*>(Pb + c4);
+      for (int k = 0; k < D0; ++k) v += R0[r * kD0 + k] * *reinterpret_cast<const f32x4*>(PW + k * 32 + c4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (c4 + j < D && v[j] > 0.0f) ? v[j] : 0.0f;
+      *reinterpret_cast<f32x4*>(X + r * kXP + c4) = v;
+    }
+    __syncthreads();
+    for (int i = wave; i < n; i += kWaves) {
+      const int64_t row = g * n + i;
+      int sv[2];
+      f32x4 ev[2];
+      float av[2][kH];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = lane + 64 * u;
+        const bool in = c < C;
+        const int s = in ? p.sidx[row * C + c] : -1;
+        const int e = in ? p.cand[i * C + c] : 0;
+        sv[u] = s;
+        ev[u] = s >= 0 ? *reinterpret_cast<const f32x4*>(p.ef + g * p.ef_gstride + (int64_t)e * 4)
+                       : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int h = 0; h < kH; ++h) av[u][h] = s >= 0 ? p.attn[(row * H + h) * C + c] : 0.0f;
+      }
+      float x[2][32];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const f32x4* xr = reinterpret_cast<const f32x4*>(X + (sv[u] >= 0 ? sv[u] : 0) * kXP);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const f32x4 t = xr[q];
+          x[u][4 * q] = t[0];
+          x[u][4 * q + 1] = t[1];
+          x[u][4 * q + 2] = t[2];
+          x[u][4 * q + 3] = t[3];
+        }
+      }
+      const float* gv = GS + i * kGP;
+      const float* qv = QT + i * kQP;
+      // softmax backward: da_h = dxbar_h . x + debar_h . ef + dsig_h (+ da_add)
+      float dl[2][kH], dbeta[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float da[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float acc = 0.0f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const f32x4 gq = reinterpret_cast<const f32x4*>(gv + 32 * h)[q];
+            acc += x[u][4 * q] * gq[0] + x[u][4 * q + 1] * gq[1] + x[u][4 * q + 2] * gq[2] + x[u][4 * q + 3] * gq[3];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc += gv[96 + 4 * h + j] * ev[u][j];
+          acc += gv[108 + h];
+          const int c = lane + 64 * u;
+          if (p.da_add && sv[u] >= 0) acc += p.da_add[(row * H + h) * C + c];
+          da[u] = sv[u] >= 0 ? acc : 0.0f;
+        }
+        const float dot = sum64(av[0][h] * da[0] + av[1][h] * da[1]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) dl[u][h] = sv[u] >= 0 ? av[u][h] * (da[u] - dot) * p.scale : 0.0f;
+        dbeta[h] = sum64(dl[0][h] + dl[1][h]);
+      }
+      if (lane < kH) p.dbeta[row * dbeta_ld(p) + lane] = lane == 0 ? dbeta[0] : (lane == 1 ? dbeta[1] : dbeta[2]);
+      if (p.dq)
+        for (int kk = lane; kk < H * F; kk += 64) {
+          const int h = kk / F;
+          p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
+        }
+      // dqt_h = sum_c dl_h x_c: both slots folded per lane, transposed reduction per half, halves combined
+#pragma unroll 1
+      for (int h = 0; h < kH; ++h) {  // one head at a time (register budget)
+        const float l0 = h == 0 ? dl[0][0] : (h == 1 ? dl[0][1] : dl[0][2]);
+        const float l1 = h == 0 ? dl[1][0] : (h == 1 ? dl[1][1] : dl[1][2]);
+        float v[32];
+#pragma unroll
+        for (int d = 0; d < 32; ++d) v[d] = l0 * x[0][d] + l1 * x[1][d];
+        int cnt;
+        const int base = lanes::treduce32(v, cnt);
+        const float tot = v[0] + __shfl_xor(v[0], 32, 64);
+        if (lane < 32 && cnt > 0 && base < D) p.dqt[row * dqt_ld(p) + h * D + base] = tot;
+      }
+      // sender gradients
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (64 * u >= C) break;  // wave-uniform
+        const int s = sv[u];
+        f32x4 cq[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          cq[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int h = 0; h < kH; ++h)
+            cq[q] += av[u][h] * reinterpret_cast<const f32x4*>(gv + 32 * h)[q] +
+                     dl[u][h] * reinterpret_cast<const f32x4*>(qv + 32 * h)[q];
+        }
+        if (want_dxa && s >= 0 && s < n) {
+          f32x4* dst = reinterpret_cast<f32x4*>(dxw + s * 32);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) dst[q] += cq[q];
+        }
+        if (want_pre) {
+          const bool viapre = s >= n;
+#pragma unroll 1
+          for (int ch = 0; ch < 4; ++ch) {
+            if (64 * u + 16 * ch >= C) break;  // wave-uniform
+            if (kq == ch) {
+              float* sp = stg + i16 * kPS;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {  // the ReLU gate from the staged row (x is dead by now)
+                const f32x4 xq = reinterpret_cast<const f32x4*>(X + (viapre ? s : 0) * kXP)[q];
+                f32x4 dz;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dz[j] = (viapre && xq[j] > 0.0f) ? cq[q][j] : 0.0f;
+                reinterpret_cast<f32x4*>(sp)[q] = dz;
+              }
+              const float* rr = R0 + (viapre ? s : 0) * kD0;
+              const f32x4 r0 = reinterpret_cast<const f32x4*>(rr)[0], r1 = reinterpret_cast<const f32x4*>(rr)[1];
+              const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+              reinterpret_cast<f32x4*>(sp + 32)[0] = viapre ? r0 : z;
+              reinterpret_cast<f32x4*>(sp + 32)[1] = viapre ? r1 : z;
+              sp[40] = viapre ? 1.0f : 0.0f;
+            }
+            wave_sync();
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              const int pp = 4 * ks + kq;
+              const float a = i16 <= kD0 ? stg[pp * kPS + 32 + i16] : 0.0f;
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct)
+                gacc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, stg[pp * kPS + 16 * ct + i16], gacc[ct], 0, 0, 0);
+            }
+            wave_sync();
+          }
+        }
+      }
+    }
+    if (want_dxa) {  // agent j's gradient: the wave images in fixed wave order
+      __syncthreads();
+      const float* img = GS + (size_t)n * kGP;
+      const size_t ws = (size_t)n * 32 + 16 * kPS;
+      for (int e = threadIdx.x; e < n * D; e += 512) {
+        const int j = e / D, d = e - j * D;
+        float acc = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) acc += img[w * ws + j * 32 + d];
+        p.dxa[g * p.dxa_gstride + j * D + d] += acc;
+      }
+    }
+  }
+  if (want_pre) {  // fixed-order combine of the 8 waves' accumulators -> this workgroup's partial row
+    __syncthreads();
+    float* red = GS + (size_t)n * kGP;  // [16][33] (the wave areas are free now)
+    for (int w = 0; w < kWaves; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* dst = red + (4 * kq + r) * 33 + 16 * ct + i16;
+            *dst = (w == 0 ? 0.0f : *dst) + gacc[ct][r];
+          }
+      }
+      __syncthreads();
+    }
+    const int PK = D0 * D + D;
+    for (int o = threadIdx.x; o < PK; o += 512) {
+      const int m = o < D0 * D ? o / D : kD0;
+      const int d = o < D0 * D ? o - m * D : o - D0 * D;
+      p.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * 33 + d];
+    }
+  }
+}
+
+bool gbwd32_ok(const dgppo_gnn_attn_args* p) {
+  static const bool off = [] {
+    const char* e = getenv("DGPPO_ATTN_GRAPH");
+    const char* e32 = getenv("DGPPO_ATTN_GBWD32");
+    return (e && atoi(e) == 0) || (e32 && atoi(e32) == 0);
+  }();
+  return !off && p->H == kH && p->C > 32 && p->C <= gfwd::kMaxC && p->D > 8 && p->D <= 32 && p->sidx && p->xa &&
+         p->pre_W && p->pre_b && p->D0 <= kD0 && !p->dx && p->N > p->n_agents &&
+         gbwd32::lds_floats(p->N, p->n_agents) * sizeof(float) <= 160 * 1024;
+}
+
+// one resident 512-thread workgroup per CU (the LDS of one graph fills most of a CU)
+int64_t gbwd32_grid(const dgppo_gnn_attn_args* p) {
+  static const int64_t knob = [] {
+    const char* e = getenv("DGPPO_GBWD32_BLOCKS");
+    return e ? (int64_t)atoi(e) : (int64_t)0;
+  }();
+  const int64_t cap = knob > 0 ? knob : 256;
+  return p->G < cap ? p->G : cap;
+}
+
+void gbwd32_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
+  const size_t bytes = gbwd32::lds_floats(p->N, p->n_agents) * sizeof(float);
+  if (bytes > 64 * 1024) allow_lds((const void*)attn_bwd_graph32_kernel);
+  hipLaunchKernelGGL(attn_bwd_graph32_kernel, dim3((unsigned)gbwd32_grid(p)), dim3(512), bytes, s, *p);
+}
+
 size_t gbwd_lds_floats(const dgppo_gnn_attn_args* p) {
   return (size_t)p->N * (8 + 1) + (size_t)p->n_agents * kH * (p->D + 5) + 4 * (size_t)gfwd::kMaxC * (kH + 1);
 }
@@ -2580,6 +2860,10 @@ int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
     if (p->G > 0) fwd2_launch(p, s);
     return 0;
   }
+  if (bwd && gbwd32_ok(p)) {
+    if (p->G > 0) gbwd32_launch(p, s);
+    return 0;
+  }
   if (bwd && gbwd_ok(p)) {
     if (p->G > 0) gbwd_launch(p, s);
     return 0;
@@ -2627,6 +2911,7 @@ extern "C" int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, in
 
 extern "C" int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* p) {
   if (!dgppo::valid(p)) return 0;
+  if (dgppo::gbwd32_ok(p)) return dgppo::gbwd32_grid(p);
   if (dgppo::bwd2_ok(p)) {
     int64_t nblk;
     return dgppo::bwd2_grid(p, &nblk);

@@ -775,6 +775,14 @@ void wgrad_shape(int M, int N, int* MT, int* NT) {
   const int macc = wgrad_max_acc();
   *NT = nt >= 6 ? 6 : nt >= 3 ? 3 : nt;   // 1, 2, 3 or 6 (groups of 3/6 cover larger N)
   if (nt == 4 || nt == 5) *NT = 3;
+  // one M tile and four N tiles (e.g. the Q-free projections' Gaug = x^T [dqt | dbeta], N = 99): one pass over
+  // the rows instead of a 96-column group plus a 3-column group that re-reads the whole A panel
+  static const int nt4 = env_knob("DGPPO_WGRAD_NT4", 1);
+  if (nt == 4 && mt == 1 && nt4 && macc >= 4) {
+    *NT = 4;
+    *MT = 1;
+    return;
+  }
   while (*NT > 1 && *NT > macc) *NT = *NT == 6 ? 3 : (*NT == 3 ? 1 : *NT - 1);
   const int mmax = macc / *NT > 0 ? macc / *NT : 1;
   *MT = mt < mmax ? mt : mmax;
@@ -797,7 +805,7 @@ int launch_wgrad(const dgppo_gemm_args* p, hipStream_t s) {
   if (chunks > 1 && !p->workspace) return DGPPO_EINVAL;
 #define DG_W(a, b) \
   if (MT == a && NT == b) { launch_wgrad_t<a, b>(p, chunks, s); goto launched; }
-  DG_W(1, 1) DG_W(1, 2) DG_W(1, 3) DG_W(1, 6) DG_W(2, 1) DG_W(2, 2) DG_W(2, 3) DG_W(2, 6)
+  DG_W(1, 1) DG_W(1, 2) DG_W(1, 3) DG_W(1, 4) DG_W(1, 6) DG_W(2, 1) DG_W(2, 2) DG_W(2, 3) DG_W(2, 6)
   DG_W(3, 1) DG_W(3, 2) DG_W(3, 3) DG_W(4, 1) DG_W(4, 2) DG_W(4, 3)
 #undef DG_W
   return DGPPO_EINVAL;

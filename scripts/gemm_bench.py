@@ -27,6 +27,8 @@ SHAPES = [
     ("wgrad M64 N64", 64, 64, M, 1, 0, 1, False, 1.0),
     ("wgrad M111 N64", 111, 64, M, 1, 0, 1, False, 1.0),
     ("wgrad M32 N192", 32, 192, M, 1, 0, 1, False, 1.0),
+    ("wgrad M32 N99 (Gaug)", 32, 99, M, 1, 0, 1, False, 0.0),
+    ("wgrad M8 N27 (Gaug)", 8, 27, M, 1, 0, 1, False, 0.0),
 ]
 iters = int(os.environ.get("ITERS", "20"))
 if os.environ.get("COPY", "0") == "1":  # HBM calibration: read + write of an (M, 64) fp32 buffer
