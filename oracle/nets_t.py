@@ -31,6 +31,24 @@ def dense(x, p):
     return y + p["bias"] if "bias" in p else y
 
 
+# Test instrument for ReLU gates that fp32 rounding decides (tests/test_update_dynamics_gpu.py): with GATE_MODE
+# "on" / "off", a GNN update ReLU whose float64 pre-activation lies within GATE_TAU of the fp32 rounding scale of
+# its dot product (|x| |W| + |b|) of zero is forced open / shut (value 0 or the pre-activation itself, gradient
+# 1 or 0); None keeps torch.relu.  Any fp32 implementation may take either decision for such an entry.
+GATE_MODE = None
+GATE_TAU = 8 * 2.0 ** -24
+
+
+def _gnn_relu(pre, x, p):
+    if GATE_MODE is None:
+        return torch.relu(pre)
+    with torch.no_grad():
+        scale = x.abs() @ p["kernel"].abs() + (p["bias"].abs() if "bias" in p else 0.0)
+        amb = pre.abs() <= GATE_TAU * scale
+    forced = pre if GATE_MODE == "on" else pre * 0.0
+    return torch.where(amb, forced, torch.relu(pre))
+
+
 def layernorm(x, p, eps=1e-6):
     mean = x.mean(-1, keepdim=True)
     var = torch.clamp((x * x).mean(-1, keepdim=True) - mean * mean, min=0.0)
@@ -113,7 +131,7 @@ def graph_transformer(p, nodes, edges, recv, send, n_heads, out_dim):
     attn = segment_softmax(attn, recv, N)[..., None]
     msgs = (attn * (v + e)).mean(dim=1)
     agg = torch.zeros((N, out_dim), dtype=nodes.dtype).index_add(0, recv, msgs)
-    return torch.relu(dense(nodes, p["Dense_4"]) + agg)
+    return _gnn_relu(dense(nodes, p["Dense_4"]) + agg, nodes, p["Dense_4"])
 
 
 def gnn(layers, graph, n_agents, out_dim=64, msg_dim=32, n_heads=3):

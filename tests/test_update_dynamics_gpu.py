@@ -112,14 +112,35 @@ def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
             algo.grad_flat.copy_(mb["grad"])
             gpu = _net_trees(algo, grad=True)
             algo.grad_flat.copy_(keep)
-            for tag, g, r64, r32 in zip(("actor", "Vl", "Vh"), gpu, rg[torch.float64], rg[torch.float32]):
-                for (path, a, b), (_, c, _) in zip(_walk(g, r64), _walk(r32, r64)):
+            gate_floor = None  # |grad(ambiguous gates open) - grad(shut)|, computed on demand
+
+            def gate_floors():
+                out = []
+                try:
+                    for mode in ("on", "off"):
+                        R.GATE_MODE = mode
+                        ts = [R.to_t(x, requires_grad=True) for x in (pa, pl, ph)]
+                        R.dgppo_minibatch_grads(*ts, hr, hd, np.asarray(mb["envs"]), Ql, Qh_det, A, n, L,
+                                                algo.entropy_eps.cpu().numpy(), algo.clip_eps, algo.coef_ent)
+                        out.append([R.grads(t) for t in ts])
+                finally:
+                    R.GATE_MODE = None
+                return [[np.abs(np.asarray(x, np.float64) - np.asarray(y, np.float64)) for (_, x, y) in _walk(a, b)]
+                        for a, b in zip(*out)]
+
+            for ti, (tag, g, r64, r32) in enumerate(zip(("actor", "Vl", "Vh"), gpu, rg[torch.float64], rg[torch.float32])):
+                for li, ((path, a, b), (_, c, _)) in enumerate(zip(_walk(g, r64), _walk(r32, r64))):
                     b = np.asarray(b, np.float64)
                     d = np.abs(np.asarray(a, np.float64) - b)
-                    err = d.max()
                     floor = np.abs(np.asarray(c, np.float64) - b).max()
                     tol = 2e-5 * np.abs(b).max() + 1e-6 + 8 * floor
-                    assert err <= tol, \
+                    if d.max() > tol:
+                        # entries whose float64 value hangs on a ReLU gate within fp32 rounding of zero: either
+                        # decision is a correct fp32 result, so those entries may differ by the gate's effect
+                        gate_floor = gate_floor or gate_floors()
+                        tol = tol + gate_floor[ti][li]
+                    err = d.max()
+                    assert (d <= tol).all(), \
                         (f"update {it} mb {k} {tag} grad {path}: {err:.3e} (fp32 floor {floor:.3e}); "
                          f"{int((d > tol).sum())} of {d.size} entries over, worst at {np.unravel_index(d.argmax(), d.shape)} "
                          f"gpu {np.asarray(a).ravel()[d.argmax()]:.6e} ref {b.ravel()[d.argmax()]:.6e}, "
