@@ -33,10 +33,12 @@ def dense(x, p):
 
 # Test instrument for ReLU gates that fp32 rounding decides (tests/test_update_dynamics_gpu.py): with GATE_MODE
 # "on" / "off", a GNN update ReLU whose float64 pre-activation lies within GATE_TAU of the fp32 rounding scale of
-# its dot product (|x| |W| + |b|) of zero is forced open / shut (value 0 or the pre-activation itself, gradient
-# 1 or 0); None keeps torch.relu.  Any fp32 implementation may take either decision for such an entry.
+# its dot product (|x| |W| + |b|) of zero, or an MLP-head ReLU(LayerNorm) output within GATE_TAU_LN of zero, is
+# forced open / shut (value 0 or the pre-activation itself, gradient 1 or 0); None keeps torch.relu.  Any fp32
+# implementation may take either decision for such an entry.
 GATE_MODE = None
 GATE_TAU = 8 * 2.0 ** -24
+GATE_TAU_LN = 1e-5
 
 
 def _gnn_relu(pre, x, p):
@@ -57,8 +59,20 @@ def layernorm(x, p, eps=1e-6):
 
 def mlp_head(x, p):
     for i in range(2):
-        x = torch.relu(layernorm(dense(x, p[f"Dense_{i}"]), p[f"LayerNorm_{i}"]))
+        ln = p[f"LayerNorm_{i}"]
+        x = _ln_relu(layernorm(dense(x, p[f"Dense_{i}"]), ln), ln)
     return x
+
+
+def _ln_relu(pre, ln):
+    """relu of a LayerNorm output; under GATE_MODE the gates of outputs within GATE_TAU_LN (|scale| + |bias|) of
+    zero (normalised scale: the forward's accumulated fp32 deviation, amplified by 1/std) are forced."""
+    if GATE_MODE is None:
+        return torch.relu(pre)
+    with torch.no_grad():
+        amb = pre.abs() <= GATE_TAU_LN * (ln["scale"].abs() + ln["bias"].abs())
+    forced = pre if GATE_MODE == "on" else pre * 0.0
+    return torch.where(amb, forced, torch.relu(pre))
 
 
 def gru_cell(p, h, x):
