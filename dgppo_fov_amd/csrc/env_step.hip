@@ -288,6 +288,140 @@ __device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d
   }
 }
 
+// MPE graph writer without divergent sections: every element's LDS source row is chosen by selects and read with
+// one unconditional load, so an iteration costs one LDS round trip instead of one per row kind (the if-chains of
+// write_graph serialise the kinds' LDS latencies across the wave).  Same values, same arithmetic.
+template <int GOAL, int SD, class D>
+__device__ __forceinline__ void write_graph_mpe(const dgppo_env_cfg& cfg, const D& d, const float* nxt,
+                                                const float* goal, const float* obs, GraphOut out, bool edges_vec4,
+                                                int tid, int nthr) {
+  constexpr int ND = SD + 3;
+  const int n = d.n, O = d.O;
+  const int N = 2 * n + O + 1;
+  const int n_ag = GOAL == DGPPO_GOAL_SPREAD ? n * n : n;
+  const int n_aa = n * n;
+  const int E = n_aa + n_ag + n * O;
+  const int pad = N - 1;
+  // row r's state row in LDS (the pad row reads row 0 and is masked)
+  auto row_ptr = [&](int r) -> const float* {
+    const float* p = r < n ? nxt + r * SD : (r < 2 * n ? goal + (r - n) * SD : obs + (r - 2 * n) * SD);
+    return r < pad ? p : nxt;
+  };
+#pragma unroll 1
+  for (int idx = tid; idx < N * ND; idx += nthr) {
+    const int r = idx / ND;
+    const int c = idx - r * ND;
+    const float x = row_ptr(r)[c < SD ? c : 0];
+    const int hot = r < n ? SD + 2 : (r < 2 * n ? SD + 1 : SD);  // agent / goal / obstacle one-hot column
+    out.nodes[idx] = r == pad ? 0.0f : (c < SD ? x : (c == hot ? 1.0f : 0.0f));
+  }
+#pragma unroll 1
+  for (int idx = tid; idx < N * SD; idx += nthr) {
+    const int r = idx / SD;
+    const int c = idx - r * SD;
+    const float x = row_ptr(r)[c];
+    out.states[idx] = r == pad ? -1.0f : x;
+  }
+#pragma unroll 1
+  for (int e = tid; e < E; e += nthr) {
+    const bool aa = e < n_aa, ag = !aa && e < n_aa + n_ag;
+    const int q = aa ? e : (ag ? e - n_aa : e - n_aa - n_ag);
+    int i, j;
+    if (GOAL == DGPPO_GOAL_SPREAD || !ag) {
+      const int m = ag || aa ? n : O;
+      i = q / m;
+      j = q - i * m;
+    } else {
+      i = q;
+      j = q;
+    }
+    const float* si = nxt + i * SD;
+    const float* so = aa ? nxt + j * SD : (ag ? goal + j * SD : obs + j * SD);
+    const float s0 = si[0], s1 = si[1], s2 = si[2], s3 = si[3];
+    const float o0 = so[0], o1 = so[1], o2 = so[2], o3 = so[3];
+    const float f0 = s0 - o0, f1 = s1 - o1, f2 = s2 - o2, f3 = s3 - o3;
+    const float d2 = sq2(s0 - o0, s1 - o1);
+    bool m;
+    if (aa) m = i == j ? ((d2 == 0.0f) & (cfg.c_self_dist < cfg.comm_radius)) : (d2 < cfg.t2_comm);
+    else m = ag ? true : (d2 < cfg.t2_comm);
+    const int sv0 = aa ? j : (ag ? n + j : 2 * n + j);
+    if (edges_vec4) {
+      reinterpret_cast<float4*>(out.edges)[e] = make_float4(f0, f1, f2, f3);
+    } else {
+      out.edges[4 * e + 0] = f0;
+      out.edges[4 * e + 1] = f1;
+      out.edges[4 * e + 2] = f2;
+      out.edges[4 * e + 3] = f3;
+    }
+    out.recv[e] = m ? i : pad;
+    out.send[e] = m ? sv0 : pad;
+  }
+}
+
+// MPE step tasks (block_step phase B) without divergent sections, when they fit one pass of the workgroup: lane q
+// reads the operands of every task kind it could be (dynamics of agent q, or one distance), all loads issued
+// together, then computes and stores its own kind.  Same arithmetic as the generic task loop.
+template <int GOAL, int SD>
+__device__ __forceinline__ void mpe_tasks(const dgppo_env_cfg& cfg, float* lds, const Carve& cv, int n, int O, int q) {
+  const float* cur = lds + cv.cur;
+  const float* goal = cur + n * SD;
+  const float* obs = cur + 2 * n * SD;
+  float* dist = lds + cv.dist;
+  const int n_aa = n * n;
+  const int n_ga = GOAL == DGPPO_GOAL_SPREAD ? n * n : n;
+  const int n_task = n + n_aa + n_ga + n * O;
+  // dynamics operands (agent q)
+  const int id = q < n ? q : 0;
+  const float* x = cur + id * SD;
+  const float* a = lds + cv.act + 2 * id;
+  const float x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], a0 = a[0], a1 = a[1];
+  // distance operands: A - B with (A, B) = (agent i, agent j) | (goal gj, agent ai) | (agent i, obstacle o)
+  const int t = q - n;
+  const bool aa = t >= 0 && t < n_aa, ga = t >= n_aa && t < n_aa + n_ga;
+  const int tg = t - n_aa, to = t - n_aa - n_ga;
+  int ia, ib, slot;
+  const float *pa, *pb;
+  if (aa) {
+    ia = t / n;
+    ib = t - ia * n;
+    pa = cur + ia * SD;
+    pb = cur + ib * SD;
+    slot = t;
+  } else if (ga) {
+    const int gj = GOAL == DGPPO_GOAL_SPREAD ? tg / n : tg;
+    const int ai = GOAL == DGPPO_GOAL_SPREAD ? tg - gj * n : tg;
+    ia = gj;
+    ib = ai;
+    pa = goal + gj * SD;
+    pb = cur + ai * SD;
+    slot = n_aa + tg;
+  } else {
+    const int tt = (to >= 0 && q < n_task) ? to : 0;  // lanes past the tasks read obstacle 0 of agent 0
+    const int i = O > 0 ? tt / O : 0, o = tt - i * (O > 0 ? O : 1);
+    ia = i;
+    ib = o;
+    pa = cur + i * SD;
+    pb = obs + o * SD;
+    slot = 2 * n_aa + tt;
+  }
+  const float pa0 = pa[0], pa1 = pa[1], pb0 = pb[0], pb1 = pb[1];
+  if (q < n) {  // dynamics (mpe/base.py double integrator), then clip_state
+    float y[SD];
+    y[0] = x2 * cfg.dt + x0;
+    y[1] = x3 * cfg.dt + x1;
+    y[2] = (a0 * 10.0f) * cfg.dt + x2;
+    y[3] = (a1 * 10.0f) * cfg.dt + x3;
+#pragma unroll
+    for (int c = 0; c < SD; ++c) lds[cv.nxt + q * SD + c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+    const float an = norm2(a0, a1);
+    lds[cv.red + 2 * n + q] = an * an;
+  } else if (q < n_task) {
+    float dj = norm2(pa0 - pb0, pa1 - pb1);
+    if (aa && ia == ib) dj = dj + 1e6f;
+    dist[slot] = dj;
+  }
+}
+
 // ---- lidar: per-ray hit distance, then a stable NaN-last rank -> top-k hits -------------------
 // jnp.argsort (stable, NaN last, -0 == +0) as one 64-bit key per ray: high word = the alpha bits
 // mapped to an unsigned total order (every NaN -> 0xFFFFFFFF, -0 -> +0), low word = ray index.
@@ -535,8 +669,10 @@ __device__ __forceinline__ void block_step(const dgppo_env_cfg& cfg, const dgppo
   const int n_ga = GOAL == DGPPO_GOAL_SPREAD ? n * n : n;
   const int n_t3 = lidar ? n * k : (mpe ? n * O : 0);
   const int n_task = n + n_aa + n_ga + n_t3;
+  const bool bf = mpe && n_task <= BLOCK;  // the branch-free MPE form (one pass)
+  if (bf) mpe_tasks<GOAL, SD>(cfg, lds, cv, n, O, tid);
 #pragma unroll 1
-  for (int q = tid; q < n_task; q += BLOCK) {
+  for (int q = bf ? n_task : tid; q < n_task; q += BLOCK) {
     if (q < n) {  // dynamics (lidar_env/base.py:142-149 / bicycle 92-111), then clip_state
       const int i = q;
       const float* x = cur + i * SD;
@@ -672,7 +808,8 @@ __device__ __forceinline__ void block_step(const dgppo_env_cfg& cfg, const dgppo
   out.send = io.senders + env * io.edge_index_stride;
   const bool vec4 = ((io.edges_stride & 3) == 0) && ((reinterpret_cast<uintptr_t>(io.edges) & 15) == 0);
   const float* third = mpe ? cur + 2 * n * SD : lds + cv.hits;
-  write_graph<ENGINE, GOAL, SD>(cfg, d, lds + cv.nxt, goal, third, out, vec4, tid, BLOCK);
+  if constexpr (mpe) write_graph_mpe<GOAL, SD>(cfg, d, lds + cv.nxt, goal, third, out, vec4, tid, BLOCK);
+  else write_graph<ENGINE, GOAL, SD>(cfg, d, lds + cv.nxt, goal, third, out, vec4, tid, BLOCK);
   BLK_STAMP(4);
 #ifdef DGPPO_ENV_STAMPS
   if (tid == 0)
