@@ -267,15 +267,23 @@ def read_mfma_pmc():
                 "window_executed_tflops": d["total_mfma_tflops_over_window"],
                 "window_frac_of_peak": round(d["total_mfma_tflops_over_window"] / FP32_MFMA_PEAK_TFLOPS, 4),
                 "update_window_ms": None if "update_window_s" not in d else round(d["update_window_s"] * 1e3, 2),
-                "update_mfma_tflop": d.get("update_mfma_tflop"), "lib_sha256": d.get("lib_sha256")}
+                "update_mfma_tflop": d.get("update_mfma_tflop"), "src_sha256": d.get("src_sha256")}
     except Exception:
         return None
 
 
-def _sha256(fn):
+def source_sha256():
+    """sha256 over the native sources (dgppo_fov_amd/csrc/*, include/dgppo_hip.h) in name order: the identity of
+    the build a committed PMC profile measured."""
+    import glob
     import hashlib
 
-    return hashlib.sha256(open(fn, "rb").read()).hexdigest() if fn and os.path.exists(fn) else None
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "dgppo_fov_amd", "csrc", "*"))) + [os.path.join(ROOT, "include", "dgppo_hip.h")]
+    for fn in files:
+        h.update(os.path.basename(fn).encode())
+        h.update(open(fn, "rb").read())
+    return h.hexdigest()
 
 
 PPO_BATCH, RNN_STEP = 16384, 16  # BASELINE.md synthetic-input plan (batch_size, rnn_step)
@@ -329,23 +337,21 @@ def ppo_bench(env, dev, world, rank, iters, strong=False):
     executed = None
     if pmc is not None and pmc.get("update_mfma_tflop") is not None:
         # the hardware's executed fp32 MFMA flops of one update (PMC profile of the same config: a count, independent
-        # of timing) over THIS run's measured update time -- quoted only when the profile measured the library this
-        # process loaded (sha256), so a stale profile fails instead of being quoted.  The profiled update window is
+        # of timing) over THIS run's measured update time -- quoted only when the profile measured this tree's native
+        # sources (sha256), so a stale profile fails instead of being quoted.  The profiled update window is
         # reported beside it; it runs longer than the live update because kernel tracing adds per-dispatch overhead
         # to the ~6,000 dispatches of an update.
-        from dgppo_fov_amd import _lib as LIB
-
-        live = _sha256(str(LIB.LIB_PATH))
-        if pmc.get("lib_sha256") != live:
-            executed = {"status": f"not quoted: {pmc['source'].split()[0]} profiled library {pmc.get('lib_sha256')}, "
-                                  f"this process loaded {live}"}
+        live = source_sha256()
+        if pmc.get("src_sha256") != live:
+            executed = {"status": f"not quoted: {pmc['source'].split()[0]} profiled sources {pmc.get('src_sha256')}, "
+                                  f"this tree's sources are {live}"}
         elif world != 1 or strong:
             executed = {"status": "not quoted: the profile is a 1-GPU weak-scaling run"}
         else:
             ach = pmc["update_mfma_tflop"] / t_upd
             executed = {"achieved": round(ach, 2), "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                         "tflop_per_update": pmc["update_mfma_tflop"], "profile_update_ms_traced": pmc["update_window_ms"],
-                        "lib_sha256": live}
+                        "src_sha256": live}
     upd_tf = UPDATE_TFLOP_PER_4096_ENVS * (B_PER_GPU / 4096) * world + ROLLOUT_TFLOP_PER_4096_ENVS / 2 * (
         B_PER_GPU / 4096) * world  # the update runs the deterministic rollout too
     return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),

@@ -69,10 +69,11 @@ if marks:
     out["update_mfma_tflop"] = round(uf / 1e12, 4)
     out["update_executed_tflops"] = round(uf / uspan / 1e12, 2)
     out["update_frac_of_peak"] = round(uf / uspan / PEAK, 4)
-# the library the profile measured: bench.py quotes the executed-MFMA figure only for this exact build
-import hashlib  # noqa: E402
+# the build the profile measured: bench.py quotes the executed-MFMA figure only for the same sources (a hash of
+# dgppo_fov_amd/csrc/* and include/dgppo_hip.h -- a rebuild of the same sources is the same build)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_sha256  # noqa: E402
 
-_lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dgppo_fov_amd", "lib", "libdgppo_hip.so")
-out["lib_sha256"] = hashlib.sha256(open(_lib, "rb").read()).hexdigest() if os.path.exists(_lib) else None
+out["src_sha256"] = source_sha256()
 print(json.dumps(out, indent=1))
 json.dump(out, open(os.path.join(root, "mfma_util.json"), "w"), indent=1)
