@@ -1,7 +1,7 @@
 #!/bin/bash
 # this round's evidence on the current build: GPU parity suite, the default bench line, bench kernel stats +
 # executed-MFMA PMC + env-rollout PMC (scripts/round_profiles.sh), every BASELINE config (scripts/config_bench.py)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 TLIM=600 PYARGS=" " bash scripts/gpu_tests.sh > gpurun_out/final_tests_tail.txt 2>&1; rc=$?
 grep -E 'passed|failed' gpurun_out/pytest_gpu.log | tail -2; [ $rc -eq 0 ] || exit $rc

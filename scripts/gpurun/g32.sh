@@ -1,6 +1,6 @@
 #!/bin/bash
 # graph-form agent-mode backward (n = 32): parity, per-pass kernel split vs the block kernel; trajectory-test A/B
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 PT="python -u -m pytest -q --timeout 200 --timeout-method thread -p no:cacheprovider"

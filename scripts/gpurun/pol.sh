@@ -1,3 +1,4 @@
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 # fused policy step + register-form update forward: parity (nets / rollout tests) + timings
 timeout -k 10 600 python -u -m pytest tests/test_nets_gpu.py tests/test_rollout_gpu.py -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/pol_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -5 gpurun_out/pol_tests.log; [ $rc -eq 0 ] || exit $rc

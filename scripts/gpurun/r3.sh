@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-3 re-entry check: the trajectory test under both attention-backward forms, the default bench line, then
 # this round's profiles
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 T=tests/test_update_dynamics_gpu.py::test_trajectory_matches_oracle_loop
 timeout -k 10 300 python -u -m pytest "$T" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_traj_reg.log 2>&1; echo "reg rc=$?"

@@ -1,5 +1,5 @@
 #!/bin/bash
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 PT="python -u -m pytest -q --timeout 200 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 300 $PT tests/test_env_gpu.py tests/test_rollout_gpu.py > gpurun_out/st32_tests.log 2>&1
