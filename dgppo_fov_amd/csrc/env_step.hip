@@ -75,6 +75,9 @@ struct Carve {
   }
 };
 
+// persistent block rollout: episodes with T * 2n <= kActStage action floats stage them all in LDS (after the carve)
+constexpr int kActStage = 4096;
+
 // Sizes: compile-time where a specialisation fixes them (0 / -1 = read from cfg at run time)
 template <int NA, int NO, int NR, int NK>
 struct Dims {
@@ -842,11 +845,23 @@ __global__ __launch_bounds__(BLOCK) void env_rollout_block_kernel(dgppo_env_cfg 
   static_assert(BLOCK >= 64, "2 n <= 64 actions per step, one per thread");
   const int na = 2 * n;
   const float* act0 = r.step.action + env * r.step.action_stride;
-  float a_nxt = threadIdx.x < na ? act0[threadIdx.x] : 0.0f;
+  // Small episodes (T * 2n <= kActStage floats, e.g. MPE): every step's clipped actions are staged in LDS once, so
+  // the step loop issues no global load at all.  A per-step action load would be waited for with vmcnt(0) at the
+  // next step (the graph writer's store count is not static), i.e. behind the whole previous step's store drain.
+  const bool stage = (int64_t)r.T * na <= kActStage;
+  float* acts = lds + cv.total;
+  if (stage) {
+    for (int idx = threadIdx.x; idx < r.T * na; idx += BLOCK) {
+      const int t = idx / na, j = idx - t * na;
+      acts[idx] = clampf_nan(act0[(int64_t)t * r.t_action + j], -1.0f, 1.0f);
+    }
+    __syncthreads();
+  }
+  float a_nxt = (!stage && threadIdx.x < na) ? act0[threadIdx.x] : 0.0f;
 #pragma unroll 1
   for (int t = 0; t < r.T; ++t) {
-    if (threadIdx.x < na) lds[cv.act + threadIdx.x] = clampf_nan(a_nxt, -1.0f, 1.0f);
-    if (t + 1 < r.T && threadIdx.x < na) a_nxt = act0[(t + 1) * r.t_action + threadIdx.x];
+    if (threadIdx.x < na) lds[cv.act + threadIdx.x] = stage ? acts[t * na + threadIdx.x] : clampf_nan(a_nxt, -1.0f, 1.0f);
+    if (!stage && t + 1 < r.T && threadIdx.x < na) a_nxt = act0[(t + 1) * r.t_action + threadIdx.x];
     dgppo_env_step_io q = r.step;
     q.states = r.step.out_states + t * r.t_states;
     q.action = r.step.action + t * r.t_action;
@@ -3188,7 +3203,9 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
       cfg->n_agents <= 32) {  // (2 n actions per step staged one per thread of a >= 64-thread workgroup)
     const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                    cfg->engine != DGPPO_ENGINE_MPE);
-    dispatch_rollout_block(*cfg, *r, (size_t)cv.total * sizeof(float), s);
+    const int64_t act_floats = (int64_t)r->T * 2 * cfg->n_agents;
+    const int64_t extra = act_floats <= kActStage ? ((act_floats + 3) & ~(int64_t)3) : 0;
+    dispatch_rollout_block(*cfg, *r, (size_t)(cv.total + extra) * sizeof(float), s);
     return (int)hipGetLastError();
   }
   for (int t = 0; t < r->T; ++t) {
