@@ -586,12 +586,23 @@ class DGPPO:
             if self.world > 1:
                 dist.all_reduce(safe)
             info["eval/safe_data"] = safe / (B * self.world * T * n)
+            # learning diagnostics (not reference metrics): per cost column, the mean Vh over the rollout's
+            # graphs, the det rollout's Vh / Qh_det targets and its costs -- one device vector, one copy
+            info["diag/vec"] = torch.cat([Vh[:, :T].mean((0, 1, 2)), Vh_det[:, :T].mean((0, 1, 2)),
+                                          Qh_det.mean((0, 1, 2)), det.costs.mean((0, 1, 2))])
         ph.report()
         return self._finish_info(info)
 
     def _finish_info(self, info) -> dict:
         out = {}
         st = info.pop("policy/stats", None)
+        dv = info.pop("diag/vec", None)
+        if dv is not None:
+            nh = self._env.n_cost
+            d = dv.cpu().numpy().reshape(4, nh)
+            for i, tag in enumerate(("Vh/mean", "Vh/det_mean", "Vh/det_target_mean", "det/cost_mean")):
+                for j in range(nh):
+                    out[f"{tag}_h{j}"] = float(d[i, j])
         for k, v in info.items():
             out[k] = float(v.reshape(-1)[0].item()) if torch.is_tensor(v) else v
         if st is not None:

@@ -37,8 +37,14 @@ class Trainer:
         self.eval_epi = params["eval_epi"]
         self.save_interval = params["save_interval"]
         self.update_steps = 0
+        self.start_step = 0
         self.rng = np.random.default_rng(seed)
         self._test_engine = None
+        # not in the reference (it logs every update to wandb and trains in one process lifetime):
+        # log.jsonl keeps every log_interval-th update, and train() returns after max_minutes of wall
+        # time with a resumable state (save_state / load_state), so a long run can span processes
+        self.log_interval = int(params.get("log_interval", 1))
+        self.max_minutes = params.get("max_minutes")
 
     @staticmethod
     def _check_params(params: dict) -> bool:
@@ -66,10 +72,42 @@ class Trainer:
         r = self._test_engine.run(key)
         return eval_info(r.rewards, r.costs)
 
+    # ---- resumable state (params + optimiser + RNG; the reference saves params only) ----------
+    STATE_FILE = "trainer_state.json"
+
+    def save_state(self, step: int):
+        """models/<step>/ (params + Adam moments + counters, algo.save) and trainer_state.json: the next
+        step and every host RNG the loop draws from, so load_state() continues the exact sequence."""
+        if not self.save_log:
+            return
+        self.algo.save(self.model_dir, step)
+        st = {"next_step": step + 1, "update_steps": self.update_steps, "model_step": step,
+              "trainer_rng": self.rng.bit_generator.state, "algo_key": self.algo.key.bit_generator.state,
+              "algo_np_rng": self.algo.np_rng.bit_generator.state}
+        tmp = os.path.join(self.log_dir, self.STATE_FILE + ".tmp")
+        with open(tmp, "w") as f:
+            json.dump(st, f)
+        os.replace(tmp, os.path.join(self.log_dir, self.STATE_FILE))
+
+    def load_state(self, run_dir: str):
+        """Continue a run saved by save_state (its log_dir): parameters, Adam state, step and RNG streams."""
+        with open(os.path.join(run_dir, self.STATE_FILE)) as f:
+            st = json.load(f)
+        self.algo.load(os.path.join(run_dir, "models"), st["model_step"])
+        self.rng.bit_generator.state = st["trainer_rng"]
+        self.algo.key.bit_generator.state = st["algo_key"]
+        self.algo.np_rng.bit_generator.state = st["algo_np_rng"]
+        self.start_step, self.update_steps = st["next_step"], st["update_steps"]
+        return st
+
     def train(self):
         start_time = time()
         test_key = int(self.seed)
-        for step in range(0, self.steps + 1):
+        for step in range(self.start_step, self.steps + 1):
+            if self.max_minutes is not None and time() - start_time > 60.0 * float(self.max_minutes):
+                self.save_state(step - 1)
+                print(f"> stopping after {time() - start_time:.0f}s at step {step} (resume with --resume)", flush=True)
+                return False
             if step % self.eval_interval == 0 and self.rank == 0:
                 info = self.evaluate(test_key)
                 print(f"step: {step:3}, time: {time() - start_time:5.0f}s, reward: {info['eval/reward']:9.4f}, "
@@ -82,8 +120,12 @@ class Trainer:
             rollouts = self.algo.collect(self.algo.params, key, n_env=self.n_env_train)
             train_stats = self._train_stats(rollouts)  # device scalars: no host sync before the update
             update_info = self.algo.update(rollouts, step)
-            self._log({"step": self.update_steps, **update_info, **self._read_stats(train_stats)})
+            if step % self.log_interval == 0:
+                self._log({"step": self.update_steps, **update_info, **self._read_stats(train_stats)})
             self.update_steps += 1
+        if self.max_minutes is not None:
+            self.save_state(self.steps)
+        return True
 
     def _train_stats(self, rollouts):
         """The stochastic rollouts' own metrics as ONE device vector, enqueued right after collect (the next

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Between gpurun calls of scripts/long_run.sh: make the runs the last call left in gpurun_out/long/
+# the ones the next call resumes (runs_long/ travels to the GPU box with the snapshot; it is git-ignored).
+cd "$(dirname "$0")/.."
+[ -d gpurun_out/long/LidarSpread ] || { echo "nothing to sync"; exit 1; }
+rm -rf runs_long && mkdir -p runs_long
+cp -r gpurun_out/long/LidarSpread runs_long/
+du -sh runs_long

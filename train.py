@@ -50,30 +50,39 @@ def train(args):
         print(f"> Loading checkpoint from {args.load_checkpoint}, step {args.load_step}")
         algo.load(args.load_checkpoint, args.load_step)
 
-    rng_ = np.random.default_rng()
-    rand_id = "".join([chr(rng_.integers(65, 91)) for _ in range(4)])
-    start_time = int(datetime.datetime.now().strftime("%m%d%H%M%S"))
-    base = f"{args.log_dir}/{args.env}/{args.algo}"
-    if not args.debug and rank == 0:
-        os.makedirs(base, exist_ok=True)
-    while os.path.exists(f"{base}/seed{args.seed}_{start_time}_{rand_id}"):
-        start_time += 1
-    log_dir = f"{base}/seed{args.seed}_{start_time}_{rand_id}"
-    run_name = "{}_seed{:03}_{}_{}".format(args.algo, args.seed, start_time, rand_id)
-    if args.name is not None:
-        run_name = "{}_{}_seed{:03}_{}_{}".format(run_name, args.name, args.seed, start_time, rand_id)
+    if args.resume:
+        log_dir = args.resume.rstrip("/")
+        run_name = os.path.basename(log_dir)
+    else:
+        rng_ = np.random.default_rng()
+        rand_id = "".join([chr(rng_.integers(65, 91)) for _ in range(4)])
+        start_time = int(datetime.datetime.now().strftime("%m%d%H%M%S"))
+        base = f"{args.log_dir}/{args.env}/{args.algo}"
+        if not args.debug and rank == 0:
+            os.makedirs(base, exist_ok=True)
+        while os.path.exists(f"{base}/seed{args.seed}_{start_time}_{rand_id}"):
+            start_time += 1
+        log_dir = f"{base}/seed{args.seed}_{start_time}_{rand_id}"
+        run_name = "{}_seed{:03}_{}_{}".format(args.algo, args.seed, start_time, rand_id)
+        if args.name is not None:
+            run_name = "{}_{}_seed{:03}_{}_{}".format(run_name, args.name, args.seed, start_time, rand_id)
     train_params = {"run_name": run_name, "training_steps": args.steps, "eval_interval": args.eval_interval,
-                    "eval_epi": args.eval_epi, "save_interval": args.save_interval}
+                    "eval_epi": args.eval_epi, "save_interval": args.save_interval,
+                    "log_interval": args.log_interval, "max_minutes": args.max_minutes}
     trainer = Trainer(env=env, env_test=env_test, algo=algo, gamma=0.99, log_dir=log_dir,
                       n_env_train=args.n_env_train, n_env_test=args.n_env_test, seed=args.seed,
                       params=train_params, save_log=not args.debug)
-    if not args.debug and rank == 0:
+    if args.resume:
+        st = trainer.load_state(log_dir)
+        print(f"> Resuming {log_dir} at step {st['next_step']}")
+    elif not args.debug and rank == 0:
         with open(f"{log_dir}/config.yaml", "w") as f:
             yaml.safe_dump(vars(args), f)
             yaml.safe_dump(algo.config, f)
-    trainer.train()
+    done = trainer.train()
     if world > 1:
         dist.destroy_process_group()
+    return done
 
 
 def main():
@@ -118,6 +127,10 @@ def main():
     parser.add_argument("--eval-interval", type=int, default=50)
     parser.add_argument("--eval-epi", type=int, default=1)
     parser.add_argument("--save-interval", type=int, default=50)
+    # not reference flags: resumable long runs (trainer_state.json + models/<step>/ with Adam state)
+    parser.add_argument("--resume", type=str, default=None, help="continue the run saved in this log dir")
+    parser.add_argument("--max-minutes", type=float, default=None, help="save a resumable state and stop after")
+    parser.add_argument("--log-interval", type=int, default=1, help="log.jsonl keeps every k-th update")
     args = parser.parse_args()
     if args.load_checkpoint and args.load_step is None:
         parser.error("--load-checkpoint requires --load-step")
