@@ -832,7 +832,8 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
 // time-major (T + 1) buffers, reward[t], cost[t] -- the same arithmetic as T per-step launches, without their
 // launch floor and their re-reads of every graph.
 template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
-__global__ __launch_bounds__(BLOCK) void env_rollout_block_kernel(dgppo_env_cfg cfg, dgppo_env_rollout_io r) {
+__global__ __launch_bounds__(BLOCK) void env_rollout_block_kernel(dgppo_env_cfg cfg, dgppo_env_rollout_io r,
+                                                                   int stage_acts) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
   const Dims<NA, NO, NR, NK> d(cfg);
@@ -848,7 +849,8 @@ __global__ __launch_bounds__(BLOCK) void env_rollout_block_kernel(dgppo_env_cfg 
   // Small episodes (T * 2n <= kActStage floats, e.g. MPE): every step's clipped actions are staged in LDS once, so
   // the step loop issues no global load at all.  A per-step action load would be waited for with vmcnt(0) at the
   // next step (the graph writer's store count is not static), i.e. behind the whole previous step's store drain.
-  const bool stage = (int64_t)r.T * na <= kActStage;
+  // The host decides (stage_acts) and sized the dynamic LDS for it: the two can never disagree.
+  const bool stage = stage_acts != 0;
   float* acts = lds + cv.total;
   if (stage) {
     for (int idx = threadIdx.x; idx < r.T * na; idx += BLOCK) {
@@ -2798,41 +2800,43 @@ static void launch_step(const dgppo_env_cfg& c, const dgppo_env_step_io& io, siz
 }
 
 template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
-static void launch_rollout_block(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem, hipStream_t s) {
+static void launch_rollout_block(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem, hipStream_t s,
+                                 int stage) {
   hipLaunchKernelGGL((env_rollout_block_kernel<ENGINE, GOAL, SD, BLOCK, NA, NO, NR, NK>), dim3((unsigned)r.step.n_env),
-                     dim3(BLOCK), shmem, s, c, r);
+                     dim3(BLOCK), shmem, s, c, r, stage);
 }
 
 // the same compile-time size selection as dispatch_step_sized
 template <int ENGINE, int GOAL, int SD>
 static void dispatch_rollout_block_sized(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem,
-                                         hipStream_t s) {
+                                         hipStream_t s, int stage) {
   const int n = c.n_agents, O = c.n_obs, R = c.n_rays, k = c.top_k;
   if (ENGINE == DGPPO_ENGINE_MPE) {
-    if (n == 3 && O == 3) return launch_rollout_block<ENGINE, GOAL, SD, 64, 3, 3, 0, 0>(c, r, shmem, s);
-    if (n == 3 && O == 0) return launch_rollout_block<ENGINE, GOAL, SD, 64, 3, 0, 0, 0>(c, r, shmem, s);
-    return launch_rollout_block<ENGINE, GOAL, SD, 64, 0, -1, 0, 0>(c, r, shmem, s);
+    if (n == 3 && O == 3) return launch_rollout_block<ENGINE, GOAL, SD, 64, 3, 3, 0, 0>(c, r, shmem, s, stage);
+    if (n == 3 && O == 0) return launch_rollout_block<ENGINE, GOAL, SD, 64, 3, 0, 0, 0>(c, r, shmem, s, stage);
+    return launch_rollout_block<ENGINE, GOAL, SD, 64, 0, -1, 0, 0>(c, r, shmem, s, stage);
   }
   if (R == 32 && k == 8) {
-    if (n == 8 && O == 3) return launch_rollout_block<ENGINE, GOAL, SD, 256, 8, 3, 32, 8>(c, r, shmem, s);
-    if (n == 32 && O == 8) return launch_rollout_block<ENGINE, GOAL, SD, 256, 32, 8, 32, 8>(c, r, shmem, s);
+    if (n == 8 && O == 3) return launch_rollout_block<ENGINE, GOAL, SD, 256, 8, 3, 32, 8>(c, r, shmem, s, stage);
+    if (n == 32 && O == 8) return launch_rollout_block<ENGINE, GOAL, SD, 256, 32, 8, 32, 8>(c, r, shmem, s, stage);
   }
-  if (n * R >= 256) return launch_rollout_block<ENGINE, GOAL, SD, 256, 0, -1, 0, 0>(c, r, shmem, s);
-  return launch_rollout_block<ENGINE, GOAL, SD, 128, 0, -1, 0, 0>(c, r, shmem, s);
+  if (n * R >= 256) return launch_rollout_block<ENGINE, GOAL, SD, 256, 0, -1, 0, 0>(c, r, shmem, s, stage);
+  return launch_rollout_block<ENGINE, GOAL, SD, 128, 0, -1, 0, 0>(c, r, shmem, s, stage);
 }
 
-static void dispatch_rollout_block(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem, hipStream_t s) {
+static void dispatch_rollout_block(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, size_t shmem, hipStream_t s,
+                                   int stage) {
   const bool spread = c.goal_mode == DGPPO_GOAL_SPREAD;
   switch (c.engine) {
     case DGPPO_ENGINE_MPE:
-      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, r, shmem, s)
-                    : dispatch_rollout_block_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, r, shmem, s);
+      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_SPREAD, 4>(c, r, shmem, s, stage)
+                    : dispatch_rollout_block_sized<DGPPO_ENGINE_MPE, DGPPO_GOAL_TARGET, 4>(c, r, shmem, s, stage);
     case DGPPO_ENGINE_BICYCLE:
-      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, r, shmem, s)
-                    : dispatch_rollout_block_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, r, shmem, s);
+      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(c, r, shmem, s, stage)
+                    : dispatch_rollout_block_sized<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_TARGET, 5>(c, r, shmem, s, stage);
     default:
-      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, r, shmem, s)
-                    : dispatch_rollout_block_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, r, shmem, s);
+      return spread ? dispatch_rollout_block_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_SPREAD, 4>(c, r, shmem, s, stage)
+                    : dispatch_rollout_block_sized<DGPPO_ENGINE_LIDAR, DGPPO_GOAL_TARGET, 4>(c, r, shmem, s, stage);
   }
 }
 
@@ -3203,9 +3207,13 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
       cfg->n_agents <= 32) {  // (2 n actions per step staged one per thread of a >= 64-thread workgroup)
     const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                    cfg->engine != DGPPO_ENGINE_MPE);
+    // the whole episode's actions are staged in LDS only when they fit kActStage AND the total stays within
+    // the 64 KB default dynamic LDS (n = 32 / 8 obstacles carves 59 KB before staging); the kernel reads the flag
     const int64_t act_floats = (int64_t)r->T * 2 * cfg->n_agents;
-    const int64_t extra = act_floats <= kActStage ? ((act_floats + 3) & ~(int64_t)3) : 0;
-    dispatch_rollout_block(*cfg, *r, (size_t)(cv.total + extra) * sizeof(float), s);
+    const int64_t act_lds = (act_floats + 3) & ~(int64_t)3;
+    const bool stage = act_floats <= kActStage && (cv.total + act_lds) * (int64_t)sizeof(float) <= 64 * 1024;
+    const int64_t extra = stage ? act_lds : 0;
+    dispatch_rollout_block(*cfg, *r, (size_t)(cv.total + extra) * sizeof(float), s, stage ? 1 : 0);
     return (int)hipGetLastError();
   }
   for (int t = 0; t < r->T; ++t) {

@@ -102,6 +102,20 @@ __device__ __forceinline__ void gemm_tile(const GemmTileArgs& g, int m0, int n0,
   }
 }
 
+// The one epilogue order of every GEMM path (tiled, split-K reduce, rows / pf / breg via epi_load + epi_store):
+// v = (alpha acc + bias) + (beta C + addend), ReLU last -- the dispatch (shape, DGPPO_ROWS_* knobs) never changes
+// the bits of a result.  cp / dp are the C and addend elements (dp null when the call has no addend).
+__device__ __forceinline__ float epi_combine(const dgppo_gemm_args& p, float acc, float bias, const float* cp,
+                                             const float* dp) {
+  float v = p.alpha * acc + bias;
+  if (p.beta != 0.0f || dp) {
+    float x = p.beta != 0.0f ? p.beta * *cp : 0.0f;
+    if (dp) x = p.beta != 0.0f ? x + *dp : *dp;
+    v += x;
+  }
+  return p.relu ? (v > 0.0f ? v : 0.0f) : v;
+}
+
 __global__ __launch_bounds__(256) void gemm_kernel(dgppo_gemm_args p) {
   __shared__ float As[kBK * kPitch];
   __shared__ float Bs[kBK * kPitch];
@@ -151,12 +165,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(dgppo_gemm_args p) {
     const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (row < p.M && col < p.N) {
       float* cp = C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
-      float v = p.alpha * acc[r];
-      if (p.beta != 0.0f) v += p.beta * *cp;
-      if (p.bias) v += p.bias[col];
-      if (D) v += D[row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
-      if (p.relu) v = v > 0.0f ? v : 0.0f;
-      *cp = v;
+      const float* dp = D ? D + row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col : nullptr;
+      *cp = epi_combine(p, acc[r], p.bias ? p.bias[col] : 0.0f, cp, dp);
     }
   }
 }
@@ -172,12 +182,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(dgppo_gemm_args p) {
     float s = 0.0f;
     for (int sp = 0; sp < p.split_k; ++sp) s += p.workspace[((int64_t)sp * p.batch + b) * MN + e];
     float* C = p.C + (int64_t)b * p.stride_c + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col;
-    float v = p.alpha * s;
-    if (p.beta != 0.0f) v += p.beta * *C;
-    if (p.bias) v += p.bias[col];
-    if (p.addend) v += p.addend[(int64_t)b * p.stride_add + row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col];
-    if (p.relu) v = v > 0.0f ? v : 0.0f;
-    *C = v;
+    const float* dp =
+        p.addend ? p.addend + (int64_t)b * p.stride_add + row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col : nullptr;
+    *C = epi_combine(p, s, p.bias ? p.bias[col] : 0.0f, C, dp);
   }
 }
 
@@ -220,9 +227,9 @@ __device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* 
           const float* cs = ok ? C + row_off(row, p.ldc, p.c_grp, p.c_gstride) + col : (const float*)g_zero_row;
           x = p.beta * *cs;
         }
-        if (EXTRA & 1) {
+        if (EXTRA & 1) {  // beta C + addend, or the addend alone (epi_combine's operand order)
           const float* ds = ok ? Dd + row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col : (const float*)g_zero_row;
-          x += *ds;
+          x = (EXTRA & 2) ? x + *ds : *ds;
         }
         xv[t][r] = x;
       }

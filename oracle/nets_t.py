@@ -39,6 +39,14 @@ def dense(x, p):
 GATE_MODE = None
 GATE_TAU = 8 * 2.0 ** -24
 GATE_TAU_LN = 1e-5
+# when a list: every gated call under GATE_MODE "on" appends (ambiguous gates, gates evaluated), so the test can
+# bound how many decisions the fallback tolerance covers
+GATE_STATS = None
+
+
+def _gate_count(amb):
+    if GATE_STATS is not None and GATE_MODE == "on":
+        GATE_STATS.append((int(amb.sum().item()), int(amb.numel())))
 
 
 def _gnn_relu(pre, x, p):
@@ -47,6 +55,7 @@ def _gnn_relu(pre, x, p):
     with torch.no_grad():
         scale = x.abs() @ p["kernel"].abs() + (p["bias"].abs() if "bias" in p else 0.0)
         amb = pre.abs() <= GATE_TAU * scale
+        _gate_count(amb)
     forced = pre if GATE_MODE == "on" else pre * 0.0
     return torch.where(amb, forced, torch.relu(pre))
 
@@ -71,6 +80,7 @@ def _ln_relu(pre, ln):
         return torch.relu(pre)
     with torch.no_grad():
         amb = pre.abs() <= GATE_TAU_LN * (ln["scale"].abs() + ln["bias"].abs())
+        _gate_count(amb)
     forced = pre if GATE_MODE == "on" else pre * 0.0
     return torch.where(amb, forced, torch.relu(pre))
 

@@ -25,6 +25,10 @@ CONFIGS = [
     ("MPESpread n3 o3 x1024", "MPESpread", 3, 3, 1024),
     ("LidarSpread n8 o3 x4096", "LidarSpread", 8, 3, 4096),
     ("LidarBicycleTarget n8 o3 x4096/GPU (8-GPU config)", "LidarBicycleTarget", 8, 3, 4096),
+    # config 4's strong-scaling share: 4096 envs over 8 GPUs = 512 per GPU; the global 16384-sample minibatch is
+    # 2048 samples per rank (batch 2048 here gives the per-rank plan: 32 minibatches of 16 envs; no all-reduce)
+    ("LidarBicycleTarget n8 o3 x512/GPU (config 4 strong share, 2048-sample rank minibatch)", "LidarBicycleTarget", 8,
+     3, 512, 2048),
     ("LidarSpread n32 o8 x1024/GPU (8192 envs over 8 GPUs)", "LidarSpread", 32, 8, 1024),
     ("LidarOmniTarget n8 o3 x4096", "LidarOmniTarget", 8, 3, 4096),
     # env variants (no BASELINE config names them): same per-GPU shapes as their base envs
@@ -88,42 +92,55 @@ def episode_ms(env, B, dev, T=128, reps=10):
     return sorted(ts)[len(ts) // 2]
 
 
-def ppo_ms(env, B, dev):
+def ppo_ms(env, B, dev, batch=16384, reps=1):
+    """Median over `reps` timed collect + update iterations (after one untimed one)."""
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
-                     action_dim=env.action_dim, n_agents=env.num_agents, batch_size=16384, rnn_step=16, seed=0,
+                     action_dim=env.action_dim, n_agents=env.num_agents, batch_size=batch, rnn_step=16, seed=0,
                      device=dev, train_steps=1000)
     r = algo.collect(algo.params, 0, n_env=B)
     algo.update(r, 0)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    r = algo.collect(algo.params, 1, n_env=B)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    algo.update(r, 1)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    return (t1 - t0) * 1e3, (t2 - t1) * 1e3
+    cs, us = [], []
+    for k in range(reps):
+        t0 = time.perf_counter()
+        r = algo.collect(algo.params, 1 + k, n_env=B)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        algo.update(r, 1 + k)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        cs.append((t1 - t0) * 1e3)
+        us.append((t2 - t1) * 1e3)
+    return sorted(cs)[len(cs) // 2], sorted(us)[len(us) // 2]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-ppo", action="store_true")
     ap.add_argument("--only", default="", help="run only the configs whose label contains this string")
+    ap.add_argument("--step-kernel", default="auto", choices=["auto", "block"],
+                    help="block: force the workgroup-per-env env kernels (dgppo_env_set_step_kernel(1))")
+    ap.add_argument("--reps", type=int, default=1, help="timed collect + update iterations (median)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    for label, eid, n, obs, B in CONFIGS:
+    if args.step_kernel == "block":
+        from dgppo_fov_amd import _lib
+        _lib.load().dgppo_env_set_step_kernel(1)
+    for label, eid, n, obs, B, *rest in CONFIGS:
+        batch = rest[0] if rest else 16384
         if args.only not in label:
             continue
         env = make_env(eid, n, num_obs=obs, max_step=128, device=dev)
         us = step_us(env, B, dev)
         row = {"config": label, "env": eid, "n": n, "n_obs": obs, "envs_per_gpu": B, "env_step_us": round(us, 2),
-               "env_steps_per_s": round(B / us * 1e6, 1)}
+               "env_steps_per_s": round(B / us * 1e6, 1), "step_kernel": args.step_kernel,
+               "update_graph": os.environ.get("DGPPO_UPDATE_GRAPH", "0")}
         ep = episode_ms(env, B, dev)
         row.update({"episode_ms": round(ep, 3), "episode_env_steps_per_s": round(B * 128 / ep * 1e3, 1)})
         if not args.no_ppo:
-            c, u = ppo_ms(env, B, dev)
-            row.update({"collect_ms": round(c, 2), "update_ms": round(u, 2),
-                        "minibatches": B * 128 // 16384})
+            c, u = ppo_ms(env, B, dev, batch, args.reps)
+            row.update({"collect_ms": round(c, 2), "update_ms": round(u, 2), "batch_size": batch,
+                        "minibatches": B * 128 // batch})
         print(json.dumps(row), flush=True)
 
 

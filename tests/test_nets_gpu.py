@@ -97,6 +97,32 @@ def test_gemm_weight_grad_with_fused_bias_grad(cuda, M, N, Kd, batch, grp):
     assert (bd.double().cpu() - refb).abs().max().item() <= 2e-6 * B.abs().sum(1).max().item() + 1e-5
 
 
+@pytest.mark.parametrize("M,N,Kd", [(300, 64, 32), (300, 64, 64), (300, 64, 96), (300, 192, 64), (70, 40, 20)])
+@pytest.mark.parametrize("beta,with_add", [(0.0, True), (0.7, False), (0.7, True)])
+def test_gemm_epilogue_order_is_path_independent(cuda, M, N, Kd, beta, with_add):
+    """Every GEMM path applies one epilogue order, (alpha acc + bias) + (beta C + addend): the rows kernels
+    (whole-unit prefetch K <= 32 / N > 64, B-in-registers N <= 64 K = 64, plain K > 64), the tiled kernel (taken
+    for op(A) = A^T) and its split-K reduce give the same bits.  Integer A and B make every accumulation exact in
+    any order, so the epilogue is the only possible difference."""
+    g = torch.Generator().manual_seed(M + N + Kd)
+    A = torch.randint(-3, 4, (M, Kd), generator=g).float()
+    B = torch.randint(-3, 4, (Kd, N), generator=g).float()
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    add = torch.randn(M, N, generator=g) if with_add else None
+    outs = []
+    for ta, split in ((False, 1), (True, 1), (True, 2)):
+        Cd = C0.to(cuda).clone()
+        Ad = (A.t().contiguous() if ta else A).to(cuda)
+        K.gemm(Ad, B.to(cuda), Cd, M, N, Kd, ta=ta, bias=bias.to(cuda), addend=None if add is None else add.to(cuda),
+               alpha=0.3, beta=beta, split_k=split)
+        torch.cuda.synchronize()
+        outs.append(Cd.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    ref = (0.3 * A.double() @ B.double() + bias.double()) + (beta * C0.double() + (0 if add is None else add.double()))
+    assert (outs[0].double() - ref).abs().max().item() <= 1e-5 * (1 + ref.abs().max().item())
+
+
 def test_gemm_row_grouping(cuda):
     """agent rows (first n of N per graph) as GEMM rows, in and out."""
     G, N, n, D, F = 5, 9, 3, 6, 4

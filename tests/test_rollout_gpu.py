@@ -184,6 +184,31 @@ def test_persistent_env_rollout_bit_exact(cuda, eid, n, obs, B, graph):
         assert np.array_equal(x, y), k
 
 
+@pytest.mark.parametrize("eid,n,obs,B,T", [
+    ("MPESpread", 3, 3, 9, 128),     # T * 2n = 768 action floats: staged in LDS at kernel start
+    ("MPESpread", 3, 3, 9, 700),     # 4200 > kActStage: per-step action prefetch from HBM
+    ("LidarSpread", 32, 8, 3, 128),  # 8192 > kActStage (the default n = 32 episode): prefetch path
+    ("LidarSpread", 32, 8, 3, 24),   # 1536 fits kActStage, but 59 KB of carve + 6 KB > 64 KB: not staged
+])
+def test_persistent_block_rollout_action_staging_branches(cuda, eid, n, obs, B, T):
+    """Both branches of the block persistent rollout's action staging (the host decides it from kActStage and
+    the 64 KB dynamic-LDS budget) match T single-step launches bit for bit, at the default T = 128 too."""
+    env = make_env(eid, n, num_obs=obs, device=cuda)
+    outs = []
+    for fused in (False, True):
+        eng = RolloutEngine(env, B, T, cuda, fused=fused)
+        gen = torch.Generator(device=cuda)
+        gen.manual_seed(5)
+        eng.actions.uniform_(-1.2, 1.2, generator=gen)
+        eng.run(key=17)
+        torch.cuda.synchronize(cuda)
+        b = eng.buf
+        outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders, eng.rewards,
+                                              eng.costs)])
+    for k, (x, y) in enumerate(zip(*outs)):
+        assert np.array_equal(x, y), k
+
+
 def test_block_persistent_rollout_matches_wave_steps(cuda):
     """With the workgroup-per-env kernels forced (dgppo_env_set_step_kernel(1)), the n = 8 Lidar configs take the
     block persistent rollout; it matches the default path (wave kernels) bit for bit."""

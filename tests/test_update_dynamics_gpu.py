@@ -64,12 +64,19 @@ def _trees_at(algo, flats):
             net.ps.flat.copy_(keep[k])
 
 
-@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("MPETarget", 2, 0)])
-def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
-    B, T, L, K_UPD = 8, 32, 16, 5
+def _trajectory(cuda, eid, n, obs, K_UPD=5, perturb=None):
+    """The teacher-forced K_UPD x 4-minibatch check (module docstring).  `perturb(algo, it, k)` may change the
+    algorithm before minibatch k of update it runs (negative controls).  Returns per-minibatch fallback
+    records: (update, minibatch, entries over the base tolerance, entries checked, ambiguous gates, gates)."""
+    B, T, L = 8, 32, 16
     algo, env = _algo(cuda, eid, n, obs, T, batch=2 * T, L=L)  # 2 envs per minibatch -> 4 minibatches
     nets = (("Vl", algo.Vl), ("Vh", algo.Vh), ("policy", algo.actor))
+    if perturb is not None:
+        for name, opt in algo.opt.items():
+            opt.step = _counting_step(opt, name, algo, perturb)
+    fallbacks = []
     for it in range(K_UPD):
+        algo._traj_it = it
         roll = algo.collect(algo.params, 100 + it, n_env=B)
         start = {k: net.ps.flat.clone() for k, net in nets}
         algo.trace = {}
@@ -122,12 +129,14 @@ def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
             gpu = _net_trees(algo, grad=True)
             algo.grad_flat.copy_(keep)
             gate_floor = None  # effect of the ReLU gates fp32 rounding decides, computed on demand
+            gate_stats = []
             r64_leaves = rg[torch.float64]
 
             def gate_floors():
                 # |on - off| + |on - natural| + |off - natural| per entry: one ambiguous gate's effect is |on - off|;
                 # the one-sided toggles bound mixed decisions over several ambiguous gates
                 out = [r64_leaves]
+                R.GATE_STATS = gate_stats
                 try:
                     for mode in ("on", "off"):
                         R.GATE_MODE = mode
@@ -137,19 +146,23 @@ def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
                         out.append([R.grads(t) for t in ts])
                 finally:
                     R.GATE_MODE = None
+                    R.GATE_STATS = None
                 nat, on, off = out
                 return [[np.abs(x - y) + np.abs(x - z) + np.abs(y - z) for (_, x, y), (_, _, z) in
                          zip(_walk(_as64(a), _as64(b)), _walk(_as64(a), _as64(c)))] for a, b, c in zip(on, off, nat)]
 
+            n_over = n_checked = 0
             for ti, (tag, g, r64, r32) in enumerate(zip(("actor", "Vl", "Vh"), gpu, rg[torch.float64], rg[torch.float32])):
                 for li, ((path, a, b), (_, c, _)) in enumerate(zip(_walk(g, r64), _walk(r32, r64))):
                     b = np.asarray(b, np.float64)
                     d = np.abs(np.asarray(a, np.float64) - b)
                     floor = np.abs(np.asarray(c, np.float64) - b).max()
                     tol = 2e-5 * np.abs(b).max() + 1e-6 + 8 * floor
+                    n_checked += d.size
                     if d.max() > tol:
                         # entries whose float64 value hangs on a ReLU gate within fp32 rounding of zero: either
                         # decision is a correct fp32 result, so those entries may differ by the gate's effect
+                        n_over += int((d > tol).sum())
                         gate_floor = gate_floor or gate_floors()
                         tol = tol + gate_floor[ti][li]
                     err = d.max()
@@ -161,7 +174,11 @@ def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
                          f"median err {np.median(d):.2e}, fp32 oracle {np.asarray(c, np.float64).ravel()[d.argmax()]:.6e}, "
                          f"gate floor {0.0 if gate_floor is None else gate_floor[ti][li].ravel()[d.argmax()]:.3e}; "
                          f"largest excess at {worst}: err {d[worst]:.3e} tol {np.broadcast_to(tol, d.shape)[worst]:.3e}")
-            # clip + Adam with the carried moments -> the parameters the next minibatch starts from
+            amb, gates = sum(x for x, _ in gate_stats), sum(y for _, y in gate_stats)
+            fallbacks.append((it, k, n_over, n_checked, amb, gates))
+            # clip + Adam with the carried moments -> the parameters the next minibatch starts from.  Tolerance
+            # 2^-22 |p| (the fp32 store of p - step) + 1e-5 lr (the fp32 step's relative error is ~1e-7): tight
+            # enough that a 0.1% learning-rate error on one minibatch fails (test_trajectory_negative_control)
             nxt = tr["mb"][k + 1]["before"] if k + 1 < len(tr["mb"]) else {nm: net.ps.flat for nm, net in nets}
             off = 0
             for name, net in nets:
@@ -171,12 +188,54 @@ def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
                 (gc,), _ = O.clip_by_global_norm_ref([g], algo.max_grad_norm)
                 count = int(mb["state_before"][name][2].item())
                 assert count == it * 4 + k, (it, k, name, count)  # every step so far was finite
+                lr = algo.opt[name].__dict__.get("lr_ref", algo.opt[name].lr)
                 (rp,), _, _ = O.adam_step([mb["before"][name].double().cpu().numpy()], [gc],
                                           [mb["m_before"][name].double().cpu().numpy()],
-                                          [mb["v_before"][name].double().cpu().numpy()], count, algo.opt[name].lr)
-                err = np.abs(nxt[name].double().cpu().numpy() - rp).max()
-                assert err <= 1e-6, f"update {it} mb {k} {name} Adam: {err:.3e}"
+                                          [mb["v_before"][name].double().cpu().numpy()], count, lr)
+                got = nxt[name].double().cpu().numpy()
+                tol = 2.0 ** -22 * np.maximum(np.abs(rp), np.abs(got)) + 1e-5 * lr
+                err = np.abs(got - rp)
+                assert (err <= tol).all(), f"update {it} mb {k} {name} Adam: {err.max():.3e} (tol {tol.min():.3e}+)"
         assert np.isfinite(info["policy/loss"])
+    return fallbacks
+
+
+def _counting_step(opt, name, algo, perturb):
+    """opt.step wrapped so perturb(algo, name, update, minibatch) runs before each minibatch's Adam step."""
+    orig = opt.step
+    opt._mb = -1
+
+    def step():
+        opt._mb += 1
+        perturb(algo, opt, name, getattr(algo, "_traj_it", 0), opt._mb % 4)
+        orig()
+    return step
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("MPETarget", 2, 0)])
+def test_trajectory_matches_oracle_loop(cuda, eid, n, obs):
+    fb = _trajectory(cuda, eid, n, obs)
+    # the gate fallback is bounded: at most 0.1% of the ReLU gates a minibatch evaluates may be decided by fp32
+    # rounding, and at most a quarter of the minibatches may need the fallback at all (the rounds so far: 0 or 1
+    # of 20); every count is printed (pytest -s / the log on failure)
+    for it, k, n_over, n_checked, amb, gates in fb:
+        print(f"{eid} update {it} mb {k}: {n_over} of {n_checked} gradient entries over the base tolerance; "
+              f"{amb} ambiguous of {gates} ReLU gates")
+        assert amb <= max(2, 1e-3 * gates), (it, k, amb, gates)
+    used = sum(1 for r in fb if r[2] > 0)
+    assert used <= len(fb) // 4, f"{used} of {len(fb)} minibatches needed the gate fallback"
+
+
+def test_trajectory_negative_control(cuda):
+    """A 0.1% learning-rate error in ONE minibatch's policy Adam step (update 0, minibatch 1) must fail the
+    trajectory check: the teacher-forced comparison is sensitive to a real orchestration error of that size."""
+    def perturb(algo, opt, name, it, k):
+        if name == "policy":
+            opt.lr_ref = opt.__dict__.get("lr_ref", opt.lr)
+            opt.lr = opt.lr_ref * (1.001 if (it, k) == (0, 1) else 1.0)
+
+    with pytest.raises(AssertionError, match="mb 1 policy Adam"):
+        _trajectory(cuda, "LidarSpread", 3, 2, K_UPD=1, perturb=perturb)
 
 
 def test_streams_bit_identical(cuda, monkeypatch):
