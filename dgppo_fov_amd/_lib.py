@@ -271,6 +271,7 @@ SIGNATURES = {
     "dgppo_gru_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _V]),
     "dgppo_gru_seq_blocks": (ctypes.c_int64, [_I32]),
     "dgppo_gnn_attn_partial_blocks": (ctypes.c_int64, [_V]),
+    "dgppo_gnn_set_attn_kernel": (ctypes.c_int, [ctypes.c_int]),
     "dgppo_policy_step_supported": (ctypes.c_int, [_V]),
     "dgppo_policy_work_floats": (ctypes.c_int64, []),
     "dgppo_policy_prepare": (ctypes.c_int, [_V, _V]),
@@ -302,7 +303,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 8  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 9  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

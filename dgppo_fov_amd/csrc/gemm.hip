@@ -107,7 +107,8 @@ __device__ __forceinline__ void gemm_tile(const GemmTileArgs& g, int m0, int n0,
 // the bits of a result.  cp / dp are the C and addend elements (dp null when the call has no addend).
 __device__ __forceinline__ float epi_combine(const dgppo_gemm_args& p, float acc, float bias, const float* cp,
                                              const float* dp) {
-  float v = p.alpha * acc + bias;
+#pragma clang fp contract(off)  // the same roundings on every path: one explicit fma, then plain mul / adds
+  float v = __builtin_fmaf(p.alpha, acc, bias);
   if (p.beta != 0.0f || dp) {
     float x = p.beta != 0.0f ? p.beta * *cp : 0.0f;
     if (dp) x = p.beta != 0.0f ? x + *dp : *dp;
@@ -212,6 +213,7 @@ constexpr int kRowsLdsFloats = 12800;  // 50 KB: K16 * (N + 1) must fit
 template <int NTW, int EXTRA>
 __device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* C, const float* Dd, int m0, int col0,
                                          int i, int h, float (&bv)[NTW], float (&xv)[NTW][16]) {
+#pragma clang fp contract(off)  // epi_combine's roundings
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
     const int col = col0 + 32 * t + i;
@@ -240,6 +242,7 @@ __device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* 
 template <int NTW, int EXTRA>
 __device__ __forceinline__ void epi_store(const dgppo_gemm_args& p, float* C, const f32x16 (&acc)[NTW], int m0,
                                           int col0, int i, int h, const float (&bv)[NTW], const float (&xv)[NTW][16]) {
+#pragma clang fp contract(off)  // epi_combine's roundings
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
     const int col = col0 + 32 * t + i;
@@ -248,7 +251,7 @@ __device__ __forceinline__ void epi_store(const dgppo_gemm_args& p, float* C, co
     for (int r = 0; r < 16; ++r) {
       const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (row < p.M) {
-        float v = p.alpha * acc[t][r] + bv[t];
+        float v = __builtin_fmaf(p.alpha, acc[t][r], bv[t]);
         if (EXTRA) v += xv[t][r];
         if (p.relu) v = v > 0.0f ? v : 0.0f;
         C[row_off(row, p.ldc, p.c_grp, p.c_gstride) + col] = v;

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 8  /* 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 9  /* 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -286,6 +286,10 @@ typedef struct dgppo_gnn_attn_args {
 } dgppo_gnn_attn_args;
 
 int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
+/* Attention-kernel selection (no reference counterpart; A/B and kernel-vs-kernel parity tests): 1 = the graph-form
+ * MFMA kernels where they apply (graphs of N <= 96 nodes, n <= 10 agents; the default), 0 = the row-block /
+ * graph / generic kernels everywhere.  Returns the previous mode or DGPPO_EINVAL.  Initial mode: DGPPO_ATTN_GM. */
+int dgppo_gnn_set_attn_kernel(int mode);
 /* sidx[(g*n + i)*C + c] = senders[g][cand[i][c]] if that edge's receiver is i, else -1: the
  * candidate resolution shared by every attention launch on one graph batch */
 int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, int32_t E, const int32_t* cand,
