@@ -476,11 +476,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8))) void
 }  // namespace gm
 
 // ---- dispatch ------------------------------------------------------------------------------------------------
+// Off by default: measured 2.3-4.8x SLOWER than the row-block kernels at the bench shape (LidarSpread n8, 16384
+// graphs: fwd D=8 209 vs 79 us, fwd D=32 708 vs 180, bwd D=8 391 vs 81, bwd D=32 877 vs 390; profiles/r04_attn_gm_*):
+// the node-space softmax / weight / edge work is dense over the graph's 96 node slots per receiver row where the
+// candidate-space kernels touch 24, so the MFMA products save less than the 4x elementwise work costs (PMC: 1.1-1.7x
+// the VALU instructions of the row-block kernels on 16x fewer waves).  Kept, tested against the row-block kernels,
+// for DGPPO_ATTN_GM=1 / dgppo_gnn_set_attn_kernel(1).
 int g_attn_gm = -1;  // dgppo_gnn_set_attn_kernel
 inline bool gm_enabled() {
   if (g_attn_gm < 0) {
     const char* e = getenv("DGPPO_ATTN_GM");
-    g_attn_gm = (e && atoi(e) == 0) ? 0 : 1;
+    g_attn_gm = (e && atoi(e) == 1) ? 1 : 0;
   }
   return g_attn_gm == 1;
 }

@@ -287,8 +287,9 @@ typedef struct dgppo_gnn_attn_args {
 
 int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
 /* Attention-kernel selection (no reference counterpart; A/B and kernel-vs-kernel parity tests): 1 = the graph-form
- * MFMA kernels where they apply (graphs of N <= 96 nodes, n <= 10 agents; the default), 0 = the row-block /
- * graph / generic kernels everywhere.  Returns the previous mode or DGPPO_EINVAL.  Initial mode: DGPPO_ATTN_GM. */
+ * MFMA kernels where they apply (graphs of N <= 96 nodes, n <= 10 agents), 0 = the row-block / graph / generic
+ * kernels everywhere (the default: measured faster).  Returns the previous mode or DGPPO_EINVAL.  Initial mode:
+ * DGPPO_ATTN_GM=1|0 (default 0). */
 int dgppo_gnn_set_attn_kernel(int mode);
 /* sidx[(g*n + i)*C + c] = senders[g][cand[i][c]] if that edge's receiver is i, else -1: the
  * candidate resolution shared by every attention launch on one graph batch */
