@@ -157,6 +157,10 @@ class GemmArgs(ctypes.Structure):
         ("split_k", ctypes.c_int32),
         ("workspace", c_f32p),
         ("bias_grad", c_f32p),
+        ("epi", ctypes.c_int32), ("pad3_", ctypes.c_int32),
+        ("mask", c_f32p), ("ld_mask", ctypes.c_int64),
+        ("ln_scale", c_f32p), ("ln_bias", c_f32p),
+        ("ln_h", c_f32p), ("ln_mean", c_f32p), ("ln_rstd", c_f32p), ("ln_part", c_f32p),
     ]
 
 
@@ -272,6 +276,7 @@ SIGNATURES = {
     "dgppo_gru_seq_blocks": (ctypes.c_int64, [_I32]),
     "dgppo_gnn_attn_partial_blocks": (ctypes.c_int64, [_V]),
     "dgppo_gnn_set_attn_kernel": (ctypes.c_int, [ctypes.c_int]),
+    "dgppo_gemm_partial_rows": (ctypes.c_int64, [ctypes.POINTER(GemmArgs)]),
     "dgppo_policy_step_supported": (ctypes.c_int, [_V]),
     "dgppo_policy_work_floats": (ctypes.c_int64, []),
     "dgppo_policy_prepare": (ctypes.c_int, [_V, _V]),

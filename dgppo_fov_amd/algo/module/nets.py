@@ -195,10 +195,12 @@ class ActorNet(_Net):
         self._bptt(dH2.view(S, L, n, 64), gcs, S, L, tc, g)
 
     def _bptt(self, dHs, gcs, S, L, tc, g):
-        dY, _ = self.gru.seq_bwd(gcs, dHs.reshape(S * L * self.n, 64))
         gc, hc = tc
-        dz = self.head.bwd(hc, dY)
-        self.gnn.bwd(gc, dz, g)
+        ln = self.head.ln1_bwd_args(hc) if self.gru.simple else None  # LayerNorm_1 bwd in the GRU's dx GEMM
+        dY, _ = self.gru.seq_bwd(gcs, dHs.reshape(S * L * self.n, 64), ln=ln)
+        fused = ln is not None
+        dz = self.head.bwd(hc, dY, dy_is_dh1=fused, mask_input=fused)
+        self.gnn.bwd(gc, dz, g, top_masked=fused)
 
 
 class VlNet(_Net):
@@ -242,8 +244,9 @@ class VlNet(_Net):
         n, dev = self.n, dv.device
         G = S * L
         dH = self.out.bwd(Hs, dv.reshape(G, 1).contiguous(), G)
-        dY, _ = self.gru.seq_bwd(gcs, dH)
-        dzm = self.head.bwd(hc, dY)
+        ln = self.head.ln1_bwd_args(hc) if self.gru.simple else None
+        dY, _ = self.gru.seq_bwd(gcs, dH, ln=ln)
+        dzm = self.head.bwd(hc, dY, dy_is_dh1=ln is not None)
         dz = torch.empty_like(z)
         K.agent_mean_bwd(dzm, dz, G, n, 64, n * 64)
         self.gnn.bwd(gc, dz, g)
@@ -283,9 +286,11 @@ class VhNet(_Net):
         g, gc, hc, rc, h2 = cache
         rows = g.G * self.n
         dh2 = self.out.bwd(h2, dout, rows)
-        dy, _ = self.gru.seq_bwd(rc, dh2)
-        dz = self.head.bwd(hc, dy)
-        self.gnn.bwd(gc, dz, g)
+        ln = self.head.ln1_bwd_args(hc) if self.gru.simple else None
+        dy, _ = self.gru.seq_bwd(rc, dh2, ln=ln)
+        fused = ln is not None
+        dz = self.head.bwd(hc, dy, dy_is_dh1=fused, mask_input=fused)
+        self.gnn.bwd(gc, dz, g, top_masked=fused)
 
 
 class VhGlobalNet(_Net):

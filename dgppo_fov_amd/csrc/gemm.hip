@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include "../../include/dgppo_hip.h"
+#include "lanes.h"
 
 namespace dgppo {
 
@@ -36,6 +37,7 @@ constexpr int kBM = 64, kBN = 64, kBK = 32, kPitch = kBM + 1;
 // 64 zero bytes in global memory: out-of-range lanes of the streamed A loads read these instead of
 // taking a branch or a select, so the prefetch stays a plain straight-line load
 __device__ float4 g_zero_row[4];
+__device__ float g_sink[64];  // target of the epilogue stores a lane must not make (kept branch-free)
 
 struct GemmTileArgs {
   int M, N, K, k_begin, k_end;
@@ -210,16 +212,64 @@ constexpr int kRowsLdsFloats = 12800;  // 50 KB: K16 * (N + 1) must fit
 // prefetch and consumed after the MFMAs.  A load issued after the prefetch (or guarded by a branch) makes its
 // in-order vmcnt wait cover the whole prefetch -- one HBM round trip per epilogue element when guarded.
 // EXTRA bit 0: addend, bit 1: beta * C (only the operands a call has are loaded)
-template <int NTW, int EXTRA>
+//
+// EPI (dgppo_gemm_args.epi, ABI 9) fuses the elementwise pass that follows the GEMM into its epilogue:
+//   1 relu mask:  v = mask > 0 ? v : 0 (the ReLU backward of the layer whose output `mask` is; replaces relu_bwd)
+//   2 LayerNorm(64) + ReLU forward (flax LayerNorm eps 1e-6, nn/mlp.py:20-30): h = the GEMM result is stored to ln_h,
+//     y = relu(((h - mean) rstd) scale + bias) to C, the row mean / rstd to ln_mean / ln_rstd (a wave owns whole
+//     64-wide rows: NTW = 2, one column group)
+//   3 LayerNorm(64) + ReLU backward: the GEMM result is dy; with h from ln_h the row statistics and the ReLU gate
+//     are recomputed by the same instruction sequence as EPI 2 (bit-identical decisions), dx goes to C and the
+//     workgroup's [dscale | dbias] column partials to ln_part (dgppo_gemm_partial_rows rows; the host sums them)
+constexpr int kEpiMask = 1, kEpiLnFwd = 2, kEpiLnBwd = 3;
+template <int NTW, int EPI>
+struct EpiX {
+  float m[(EPI == dgppo::kEpiMask || EPI == dgppo::kEpiLnBwd) ? NTW : 1][16];  // mask rows (1) / pre-LN rows (3)
+  float sc[NTW], bi[NTW];                                        // LayerNorm scale / bias at this lane's columns
+};
+template <int NTW>
+struct EpiAcc {  // EPI 3: this lane's column partials of dscale / dbias over the rows it has stored
+  float ds[NTW], db[NTW];
+};
+
+__device__ __forceinline__ float swz16(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));
+}
+// all-reduce over the 32 lanes of a half-wave (every lane gets the identical sum)
+__device__ __forceinline__ float red32(float v) {
+  v = lanes::sum16(v);
+  return v + swz16(v);
+}
+// row statistics of 64 values (v0 at column i, v1 at column 32 + i of the half-wave's 32 lanes): EPI 2 and 3
+// call this with the same bits, so the bwd recomputes the fwd's mean / rstd exactly
+__device__ __forceinline__ void ln_stats(float v0, float v1, float& mean, float& rstd) {
+#pragma clang fp contract(off)
+  const float s1 = red32(v0 + v1);
+  const float s2 = red32(v0 * v0 + v1 * v1);
+  mean = s1 / 64.0f;
+  float var = s2 / 64.0f - mean * mean;
+  var = var > 0.0f ? var : 0.0f;
+  rstd = 1.0f / sqrtf(var + 1e-6f);
+}
+__device__ __forceinline__ float ln_pre(float v, float mean, float rstd, float sc, float bi) {
+#pragma clang fp contract(off)
+  return ((v - mean) * rstd) * sc + bi;
+}
+
+template <int NTW, int EXTRA, int EPI>
 __device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* C, const float* Dd, int m0, int col0,
-                                         int i, int h, float (&bv)[NTW], float (&xv)[NTW][16]) {
+                                         int i, int h, float (&bv)[NTW], float (&xv)[NTW][16], EpiX<NTW, EPI>& ex) {
 #pragma clang fp contract(off)  // epi_combine's roundings
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
     const int col = col0 + 32 * t + i;
     const bool cok = col < p.N;
     bv[t] = (p.bias && cok) ? p.bias[col] : 0.0f;
-    if (EXTRA) {
+    if (EPI == dgppo::kEpiLnFwd || EPI == dgppo::kEpiLnBwd) {
+      ex.sc[t] = p.ln_scale[col];  // N == 64: every column is real
+      ex.bi[t] = p.ln_bias[col];
+    }
+    if (EXTRA || EPI == dgppo::kEpiMask || EPI == dgppo::kEpiLnBwd) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -233,16 +283,76 @@ __device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* 
           const float* ds = ok ? Dd + row_off(row, p.ld_add, p.add_grp, p.add_gstride) + col : (const float*)g_zero_row;
           x = (EXTRA & 2) ? x + *ds : *ds;
         }
-        xv[t][r] = x;
+        if (EXTRA) xv[t][r] = x;
+        if (EPI == dgppo::kEpiMask) {
+          const float* ms = ok ? p.mask + row_off(row, p.ld_mask, p.c_grp, p.c_gstride) + col : (const float*)g_zero_row;
+          ex.m[t][r] = *ms;
+        }
+        if (EPI == dgppo::kEpiLnBwd) ex.m[t][r] = *(ok ? p.ln_h + (int64_t)row * 64 + col : (const float*)g_zero_row);
       }
     }
   }
 }
 
-template <int NTW, int EXTRA>
+template <int NTW, int EXTRA, int EPI>
 __device__ __forceinline__ void epi_store(const dgppo_gemm_args& p, float* C, const f32x16 (&acc)[NTW], int m0,
-                                          int col0, int i, int h, const float (&bv)[NTW], const float (&xv)[NTW][16]) {
+                                          int col0, int i, int h, const float (&bv)[NTW], const float (&xv)[NTW][16],
+                                          const EpiX<NTW, EPI>& ex, EpiAcc<NTW>& ea) {
 #pragma clang fp contract(off)  // epi_combine's roundings
+  if constexpr (EPI == dgppo::kEpiLnFwd || EPI == dgppo::kEpiLnBwd) {
+    static_assert(NTW == 2 && EXTRA == 0, "LayerNorm epilogues: whole 64-wide rows, no beta C / addend");
+    float mo = 0.0f, ro = 0.0f;  // this lane's row statistic to store (lanes i < 16: register r = i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const bool rok = row < p.M;
+      const int64_t off = row_off(row, p.ldc, p.c_grp, p.c_gstride);
+      float* dst0 = rok ? C + off + i : (float*)g_sink;
+      float* dst1 = rok ? C + off + 32 + i : (float*)g_sink;
+      if constexpr (EPI == dgppo::kEpiLnFwd) {
+        const float v0 = __builtin_fmaf(p.alpha, acc[0][r], bv[0]);
+        const float v1 = __builtin_fmaf(p.alpha, acc[1][r], bv[1]);
+        float mean, rstd;
+        ln_stats(v0, v1, mean, rstd);
+        float* h0 = rok ? p.ln_h + (int64_t)row * 64 + i : (float*)g_sink;
+        float* h1 = rok ? p.ln_h + (int64_t)row * 64 + 32 + i : (float*)g_sink;
+        *h0 = v0;
+        *h1 = v1;
+        const float y0 = ln_pre(v0, mean, rstd, ex.sc[0], ex.bi[0]);
+        const float y1 = ln_pre(v1, mean, rstd, ex.sc[1], ex.bi[1]);
+        *dst0 = y0 > 0.0f ? y0 : 0.0f;
+        *dst1 = y1 > 0.0f ? y1 : 0.0f;
+        mo = i == r ? mean : mo;
+        ro = i == r ? rstd : ro;
+      } else {
+        const float hv0 = ex.m[0][r], hv1 = ex.m[1][r];
+        float mean, rstd;
+        ln_stats(hv0, hv1, mean, rstd);
+        const float dy0 = rok ? __builtin_fmaf(p.alpha, acc[0][r], bv[0]) : 0.0f;
+        const float dy1 = rok ? __builtin_fmaf(p.alpha, acc[1][r], bv[1]) : 0.0f;
+        const float g0 = ln_pre(hv0, mean, rstd, ex.sc[0], ex.bi[0]) > 0.0f ? dy0 : 0.0f;
+        const float g1 = ln_pre(hv1, mean, rstd, ex.sc[1], ex.bi[1]) > 0.0f ? dy1 : 0.0f;
+        const float xh0 = (hv0 - mean) * rstd, xh1 = (hv1 - mean) * rstd;
+        ea.ds[0] += g0 * xh0;
+        ea.ds[1] += g1 * xh1;
+        ea.db[0] += g0;
+        ea.db[1] += g1;
+        const float gx0 = g0 * ex.sc[0], gx1 = g1 * ex.sc[1];
+        const float s1 = red32(gx0 + gx1) / 64.0f;
+        const float s2 = red32(gx0 * xh0 + gx1 * xh1) / 64.0f;
+        *dst0 = rstd * ((gx0 - s1) - xh0 * s2);
+        *dst1 = rstd * ((gx1 - s1) - xh1 * s2);
+      }
+    }
+    if constexpr (EPI == dgppo::kEpiLnFwd) {
+      const int row = m0 + (i & 3) + 8 * ((i & 15) >> 2) + 4 * h;
+      if (i < 16 && row < p.M) {
+        p.ln_mean[row] = mo;
+        p.ln_rstd[row] = ro;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
     const int col = col0 + 32 * t + i;
@@ -254,13 +364,41 @@ __device__ __forceinline__ void epi_store(const dgppo_gemm_args& p, float* C, co
         float v = __builtin_fmaf(p.alpha, acc[t][r], bv[t]);
         if (EXTRA) v += xv[t][r];
         if (p.relu) v = v > 0.0f ? v : 0.0f;
+        if (EPI == dgppo::kEpiMask) v = ex.m[t][r] > 0.0f ? v : 0.0f;
         C[row_off(row, p.ldc, p.c_grp, p.c_gstride) + col] = v;
       }
     }
   }
 }
 
-template <int NTW, bool VEC, int EXTRA>
+// EPI 3 at kernel end: this workgroup's [dscale (64) | dbias (64)] partial row, halves then waves in fixed order
+// (red: >= 4 x 128 floats of the B staging area, free after the unit loop)
+template <int NTW, int EPI>
+__device__ __forceinline__ void epi_finish(const dgppo_gemm_args& p, EpiAcc<NTW>& ea, float* red, int i, int h,
+                                           int wave) {
+  if constexpr (EPI == dgppo::kEpiLnBwd) {
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      ea.ds[t] += __shfl_xor(ea.ds[t], 32, 64);
+      ea.db[t] += __shfl_xor(ea.db[t], 32, 64);
+    }
+    __syncthreads();  // every wave is done reading the staged B
+    if (h == 0) {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+        red[wave * 128 + 32 * t + i] = ea.ds[t];
+        red[wave * 128 + 64 + 32 * t + i] = ea.db[t];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const float v = ((red[threadIdx.x] + red[128 + threadIdx.x]) + red[256 + threadIdx.x]) + red[384 + threadIdx.x];
+      p.ln_part[(int64_t)blockIdx.x * 128 + threadIdx.x] = v;
+    }
+  }
+}
+
+template <int NTW, bool VEC, int EXTRA, int EPI = 0>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int ncg) {
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
   const int NC = 32 * NTW * ncg, NP = NC + 1;
@@ -336,6 +474,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
   __syncthreads();
   float* C = p.C + (int64_t)b * p.stride_c;
   const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  EpiAcc<NTW> ea = {};
   for (; u < nunits; u += ustep) {
     const int panel = (int)(u / ncg), cg = (int)(u - (int64_t)panel * ncg);
     const int m0 = panel * 32;
@@ -346,7 +485,8 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
     const float* bcol = Bs + 8 * h * NP + cg * 32 * NTW + i;
     float bv[NTW], xv[NTW][16];
-    epi_load<NTW, EXTRA>(p, C, Dd, m0, cg * NTW * 32, i, h, bv, xv);
+    EpiX<NTW, EPI> ex;
+    epi_load<NTW, EXTRA, EPI>(p, C, Dd, m0, cg * NTW * 32, i, h, bv, xv, ex);
     bool rokn = false;
     const float* Arn = Ar;
     for (int c = 0; c < nch; ++c) {
@@ -369,8 +509,9 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
     Ar = Arn;
     rok = rokn;
     // epilogue: lane holds column (cg NTW + t) 32 + i, rows (r&3) + 8 (r>>2) + 4 h of the panel
-    epi_store<NTW, EXTRA>(p, C, acc, m0, cg * NTW * 32, i, h, bv, xv);
+    epi_store<NTW, EXTRA, EPI>(p, C, acc, m0, cg * NTW * 32, i, h, bv, xv, ex, ea);
   }
+  epi_finish<NTW, EPI>(p, ea, Bs, i, h, wave);
 }
 
 // ================================================================================================
@@ -380,7 +521,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(dgppo_gemm_args p, int n
 // K = 64) a wave owns one or two units, so the chunk-at-a-time pipeline above serialised NCH HBM round trips
 // per unit; here one round trip covers the unit and every wave's bytes are in flight together.
 // ================================================================================================
-template <int NTW, int NCH, int EXTRA>
+template <int NTW, int NCH, int EXTRA, int EPI = 0>
 __global__ __launch_bounds__(256) void gemm_rows_pf_kernel(dgppo_gemm_args p, int ncg) {
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
   const int NC = 32 * NTW * ncg, NP = NC + 1;
@@ -444,12 +585,14 @@ __global__ __launch_bounds__(256) void gemm_rows_pf_kernel(dgppo_gemm_args p, in
   __syncthreads();
   float* C = p.C + (int64_t)b * p.stride_c;
   const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  EpiAcc<NTW> ea = {};
   for (; u < nunits; u += ustep) {
     const int panel = (int)(u / ncg), cg = (int)(u - (int64_t)panel * ncg);
     const int m0 = panel * 32;
     // this unit's epilogue operands are requested before the next unit's prefetch (epi_load)
     float bv[NTW], xv[NTW][16];
-    epi_load<NTW, EXTRA>(p, C, Dd, m0, cg * NTW * 32, i, h, bv, xv);
+    EpiX<NTW, EPI> ex;
+    epi_load<NTW, EXTRA, EPI>(p, C, Dd, m0, cg * NTW * 32, i, h, bv, xv, ex);
     bool rokn;
     const float* Arn = row_ptr(u + ustep, rokn);
     load_unit(Arn, rokn, a1);  // the next unit's bytes are in flight during this unit's MFMAs and stores
@@ -469,7 +612,7 @@ __global__ __launch_bounds__(256) void gemm_rows_pf_kernel(dgppo_gemm_args p, in
         for (int t = 0; t < NTW; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[c][q], brow[q * NP + 32 * t], acc[t], 0, 0, 0);
     }
-    epi_store<NTW, EXTRA>(p, C, acc, m0, cg * NTW * 32, i, h, bv, xv);
+    epi_store<NTW, EXTRA, EPI>(p, C, acc, m0, cg * NTW * 32, i, h, bv, xv, ex, ea);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -477,6 +620,7 @@ __global__ __launch_bounds__(256) void gemm_rows_pf_kernel(dgppo_gemm_args p, in
     Ar = Arn;
     rok = rokn;
   }
+  epi_finish<NTW, EPI>(p, ea, Bs, i, h, wave);
 }
 
 // ================================================================================================
@@ -485,7 +629,7 @@ __global__ __launch_bounds__(256) void gemm_rows_pf_kernel(dgppo_gemm_args p, in
 // registers, so the main loop issues MFMAs fed by the streamed A chunks and registers only (no LDS
 // read per MFMA).  Same unit walk, A chunk pipeline and epilogue as gemm_rows_kernel.
 // ================================================================================================
-template <int NTW, int NCH, int EXTRA>
+template <int NTW, int NCH, int EXTRA, int EPI = 0>
 __global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) {
   extern __shared__ __attribute__((aligned(16))) float Bs[];  // [K16][NP] k-major
   constexpr int NC = 32 * NTW, NP = NC + 1, K16 = 16 * NCH;
@@ -551,10 +695,12 @@ __global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) 
       for (int t = 0; t < NTW; ++t) bf[c][q][t] = Bs[(16 * c + 8 * h + q) * NP + 32 * t + i];
   float* C = p.C + (int64_t)b * p.stride_c;
   const float* Dd = p.addend ? p.addend + (int64_t)b * p.stride_add : nullptr;
+  EpiAcc<NTW> ea = {};
   for (; u < nunits; u += ustep) {
     const int m0 = (int)u * 32;
     float bv[NTW], xv[NTW][16];
-    epi_load<NTW, EXTRA>(p, C, Dd, m0, 0, i, h, bv, xv);
+    EpiX<NTW, EPI> ex;
+    epi_load<NTW, EXTRA, EPI>(p, C, Dd, m0, 0, i, h, bv, xv, ex);
     f32x16 acc[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
@@ -581,8 +727,9 @@ __global__ __launch_bounds__(256) void gemm_rows_breg_kernel(dgppo_gemm_args p) 
     }
     Ar = Arn;
     rok = rokn;
-    epi_store<NTW, EXTRA>(p, C, acc, m0, 0, i, h, bv, xv);
+    epi_store<NTW, EXTRA, EPI>(p, C, acc, m0, 0, i, h, bv, xv, ex, ea);
   }
+  epi_finish<NTW, EPI>(p, ea, Bs, i, h, wave);
 }
 
 // ================================================================================================
@@ -838,80 +985,126 @@ void rows_split(int N, int* ntw, int* ncg) {
   else { *ntw = 2; *ncg = (nt + 1) / 2; }
 }
 
-template <int NTW>
-void launch_rows_t(const dgppo_gemm_args* p, int ncg, hipStream_t s) {
-  const int K16 = (p->K + 15) & ~15;
-  const size_t lds = (size_t)K16 * (32 * NTW * ncg + 1) * sizeof(float);
-  const int64_t units = (int64_t)((p->M + 31) / 32) * ncg;
-  int per_cu = (int)((160 * 1024) / (lds > 0 ? lds : 1));
+// kernel choice, grid and dynamic LDS of a rows-path call (shared by the launch and dgppo_gemm_partial_rows)
+struct RowsPlan {
+  int ntw, ncg, K16, grid;
+  size_t lds;
+  bool vec, use_pf, use_breg;
+};
+RowsPlan rows_plan(const dgppo_gemm_args* p) {
+  RowsPlan r;
+  rows_split(p->N, &r.ntw, &r.ncg);
+  r.K16 = (p->K + 15) & ~15;
+  r.lds = (size_t)r.K16 * (32 * r.ntw * r.ncg + 1) * sizeof(float);
+  const int64_t units = (int64_t)((p->M + 31) / 32) * r.ncg;
+  int per_cu = (int)((160 * 1024) / (r.lds > 0 ? r.lds : 1));
   per_cu = per_cu < 1 ? 1 : per_cu > 5 ? 5 : per_cu;
   static int knob = -2;
   if (knob == -2) {
     const char* v = getenv("DGPPO_ROWS_WG_PER_CU");
     knob = v ? atoi(v) : -1;
   }
-  const bool vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
-                   (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
+  r.vec = (p->K % 8 == 0) && (p->lda % 4 == 0) && (((uintptr_t)p->A & 15) == 0) &&
+          (p->a_grp <= 0 || p->a_gstride % 4 == 0) && (p->stride_a % 4 == 0);
   // kernel choice and workgroups per CU, measured on the update's shapes (scripts/ab_gemm_pf.sh,
   // profiles/r03_gemm_rows_ab.txt, 131072 rows): the whole-unit prefetch form wins for K <= 32 and for N > 64
   // (N99 K32 35.7 -> 27.8 us, N64 K32 + addend 39.8 -> 22.4, N192 K32 52.4 -> 41.3, N192 K64 68.8 -> 63.9) at 3
   // workgroups per CU; the B-in-registers form stays best for N <= 64, K = 64 at 2 (28.0 -> 24.4-24.8 us)
   static const int pf = env_knob("DGPPO_ROWS_PF", 1);
   static const int breg = env_knob("DGPPO_ROWS_BREG", 1);
-  const bool use_pf = vec && pf && K16 <= 64 && (K16 <= 32 || ncg > 1 || !breg);
-  const bool use_breg = !use_pf && vec && breg && ncg == 1 && K16 <= 64;
-  if (use_pf && per_cu > 3) per_cu = 3;
-  if (use_breg && per_cu > 2) per_cu = 2;
+  r.use_pf = r.vec && pf && r.K16 <= 64 && (r.K16 <= 32 || r.ncg > 1 || !breg);
+  r.use_breg = !r.use_pf && r.vec && breg && r.ncg == 1 && r.K16 <= 64;
+  if (r.use_pf && per_cu > 3) per_cu = 3;
+  if (r.use_breg && per_cu > 2) per_cu = 2;
   if (knob > 0 && knob < per_cu) per_cu = knob;
   const int64_t want = (units + 3) / 4, cap = 256LL * per_cu;
-  const int grid = (int)(want < cap ? want : cap);
+  r.grid = (int)(want < cap ? want : cap);
+  if (r.grid < 1) r.grid = 1;
+  return r;
+}
+
+// EPI != 0 instantiates only the combinations the epilogue supports (LayerNorm: NTW 2, no beta C / addend;
+// relu mask: any NTW, beta C allowed, no addend)
+template <int EPI, int NTW, int EXTRA>
+constexpr bool epi_combo() {
+  return EPI == 0 || (EPI == dgppo::kEpiMask && (EXTRA == 0 || EXTRA == 2)) || (NTW == 2 && EXTRA == 0);
+}
+
+template <int NTW, int EPI>
+int launch_rows_t(const dgppo_gemm_args* p, const RowsPlan& r, hipStream_t s) {
   const int extra = (p->addend != nullptr ? 1 : 0) | (p->beta != 0.0f ? 2 : 0);
-  if (use_pf) {
-#define DG_PF(c)                                                                                               \
-  if (K16 == 16 * c) {                                                                                         \
-    switch (extra) {                                                                                           \
-      case 0: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 0>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); break; \
-      case 1: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 1>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); break; \
-      case 2: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 2>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); break; \
-      default: hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, 3>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg); \
-    }                                                                                                          \
-    return;                                                                                                    \
-  }
-    DG_PF(1) DG_PF(2) DG_PF(3) DG_PF(4)
+  const int ncg = r.ncg, grid = r.grid, K16 = r.K16;
+  const size_t lds = r.lds;
+  bool done = false;
+  if (r.use_pf) {
+#define DG_PF(c, x)                                                                                               \
+  if constexpr (epi_combo<EPI, NTW, x>())                                                                         \
+    if (!done && K16 == 16 * c && extra == x) {                                                                   \
+      hipLaunchKernelGGL((dgppo::gemm_rows_pf_kernel<NTW, c, x, EPI>), dim3(grid, 1, p->batch), dim3(256), lds, s, \
+                         *p, ncg);                                                                               \
+      done = true;                                                                                                \
+    }
+    DG_PF(1, 0) DG_PF(1, 1) DG_PF(1, 2) DG_PF(1, 3) DG_PF(2, 0) DG_PF(2, 1) DG_PF(2, 2) DG_PF(2, 3)
+    DG_PF(3, 0) DG_PF(3, 1) DG_PF(3, 2) DG_PF(3, 3) DG_PF(4, 0) DG_PF(4, 1) DG_PF(4, 2) DG_PF(4, 3)
 #undef DG_PF
-  }
-  if (use_breg) {
-#define DG_RB(c)                                                                                              \
-  if (K16 == 16 * c) {                                                                                        \
-    switch (extra) {                                                                                          \
-      case 0: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 0>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); break; \
-      case 1: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 1>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); break; \
-      case 2: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 2>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); break; \
-      default: hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, 3>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p); \
-    }                                                                                                         \
-    return;                                                                                                   \
-  }
-    DG_RB(1) DG_RB(2) DG_RB(3) DG_RB(4)
+  } else if (r.use_breg) {
+#define DG_RB(c, x)                                                                                                  \
+  if constexpr (epi_combo<EPI, NTW, x>())                                                                            \
+    if (!done && K16 == 16 * c && extra == x) {                                                                      \
+      hipLaunchKernelGGL((dgppo::gemm_rows_breg_kernel<NTW, c, x, EPI>), dim3(grid, 1, p->batch), dim3(256), lds, s, \
+                         *p);                                                                                        \
+      done = true;                                                                                                   \
+    }
+    DG_RB(1, 0) DG_RB(1, 1) DG_RB(1, 2) DG_RB(1, 3) DG_RB(2, 0) DG_RB(2, 1) DG_RB(2, 2) DG_RB(2, 3)
+    DG_RB(3, 0) DG_RB(3, 1) DG_RB(3, 2) DG_RB(3, 3) DG_RB(4, 0) DG_RB(4, 1) DG_RB(4, 2) DG_RB(4, 3)
 #undef DG_RB
-  }
-#define DG_R(v, x) \
-  if (vec == v && extra == x) hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, v, x>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, ncg);
-  DG_R(true, 0) DG_R(true, 1) DG_R(true, 2) DG_R(true, 3) DG_R(false, 0) DG_R(false, 1) DG_R(false, 2) DG_R(false, 3)
+  } else {
+#define DG_R(v, x)                                                                                                  \
+  if constexpr (epi_combo<EPI, NTW, x>())                                                                           \
+    if (!done && r.vec == v && extra == x) {                                                                        \
+      hipLaunchKernelGGL((dgppo::gemm_rows_kernel<NTW, v, x, EPI>), dim3(grid, 1, p->batch), dim3(256), lds, s, *p, \
+                         ncg);                                                                                      \
+      done = true;                                                                                                  \
+    }
+    DG_R(true, 0) DG_R(true, 1) DG_R(true, 2) DG_R(true, 3) DG_R(false, 0) DG_R(false, 1) DG_R(false, 2)
+    DG_R(false, 3)
 #undef DG_R
+  }
+  return done ? 0 : DGPPO_EINVAL;
 }
 
 int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {
-  int ntw, ncg;
-  rows_split(p->N, &ntw, &ncg);
-  switch (ntw) {
-    case 1: launch_rows_t<1>(p, ncg, s); return 0;
-    case 2: launch_rows_t<2>(p, ncg, s); return 0;
-    case 3: launch_rows_t<3>(p, ncg, s); return 0;
-    case 6: launch_rows_t<6>(p, ncg, s); return 0;
+  const RowsPlan r = rows_plan(p);
+  switch (p->epi) {
+    case 0:
+      switch (r.ntw) {
+        case 1: return launch_rows_t<1, 0>(p, r, s);
+        case 2: return launch_rows_t<2, 0>(p, r, s);
+        case 3: return launch_rows_t<3, 0>(p, r, s);
+        case 6: return launch_rows_t<6, 0>(p, r, s);
+      }
+      return DGPPO_EINVAL;
+    case dgppo::kEpiMask:
+      if (!p->mask || p->addend || p->relu) return DGPPO_EINVAL;
+      if (r.ntw == 1) return launch_rows_t<1, dgppo::kEpiMask>(p, r, s);
+      if (r.ntw == 2) return launch_rows_t<2, dgppo::kEpiMask>(p, r, s);
+      return DGPPO_EINVAL;
+    case dgppo::kEpiLnFwd:
+    case dgppo::kEpiLnBwd:
+      if (p->N != 64 || r.ntw != 2 || r.ncg != 1 || p->batch != 1 || p->addend || p->beta != 0.0f || p->relu ||
+          !p->ln_scale || !p->ln_bias || !p->ln_h || (p->epi == dgppo::kEpiLnFwd && (!p->ln_mean || !p->ln_rstd)) ||
+          (p->epi == dgppo::kEpiLnBwd && !p->ln_part))
+        return DGPPO_EINVAL;
+      return p->epi == dgppo::kEpiLnFwd ? launch_rows_t<2, dgppo::kEpiLnFwd>(p, r, s) : launch_rows_t<2, dgppo::kEpiLnBwd>(p, r, s);
   }
   return DGPPO_EINVAL;
 }
 }  // namespace
+
+extern "C" int64_t dgppo_gemm_partial_rows(const dgppo_gemm_args* p) {
+  if (!p || p->M < 1 || p->N < 1 || gemm_path(p) != kPathRows) return 0;
+  return rows_plan(p).grid;
+}
 
 extern "C" int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* p) {
   if (!p) return 0;
@@ -934,6 +1127,7 @@ extern "C" int dgppo_gemm(const dgppo_gemm_args* p, void* stream) {
   if (p->M == 0 || p->N == 0) return 0;
   if (!p->A || !p->B || !p->C) return DGPPO_EINVAL;
   if (p->bias_grad && gemm_path(p) != kPathWgrad) return DGPPO_EINVAL;
+  if (p->epi && gemm_path(p) != kPathRows) return DGPPO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const GemmPath path = gemm_path(p);
   if (path == kPathWgrad) {

@@ -44,9 +44,13 @@ GEMM_LOG = None  # set to a list to record (M, N, K, batch, ta, tb, split_k, has
 def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
          a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
          bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
-         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None):
+         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None, mask=None, ld_mask=None, ln=None):
     """C = alpha op(A) op(B) + beta C + bias + addend (see dgppo_gemm).  Element offsets/strides.
-    bias_grad (ta only): bias_grad = alpha colsum(B) + beta bias_grad, fused into the dW GEMM."""
+    bias_grad (ta only): bias_grad = alpha colsum(B) + beta bias_grad, fused into the dW GEMM.
+    mask: C = mask > 0 ? result : 0 (the ReLU backward fused into the epilogue, ABI 9 epi 1).
+    ln: LayerNorm(64) + ReLU epilogue (epi 2 / 3): dict(mode="fwd" | "bwd", scale, bias, h, mean, rstd,
+    dscale, dbias) -- fwd writes h (pre-LN rows), mean, rstd and C = y; bwd reads h, writes C = dx and
+    accumulates dscale / dbias (per-workgroup partials summed by dgppo_colsum)."""
     lib = _lib.load()
     _lib.require_gpu(C.device, "gemm")
     g = _lib.GemmArgs()
@@ -66,11 +70,26 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
         split_k = max(1, min(math.ceil(K / 512), 1024 // max(tiles, 1))) if K >= 2048 else 1
     g.split_k = int(split_k)
     g.bias_grad = _p(bias_grad)
+    part = None
+    if mask is not None:
+        g.epi, g.mask, g.ld_mask = 1, _p(mask), int(ld_mask if ld_mask is not None else N)
+    if ln is not None:
+        g.epi = 2 if ln["mode"] == "fwd" else 3
+        g.ln_scale, g.ln_bias, g.ln_h = _p(ln["scale"]), _p(ln["bias"]), _p(ln["h"])
+        if g.epi == 2:
+            g.ln_mean, g.ln_rstd = _p(ln["mean"]), _p(ln["rstd"])
+        else:
+            nrow = _lib.load().dgppo_gemm_partial_rows(ctypes.byref(g))
+            part = workspace(nrow * 128, C.device, "gemm_ln_part")
+            g.ln_part = _p(part)
     if GEMM_LOG is not None:
         GEMM_LOG.append((int(M), int(N), int(K), int(batch), int(ta), int(tb), int(split_k), bias is not None))
     nws = lib.dgppo_gemm_workspace_floats(ctypes.byref(g))
     g.workspace = _p(workspace(nws, C.device, "gemm")) if nws > 0 else None
     _chk(lib.dgppo_gemm(ctypes.byref(g), _stream(C)), "dgppo_gemm")
+    if part is not None:  # [dscale | dbias] partial rows -> += the LayerNorm parameter gradients
+        colsum(part, nrow, 64, ln["dscale"], ld=128, beta=1.0)
+        colsum(part, nrow, 64, ln["dbias"], ld=128, x_off=64, beta=1.0)
 
 
 def colsum(x, rows, cols, out, *, ld=None, grp=0, gs=0, x_off=0, alpha=1.0, beta=0.0):

@@ -21,6 +21,7 @@ Kernel-side parameter layouts (converted from / to the flax layout by `to_flax` 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -28,6 +29,10 @@ import torch
 
 from .. import ops
 from . import kernels as K
+
+# LayerNorm + ReLU of the MLP heads and the GNN layers' ReLU backward fused into the neighbouring GEMMs' epilogues
+# (gemm epi 1-3, ABI 9); DGPPO_FUSE_LN=0 runs the separate layernorm64 / relu_bwd kernels (A/B, parity tests)
+FUSE_LN = os.environ.get("DGPPO_FUSE_LN", "1") == "1"
 
 
 # ---- parameter space ------------------------------------------------------------------------
@@ -145,12 +150,15 @@ class Dense:
         K.gemm(x, self.W(), y, rows, self.d_out, self.d_in, bias=self.b(), relu=relu)
         return y
 
-    def bwd(self, x, dy, rows, need_dx=True, dx_out=None, accumulate=False):
+    def bwd(self, x, dy, rows, need_dx=True, dx_out=None, accumulate=False, mask=None, ln=None):
+        """dW, db += ...; returns dx.  mask: dx = mask > 0 ? dx : 0 (the input's ReLU backward, fused into the dx
+        GEMM); ln: the LayerNorm + ReLU backward of the layer that produced x (GEMM epilogue epi 3)."""
         K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0, bias_grad=self.b(True))
         if not need_dx:
             return None
         dx = dx_out if dx_out is not None else torch.empty((rows, self.d_in), device=dy.device)
-        K.gemm(dy, self.W(), dx, rows, self.d_in, self.d_out, tb=True, ldb=self.d_out, beta=1.0 if accumulate else 0.0)
+        K.gemm(dy, self.W(), dx, rows, self.d_in, self.d_out, tb=True, ldb=self.d_out, beta=1.0 if accumulate else 0.0,
+               mask=mask, ln=ln)
         return dx
 
 
@@ -180,11 +188,34 @@ class LayerNormReLU:
         return y, (x, y, mean, rstd)
 
     def bwd(self, cache, dy):
-        x, y, mean, rstd = cache
+        x, y, mean, rstd = cache[:4]
         dx = torch.empty_like(x)
         K.layernorm_bwd(x, y, dy, self.ps.view(self.name + ".scale"), mean, rstd, dx,
                         self.ps.view(self.name + ".scale", True), self.ps.view(self.name + ".bias", True))
         return dx
+
+    # ---- fused into the neighbouring GEMMs (gemm epilogues epi 2 / 3, DGPPO_FUSE_LN=0 keeps the kernels above) ----
+    def fwd_fused(self, dense: "Dense", x, rows):
+        """y = relu(LayerNorm(x W + b)) as ONE GEMM (its epilogue normalises each 64-wide row); the cache has the
+        unfused layout plus a marker, so bwd_args can hand the backward to the next GEMM's epilogue."""
+        dev = x.device
+        h = torch.empty((rows, self.F), device=dev)
+        y = torch.empty((rows, self.F), device=dev)
+        mean = torch.empty(rows, device=dev)
+        rstd = torch.empty(rows, device=dev)
+        K.gemm(x, dense.W(), y, rows, self.F, dense.d_in, bias=dense.b(),
+               ln=dict(mode="fwd", scale=self.ps.view(self.name + ".scale"), bias=self.ps.view(self.name + ".bias"),
+                       h=h, mean=mean, rstd=rstd))
+        return y, (h, y, mean, rstd, "fused")
+
+    def bwd_args(self, cache):
+        """The epi 3 argument dict for the GEMM that produces this LayerNorm's output gradient, or None when the
+        forward ran unfused (the epilogue recomputes the fused forward's statistics and ReLU gates bit for bit)."""
+        if len(cache) < 5:
+            return None
+        return dict(mode="bwd", scale=self.ps.view(self.name + ".scale"), bias=self.ps.view(self.name + ".bias"),
+                    h=cache[0], dscale=self.ps.view(self.name + ".scale", True),
+                    dbias=self.ps.view(self.name + ".bias", True))
 
 
 class MLPHead:
@@ -210,19 +241,34 @@ class MLPHead:
 
     def fwd(self, x):
         rows = x.shape[0]
+        if FUSE_LN and self.d0.d_out == 64 and self.d1.d_out == 64:  # Dense + LayerNorm + ReLU as one GEMM each
+            y0, c0 = self.ln0.fwd_fused(self.d0, x, rows)
+            y1, c1 = self.ln1.fwd_fused(self.d1, y0, rows)
+            return y1, (x, y0, c0, c1)
         h0 = self.d0.fwd(x, rows)
         y0, c0 = self.ln0.fwd(h0)
         h1 = self.d1.fwd(y0, rows)
         y1, c1 = self.ln1.fwd(h1)
         return y1, (x, y0, c0, c1)
 
-    def bwd(self, cache, dy, need_dx=True):
+    def ln1_bwd_args(self, cache):
+        """epi 3 arguments for the GEMM producing d(head output) (the GRU's input-gradient GEMM), or None."""
+        return self.ln1.bwd_args(cache[3])
+
+    def bwd(self, cache, dy, need_dx=True, dy_is_dh1=False, mask_input=False):
+        """dy = d(head output), or already d(Dense_1 output) when the producer fused LayerNorm_1's backward
+        (dy_is_dh1); mask_input: the head input is a ReLU output (the GNN's agent rows), so its ReLU backward is
+        fused into the input-gradient GEMM and the caller skips it."""
         x, y0, c0, c1 = cache
         rows = x.shape[0]
-        dh1 = self.ln1.bwd(c1, dy)
-        dy0 = self.d1.bwd(y0, dh1, rows)
-        dh0 = self.ln0.bwd(c0, dy0)
-        return self.d0.bwd(x, dh0, rows, need_dx)
+        dh1 = dy if dy_is_dh1 else self.ln1.bwd(c1, dy)
+        ln0 = self.ln0.bwd_args(c0)
+        if ln0 is not None:
+            dh0 = self.d1.bwd(y0, dh1, rows, ln=ln0)  # dx GEMM epilogue = LayerNorm_0 + ReLU backward
+        else:
+            dy0 = self.d1.bwd(y0, dh1, rows)
+            dh0 = self.ln0.bwd(c0, dy0)
+        return self.d0.bwd(x, dh0, rows, need_dx, mask=x if (mask_input and need_dx) else None)
 
 
 class GRUCell:
@@ -271,8 +317,9 @@ class GRUCell:
         K.gru_seq(True, Q, L, n, gi, self.v("Wh"), self.v("bhn"), h0, hs, hT=hT_out)
         return hs, (x, gi, hs, h0, Q, L, n)
 
-    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False):
-        """Backward of seq_fwd: accumulates dWi, dbi, dWh, dbhn; returns (dx, dh0)."""
+    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False, ln=None):
+        """Backward of seq_fwd: accumulates dWi, dbi, dWh, dbhn; returns (dx, dh0).  ln: epi 3 arguments of the
+        LayerNorm + ReLU that produced x (then dx is the gradient BEFORE that LayerNorm)."""
         x, gi, hs, h0, Q, L, n = cache
         rows, H, dev = Q * L, self.H, dhs.device
         dgi = torch.empty((rows, 3 * H), device=dev)
@@ -294,7 +341,7 @@ class GRUCell:
         dx = None
         if need_dx:
             dx = torch.empty_like(x)
-            K.gemm(dgi, self.v("Wi"), dx, rows, self.d_in, 3 * H, tb=True, ldb=3 * H)
+            K.gemm(dgi, self.v("Wi"), dx, rows, self.d_in, 3 * H, tb=True, ldb=3 * H, ln=ln)
         return dx, dh0
 
     def fwd(self, x, h, h_out=None):
@@ -474,10 +521,12 @@ class RNNStack:
             off += w
         return x, caches
 
-    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False):
-        """Backward of seq_fwd: returns (dx, dh0 (Q, W))."""
+    def seq_bwd(self, cache, dhs, need_dx=True, need_dh0=False, ln=None):
+        """Backward of seq_fwd: returns (dx, dh0 (Q, W)).  ln (the 1-layer GRU only; see fuses_ln): the input's
+        LayerNorm + ReLU backward fused into the input-gradient GEMM."""
         if self.simple:
-            return self.cells[0].seq_bwd(cache, dhs, need_dx=need_dx, need_dh0=need_dh0)
+            return self.cells[0].seq_bwd(cache, dhs, need_dx=need_dx, need_dh0=need_dh0, ln=ln)
+        assert ln is None, "LayerNorm-fused input gradient: 1-layer GRU only"
         if not self.cells:
             return (dhs if need_dx else None), (torch.zeros((dhs.shape[0], self.W), device=dhs.device)
                                                 if need_dh0 else None)
@@ -500,9 +549,9 @@ class RNNStack:
         y, c = self.seq_fwd(x, rows, 1, 1, h0=h, hT_out=h2)
         return y, h2, c
 
-    def bwd(self, cache, dy, need_dx=True):
+    def bwd(self, cache, dy, need_dx=True, ln=None):
         """returns (dx, dh)"""
-        return self.seq_bwd(cache, dy, need_dx=need_dx, need_dh0=True)
+        return self.seq_bwd(cache, dy, need_dx=need_dx, need_dh0=True, ln=ln)
 
 
 class GraphTransformer:
@@ -653,10 +702,12 @@ class GraphTransformer:
         x = xfull if xfull is not None else g.nodes
         return x, dict(lda=self.D, a_grp=g.n, a_gs=g.N * self.D)
 
-    def bwd(self, cache, dY, g: "GraphBatch"):
+    def bwd(self, cache, dY, g: "GraphBatch", masked=False, mask_dxa=False):
         """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, d xfull (G, N, D)
         when every node's row was given, else None; accumulates this layer's grads and, in agent mode
-        with `pre`, pre's Dense_4 grads from the transformed senders."""
+        with `pre`, pre's Dense_4 grads from the transformed senders.  masked: dY already carries this layer's
+        ReLU gate (its producer's GEMM epilogue applied it); mask_dxa: apply the previous layer's ReLU gate
+        (xa > 0) in the last GEMM that forms d xa, so the previous layer's bwd runs with masked=True."""
         xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull = cache
         G, N, n = g.G, g.N, g.n
         D, F, H, C = self.D, self.F, self.H, g.C
@@ -665,7 +716,8 @@ class GraphTransformer:
         HD, WQ = H * D, H * D + H
         dev = dY.device
         A, akw = self._rows_in(g, xa, xfull)
-        K.relu_bwd_(dY, Y)  # dY := dZ
+        if not masked:
+            K.relu_bwd_(dY, Y)  # dY := dZ
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
         K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)
@@ -722,7 +774,8 @@ class GraphTransformer:
         K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
         if dXa is not None:
             K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
-            K.gemm(dQB, QBW, dXa, R, D, WQ, tb=True, ldb=WQ, beta=1.0)  # d[qt | beta] / dx = QBW[:D]^T
+            K.gemm(dQB, QBW, dXa, R, D, WQ, tb=True, ldb=WQ, beta=1.0,  # d[qt | beta] / dx = QBW[:D]^T
+                   mask=xa if mask_dxa else None)
             return dXa
         if dXf is not None:  # the agents' rows also fed Dense_4 and the queries: added in place (row-grouped C)
             cg = dict(c_grp=n, c_gs=N * D, ldc=D, beta=1.0)
@@ -877,11 +930,13 @@ class GNN:
             caches.append(c)
         return Y, (caches, Zs)
 
-    def bwd(self, caches, dZ, g: GraphBatch):
+    def bwd(self, caches, dZ, g: GraphBatch, top_masked=False):
+        """top_masked: dZ already carries the last layer's ReLU gate (fused into its producer's GEMM)."""
         caches, Zs = caches
         G, N, n = g.G, g.N, g.n
         rows = G * N
         d = dZ
+        fused_in = False
         acc = None  # gradient of the never-receivers' lifted rows Z_i (rows, D_i), deep stacks only
         for i in range(len(self.layers) - 1, -1, -1):
             L = self.layers[i]
@@ -905,4 +960,6 @@ class GNN:
                 K.relu_bwd_(acc, Zs[1])
                 K.gemm(Zs[0], acc, P.v("Wu", True), P.D, P.F, rows, ta=True, beta=1.0, bias_grad=P.v("bu", True))
                 acc = None
-            d = L.bwd(caches[i], d, g)
+            last = i == len(self.layers) - 1
+            d = L.bwd(caches[i], d, g, masked=(top_masked if last else fused_in), mask_dxa=(i == 1 and FUSE_LN))
+            fused_in = i == 1 and FUSE_LN  # layer 0's dY got its ReLU gate in layer 1's d xa GEMM

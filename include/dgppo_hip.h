@@ -232,9 +232,22 @@ typedef struct dgppo_gemm_args {
   float* workspace;
   float* bias_grad;  /* trans_a && !trans_b only: bias_grad[n] = alpha * sum_k B[k][n] + beta * bias_grad[n]
                         (the dense layer's db fused into its dW = X^T dY), or NULL */
+  /* ABI 9: elementwise pass fused into the epilogue of the row-GEMM paths (!trans_a, N <= 192, K <= 256; else
+   * DGPPO_EINVAL).  epi 0: none.  1: relu mask, C = mask > 0 ? result : 0 (mask rows addressed like C with
+   * ld_mask; the ReLU backward of the layer that produced `mask`, nn/gnn.py:116).  2: LayerNorm(64) + ReLU
+   * forward (flax LayerNorm eps 1e-6 + relu, nn/mlp.py:20-30; N == 64, no beta / addend / relu): ln_h (M, 64)
+   * <- result, C <- relu(((ln_h - mean) rstd) ln_scale + ln_bias), ln_mean / ln_rstd (M) <- the row
+   * statistics.  3: its backward: the result is dy; with ln_h from epi 2, C <- dx and the per-workgroup
+   * partials [dscale (64) | dbias (64)] to ln_part (dgppo_gemm_partial_rows rows of 128; sum them). */
+  int32_t epi, pad3_;
+  const float* mask; int64_t ld_mask;
+  const float* ln_scale; const float* ln_bias;
+  float* ln_h; float* ln_mean; float* ln_rstd; float* ln_part;
 } dgppo_gemm_args;
 
 int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* args);
+/* rows of ln_part an epi 3 call writes (its workgroup count; 0 when the call is not on the row-GEMM paths) */
+int64_t dgppo_gemm_partial_rows(const dgppo_gemm_args* args);
 int dgppo_gemm(const dgppo_gemm_args* args, void* stream);
 
 /* GraphTransformer attention core (dgppo/nn/gnn.py:78-117 + jraph.segment_softmax/segment_sum),

@@ -12,5 +12,5 @@ echo "tests rc=$trc"
 wait $lp
 lrc=$?
 echo "long rc=$lrc"
-tail -5 gpurun_out/long_run_driver.log
+tail -n 5 gpurun_out/long_run_driver.log
 exit $(( trc != 0 ? trc : lrc ))
