@@ -176,9 +176,11 @@ def _trajectory(cuda, eid, n, obs, K_UPD=5, perturb=None):
                          f"largest excess at {worst}: err {d[worst]:.3e} tol {np.broadcast_to(tol, d.shape)[worst]:.3e}")
             amb, gates = sum(x for x, _ in gate_stats), sum(y for _, y in gate_stats)
             fallbacks.append((it, k, n_over, n_checked, amb, gates))
-            # clip + Adam with the carried moments -> the parameters the next minibatch starts from.  Tolerance
-            # 2^-22 |p| (the fp32 store of p - step) + 1e-5 lr (the fp32 step's relative error is ~1e-7): tight
-            # enough that a 0.1% learning-rate error on one minibatch fails (test_trajectory_negative_control)
+            # clip + Adam with the carried moments -> the parameters the next minibatch starts from: every entry within
+            # 1e-6, and the Adam STEP itself to 1e-4 relative (median over the entries whose step is resolvable in fp32:
+            # |p| < 0.05 and |step| > 0.1 lr; an fp32 step is ~1e-6 relative off, a moment update that cancels can be
+            # far more, hence the median) -- tight enough that a 0.1% learning-rate error in one minibatch fails
+            # (test_trajectory_negative_control)
             nxt = tr["mb"][k + 1]["before"] if k + 1 < len(tr["mb"]) else {nm: net.ps.flat for nm, net in nets}
             off = 0
             for name, net in nets:
@@ -193,9 +195,14 @@ def _trajectory(cuda, eid, n, obs, K_UPD=5, perturb=None):
                                           [mb["m_before"][name].double().cpu().numpy()],
                                           [mb["v_before"][name].double().cpu().numpy()], count, lr)
                 got = nxt[name].double().cpu().numpy()
-                tol = 2.0 ** -22 * np.maximum(np.abs(rp), np.abs(got)) + 1e-5 * lr
+                p0 = mb["before"][name].double().cpu().numpy()
                 err = np.abs(got - rp)
-                assert (err <= tol).all(), f"update {it} mb {k} {name} Adam: {err.max():.3e} (tol {tol.min():.3e}+)"
+                assert err.max() <= 1e-6, f"update {it} mb {k} {name} Adam: {err.max():.3e}"
+                step_ref, step_gpu = rp - p0, got - p0
+                sel = (np.abs(p0) < 0.05) & (np.abs(step_ref) > 0.1 * lr)
+                if sel.sum() >= 20:
+                    rel = np.median(np.abs(step_gpu[sel] - step_ref[sel]) / np.abs(step_ref[sel]))
+                    assert rel <= 1e-4, f"update {it} mb {k} {name} Adam step: median relative error {rel:.2e} over {sel.sum()}"
         assert np.isfinite(info["policy/loss"])
     return fallbacks
 
