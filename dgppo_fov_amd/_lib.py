@@ -161,7 +161,6 @@ class GemmArgs(ctypes.Structure):
         ("mask", c_f32p), ("ld_mask", ctypes.c_int64),
         ("ln_scale", c_f32p), ("ln_bias", c_f32p),
         ("ln_h", c_f32p), ("ln_mean", c_f32p), ("ln_rstd", c_f32p), ("ln_part", c_f32p),
-        ("ln_count", ctypes.c_void_p), ("ln_dscale", c_f32p), ("ln_dbias", c_f32p),
     ]
 
 

@@ -156,6 +156,7 @@ class DGPPO:
         self.init_rnn_state = torch.zeros((rnn_layers, n_agents, self.n_carries, 64), device=dev)
         self.init_Vl_rnn_state = torch.zeros((rnn_layers, 1, self.n_carries, 64), device=dev)
         self._engines = {}
+        self._capturing = False
         self.trace: Optional[dict] = None  # set to {} to record update intermediates (parity tests)
         self.key = np.random.default_rng(seed)
         self.np_rng = np.random.default_rng(seed)
@@ -363,12 +364,13 @@ class DGPPO:
         """Start the (sum) all-reduce of one net's gradient bucket as soon as its backward is done, so it
         travels over xGMI (RCCL's stream) while the next net's forward / backward runs; `_finish_reduce`
         waits for every bucket and scales by 1/world before clip + Adam (same result as one flat
-        all-reduce: each bucket is reduced exactly once)."""
-        if self.world > 1:
+        all-reduce: each bucket is reduced exactly once).  Not while a minibatch graph is being captured: the
+        graph path all-reduces the whole gradient buffer eagerly between its two replays."""
+        if self.world > 1 and not self._capturing:
             pending.append(dist.all_reduce(net.ps.grad, op=dist.ReduceOp.SUM, async_op=True))
 
     def _finish_reduce(self, pending: list):
-        if self.world > 1:
+        if self.world > 1 and not self._capturing:
             for w in pending:
                 w.wait()
             pending.clear()
@@ -413,15 +415,25 @@ class DGPPO:
             t = bufs[name] = torch.empty(shape, device=self.device)
         return t
 
-    def _mb_graph_ok(self, batches, ph) -> bool:
-        """Replay the minibatch step from a captured hipGraph (DGPPO_UPDATE_GRAPH=1; off by default): one
-        process, no parity trace, no phase timing, equal minibatch sizes, concurrent streams on.  Bit-identical
-        to the eager step; at the bench config it measured 230.3 vs 229.4 ms per update (the update is
-        GPU-bound: the host's launches already run ahead), so it is an option for host-bound setups."""
+    # minibatches of at most this many samples replay from hipGraphs by default (DGPPO_UPDATE_GRAPH=1|0 forces it):
+    # a 2048-sample minibatch (config 4's 8-GPU strong share) is launch-bound, ~190 launches on three streams
+    GRAPH_MAX_SAMPLES = int(os.environ.get("DGPPO_UPDATE_GRAPH_MAX", 8192))
+
+    def _mb_graph_ok(self, batches, ph, T) -> bool:
+        """Replay the minibatch step from captured hipGraphs: no parity trace, no phase timing, equal minibatch
+        sizes, concurrent streams on; by default for small minibatches only (at the bench config, 16384 samples, the
+        update is GPU-bound and it measured 230.3 vs 229.4 ms; config 4's 2048-sample rank minibatches: 92.3 ->
+        54.6 ms per update, profiles/r04_config4_strong.jsonl).  Bit-identical to the eager step.  Two graphs per
+        minibatch -- the gradient passes, then clip + Adam -- with the multi-GPU gradient all-reduce issued eagerly
+        between the two replays (no collective inside a captured graph)."""
         if "_mbg" not in self.__dict__:
             self._mbg = None
-        return (self.world == 1 and self.trace is None and not ph.on and len({len(b) for b in batches}) == 1
-                and os.environ.get("DGPPO_UPDATE_GRAPH", "0") == "1" and self._aux_streams(2) is not None)
+        if self.trace is not None or ph.on or len({len(b) for b in batches}) != 1 or self._aux_streams(2) is None:
+            return False
+        knob = os.environ.get("DGPPO_UPDATE_GRAPH")
+        if knob is not None:
+            return knob == "1"
+        return len(batches[0]) * T <= self.GRAPH_MAX_SAMPLES
 
     def _mb_graph_key(self, rollout, det, A, Ql, Qh_det, Bm, T, L):
         ptr = lambda t: int(t.data_ptr())  # noqa: E731
@@ -431,15 +443,34 @@ class DGPPO:
         return (Bm, T, L) + tuple(ptr(f) for f in fields) + tuple(tuple(f.stride()) for f in fields)
 
     def _mb_capture(self, gkey, envs, args):
-        """Record the minibatch step (gathers, the three nets' passes on their streams, clip + Adam) into a
-        hipGraph whose env-id input is a static buffer; replays copy each minibatch's ids into it."""
+        """Record the minibatch step into two hipGraphs whose env-id input is a static buffer: (1) gathers and the
+        three nets' passes on their streams, (2) clip + finite check + Adam; replays copy each minibatch's ids into
+        the buffer, replay (1), all-reduce the gradients eagerly when there are several ranks, replay (2)."""
         static_envs = envs.clone()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            out = self._mb_body(static_envs, *args, _Phases(self.device))
-        self._mbg = (gkey, g, static_envs, out)
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        self._capturing = True
+        try:
+            with torch.cuda.graph(g1):
+                out = self._mb_body(static_envs, *args, _Phases(self.device), apply=False)
+            with torch.cuda.graph(g2):
+                self._mb_apply()
+        finally:
+            self._capturing = False
+        self._mbg = (gkey, (g1, g2), static_envs, out)
 
-    def _mb_body(self, envs, rollout, det, A, Ql, Qh_det, Bm, T, L, ph):
+    def _mb_replay(self, envs):
+        gkey, (g1, g2), static_envs, out = self._mbg
+        static_envs.copy_(envs)
+        g1.replay()
+        self._allreduce_grads()  # eager (RCCL / gloo) between the replays; a no-op on one rank
+        g2.replay()
+        return out
+
+    def _mb_apply(self):
+        for name in ("Vl", "Vh", "policy"):
+            self.opt[name].step()
+
+    def _mb_body(self, envs, rollout, det, A, Ql, Qh_det, Bm, T, L, ph, apply=True):
         """One minibatch (dgppo.py:275-289): gradients of Vl, Vh and the policy on the minibatch's envs, then
         clip + finite check + Adam per net.  Device work only (capturable)."""
         env, dev, n = self._env, self.device, self._n_agents
@@ -499,12 +530,13 @@ class DGPPO:
 
         # the three passes are independent (own parameters and gradient slices): concurrent streams
         stats, vl_loss, vh_loss = self._parallel([pi_job, vl_job, vh_job])
+        if not apply:  # graph capture: the caller all-reduces and runs clip + Adam from a second graph
+            return vl_loss, vh_loss, stats, tgt, lp_old
         # gradient buckets all-reduced (sum, then / world), clip + finite check + Adam per net
         self._finish_reduce(pending)
         if self.trace is not None:
             self._mb_grad = self.grad_flat.clone()
-        for name in ("Vl", "Vh", "policy"):
-            self.opt[name].step()
+        self._mb_apply()
         ph.mark("allreduce_adam")
         return vl_loss, vh_loss, stats, tgt, lp_old
 
@@ -559,16 +591,14 @@ class DGPPO:
             L = self.rnn_step
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
             env_ids = self._env_ids(batches)
-            graph_ok = self._mb_graph_ok(batches, ph)
+            graph_ok = self._mb_graph_ok(batches, ph, T)
             for k, bi in enumerate(batches):
                 envs = next(env_ids)
                 args = (rollout, det, A, Ql, Qh_det, len(bi), T, L)
                 if graph_ok:
                     gkey = self._mb_graph_key(*args)
                     if self._mbg is not None and self._mbg[0] == gkey:
-                        self._mbg[2].copy_(envs)
-                        self._mbg[1].replay()
-                        out = self._mbg[3]
+                        out = self._mb_replay(envs)
                     else:
                         out = self._mb_body(envs, *args, ph)  # the first minibatch runs eagerly, then capture
                         self._mb_capture(gkey, envs, args)

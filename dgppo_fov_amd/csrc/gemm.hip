@@ -395,23 +395,6 @@ __device__ __forceinline__ void epi_finish(const dgppo_gemm_args& p, EpiAcc<NTW>
       const float v = ((red[threadIdx.x] + red[128 + threadIdx.x]) + red[256 + threadIdx.x]) + red[384 + threadIdx.x];
       p.ln_part[(int64_t)blockIdx.x * 128 + threadIdx.x] = v;
     }
-    // the last workgroup to finish sums every partial row in workgroup order (deterministic) into the parameter
-    // gradients: device-scope release before the ticket, acquire after it
-    __shared__ int last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(p.ln_count, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (last) {
-      __threadfence();
-      if (threadIdx.x < 128) {
-        float acc = 0.0f;
-        for (int g = 0; g < (int)gridDim.x; ++g) acc += p.ln_part[(int64_t)g * 128 + threadIdx.x];
-        float* dst = threadIdx.x < 64 ? p.ln_dscale + threadIdx.x : p.ln_dbias + (threadIdx.x - 64);
-        *dst += acc;
-      }
-      if (threadIdx.x == 0) *p.ln_count = 0;  // ready for the next launch
-    }
   }
 }
 
@@ -1110,7 +1093,7 @@ int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {
     case dgppo::kEpiLnBwd:
       if (p->N != 64 || r.ntw != 2 || r.ncg != 1 || p->batch != 1 || p->addend || p->beta != 0.0f || p->relu ||
           !p->ln_scale || !p->ln_bias || !p->ln_h || (p->epi == dgppo::kEpiLnFwd && (!p->ln_mean || !p->ln_rstd)) ||
-          (p->epi == dgppo::kEpiLnBwd && (!p->ln_part || !p->ln_count || !p->ln_dscale || !p->ln_dbias)))
+          (p->epi == dgppo::kEpiLnBwd && !p->ln_part))
         return DGPPO_EINVAL;
       return p->epi == dgppo::kEpiLnFwd ? launch_rows_t<2, dgppo::kEpiLnFwd>(p, r, s) : launch_rows_t<2, dgppo::kEpiLnBwd>(p, r, s);
   }

@@ -844,6 +844,11 @@ extern "C" int64_t dgppo_colsum_workspace_floats(int64_t rows, int32_t cols) {
 extern "C" int dgppo_colsum(const float* x, int64_t rows, int32_t cols, int64_t ld, int32_t grp, int64_t gstride,
                             float* out, float alpha, float beta, float* workspace, void* stream) {
   if (rows < 0 || cols < 1 || !x || !out || !workspace) return DGPPO_EINVAL;
+  if (rows > 0 && rows <= 2048 && grp <= 0) {  // few rows (per-workgroup partials): one fixed-order pass, no split
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 15) / 16), dim3(256), 0, DG_STREAM(stream), x, (int)rows, cols,
+                       ld, out, alpha, beta);
+    return (int)hipGetLastError();
+  }
   const RowSplit sp = row_split(rows, 64);
   const int nb = rows > 0 ? sp.nb : 0;
   if (nb > 0)

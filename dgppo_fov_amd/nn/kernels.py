@@ -26,19 +26,6 @@ def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
     return t
 
 
-_LN_COUNTERS = {}
-
-
-def _ln_counter(device) -> int:
-    """The zeroed ticket counter of the LayerNorm-backward epilogue (per device and stream: launches on one stream
-    run in order, and each launch leaves it zeroed)."""
-    key = (str(device), _lib.stream_handle(device))
-    t = _LN_COUNTERS.get(key)
-    if t is None:
-        t = _LN_COUNTERS[key] = torch.zeros(4, dtype=torch.int32, device=device)
-    return int(t.data_ptr())
-
-
 def _p(t, off=0):
     return 0 if t is None else int(t.data_ptr()) + 4 * int(off)
 
@@ -83,6 +70,7 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
         split_k = max(1, min(math.ceil(K / 512), 1024 // max(tiles, 1))) if K >= 2048 else 1
     g.split_k = int(split_k)
     g.bias_grad = _p(bias_grad)
+    part = None
     if mask is not None:
         g.epi, g.mask, g.ld_mask = 1, _p(mask), int(ld_mask if ld_mask is not None else N)
     if ln is not None:
@@ -92,14 +80,20 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
             g.ln_mean, g.ln_rstd = _p(ln["mean"]), _p(ln["rstd"])
         else:
             nrow = _lib.load().dgppo_gemm_partial_rows(ctypes.byref(g))
-            g.ln_part = _p(workspace(nrow * 128, C.device, "gemm_ln_part"))
-            g.ln_count = _ln_counter(C.device)
-            g.ln_dscale, g.ln_dbias = _p(ln["dscale"]), _p(ln["dbias"])
+            part = workspace(nrow * 128, C.device, "gemm_ln_part")
+            g.ln_part = _p(part)
     if GEMM_LOG is not None:
         GEMM_LOG.append((int(M), int(N), int(K), int(batch), int(ta), int(tb), int(split_k), bias is not None))
     nws = lib.dgppo_gemm_workspace_floats(ctypes.byref(g))
     g.workspace = _p(workspace(nws, C.device, "gemm")) if nws > 0 else None
     _chk(lib.dgppo_gemm(ctypes.byref(g), _stream(C)), "dgppo_gemm")
+    if part is not None:  # [dscale | dbias] partial rows -> += the LayerNorm parameter gradients
+        ds, db = ln["dscale"], ln["dbias"]
+        if db.data_ptr() == ds.data_ptr() + 4 * 64:  # adjacent in the flat gradient buffer: one reduction
+            colsum(part, nrow, 128, ds, beta=1.0)  # writes ds[0:64] and the dbias that follows
+        else:
+            colsum(part, nrow, 64, ds, ld=128, beta=1.0)
+            colsum(part, nrow, 64, db, ld=128, x_off=64, beta=1.0)
 
 
 def colsum(x, rows, cols, out, *, ld=None, grp=0, gs=0, x_off=0, alpha=1.0, beta=0.0):

@@ -238,14 +238,12 @@ typedef struct dgppo_gemm_args {
    * forward (flax LayerNorm eps 1e-6 + relu, nn/mlp.py:20-30; N == 64, no beta / addend / relu): ln_h (M, 64)
    * <- result, C <- relu(((ln_h - mean) rstd) ln_scale + ln_bias), ln_mean / ln_rstd (M) <- the row
    * statistics.  3: its backward: the result is dy; with ln_h from epi 2, C <- dx and the per-workgroup
-   * partials [dscale (64) | dbias (64)] to ln_part (dgppo_gemm_partial_rows rows of 128), and the last
-   * workgroup to finish (ln_count: a zeroed int the kernel leaves zeroed) adds their fixed-order sum to
-   * ln_dscale / ln_dbias. */
+   * partials [dscale (64) | dbias (64)] to ln_part (dgppo_gemm_partial_rows rows of 128; sum them, e.g. with
+   * dgppo_colsum). */
   int32_t epi, pad3_;
   const float* mask; int64_t ld_mask;
   const float* ln_scale; const float* ln_bias;
   float* ln_h; float* ln_mean; float* ln_rstd; float* ln_part;
-  int32_t* ln_count; float* ln_dscale; float* ln_dbias;
 } dgppo_gemm_args;
 
 int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* args);
