@@ -328,7 +328,28 @@ class DGPPO:
         B, T = rollout.rewards.shape
         Vl = torch.empty((B, T + 1), device=self.device)
         hT_all = torch.empty((B, self.Vl.carry_width), device=self.device)
-        for e0 in range(0, B, chunk):
+        tm = self._time_major(rollout, self._rows) if hasattr(self.Vl, "graph_means") else None
+        if tm is not None:
+            # the GNN + agent mean over the time-major graphs in place (whole time steps per chunk; graphs are
+            # independent), then head + GRU scan per env sequence from the (B, T, 64) means: bit-identical to
+            # env-chunked graph copies, without copying the graphs
+            (nodes, edges, recv, send), _ = tm
+            zm = torch.empty((T, B, 64), device=self.device)
+            tc = max(1, (chunk * T) // B)
+            for t0 in range(0, T, tc):
+                t1 = min(T, t0 + tc)
+                G = (t1 - t0) * B
+                g = GraphBatch(nodes[t0:t1].reshape(G, *nodes.shape[2:]), edges[t0:t1].reshape(G, *edges.shape[2:]),
+                               recv[t0:t1].reshape(G, -1), send[t0:t1].reshape(G, -1), self._n_agents,
+                               self._env.agent_candidates(self.device), raw_cols=self._env.nonagent_feature_cols)
+                self.Vl.graph_means(g, out=zm[t0:t1].view(G, 64))
+            zm_env = zm.transpose(0, 1).contiguous()  # (B, T, 64): rows e * T + t
+            for e0 in range(0, B, chunk):
+                e1 = min(B, e0 + chunk)
+                v, hT, _ = self.Vl.seq_fwd(None, e1 - e0, T, keep_cache=False, zm=zm_env[e0:e1].view(-1, 64))
+                Vl[e0:e1, :T].copy_(v)
+                hT_all[e0:e1].copy_(hT)
+        for e0 in range(0, B, chunk) if tm is None else ():
             e1 = min(B, e0 + chunk)
             g = self._graphs(rollout.graph, slice(e0, e1))
             v, hT, _ = self.Vl.seq_fwd(g, e1 - e0, T, keep_cache=False)
@@ -339,11 +360,35 @@ class DGPPO:
         Vl[:, T].copy_(vf[:, 0])
         return Vl
 
+    @staticmethod
+    def _time_major(rollout: Rollout, rows_fn):
+        """(T, B, ...) contiguous views of the rollout's graph fields and carry rows when the Rollout is the
+        RolloutEngine's (B, T) view of its time-major buffers (else None): passes whose graphs are independent
+        (Vh: one GRU step per graph) then read the buffers in place instead of copying env chunks."""
+        g = rollout.graph
+        f = [x.transpose(0, 1) for x in (g.nodes, g.edges, g.receivers, g.senders)]
+        h = rows_fn(rollout.rnn_states).transpose(0, 1)
+        return (f, h) if all(x.is_contiguous() for x in f + [h]) else None
+
     def _vh_all(self, rollout: Rollout, chunk: int):
-        """Vh on every (env, t) graph with the stored actor carries, plus the final Vh (dgppo.py:218-228)."""
+        """Vh on every (env, t) graph with the stored actor carries, plus the final Vh (dgppo.py:218-228).  Graphs
+        are independent here, so the time-major rollout buffers are read in place, whole time steps at a time
+        (bit-identical to env chunks: no reduction crosses graphs)."""
         B, T, n = rollout.rewards.shape[0], rollout.rewards.shape[1], self._n_agents
         out = torch.empty((B, T + 1, n, self._env.n_cost), device=self.device)
-        for e0 in range(0, B, chunk):
+        tm = self._time_major(rollout, self._rows)
+        if tm is not None:
+            (nodes, edges, recv, send), hrows = tm
+            tc = max(1, (chunk * T) // B)
+            for t0 in range(0, T, tc):
+                t1 = min(T, t0 + tc)
+                G = (t1 - t0) * B
+                g = GraphBatch(nodes[t0:t1].reshape(G, *nodes.shape[2:]), edges[t0:t1].reshape(G, *edges.shape[2:]),
+                               recv[t0:t1].reshape(G, -1), send[t0:t1].reshape(G, -1), n,
+                               self._env.agent_candidates(self.device), raw_cols=self._env.nonagent_feature_cols)
+                v, _ = self.Vh.fwd(g, hrows[t0:t1].reshape(G * n, -1), keep_cache=False)
+                out[:, t0:t1].copy_(v.view(t1 - t0, B, n, -1).transpose(0, 1))
+        for e0 in range(0, B, chunk) if tm is None else ():
             e1 = min(B, e0 + chunk)
             g = self._graphs(rollout.graph, slice(e0, e1))
             h = self._rows(rollout.rnn_states[e0:e1]).reshape((e1 - e0) * T * n, -1).contiguous()

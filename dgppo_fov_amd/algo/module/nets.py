@@ -224,14 +224,28 @@ class VlNet(_Net):
         self.gnn.load_flax(d["gnn"]), self.head.load_flax(d["head"]), self.gru.load_flax(d["gru"])
         self.out.load_flax(d["out"])
 
-    def seq_fwd(self, g: GraphBatch, S: int, L: int, h0=None, keep_cache=True):
+    def graph_means(self, g: GraphBatch, out=None):
+        """The GNN part of the value: the agent mean of the last GNN layer's agent rows, (G, 64) (graphs are
+        independent here; seq_fwd's sequence structure starts after it)."""
+        z, _ = self.gnn.fwd(g)
+        zm = out if out is not None else torch.empty((g.G, 64), device=g.nodes.device)
+        K.agent_mean_fwd(z, zm, g.G, self.n, 64, self.n * 64)
+        return zm
+
+    def seq_fwd(self, g: GraphBatch, S: int, L: int, h0=None, keep_cache=True, zm=None):
         """scan_Vl (informarl.py:281-293) over S sequences of L graphs.  Returns values (S, L),
-        final carries (S, 64) and the cache for seq_bwd."""
-        n, dev = self.n, g.nodes.device
+        final carries (S, 64) and the cache for seq_bwd.  zm: the graphs' agent means already computed
+        (graph_means, rows s * L + t; forward only, g unused)."""
+        dev = self.ps.flat.device
         G = S * L
-        z, gc = self.gnn.fwd(g)  # (G*n, 64)
-        zm = torch.empty((G, 64), device=dev)
-        K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
+        if zm is not None:
+            assert not keep_cache, "seq_fwd from precomputed agent means is forward-only"
+            z = gc = None
+        else:
+            n = self.n
+            z, gc = self.gnn.fwd(g)  # (G*n, 64)
+            zm = torch.empty((G, 64), device=dev)
+            K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
         y, hc = self.head.fwd(zm)
         hT = torch.empty((S, self.gru.W), device=dev)
         Hs, gcs = self.gru.seq_fwd(y, S, L, 1, h0=h0, hT_out=hT)
