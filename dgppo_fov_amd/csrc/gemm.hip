@@ -218,14 +218,16 @@ constexpr int kRowsLdsFloats = 12800;  // 50 KB: K16 * (N + 1) must fit
 //   2 LayerNorm(64) + ReLU forward (flax LayerNorm eps 1e-6, nn/mlp.py:20-30): h = the GEMM result is stored to ln_h,
 //     y = relu(((h - mean) rstd) scale + bias) to C, the row mean / rstd to ln_mean / ln_rstd (a wave owns whole
 //     64-wide rows: NTW = 2, one column group)
-//   3 LayerNorm(64) + ReLU backward: the GEMM result is dy; with h from ln_h the row statistics and the ReLU gate
-//     are recomputed by the same instruction sequence as EPI 2 (bit-identical decisions), dx goes to C and the
-//     workgroup's [dscale | dbias] column partials to ln_part (dgppo_gemm_partial_rows rows; the host sums them)
+//   3 LayerNorm(64) + ReLU backward: the GEMM result is dy; h from ln_h and the row mean / rstd EPI 2 stored in
+//     ln_mean / ln_rstd give the ReLU gate by the same instruction sequence as EPI 2 (bit-identical decisions;
+//     no statistics are recomputed), dx goes to C and the workgroup's [dscale | dbias] column partials to ln_part
+//     (dgppo_gemm_partial_rows rows; the host sums them)
 constexpr int kEpiMask = 1, kEpiLnFwd = 2, kEpiLnBwd = 3;
 template <int NTW, int EPI>
 struct EpiX {
   float m[(EPI == dgppo::kEpiMask || EPI == dgppo::kEpiLnBwd) ? NTW : 1][16];  // mask rows (1) / pre-LN rows (3)
   float sc[NTW], bi[NTW];                                        // LayerNorm scale / bias at this lane's columns
+  float mo, ro;  // EPI 3: the forward's mean / rstd of register row (lane & 15) of this lane's half-wave
 };
 template <int NTW>
 struct EpiAcc {  // EPI 3: this lane's column partials of dscale / dbias over the rows it has stored
@@ -260,6 +262,12 @@ template <int NTW, int EXTRA, int EPI>
 __device__ __forceinline__ void epi_load(const dgppo_gemm_args& p, const float* C, const float* Dd, int m0, int col0,
                                          int i, int h, float (&bv)[NTW], float (&xv)[NTW][16], EpiX<NTW, EPI>& ex) {
 #pragma clang fp contract(off)  // epi_combine's roundings
+  if (EPI == dgppo::kEpiLnBwd) {  // lane i of a half-wave fetches register row (i & 15)'s statistics
+    const int row = m0 + (i & 3) + 8 * ((i & 15) >> 2) + 4 * h;
+    const bool ok = row < p.M;
+    ex.mo = *(ok ? p.ln_mean + row : (const float*)g_zero_row);
+    ex.ro = *(ok ? p.ln_rstd + row : (const float*)g_zero_row);
+  }
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
     const int col = col0 + 32 * t + i;
@@ -326,8 +334,7 @@ __device__ __forceinline__ void epi_store(const dgppo_gemm_args& p, float* C, co
         ro = i == r ? rstd : ro;
       } else {
         const float hv0 = ex.m[0][r], hv1 = ex.m[1][r];
-        float mean, rstd;
-        ln_stats(hv0, hv1, mean, rstd);
+        const float mean = __shfl(ex.mo, r, 32), rstd = __shfl(ex.ro, r, 32);  // lane r of this half
         const float dy0 = rok ? __builtin_fmaf(p.alpha, acc[0][r], bv[0]) : 0.0f;
         const float dy1 = rok ? __builtin_fmaf(p.alpha, acc[1][r], bv[1]) : 0.0f;
         const float g0 = ln_pre(hv0, mean, rstd, ex.sc[0], ex.bi[0]) > 0.0f ? dy0 : 0.0f;
@@ -1092,7 +1099,7 @@ int launch_rows(const dgppo_gemm_args* p, hipStream_t s) {
     case dgppo::kEpiLnFwd:
     case dgppo::kEpiLnBwd:
       if (p->N != 64 || r.ntw != 2 || r.ncg != 1 || p->batch != 1 || p->addend || p->beta != 0.0f || p->relu ||
-          !p->ln_scale || !p->ln_bias || !p->ln_h || (p->epi == dgppo::kEpiLnFwd && (!p->ln_mean || !p->ln_rstd)) ||
+          !p->ln_scale || !p->ln_bias || !p->ln_h || !p->ln_mean || !p->ln_rstd ||
           (p->epi == dgppo::kEpiLnBwd && !p->ln_part))
         return DGPPO_EINVAL;
       return p->epi == dgppo::kEpiLnFwd ? launch_rows_t<2, dgppo::kEpiLnFwd>(p, r, s) : launch_rows_t<2, dgppo::kEpiLnBwd>(p, r, s);

@@ -49,7 +49,7 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
     bias_grad (ta only): bias_grad = alpha colsum(B) + beta bias_grad, fused into the dW GEMM.
     mask: C = mask > 0 ? result : 0 (the ReLU backward fused into the epilogue, ABI 9 epi 1).
     ln: LayerNorm(64) + ReLU epilogue (epi 2 / 3): dict(mode="fwd" | "bwd", scale, bias, h, mean, rstd,
-    dscale, dbias) -- fwd writes h (pre-LN rows), mean, rstd and C = y; bwd reads h, writes C = dx and
+    dscale, dbias) -- fwd writes h (pre-LN rows), mean, rstd and C = y; bwd reads h, mean, rstd, writes C = dx and
     accumulates dscale / dbias (per-workgroup partials summed by dgppo_colsum)."""
     lib = _lib.load()
     _lib.require_gpu(C.device, "gemm")
@@ -76,9 +76,8 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
     if ln is not None:
         g.epi = 2 if ln["mode"] == "fwd" else 3
         g.ln_scale, g.ln_bias, g.ln_h = _p(ln["scale"]), _p(ln["bias"]), _p(ln["h"])
-        if g.epi == 2:
-            g.ln_mean, g.ln_rstd = _p(ln["mean"]), _p(ln["rstd"])
-        else:
+        g.ln_mean, g.ln_rstd = _p(ln["mean"]), _p(ln["rstd"])  # fwd writes them, bwd reads the fwd's
+        if g.epi == 3:
             nrow = _lib.load().dgppo_gemm_partial_rows(ctypes.byref(g))
             part = workspace(nrow * 128, C.device, "gemm_ln_part")
             g.ln_part = _p(part)

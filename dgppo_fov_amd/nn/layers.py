@@ -210,11 +210,11 @@ class LayerNormReLU:
 
     def bwd_args(self, cache):
         """The epi 3 argument dict for the GEMM that produces this LayerNorm's output gradient, or None when the
-        forward ran unfused (the epilogue recomputes the fused forward's statistics and ReLU gates bit for bit)."""
+        forward ran unfused (the epilogue reads the fused forward's h, mean and rstd and redoes its ReLU gates bit for bit)."""
         if len(cache) < 5:
             return None
         return dict(mode="bwd", scale=self.ps.view(self.name + ".scale"), bias=self.ps.view(self.name + ".bias"),
-                    h=cache[0], dscale=self.ps.view(self.name + ".scale", True),
+                    h=cache[0], mean=cache[2], rstd=cache[3], dscale=self.ps.view(self.name + ".scale", True),
                     dbias=self.ps.view(self.name + ".bias", True))
 
 

@@ -237,7 +237,8 @@ typedef struct dgppo_gemm_args {
    * ld_mask; the ReLU backward of the layer that produced `mask`, nn/gnn.py:116).  2: LayerNorm(64) + ReLU
    * forward (flax LayerNorm eps 1e-6 + relu, nn/mlp.py:20-30; N == 64, no beta / addend / relu): ln_h (M, 64)
    * <- result, C <- relu(((ln_h - mean) rstd) ln_scale + ln_bias), ln_mean / ln_rstd (M) <- the row
-   * statistics.  3: its backward: the result is dy; with ln_h from epi 2, C <- dx and the per-workgroup
+   * statistics.  3: its backward: the result is dy; with ln_h, ln_mean and ln_rstd as epi 2 wrote them (the
+   * ReLU gates are the forward's, bit for bit), C <- dx and the per-workgroup
    * partials [dscale (64) | dbias (64)] to ln_part (dgppo_gemm_partial_rows rows of 128; sum them, e.g. with
    * dgppo_colsum). */
   int32_t epi, pad3_;

@@ -49,7 +49,7 @@ def test_layernorm_epilogues(cuda, M, Kd):
     ds0, db0 = rng.standard_normal(64).astype(np.float32), rng.standard_normal(64).astype(np.float32)
     dx = torch.empty((M, 64), device=cuda)
     dsd, dbd = d(ds0.copy()), d(db0.copy())
-    K.gemm(d(G), d(Wg), dx, M, 64, Kg, tb=True, ldb=Kg, ln=dict(mode="bwd", scale=scd, bias=bid, h=h, dscale=dsd, dbias=dbd))
+    K.gemm(d(G), d(Wg), dx, M, 64, Kg, tb=True, ldb=Kg, ln=dict(mode="bwd", scale=scd, bias=bid, h=h, mean=mean, rstd=rstd, dscale=dsd, dbias=dbd))
     torch.cuda.synchronize()
     h32 = h.cpu().numpy().astype(np.float64)  # the kernel's own h (the gates follow the fp32 forward)
     y32, pre32, m32, r32 = _ln_ref(h32, sc, bi)
@@ -67,6 +67,14 @@ def test_layernorm_epilogues(cuda, M, Kd):
     slack_b = np.abs(dy * amb).sum(0)
     assert (np.abs(dsd.cpu().numpy() - (ds0 + (g * xh).sum(0))) <= 1e-4 * np.sqrt(M) + slack_s).all()
     assert (np.abs(dbd.cpu().numpy() - (db0 + g.sum(0))) <= 1e-4 * np.sqrt(M) + slack_b).all()
+    # the backward's ReLU gates are the forward's, bit for bit: with dy = 1 everywhere (G = ones, Wg = I) dbias
+    # counts the open gates per column, an exact integer in fp32, equal to the forward's (y > 0) count
+    dbd = torch.zeros(64, device=cuda)
+    K.gemm(torch.ones((M, 64), device=cuda), torch.eye(64, device=cuda), dx, M, 64, 64, tb=True, ldb=64,
+           ln=dict(mode="bwd", scale=scd, bias=bid, h=h, mean=mean, rstd=rstd, dscale=torch.zeros(64, device=cuda),
+                   dbias=dbd))
+    torch.cuda.synchronize()
+    assert torch.equal(dbd.cpu(), (y > 0).float().sum(0).cpu())
 
 
 @pytest.mark.parametrize("M,N,Kd,beta", [(1000, 64, 64, 0.0), (1000, 32, 99, 1.0), (500, 64, 32, 0.0), (300, 32, 192, 1.0)])
