@@ -194,6 +194,7 @@ class PolicyStepArgs(ctypes.Structure):
         ("std_shift", ctypes.c_float), ("std_min", ctypes.c_float),
         ("h_in", c_f32p), ("h_out", c_f32p), ("noise", c_f32p), ("action", c_f32p), ("log_pi", c_f32p),
         ("work", c_f32p),
+        ("noise_seed", c_f32p), ("noise_stream", ctypes.c_uint64),  # ABI 10: in-kernel noise (noise NULL)
     ]
 
 
@@ -308,7 +309,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 9  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 10  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

@@ -120,13 +120,17 @@ class ActorNet(_Net):
         return a
 
     def act(self, g: GraphBatch, h: torch.Tensor, mode: int, noise=None, action_out=None, log_pi_out=None,
-            h_out=None, prepare=True):
+            h_out=None, prepare=True, noise_seed=None, noise_stream=0):
         """One policy step for G graphs: mode 0 = deterministic (get_action: tanh(mean)),
         1 = sample_action with standard-normal `noise` (G*n, A).  Returns (action, log_pi, h_new).
         Runs the fused dgppo_policy_step kernel when it covers the configuration; `prepare` refreshes
-        its query-key products from the current weights (needed once after every weight change)."""
+        its query-key products from the current weights (needed once after every weight change).
+        noise_seed (a uint64 device scalar) + noise_stream: the noise is the Philox stream K.normal_ would write
+        into `noise` -- drawn inside the fused kernel (no separate launch), else written to `noise` first."""
         rows = g.G * self.n
         fa = self._fused_args(g)
+        if noise_seed is not None and mode == 1 and fa is None:
+            K.normal_(noise, stream_id=noise_stream, seed_tensor=noise_seed)
         if fa is not None:
             if prepare:
                 K._chk(_lib.load().dgppo_policy_prepare(ctypes.byref(fa), _lib.stream_handle(h.device)),
@@ -139,7 +143,11 @@ class ActorNet(_Net):
             fa.cand, fa.receivers, fa.senders = K._p(g.cand), K._p(g.receivers), K._p(g.senders)
             fa.nodes, fa.nodes_gstride = K._p(g.nodes), g.N * g.nodes.shape[2]
             fa.edges, fa.edges_gstride, fa.idx_gstride = K._p(g.edges), g.E * g.ED, g.E
-            fa.h_in, fa.h_out, fa.noise = K._p(h), K._p(h2), K._p(noise)
+            fa.h_in, fa.h_out = K._p(h), K._p(h2)
+            if noise_seed is not None and mode == 1:  # ABI 10: drawn in the kernel
+                fa.noise, fa.noise_seed, fa.noise_stream = None, K._p(noise_seed), int(noise_stream)
+            else:
+                fa.noise, fa.noise_seed, fa.noise_stream = K._p(noise), None, 0
             fa.action, fa.log_pi = K._p(action), K._p(log_pi)
             K._chk(_lib.load().dgppo_policy_step(ctypes.byref(fa), _lib.stream_handle(dev)), "dgppo_policy_step")
             return action, log_pi, h2

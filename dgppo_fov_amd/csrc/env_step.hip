@@ -3126,16 +3126,18 @@ extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_
   return (int)hipGetLastError();
 }
 
-// envs per workgroup of the persistent rollout (DGPPO_ROLLOUT_WPG = 1, 4 or 8, A/B knob; default 8).  Per
-// LidarSpread episode (reset + 128 steps, 4096 envs): 1 env 1.59 ms, 4 envs 1.37, 8 envs 1.34, 16 envs 1.41
-// (register spills); pooling the ray casts of more envs evens out their item counts between the barriers)
-static int rollout_wpg() {
-  static const int w = [] {
+// envs per workgroup of the persistent rollout (DGPPO_ROLLOUT_WPG = 1, 4 or 8 forces it).  Per LidarSpread
+// episode (reset + 128 steps, 4096 envs): 1 env 1.59 ms, 4 envs 1.37, 8 envs 1.34, 16 envs 1.41 (register
+// spills); pooling the ray casts of more envs evens out their item counts between the barriers.  Below 2048
+// envs the grid, not the pooling, sets the pace: LidarBicycleTarget at 512 envs (config 4's 8-GPU share)
+// 8 envs 0.959 ms, 4 envs 0.838, 1 env 0.894 -- so 4 there.
+static int rollout_wpg(int64_t n_env) {
+  static const int forced = [] {
     const char* e = getenv("DGPPO_ROLLOUT_WPG");
-    const int v = e ? atoi(e) : 8;
-    return v == 1 || v == 4 ? v : 8;
+    const int v = e ? atoi(e) : 0;
+    return v == 1 || v == 4 || v == 8 ? v : 0;
   }();
-  return w;
+  return forced ? forced : (n_env >= 2048 ? 8 : 4);
 }
 
 template <int ENGINE, int GOAL, int SD, int WPG>
@@ -3147,7 +3149,7 @@ static void launch_rollout_w(const dgppo_env_cfg& c, const dgppo_env_rollout_io&
 
 template <int ENGINE, int GOAL, int SD>
 static void launch_rollout(const dgppo_env_cfg& c, const dgppo_env_rollout_io& r, hipStream_t s) {
-  const int w = rollout_wpg();
+  const int w = rollout_wpg(r.step.n_env);
   if (w == 4) launch_rollout_w<ENGINE, GOAL, SD, 4>(c, r, s);
   else if (w == 8) launch_rollout_w<ENGINE, GOAL, SD, 8>(c, r, s);
   else launch_rollout_w<ENGINE, GOAL, SD, 1>(c, r, s);

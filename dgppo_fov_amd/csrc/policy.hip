@@ -32,6 +32,7 @@
 
 #include "../../include/dgppo_hip.h"
 #include "lanes.h"
+#include "noise.h"
 
 namespace dgppo {
 namespace {
@@ -694,7 +695,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
     if (threadIdx.x < 2 * A) L.outW[kHid * 2 * A + threadIdx.x] = threadIdx.x < A ? p.bm[threadIdx.x] : p.bsd[threadIdx.x - A];
   }
   const int tr = threadIdx.x >> 3, tq = threadIdx.x & 7;  // tail: row, action lane
-  const float nz = (p.mode == 1 && tr < rows && tq < A) ? p.noise[(row0 + tr) * A + tq] : 0.0f;
+  const bool nz_own = p.mode == 1 && tr < rows && tq < A;
+  const float nz = (nz_own && p.noise) ? p.noise[(row0 + tr) * A + tq] : 0.0f;  // else drawn at the tail
   // ---- level 2: resolve the (row, candidate) pairs
   {
     int rc[kPT], sd[kPT];
@@ -862,7 +864,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
       sraw += L.outW[kHid * 2 * A + A + tq];
     }
     const float sd = softplusf(sraw + p.std_shift) + p.std_min;
-    const float act = p.mode == 1 ? tanhf(mu + sd * nz) : tanhf(mu);
+    // in-kernel noise (noise == NULL): the same Philox element dgppo_normal would have written
+    const float nzv = (nz_own && !p.noise) ? noise::normal_at((int64_t)(row0 + tr) * A + tq, *p.noise_seed, p.noise_stream)
+                                           : nz;
+    const float act = p.mode == 1 ? tanhf(mu + sd * nzv) : tanhf(mu);
     constexpr float kThr = 0.999f;
     const float inv_t = atanhf(kThr), log_eps = logf(1.0f - kThr);
     const float v = fminf(fmaxf(act, -kThr), kThr);
@@ -935,7 +940,7 @@ extern "C" int dgppo_policy_prepare(const dgppo_policy_step_args* p, void* strea
 
 extern "C" int dgppo_policy_step(const dgppo_policy_step_args* p, void* stream) {
   if (!dgppo_policy_step_supported(p) || !p->cand || !p->nodes || !p->edges || !p->receivers || !p->senders ||
-      !p->h_in || !p->h_out || !p->action || (p->mode == 1 && !p->noise) || !p->work || p->G < 0)
+      !p->h_in || !p->h_out || !p->action || (p->mode == 1 && !p->noise && !p->noise_seed) || !p->work || p->G < 0)
     return DGPPO_EINVAL;
   if (p->G == 0) return 0;
   const int gpg = dgppo::kRowsG / p->n_agents;

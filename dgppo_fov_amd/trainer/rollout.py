@@ -99,11 +99,11 @@ class RolloutEngine:
         n = env.num_agents
         h = self.rnn[t].view(self.B * n, self.W)
         if self.mode == self.MODE_SAMPLE:
-            # per-step, per-shard Philox stream: (env_offset, t) -> disjoint noise across ranks
-            K.normal_(self.noise, stream_id=(self.env_offset << 32) | t, seed_tensor=self.key)
+            # per-step, per-shard Philox stream (env_offset, t) -> disjoint noise across ranks, drawn inside the
+            # fused policy step (K.normal_ into self.noise first on the unfused path)
             self.actor.act(g, h, 1, noise=self.noise, action_out=self.actions[t].view(-1, env.action_dim),
                            log_pi_out=self.log_pis[t].view(-1), h_out=self.rnn[t + 1].view(self.B * n, self.W),
-                           prepare=t == 0)
+                           prepare=t == 0, noise_seed=self.key, noise_stream=(self.env_offset << 32) | t)
         else:
             self.actor.act(g, h, 0, action_out=self.actions[t].view(-1, env.action_dim),
                            h_out=self.rnn[t + 1].view(self.B * n, self.W), prepare=t == 0)

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 9  /* 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 10  /* 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -414,10 +414,14 @@ typedef struct dgppo_policy_step_args {
   float std_shift, std_min;
   const float* h_in;   /* (G n, 64) */
   float* h_out;        /* (G n, 64) */
-  const float* noise;  /* (G n, A), mode 1 */
+  const float* noise;  /* (G n, A), mode 1; NULL: drawn in the kernel from noise_seed (ABI 10) */
   float* action;       /* (G n, A) */
   float* log_pi;       /* (G n) or NULL */
   float* work;         /* dgppo_policy_work_floats() floats */
+  /* ABI 10, mode 1 with noise == NULL: element row * A + q of the standard-normal stream
+   * (*noise_seed, noise_stream), bit-identical to dgppo_normal(buffer, G n A, noise_seed, 0, noise_stream) */
+  const uint64_t* noise_seed;
+  uint64_t noise_stream;
 } dgppo_policy_step_args;
 
 int dgppo_policy_step_supported(const dgppo_policy_step_args* args);

@@ -102,6 +102,29 @@ def test_rollout_shards_use_disjoint_noise(cuda):
     assert not torch.equal(acts[0], acts[1])
 
 
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("LidarOmniTarget", 3, 2)])
+def test_policy_step_in_kernel_noise_bit_exact(cuda, eid, n, obs):
+    """ABI 10: the fused policy step drawing its Philox noise in the kernel (noise_seed, noise_stream) gives the
+    same action, log_pi and carry bits as the step fed the buffer dgppo_normal writes for that stream."""
+    B = 37
+    env = make_env(eid, n, num_obs=obs, max_step=4, device=cuda)
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=n, batch_size=8, rnn_step=4, seed=3, device=cuda)
+    eng = RolloutEngine(env, B, 4, cuda, env_offset=0, actor=algo.actor, mode=RolloutEngine.MODE_DET)
+    eng.run(9)
+    g = eng._batch(2)
+    h = torch.randn((B * n, 64), generator=torch.Generator().manual_seed(4)).to(cuda)
+    key = torch.tensor([0x1234_5678_9ABC], dtype=torch.int64, device=cuda)
+    sid = (5 << 32) | 7
+    noise = torch.empty((B * n, env.action_dim), device=cuda)
+    K.normal_(noise, stream_id=sid, seed_tensor=key)
+    ref = algo.actor.act(g, h, 1, noise=noise)
+    got = algo.actor.act(g, h, 1, noise=torch.full_like(noise, float("nan")), noise_seed=key, noise_stream=sid)
+    torch.cuda.synchronize()
+    for a, b, what in zip(ref, got, ("action", "log_pi", "carry")):
+        assert torch.equal(a, b), what
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_env_rollout_lanes_bit_exact(cuda, graph):
     """Env-only rollout stepped as 2 env slices on 2 streams (RolloutEngine lanes=2) writes the same
