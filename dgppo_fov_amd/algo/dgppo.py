@@ -59,6 +59,11 @@ def allreduce_mean_(t: torch.Tensor, world: int):
 PREPASS_GRAPHS = int(os.environ.get("DGPPO_PREPASS_GRAPHS", 65536))
 
 
+def PHASE_EVENTS() -> bool:
+    """Timing knob: HIP-event split of update() into prepass / GAE + advantages / minibatches (no synchronisation)."""
+    return os.environ.get("DGPPO_PHASE_EVENTS", "0") == "1"
+
+
 def FORCE_SAFE() -> bool:
     """Learning-dynamics ablation (scripts/learn_ablate.sh): treat every sample as inside the safe set."""
     return os.environ.get("DGPPO_DEBUG_FORCE_SAFE", "0") == "1"
@@ -591,6 +596,11 @@ class DGPPO:
         n = self._n_agents
         ph = _Phases(dev)
         ph.mark()
+        # DGPPO_PHASE_EVENTS=1: live (non-synchronising) split of the update into prepass / GAE + advantages /
+        # minibatches from HIP events on the current stream, reported in info["time/*_ms"]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if PHASE_EVENTS() and dev.type == "cuda" else None
+        if ev:
+            ev[0].record()
         det_key = int(self.key.integers(0, 2 ** 62))
         assert B * T * self.world >= self.batch_size
         chunk = max(1, min(B, PREPASS_GRAPHS // T))
@@ -610,6 +620,8 @@ class DGPPO:
             else:
                 Vl, Vh, Vh_det = self._vl_all(rollout, chunk), self._vh_all(rollout, chunk), self._vh_all(det, chunk)
             ph.mark("prepass")
+            if ev:
+                ev[1].record()
             # ---- GAE + advantages
             costs = rollout.costs.contiguous()
             l = (-rollout.rewards).contiguous()
@@ -627,6 +639,8 @@ class DGPPO:
             dt, alpha = (math.inf, 0.0) if FORCE_SAFE() else (env.dt, self.alpha)
             K.dgppo_advantages(Ql, Vl, Vh, A, safe_cnt, dt, alpha, self.cbf_eps, self.cbf_weight_at(step))
             ph.mark("gae_adv")
+            if ev:
+                ev[2].record()
             if self.trace is not None:
                 self.trace.update(det=det, Vl=Vl.clone(), Vh=Vh.clone(), Vh_det=Vh_det.clone(), Ql=Ql.clone(),
                                   Qh=Qh.clone(), Qh_det=Qh_det.clone(), A=A.clone(), safe_cnt=safe_cnt.clone(),
@@ -666,6 +680,11 @@ class DGPPO:
             info["diag/vec"] = torch.cat([Vh[:, :T].mean((0, 1, 2)), Vh_det[:, :T].mean((0, 1, 2)),
                                           Qh_det.mean((0, 1, 2)), det.costs.mean((0, 1, 2))])
         ph.report()
+        if ev:
+            ev[3].record()
+            ev[3].synchronize()
+            for name, a, b in (("prepass", 0, 1), ("gae_adv", 1, 2), ("minibatches", 2, 3)):
+                info[f"time/{name}_ms"] = ev[a].elapsed_time(ev[b])
         return self._finish_info(info)
 
     def _finish_info(self, info) -> dict:

@@ -24,7 +24,7 @@ import torch
 
 from ... import _lib
 from ...nn import kernels as K
-from ...nn.layers import GNN, Dense, GraphBatch, MLPHead, ParamSpace, RNNStack
+from ...nn.layers import FUSE_LN, GNN, Dense, GraphBatch, MLPHead, ParamSpace, RNNStack
 
 STD_DEV_INIT_INV = math.log(math.exp(0.5) - 1.0)  # TanhNormal.std_dev_init_inv (policy.py:54-59)
 STD_DEV_MIN = 1e-5
@@ -270,8 +270,9 @@ class VlNet(_Net):
         dY, _ = self.gru.seq_bwd(gcs, dH, ln=ln)
         dzm = self.head.bwd(hc, dY, dy_is_dh1=ln is not None)
         dz = torch.empty_like(z)
-        K.agent_mean_bwd(dzm, dz, G, n, 64, n * 64)
-        self.gnn.bwd(gc, dz, g)
+        # z is the last GNN layer's ReLU output: its gate is fused into the broadcast (FUSE_LN, as the GEMM epilogues)
+        K.agent_mean_bwd(dzm, dz, G, n, 64, n * 64, mask=z if FUSE_LN else None)
+        self.gnn.bwd(gc, dz, g, top_masked=FUSE_LN)
 
 
 class VhNet(_Net):

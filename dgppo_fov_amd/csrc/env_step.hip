@@ -2205,27 +2205,25 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
   const float area = cfg.area_size;
   float* pos = lds + cv.samp;
   float* gl = pos + 2 * n;
-  if (tid == 0) {
-    if (!mpe && O > 0) {
-      float tmp[4 * kMaxObs + kMaxObs];
-      for (int o = 0; o < O; ++o) {
-        tmp[2 * o] = rng.uniform(0.0f, area);
-        tmp[2 * o + 1] = rng.uniform(0.0f, area);
-      }
-      for (int o = 0; o < O; ++o) {
-        tmp[2 * O + 2 * o] = rng.uniform(cfg.obs_len_lo, cfg.obs_len_hi);
-        tmp[2 * O + 2 * o + 1] = rng.uniform(cfg.obs_len_lo, cfg.obs_len_hi);
-      }
-      for (int o = 0; o < O; ++o) tmp[4 * O + o] = rng.uniform(cfg.obs_theta_lo, cfg.obs_theta_hi);
-      for (int o = 0; o < O; ++o)
-        make_rectangle(obst + o * DGPPO_OBST_FIELDS, tmp[2 * o], tmp[2 * o + 1], tmp[2 * O + 2 * o],
-                       tmp[2 * O + 2 * o + 1], tmp[4 * O + o]);
-    }
-    rng_count = rng.count;
+  // obstacles: draw l of the reference's sequence (centres x / y per obstacle, then sizes, then angles) is the
+  // Philox word at count l, so thread l draws it (staged in the candidate table, filled only afterwards) and
+  // thread o builds rectangle o -- the same values as one thread drawing them in order
+  float* tab = lds + cv.total;
+  const int n_ob_draws = (!mpe && O > 0) ? 5 * O : 0;
+  for (int l = tid; l < n_ob_draws; l += BLOCK) {
+    Rng r = rng;
+    r.count = (uint32_t)l;
+    const float lo = l < 2 * O ? 0.0f : (l < 4 * O ? cfg.obs_len_lo : cfg.obs_theta_lo);
+    const float hi = l < 2 * O ? area : (l < 4 * O ? cfg.obs_len_hi : cfg.obs_theta_hi);
+    tab[l] = r.uniform(lo, hi);
   }
   __syncthreads();
+  for (int o = tid; o < (n_ob_draws > 0 ? O : 0); o += BLOCK)
+    make_rectangle(obst + o * DGPPO_OBST_FIELDS, tab[2 * o], tab[2 * o + 1], tab[2 * O + 2 * o], tab[2 * O + 2 * o + 1],
+                   tab[4 * O + o]);
+  if (tid == 0) rng_count = (uint32_t)n_ob_draws;
+  __syncthreads();
   // the first kSampTab candidate pairs of the sampler's stream, drawn by every thread at once
-  float* tab = lds + cv.total;
   for (int k = tid; k < kSampTab; k += BLOCK) {
     Rng r = rng;
     r.count = rng_count + 2u * (uint32_t)k;
@@ -2239,22 +2237,14 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
     if (tid == 0) rng_count = rng.count;
   }
   __syncthreads();
-  if (tid == 0) {
+  for (int idx = tid; idx < n * SD; idx += BLOCK) {
+    const int i = idx / SD, c = idx - (idx / SD) * SD;
+    nxt[idx] = c < 2 ? pos[2 * i + c] : 0.0f;
+    goal[idx] = c < 2 ? gl[2 * i + c] : 0.0f;
+  }
+  __syncthreads();
+  if (tid == 0 && (ENGINE == DGPPO_ENGINE_OMNI || mpe)) {
     rng.count = rng_count;
-    for (int i = 0; i < n; ++i) {
-      for (int c = 0; c < SD; ++c) {
-        nxt[i * SD + c] = c < 2 ? pos[2 * i + c] : 0.0f;
-        goal[i * SD + c] = c < 2 ? gl[2 * i + c] : 0.0f;
-      }
-    }
-    if (ENGINE == DGPPO_ENGINE_BICYCLE) {
-      for (int i = 0; i < n; ++i) {
-        float s, c;
-        sincos32(rng.uniform(0.0f, 6.28318548202514648438f), &s, &c);
-        nxt[i * SD + 2] = c;
-        nxt[i * SD + 3] = s;
-      }
-    }
     if (ENGINE == DGPPO_ENGINE_OMNI) {  // chain headings toward the next agent (lidar_omni_target.py:246-272)
       for (int i = 0; i + 1 < n; ++i) {
         const float dx = pos[2 * (i + 1)] - pos[2 * i], dy = pos[2 * (i + 1) + 1] - pos[2 * i + 1];
@@ -2289,6 +2279,17 @@ __global__ __launch_bounds__(BLOCK) void env_reset_kernel(dgppo_env_cfg cfg, dgp
     }
   }
   __syncthreads();
+  if (ENGINE == DGPPO_ENGINE_BICYCLE) {  // headings: agent i's draw is the Philox word at count rng_count + i
+    for (int i = tid; i < n; i += BLOCK) {
+      Rng r = rng;
+      r.count = rng_count + (uint32_t)i;
+      float s, c;
+      sincos32(r.uniform(0.0f, 6.28318548202514648438f), &s, &c);
+      nxt[i * SD + 2] = c;
+      nxt[i * SD + 3] = s;
+    }
+    __syncthreads();
+  }
   if (states_only) {  // the wave step kernel builds the graph from these rows (dgppo_env_reset)
     if (lidar) {
       float* ob = io.obstacles + env * io.obstacles_stride;

@@ -331,14 +331,18 @@ __global__ __launch_bounds__(256) void agent_mean_fwd_kernel(const float* x, flo
   }
 }
 
+// mask (optional, (G n, F) contiguous): the ReLU output that fed the mean; dx = mask > 0 ? dy / n : 0 (the ReLU
+// backward fused, as dgppo_relu_bwd would apply it after the broadcast)
 __global__ __launch_bounds__(256) void agent_mean_bwd_kernel(const float* dy, float* dx, int64_t G, int n, int F,
-                                                             int64_t dx_gstride) {
+                                                             int64_t dx_gstride, const float* mask) {
   const int64_t total = G * n * F;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
     const int64_t g = t / ((int64_t)n * F);
     const int64_t rem = t - g * n * F;
     const int i = (int)(rem / F), f = (int)(rem - (int64_t)(rem / F) * F);
-    dx[g * dx_gstride + (int64_t)i * F + f] = dy[g * F + f] / n;
+    float v = dy[g * F + f] / n;
+    if (mask && !(mask[t] > 0.0f)) v = 0.0f;
+    dx[g * dx_gstride + (int64_t)i * F + f] = v;
   }
 }
 
@@ -859,13 +863,18 @@ extern "C" int dgppo_agent_mean_fwd(const float* x, float* y, int64_t G, int32_t
   return (int)hipGetLastError();
 }
 
-extern "C" int dgppo_agent_mean_bwd(const float* dy, float* dx, int64_t G, int32_t n, int32_t F, int64_t dx_gstride,
-                                    void* stream) {
+extern "C" int dgppo_agent_mean_bwd_masked(const float* dy, const float* mask, float* dx, int64_t G, int32_t n,
+                                           int32_t F, int64_t dx_gstride, void* stream) {
   if (G < 0 || n < 1 || F < 1 || !dx || !dy) return DGPPO_EINVAL;
   if (G == 0) return 0;
   hipLaunchKernelGGL(agent_mean_bwd_kernel, dim3(grid_for(G * n * F)), dim3(256), 0, DG_STREAM(stream), dy, dx, G,
-                     n, F, dx_gstride);
+                     n, F, dx_gstride, mask);
   return (int)hipGetLastError();
+}
+
+extern "C" int dgppo_agent_mean_bwd(const float* dy, float* dx, int64_t G, int32_t n, int32_t F, int64_t dx_gstride,
+                                    void* stream) {
+  return dgppo_agent_mean_bwd_masked(dy, nullptr, dx, G, n, F, dx_gstride, stream);
 }
 
 extern "C" int dgppo_tanh_normal(const dgppo_tanh_normal_args* p, void* stream) {

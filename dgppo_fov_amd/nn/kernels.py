@@ -163,9 +163,11 @@ def agent_mean_fwd(x, y, G, n, F, x_gstride):
          "dgppo_agent_mean_fwd")
 
 
-def agent_mean_bwd(dy, dx, G, n, F, dx_gstride):
-    _chk(_lib.load().dgppo_agent_mean_bwd(_p(dy), _p(dx), int(G), int(n), int(F), int(dx_gstride), _stream(dx)),
-         "dgppo_agent_mean_bwd")
+def agent_mean_bwd(dy, dx, G, n, F, dx_gstride, mask=None):
+    """dx = broadcast(dy) / n over each graph's n agent rows; mask: the ReLU output rows (G n, F) that fed the mean,
+    dx = mask > 0 ? dy / n : 0 (its ReLU backward fused)."""
+    _chk(_lib.load().dgppo_agent_mean_bwd_masked(_p(dy), _p(mask), _p(dx), int(G), int(n), int(F), int(dx_gstride),
+                                                 _stream(dx)), "dgppo_agent_mean_bwd_masked")
 
 
 def sender_table(G, n, C, E, cand, receivers, senders, out):

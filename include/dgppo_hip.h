@@ -433,6 +433,10 @@ int dgppo_policy_step(const dgppo_policy_step_args* args, void* stream);
 int dgppo_agent_mean_fwd(const float* x, float* y, int64_t G, int32_t n, int32_t F, int64_t x_gstride, void* stream);
 int dgppo_agent_mean_bwd(const float* dy, float* dx, int64_t G, int32_t n, int32_t F, int64_t dx_gstride,
                          void* stream);
+/* ABI 10: the same with the ReLU backward of the rows that fed the mean fused in: dx = mask > 0 ? dy / n : 0,
+ * mask (G n, F) contiguous (dgppo_agent_mean_bwd then dgppo_relu_bwd(dx, mask), in one pass) */
+int dgppo_agent_mean_bwd_masked(const float* dy, const float* mask, float* dx, int64_t G, int32_t n, int32_t F,
+                                int64_t dx_gstride, void* stream);
 
 /* TanhNormal head (dgppo/algo/module/policy.py:61-74, distribution.py:10-66): std = softplus(raw +
  * std_shift) + std_min; mode 0 = tanh(mean), 1 = tanh(mean + std * noise), 2 = evaluate `action`.

@@ -42,5 +42,6 @@ for it in range(2 + a.reps):
 knobs = {k: v for k, v in os.environ.items() if k.startswith("DGPPO_")}
 print(json.dumps({"env": a.env, "n": a.n, "envs": a.envs, "batch": a.batch, "update_ms": round(sorted(ts)[len(ts) // 2], 2),
                   "collect_ms": round(sorted(cs)[len(cs) // 2], 2), "update_ms_all": [round(t, 1) for t in ts],
-                  "knobs": knobs, "policy_loss": round(info["policy/loss"], 6), "Vl_loss": round(info["Vl/loss"], 6)}),
+                  "knobs": knobs, "policy_loss": round(info["policy/loss"], 6), "Vl_loss": round(info["Vl/loss"], 6),
+                  "phases_ms": {k[5:]: round(v, 2) for k, v in info.items() if k.startswith("time/")}}),
       flush=True)
