@@ -2162,25 +2162,81 @@ __device__ void node_goal_rng_wave(Rng& rng, const float* tab, float side, int n
   clear();
   uint32_t count = rng.count;
   const uint32_t count0 = count;
+  // The table's kSampTab candidates as wave bit masks (lane l holds candidates l + 64 q): rejected by an obstacle
+  // (either phase), out of the area (goal phases), within min_dist of a point placed so far or of the origin (the
+  // unplaced rows are zeros).  A candidate's distance test is `min_j d_j <= min_dist`, i.e. `any d_j <= min_dist`
+  // unless some d_j is NaN (min_nan then makes the minimum NaN and the test false): the masks OR in one ballot per
+  // placed point and track NaNs apart, so a phase is a first-set-bit search instead of n distances and O
+  // rectangle tests per candidate -- the same first accepted candidate, the same count.  Past the table (or after
+  // kMaxIter rejections) sample_phase runs as before.
+  static_assert(kSampTab == 256, "4 candidates per lane");
+  float tx[4], ty[4];
+  uint64_t inobs[4], oob[4], nearA[4], nearG[4], nanA[4], nanG[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    tx[q] = tab[2 * (lane + 64 * q)];
+    ty[q] = tab[2 * (lane + 64 * q) + 1];
+    inobs[q] = __ballot(inside_any(obst, O, tx[q], ty[q], r_in));
+    oob[q] = __ballot(tx[q] < 0.0f || ty[q] < 0.0f || tx[q] > side || ty[q] > side);
+  }
+  auto origin_only = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = norm2(0.0f - tx[q], 0.0f - ty[q]);
+      nearA[q] = nearG[q] = __ballot(d <= min_dist);
+      nanA[q] = nanG[q] = __ballot(d != d);
+    }
+  };
+  auto add_point = [&](uint64_t (&near)[4], uint64_t (&nan)[4], float px, float py) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = norm2(px - tx[q], py - ty[q]);
+      near[q] |= __ballot(d <= min_dist);
+      nan[q] |= __ballot(d != d);
+    }
+  };
+  auto phase = [&](bool goals, const float* pts, const uint64_t (&near)[4], const uint64_t (&nan)[4], float& ox,
+                   float& oy) -> int {
+    const int s = (int)((count - count0) / 2u);  // this phase's first candidate
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int lo = s - 64 * q;
+      if (lo >= 64) continue;
+      uint64_t good = ~(inobs[q] | (near[q] & ~nan[q]) | (goals ? oob[q] : 0ull));
+      if (lo > 0) good &= ~0ull << lo;
+      if (good) {
+        const int k = 64 * q + __ffsll((unsigned long long)good) - 1;
+        ox = tab[2 * k];
+        oy = tab[2 * k + 1];
+        count += 2u * (uint32_t)(k - s + 1);
+        return k - s;
+      }
+    }
+    return sample_phase(rng, count, count0, tab, goals, side, n, min_dist, r_in, obst, O, pts, ox, oy);
+  };
+  origin_only();
   int agent_id = 0;
   while (agent_id < n) {
     float cx, cy, gx, gy;
-    const int it_agent = sample_phase(rng, count, count0, tab, false, side, n, min_dist, r_in, obst, O, pos, cx, cy);
+    const int it_agent = phase(false, pos, nearA, nanA, cx, cy);
     if (lane == 0) {
       pos[2 * agent_id] = cx;
       pos[2 * agent_id + 1] = cy;
     }
+    add_point(nearA, nanA, cx, cy);
     wv::wave_sync();
-    const int it = sample_phase(rng, count, count0, tab, true, side, n, min_dist, r_in, obst, O, gl, gx, gy);
+    const int it = phase(true, gl, nearG, nanG, gx, gy);
     if (lane == 0) {
       gl[2 * agent_id] = gx;
       gl[2 * agent_id + 1] = gy;
     }
+    add_point(nearG, nanG, gx, gy);
     wv::wave_sync();
     ++agent_id;
     if (it_agent >= kMaxIter || it >= kMaxIter) {  // no solution: start over (utils.py:229-232)
       agent_id = 0;
       clear();
+      origin_only();
     }
   }
   rng.count = count;
