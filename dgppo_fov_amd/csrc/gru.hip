@@ -19,6 +19,7 @@
 
 #include "lds_attr.h"
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dgppo_hip.h"
 
@@ -57,6 +58,37 @@ __device__ __forceinline__ void gh_tiles(const float* A, const float* Whs, int c
     ar = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[0], ar, 0, 0, 0);
     az = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[kHid], az, 0, 0, 0);
     an = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[2 * kHid], an, 0, 0, 0);
+  }
+}
+
+// Register form of the B operand (REGB): lane (i, kq) of wave w needs, for its 16 k-steps, exactly
+// Wh[4 kk + kq][g 64 + 16 w + i] (g = r, z, n gate) -- 48 floats, loaded once per workgroup instead of
+// staging Wh (48 KB) in LDS and reading one fragment from LDS per MFMA.  The same operands reach the
+// same MFMAs in the same order, so results are bit-identical to the LDS form.
+struct WhFrag {
+  float v[3][kHid / 4];
+};
+__device__ __forceinline__ void wh_frag_load(const float* Wh, int col, int lane, WhFrag& f) {
+  const int kq = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < kHid / 4; ++kk) {
+    const float* w = Wh + (int64_t)(4 * kk + kq) * kG3 + col;
+    f.v[0][kk] = w[0];
+    f.v[1][kk] = w[kHid];
+    f.v[2][kk] = w[2 * kHid];
+  }
+}
+__device__ __forceinline__ void gh_tiles_reg(const float* A, const WhFrag& f, int lane, f32x4& ar, f32x4& az,
+                                             f32x4& an) {
+  const int i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ar[r] = az[r] = an[r] = 0.0f;
+#pragma unroll
+  for (int kk = 0; kk < kHid / 4; ++kk) {
+    const float a = A[i * kHP + 4 * kk + kq];
+    ar = __builtin_amdgcn_mfma_f32_16x16x4f32(a, f.v[0][kk], ar, 0, 0, 0);
+    az = __builtin_amdgcn_mfma_f32_16x16x4f32(a, f.v[1][kk], az, 0, 0, 0);
+    an = __builtin_amdgcn_mfma_f32_16x16x4f32(a, f.v[2][kk], an, 0, 0, 0);
   }
 }
 
@@ -101,15 +133,18 @@ __device__ __forceinline__ void store_rows16(float* dst, float4 v) {
   d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
 }
 
+template <bool REGB>
 __global__ __launch_bounds__(kThreads) void gru_seq_fwd_kernel(dgppo_gru_seq_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* Whs = lds;                   // [64][kWP]
-  float* hb = Whs + kHid * kWP;       // [2][16][kHP]
+  float* Whs = lds;                                   // [64][kWP] (LDS form only)
+  float* hb = REGB ? lds : Whs + kHid * kWP;          // [2][16][kHP]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int Q = p.Q, L = p.L, n = p.n_agents;
   const int nblk = (Q + kRows - 1) / kRows;
-  stage_wh(p.Wh, Whs);
   const int col = w * 16 + (lane & 15);
+  WhFrag wf;
+  if constexpr (REGB) wh_frag_load(p.Wh, col, lane, wf);
+  else stage_wh(p.Wh, Whs);
   const float bn = p.bhn[col];
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     const int q0 = blk * kRows;
@@ -140,7 +175,8 @@ __global__ __launch_bounds__(kThreads) void gru_seq_fwd_kernel(dgppo_gru_seq_arg
       load_gi(t + 1 < L ? t + 1 : t, gx);
       __builtin_amdgcn_sched_barrier(0);
       f32x4 ar, az, an;
-      gh_tiles(hcur, Whs, col, lane, ar, az, an);
+      if constexpr (REGB) gh_tiles_reg(hcur, wf, lane, ar, az, an);
+      else gh_tiles(hcur, Whs, col, lane, ar, az, an);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = lane_row(lane, r), q = q0 + row;
@@ -162,18 +198,28 @@ __global__ __launch_bounds__(kThreads) void gru_seq_fwd_kernel(dgppo_gru_seq_arg
   }
 }
 
+template <bool REGB>
 __global__ __launch_bounds__(kThreads) void gru_seq_bwd_kernel(dgppo_gru_seq_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* Whs = lds;                 // [64][kWP]
-  float* hp = Whs + kHid * kWP;     // [16][kHP]   h_{t-1}
+  float* Whs = lds;                                 // [64][kWP] (LDS form only)
+  float* hp = REGB ? lds : Whs + kHid * kWP;        // [16][kHP]   h_{t-1}
   float* dg = hp + kRows * kHP;     // [16][kWP]   dgh of this step
   float* red = dg + kRows * kWP;    // [4][64]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
   const int Q = p.Q, L = p.L, n = p.n_agents;
   const int nblk = (Q + kRows - 1) / kRows;
-  stage_wh(p.Wh, Whs);
   const int col = w * 16 + i;
+  // REGB: the gh fragments and, for dh_{t-1} += dgh Wh^T, wt[kk] = Wh[col][4 kk + kq] (48 more floats)
+  WhFrag wf;
+  float wt[kG3 / 4];
+  if constexpr (REGB) {
+    wh_frag_load(p.Wh, col, lane, wf);
+#pragma unroll
+    for (int kk = 0; kk < kG3 / 4; ++kk) wt[kk] = p.Wh[(int64_t)col * kG3 + 4 * kk + kq];
+  } else {
+    stage_wh(p.Wh, Whs);
+  }
   const float bn = p.bhn[col];
   float dbn = 0.0f;
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
@@ -218,7 +264,8 @@ __global__ __launch_bounds__(kThreads) void gru_seq_bwd_kernel(dgppo_gru_seq_arg
       store_rows16(hp, hv);
       __syncthreads();
       f32x4 ar, az, an;
-      gh_tiles(hp, Whs, col, lane, ar, az, an);
+      if constexpr (REGB) gh_tiles_reg(hp, wf, lane, ar, az, an);
+      else gh_tiles(hp, Whs, col, lane, ar, az, an);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = lane_row(lane, r), q = q0 + row;
@@ -257,10 +304,16 @@ __global__ __launch_bounds__(kThreads) void gru_seq_bwd_kernel(dgppo_gru_seq_arg
       __syncthreads();
       // dh_{t-1} += dgh (16 x 192) Wh^T (192 x 64): this wave's 16 hidden columns
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      if constexpr (REGB) {
+#pragma unroll
+        for (int kk = 0; kk < kG3 / 4; ++kk)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dg[i * kWP + 4 * kk + kq], wt[kk], acc, 0, 0, 0);
+      } else {
 #pragma unroll 8
-      for (int kk = 0; kk < kG3 / 4; ++kk) {
-        const int k = 4 * kk + kq;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dg[i * kWP + k], Whs[col * kWP + k], acc, 0, 0, 0);
+        for (int kk = 0; kk < kG3 / 4; ++kk) {
+          const int k = 4 * kk + kq;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dg[i * kWP + k], Whs[col * kWP + k], acc, 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) dh[r] += acc[r];
@@ -289,11 +342,29 @@ __global__ __launch_bounds__(kThreads) void gru_seq_bwd_kernel(dgppo_gru_seq_arg
   }
 }
 
-size_t fwd_lds() { return (size_t)(kHid * kWP + 2 * kRows * kHP) * sizeof(float); }
-size_t bwd_lds() { return (size_t)(kHid * kWP + kRows * kHP + kRows * kWP + 4 * kHid) * sizeof(float); }
+size_t fwd_lds(bool regb) { return (size_t)((regb ? 0 : kHid * kWP) + 2 * kRows * kHP) * sizeof(float); }
+size_t bwd_lds(bool regb) {
+  return (size_t)((regb ? 0 : kHid * kWP) + kRows * kHP + kRows * kWP + 4 * kHid) * sizeof(float);
+}
+// B operand form (DGPPO_GRU_REGB=0 or dgppo_gru_set_form(0): Wh staged in LDS, the round-3 kernels; default:
+// register fragments)
+int g_regb = -1;
+bool regb() {
+  if (g_regb < 0) {
+    const char* e = getenv("DGPPO_GRU_REGB");
+    g_regb = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_regb == 1;
+}
 
 }  // namespace
 }  // namespace dgppo
+
+extern "C" int dgppo_gru_set_form(int32_t regb) {
+  if (regb != 0 && regb != 1) return DGPPO_EINVAL;
+  dgppo::g_regb = regb;
+  return 0;
+}
 
 // persistent grid: at most kMaxBlocks workgroups, each looping over 16-row blocks
 extern "C" int64_t dgppo_gru_seq_blocks(int32_t Q) {
@@ -306,9 +377,15 @@ extern "C" int dgppo_gru_seq_fwd(const dgppo_gru_seq_args* p, void* stream) {
       (p->Q % p->n_agents) != 0)
     return DGPPO_EINVAL;
   if (p->Q == 0) return 0;
-  dgppo::allow_lds((const void*)dgppo::gru_seq_fwd_kernel);
-  hipLaunchKernelGGL(dgppo::gru_seq_fwd_kernel, dim3((unsigned)dgppo_gru_seq_blocks(p->Q)), dim3(dgppo::kThreads),
-                     dgppo::fwd_lds(), (hipStream_t)stream, *p);
+  const dim3 grid((unsigned)dgppo_gru_seq_blocks(p->Q));
+  if (dgppo::regb()) {
+    hipLaunchKernelGGL(dgppo::gru_seq_fwd_kernel<true>, grid, dim3(dgppo::kThreads), dgppo::fwd_lds(true),
+                       (hipStream_t)stream, *p);
+  } else {
+    dgppo::allow_lds((const void*)dgppo::gru_seq_fwd_kernel<false>);
+    hipLaunchKernelGGL(dgppo::gru_seq_fwd_kernel<false>, grid, dim3(dgppo::kThreads), dgppo::fwd_lds(false),
+                       (hipStream_t)stream, *p);
+  }
   return (int)hipGetLastError();
 }
 
@@ -317,8 +394,14 @@ extern "C" int dgppo_gru_seq_bwd(const dgppo_gru_seq_args* p, void* stream) {
       !p->dhs || !p->dgi || !p->dgh || (p->Q % p->n_agents) != 0)
     return DGPPO_EINVAL;
   if (p->Q == 0) return 0;
-  dgppo::allow_lds((const void*)dgppo::gru_seq_bwd_kernel);
-  hipLaunchKernelGGL(dgppo::gru_seq_bwd_kernel, dim3((unsigned)dgppo_gru_seq_blocks(p->Q)), dim3(dgppo::kThreads),
-                     dgppo::bwd_lds(), (hipStream_t)stream, *p);
+  const dim3 grid((unsigned)dgppo_gru_seq_blocks(p->Q));
+  if (dgppo::regb()) {
+    hipLaunchKernelGGL(dgppo::gru_seq_bwd_kernel<true>, grid, dim3(dgppo::kThreads), dgppo::bwd_lds(true),
+                       (hipStream_t)stream, *p);
+  } else {
+    dgppo::allow_lds((const void*)dgppo::gru_seq_bwd_kernel<false>);
+    hipLaunchKernelGGL(dgppo::gru_seq_bwd_kernel<false>, grid, dim3(dgppo::kThreads), dgppo::bwd_lds(false),
+                       (hipStream_t)stream, *p);
+  }
   return (int)hipGetLastError();
 }

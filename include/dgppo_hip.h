@@ -382,6 +382,9 @@ typedef struct dgppo_gru_seq_args {
 int64_t dgppo_gru_seq_blocks(int32_t Q);
 int dgppo_gru_seq_fwd(const dgppo_gru_seq_args* args, void* stream);
 int dgppo_gru_seq_bwd(const dgppo_gru_seq_args* args, void* stream);
+/* ABI 10, tuning / testing hook: 1 (default) = Wh as per-lane register MFMA fragments, 0 = Wh staged in LDS
+ * (the round-3 kernels); bit-identical results either way.  Process-wide; also DGPPO_GRU_REGB=0|1. */
+int dgppo_gru_set_form(int32_t regb);
 
 /* Fused policy step (one launch per env step of the rollouts): GNN -> MLP head -> GRUCell ->
  * ScaleHid -> mean/std -> TanhNormal sample (mode 1, standard-normal noise) or mode (mode 0), i.e.
