@@ -1,7 +1,7 @@
 """The row-GEMM epilogues of ABI 9 (csrc/gemm.hip, dgppo_gemm_args.epi) against float64 references of the elementwise
 passes they replace, on every row path (whole-unit prefetch K <= 32, B-in-registers K = 64, plain rows with vector and
-scalar A loads): the ReLU backward (epi 1), LayerNorm(64) + ReLU forward (epi 2, flax LayerNorm eps 1e-6 then relu,
-dgppo/nn/mlp.py:20-30) and its backward (epi 3, dscale / dbias accumulated).  Tolerances: fp32 GEMM + epilogue vs
+scalar A loads; K = 2 / 7 are the tiny-K shapes of the action and raw-row layers): the ReLU backward (epi 1),
+LayerNorm(64) + ReLU forward (epi 2, flax LayerNorm eps 1e-6 then relu, dgppo/nn/mlp.py:20-30) and its backward (epi 3, dscale / dbias accumulated).  Tolerances: fp32 GEMM + epilogue vs
 float64, 1e-5 relative to the tensor scale (2e-5 for the backward's row reductions)."""
 import numpy as np
 import pytest
@@ -77,7 +77,8 @@ def test_layernorm_epilogues(cuda, M, Kd):
     assert torch.equal(dbd.cpu(), (y > 0).float().sum(0).cpu())
 
 
-@pytest.mark.parametrize("M,N,Kd,beta", [(1000, 64, 64, 0.0), (1000, 32, 99, 1.0), (500, 64, 32, 0.0), (300, 32, 192, 1.0)])
+@pytest.mark.parametrize("M,N,Kd,beta", [(1000, 64, 64, 0.0), (1000, 32, 99, 1.0), (500, 64, 32, 0.0), (300, 32, 192, 1.0),
+                                         (1000, 64, 2, 1.0), (777, 24, 7, 0.0)])
 def test_relu_mask_epilogue(cuda, M, N, Kd, beta):
     rng = np.random.default_rng(7 + M + N)
     A = rng.standard_normal((M, Kd)).astype(np.float32)

@@ -97,7 +97,8 @@ def test_gemm_weight_grad_with_fused_bias_grad(cuda, M, N, Kd, batch, grp):
     assert (bd.double().cpu() - refb).abs().max().item() <= 2e-6 * B.abs().sum(1).max().item() + 1e-5
 
 
-@pytest.mark.parametrize("M,N,Kd", [(300, 64, 32), (300, 64, 64), (300, 64, 96), (300, 192, 64), (70, 40, 20)])
+@pytest.mark.parametrize("M,N,Kd", [(300, 64, 32), (300, 64, 64), (300, 64, 96), (300, 192, 64), (70, 40, 20),
+                                     (300, 64, 2), (70, 24, 7)])
 @pytest.mark.parametrize("beta,with_add", [(0.0, True), (0.7, False), (0.7, True)])
 def test_gemm_epilogue_order_is_path_independent(cuda, M, N, Kd, beta, with_add):
     """Every GEMM path applies one epilogue order, (alpha acc + bias) + (beta C + addend): the rows kernels
