@@ -349,11 +349,11 @@ class DGPPO:
                                self._env.agent_candidates(self.device), raw_cols=self._env.nonagent_feature_cols)
                 self.Vl.graph_means(g, out=zm[t0:t1].view(G, 64))
             zm_env = zm.transpose(0, 1).contiguous()  # (B, T, 64): rows e * T + t
-            for e0 in range(0, B, chunk):
-                e1 = min(B, e0 + chunk)
-                v, hT, _ = self.Vl.seq_fwd(None, e1 - e0, T, keep_cache=False, zm=zm_env[e0:e1].view(-1, 64))
-                Vl[e0:e1, :T].copy_(v)
-                hT_all[e0:e1].copy_(hT)
+            # head + GRU scan of every env in ONE pass (rows independent: bit-identical to env chunks); chunks of
+            # 512 envs left the scan's 128 dependent steps on 32 workgroups, one chunk after another
+            v, hT, _ = self.Vl.seq_fwd(None, B, T, keep_cache=False, zm=zm_env.view(-1, 64))
+            Vl[:, :T].copy_(v)
+            hT_all.copy_(hT)
         for e0 in range(0, B, chunk) if tm is None else ():
             e1 = min(B, e0 + chunk)
             g = self._graphs(rollout.graph, slice(e0, e1))
