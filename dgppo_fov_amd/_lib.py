@@ -293,6 +293,7 @@ SIGNATURES = {
     "dgppo_agent_mean_bwd": (ctypes.c_int, [_V, _V, _I64, _I32, _I32, _I64, _V]),
     "dgppo_agent_mean_bwd_masked": (ctypes.c_int, [_V, _V, _V, _I64, _I32, _I32, _I64, _V]),
     "dgppo_gru_set_form": (ctypes.c_int, [_I32]),
+    "dgppo_gnn_set_graph_otf": (ctypes.c_int, [_I32]),
     "dgppo_tanh_normal": (ctypes.c_int, [ctypes.POINTER(TanhNormalArgs), ctypes.c_void_p]),
     "dgppo_loss_workspace_floats": (ctypes.c_int64, []),
     "dgppo_ppo_loss": (ctypes.c_int, [_V, _V, _V, _V, _I64, _F32, _F32, _V, _V, _V, _V, _V]),

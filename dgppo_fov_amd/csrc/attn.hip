@@ -2157,58 +2157,79 @@ void launch_cp(const dgppo_gnn_attn_args* p, const Plan& pl, bool bwd, hipStream
 // ================================================================================================
 namespace gfwd {
 constexpr int kMaxC = 128;
-// per-wave buffers: 4 x kMaxC x (kH + 1 + 4) floats, reused for the pre-mode staging (N D0 + D0 D + D)
-template <int DM>
-size_t wave_floats(int N) {
-  const size_t w = 4 * (size_t)kMaxC * (kH + 1 + 4), st = (((size_t)N * kD0 + 3) & ~(size_t)3) + kD0 * DM + DM;
-  return w > st ? w : st;
-}
+constexpr int kMaxSlots = 16;
 // sender-row pitch: DM + 1 for the 8-wide first layers (scalar reads); 36 for DM = 32 (float4 row reads,
 // 16-byte aligned, bank-conflict free across 16 lanes)
 template <int DM>
 constexpr int row_pitch() { return DM == 32 ? 36 : DM + 1; }
+// ns: rows staged in LDS; cp: per-wave candidate pitch; slots: per-wave rows computed on the fly (0: every row
+// staged, the round-3 layout).  On-the-fly mode (agent mode with the pre transform, D = 32, Lidar layout
+// [agents | goals | each receiver's own hits | pad]): only the agent and goal rows (shared by all receivers) are
+// staged; a receiver's own hit rows -- used by that receiver alone -- are computed by the lane that attends over
+// them (relu(x_raw W4 + b4), the staging's order of operations) into the wave's slots.  LidarSpread n = 32: 75 KB
+// -> 37 KB of LDS per graph, 2 -> 4 resident graphs per CU.
+struct Plan {
+  int ns, cp, slots;
+};
 template <int DM>
-size_t lds_floats(int N, int n) {
-  return (size_t)N * row_pitch<DM>() + (size_t)n * (kH * DM + 4) + wave_floats<DM>(N);
+size_t wave_floats(const Plan& pl) {
+  return (size_t)pl.cp * (kH + 1 + 4) + (size_t)pl.slots * row_pitch<DM>();
+}
+template <int DM>
+size_t lds_floats(int n, const Plan& pl) {
+  const size_t w = 4 * wave_floats<DM>(pl);
+  const size_t pw = (size_t)kD0 * DM + DM;                           // pre weights | bias
+  const size_t st = (((size_t)pl.ns * kD0 + 3) & ~(size_t)3) + (pl.slots > 0 ? 0 : pw);  // staging temporaries
+  return (size_t)pl.ns * row_pitch<DM>() + (size_t)n * (kH * DM + 4) + (pl.slots > 0 ? pw : 0) + (w > st ? w : st);
 }
 }  // namespace gfwd
 
+// relu(x_raw pre_W + pre_b) for feature quad [c, c + 4): bias first, then k ascending -- the one order of operations
+// of the staged and the on-the-fly never-receiver rows (the backward recomputes them the same way)
+__device__ __forceinline__ lanes::f32x4 pre_quad(const float* raw, const float* PW, int D0, int D, int c) {
+  lanes::f32x4 v = *reinterpret_cast<const lanes::f32x4*>(PW + D0 * D + c);
+  for (int k = 0; k < D0; ++k) v += raw[k] * *reinterpret_cast<const lanes::f32x4*>(PW + k * D + c);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.0f ? v[j] : 0.0f;
+  return v;
+}
+
 template <int DM>
-__global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args p) {
+__global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args p, int ns, int cp, int slots) {
   using lanes::f32x4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int XP = gfwd::row_pitch<DM>(), QP = kH * DM + 4;
   constexpr bool V4 = DM == 32;  // float4 logits / weighted sums (rows zero-padded to DM)
-  const int n = p.n_agents, N = p.N, D = p.D, F = p.F, C = p.C, H = kH;
+  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = kH;
   const int64_t g = blockIdx.x;
-  float* X = lds;                         // [N][XP] sender rows
-  float* Q = X + (size_t)N * XP;          // [n][QP]: qt_h (DM stride) | beta_h at kH DM + h
-  float* Wb = Q + (size_t)n * QP;         // per wave: A [kMaxC][kH] | S [kMaxC] | E [kMaxC][4]
+  const bool otf = V4 && slots > 0;       // rows >= ns computed on the fly (gfwd::Plan)
+  float* X = lds;                         // [ns][XP] staged sender rows
+  float* Q = X + (size_t)ns * XP;         // [n][QP]: qt_h (DM stride) | beta_h at kH DM + h
+  float* PWp = Q + (size_t)n * QP;        // on the fly: the persistent pre weights [D0][D] | b [D]
+  float* Wb = PWp + (otf ? kD0 * DM + DM : 0);  // per wave: A [cp][kH] | S [cp] | E [cp][4] | slots [slots][XP]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool agent = p.xa != nullptr;
+  (void)F;
   // ---- stage the graph's sender rows (pre mode: raw rows and pre weights through LDS first, in the
   // per-wave buffers that are free until the row loop)
   const bool pre = agent && p.pre_W != nullptr;
   const int D0 = p.D0;
-  float* R0 = Wb;                                     // [N][D0] raw rows
-  float* PW = R0 + (((size_t)N * D0 + 3) & ~(size_t)3);  // [D0][D] | b [D] (16-byte aligned)
+  float* R0 = Wb;                                          // [ns][D0] raw rows
+  float* PW = otf ? PWp : R0 + (((size_t)ns * D0 + 3) & ~(size_t)3);  // [D0][D] | b [D] (16-byte aligned)
   if (pre) {
-    for (int e = threadIdx.x; e < N * D0; e += 256) R0[e] = p.x[g * p.x_gstride + e];
+    for (int e = threadIdx.x; e < ns * D0; e += 256) R0[e] = p.x[g * p.x_gstride + e];
     for (int e = threadIdx.x; e < D0 * D; e += 256) PW[e] = p.pre_W[e];
     for (int e = threadIdx.x; e < D; e += 256) PW[D0 * D + e] = p.pre_b[e];
     __syncthreads();
   }
   if constexpr (V4) {  // a column quad per thread and step (float4 LDS / global accesses where aligned)
     const bool q4ok = (D & 3) == 0;
-    for (int e = threadIdx.x; e < N * (DM / 4); e += 256) {
+    for (int e = threadIdx.x; e < ns * (DM / 4); e += 256) {
       const int r = e / (DM / 4), c = 4 * (e - r * (DM / 4));
       f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
       if (c < D) {
         if (agent && r >= n && pre && q4ok) {
-          v = *reinterpret_cast<const f32x4*>(PW + D0 * D + c);
-          for (int k = 0; k < D0; ++k) v += R0[r * D0 + k] * *reinterpret_cast<const f32x4*>(PW + k * D + c);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.0f ? v[j] : 0.0f;
+          v = pre_quad(R0 + r * D0, PW, D0, D, c);
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -2235,7 +2256,7 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
     }
   }
   const int DS = V4 ? 0 : D;  // staged columns of the scalar path
-  for (int e = threadIdx.x; e < N * DS; e += 256) {
+  for (int e = threadIdx.x; e < ns * DS; e += 256) {
     const int r = e / DS, d = e - r * DS;
     float v;
     if (d >= D) {
@@ -2262,10 +2283,10 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
     Q[i * QP + kH * DM + h] = q_dot_bk(p, g * n + i, h, 0, 1);
   }
   __syncthreads();
-  constexpr int kMaxC = gfwd::kMaxC;
-  float* A = Wb + wave * kMaxC * (kH + 1 + 4);
-  int* S = reinterpret_cast<int*>(A + kMaxC * kH);
-  float* E = A + kMaxC * (kH + 1);
+  float* A = Wb + (size_t)wave * (cp * (kH + 1 + 4) + slots * XP);
+  int* S = reinterpret_cast<int*>(A + cp * kH);
+  float* E = A + cp * (kH + 1);
+  float* HB = E + cp * 4;  // [slots][XP] this wave's on-the-fly rows (S = ns + slot)
   const int W = H * (D + 5);
   // the next row's senders and edge features are requested while this row computes
   int sn[2];
@@ -2290,16 +2311,39 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
     const f32x4 ev[2] = {en[0], en[1]};
     fetch(i + 4);
     float lg[2][kH];
+    // on-the-fly senders of this row get consecutive slots of the wave buffer (clamped: the host enables the mode
+    // only when a receiver has at most `slots` of them)
+    int slot[2];
+    {
+      const bool f0 = otf && sv[0] >= ns, f1 = otf && sv[1] >= ns;
+      const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      slot[0] = __popcll(m0 & below);
+      slot[1] = __popcll(m0) + __popcll(m1 & below);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) slot[u] = slot[u] < slots ? slot[u] : (slots > 0 ? slots - 1 : 0);
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = lane + 64 * u;
       const int sd = sv[u];
       const bool ok = sd >= 0;
-      const float* xr = X + (ok ? sd : 0) * XP;
+      const bool fly = otf && sd >= ns;
+      const float* xr = X + (ok && !fly ? sd : 0) * XP;
       if constexpr (V4) {
         f32x4 xv[DM / 4];
+        if (fly) {  // this receiver's own never-receiver row: relu(x_raw W4 + b4) here, kept for the weighted sums
+          const float* raw = p.x + g * p.x_gstride + (int64_t)sd * D0;
+          float* hb = HB + slot[u] * XP;
 #pragma unroll
-        for (int q = 0; q < DM / 4; ++q) xv[q] = reinterpret_cast<const f32x4*>(xr)[q];
+          for (int q = 0; q < DM / 4; ++q) {
+            xv[q] = 4 * q < D ? pre_quad(raw, PW, D0, D, 4 * q) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            reinterpret_cast<f32x4*>(hb)[q] = xv[q];
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < DM / 4; ++q) xv[q] = reinterpret_cast<const f32x4*>(xr)[q];
+        }
 #pragma unroll
         for (int h = 0; h < kH; ++h) {
           const f32x4* qt4 = reinterpret_cast<const f32x4*>(Q + i * QP + h * DM);
@@ -2324,7 +2368,7 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
       }
       if (c < C) {
         *reinterpret_cast<f32x4*>(E + c * 4) = ev[u];
-        S[c] = sd;
+        S[c] = fly ? ns + slot[u] : sd;
       }
     }
 #pragma unroll
@@ -2365,8 +2409,8 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
         const float* ar = A + c * kH;
         if (kind == 2) return f32x4{ar[0], ar[1], ar[2], 0.0f};
         const float a = sd >= 0 ? ar[h] : 0.0f;
-        const f32x4 v = kind == 0 ? reinterpret_cast<const f32x4*>(X + (sd >= 0 ? sd : 0) * XP)[q]
-                                  : reinterpret_cast<const f32x4*>(E)[c];
+        const float* xrow = sd >= ns ? HB + (sd - ns) * XP : X + (sd >= 0 ? sd : 0) * XP;
+        const f32x4 v = kind == 0 ? reinterpret_cast<const f32x4*>(xrow)[q] : reinterpret_cast<const f32x4*>(E)[c];
         return a * v;
       };
       if (kind < 3) {
@@ -2823,6 +2867,28 @@ void gbwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   hipLaunchKernelGGL(attn_bwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
 }
 
+// on-the-fly rows in the graph-form forward: -1 = unset (DGPPO_ATTN_GRAPH_OTF, default 1), else 0 / 1
+// (dgppo_gnn_set_graph_otf: A/B and the bit-identity test)
+int g_graph_otf = -1;
+
+gfwd::Plan gfwd_plan(const dgppo_gnn_attn_args* p) {
+  gfwd::Plan pl{p->N, gfwd::kMaxC, 0};  // every row staged (the round-3 layout)
+  if (g_graph_otf < 0) {
+    const char* e = getenv("DGPPO_ATTN_GRAPH_OTF");
+    g_graph_otf = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  const int otf = g_graph_otf;
+  const int n = p->n_agents, ns = 2 * n, slots = p->C - ns;
+  if (otf && p->D > 8 && (p->D & 3) == 0 && p->xa && p->pre_W && p->D0 <= kD0 && ns < p->N && slots >= 1 &&
+      slots <= gfwd::kMaxSlots)
+    pl = gfwd::Plan{ns, (p->C + 3) & ~3, slots};
+  return pl;
+}
+
+size_t gfwd_bytes(const dgppo_gnn_attn_args* p, const gfwd::Plan& pl) {
+  return (p->D <= 8 ? gfwd::lds_floats<8>(p->n_agents, pl) : gfwd::lds_floats<32>(p->n_agents, pl)) * sizeof(float);
+}
+
 bool gfwd_ok(const dgppo_gnn_attn_args* p) {
   static const bool off = [] {
     const char* e = getenv("DGPPO_ATTN_GRAPH");
@@ -2837,18 +2903,18 @@ bool gfwd_ok(const dgppo_gnn_attn_args* p) {
   if (off || p->H != kH || p->C <= 32 || p->C > gfwd::kMaxC || p->D > 32 || !p->sidx) return false;
   if (p->D > 8 && off32) return false;
   if (p->xa && p->D0 > kD0) return false;
-  const size_t bytes = (p->D <= 8 ? gfwd::lds_floats<8>(p->N, p->n_agents) : gfwd::lds_floats<32>(p->N, p->n_agents)) *
-                       sizeof(float);
-  return bytes <= 160 * 1024;
+  return gfwd_bytes(p, gfwd_plan(p)) <= 160 * 1024;
 }
 
 void gfwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const bool d8 = p->D <= 8;
-  const size_t bytes = (d8 ? gfwd::lds_floats<8>(p->N, p->n_agents) : gfwd::lds_floats<32>(p->N, p->n_agents)) *
-                       sizeof(float);
+  const gfwd::Plan pl = gfwd_plan(p);
+  const size_t bytes = gfwd_bytes(p, pl);
   if (bytes > 64 * 1024) allow_lds(d8 ? (const void*)attn_fwd_graph_kernel<8> : (const void*)attn_fwd_graph_kernel<32>);
-  if (d8) hipLaunchKernelGGL(attn_fwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
-  else hipLaunchKernelGGL(attn_fwd_graph_kernel<32>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
+  if (d8)
+    hipLaunchKernelGGL(attn_fwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p, pl.ns, pl.cp, pl.slots);
+  else
+    hipLaunchKernelGGL(attn_fwd_graph_kernel<32>, dim3((unsigned)p->G), dim3(256), bytes, s, *p, pl.ns, pl.cp, pl.slots);
 }
 
 #include "attn_gm.h"
@@ -2924,6 +2990,12 @@ extern "C" int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* p) {
     return dgppo::bwd2_grid(p, &nblk);
   }
   return dgppo::make_plan(p, true).grid;
+}
+
+extern "C" int dgppo_gnn_set_graph_otf(int32_t on) {
+  if (on != 0 && on != 1) return DGPPO_EINVAL;
+  dgppo::g_graph_otf = on;
+  return 0;
 }
 
 extern "C" int dgppo_gnn_set_attn_kernel(int mode) {

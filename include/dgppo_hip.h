@@ -306,6 +306,10 @@ int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
  * kernels everywhere (the default: measured faster).  Returns the previous mode or DGPPO_EINVAL.  Initial mode:
  * DGPPO_ATTN_GM=1|0 (default 0). */
 int dgppo_gnn_set_attn_kernel(int mode);
+/* ABI 10, tuning / testing hook: 1 (default) = the graph-form forward computes each receiver's own
+ * never-receiver rows on the fly (Lidar layout, D = 32 agent mode with pre_W: only agent and goal rows staged
+ * in LDS), 0 = every row staged; bit-identical either way.  Process-wide; also DGPPO_ATTN_GRAPH_OTF=0|1. */
+int dgppo_gnn_set_graph_otf(int32_t on);
 /* sidx[(g*n + i)*C + c] = senders[g][cand[i][c]] if that edge's receiver is i, else -1: the
  * candidate resolution shared by every attention launch on one graph batch */
 int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, int32_t E, const int32_t* cand,

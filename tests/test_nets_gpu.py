@@ -472,3 +472,28 @@ def test_rnn_options_nets_fwd_bwd(cuda, kind, layers):
     vh.ps.swap_views()
     for path, a, b in _walk(g, R.grads(ph)):
         _grad_close(a, b, f"{kind}{layers} Vh grad {path}")
+
+
+def test_graph_forward_on_the_fly_rows_bit_identical(cuda):
+    """ABI 10 dgppo_gnn_set_graph_otf: the graph-form forward of the dense n = 32 graphs with each receiver's own hit
+    rows computed on the fly (LDS holds only the agent and goal rows) gives the same bits as staging every row --
+    values, and the gradients of the backward that reads the forward's attention weights and xcat rows."""
+    from dgppo_fov_amd import _lib
+    S, L = 2, 3
+    env, gb, _ = _graphs(cuda, "LidarSpread", 32, 8, S, L, seed=5)
+    lib = _lib.load()
+    res = []
+    try:
+        for otf in (1, 0):
+            assert lib.dgppo_gnn_set_graph_otf(otf) == 0
+            net = VlNet(env.node_dim, 32, cuda, seed=9, **_nets_kw(env))
+            v, hT, cache = net.seq_fwd(gb, S, L)
+            net.ps.zero_grad()
+            net.seq_bwd(cache, torch.linspace(-1.0, 1.0, S * L, device=cuda).view(S, L))
+            torch.cuda.synchronize()
+            res.append((v.cpu(), hT.cpu(), net.ps.grad.cpu().clone()))
+    finally:
+        lib.dgppo_gnn_set_graph_otf(1)
+    for a, b, what in zip(res[0], res[1], ("values", "carries", "gradients")):
+        assert torch.equal(a, b), what
+    assert res[0][2].abs().max() > 0
