@@ -2872,7 +2872,9 @@ void gbwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
 int g_graph_otf = -1;
 
 gfwd::Plan gfwd_plan(const dgppo_gnn_attn_args* p) {
-  gfwd::Plan pl{p->N, gfwd::kMaxC, 0};  // every row staged (the round-3 layout)
+  // every row staged; per-wave candidate buffers at the call's C rounded to 4 (was kMaxC = 128: at the n = 32 first
+  // layer 31.5 -> 26.6 KB per graph, 5 -> 6 resident graphs per CU)
+  gfwd::Plan pl{p->N, (p->C + 3) & ~3, 0};
   if (g_graph_otf < 0) {
     const char* e = getenv("DGPPO_ATTN_GRAPH_OTF");
     g_graph_otf = (e && atoi(e) == 0) ? 0 : 1;
