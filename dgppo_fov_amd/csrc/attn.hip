@@ -2472,16 +2472,16 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
 // Per pair da_h = dxbar_h . x + debar_h . ef + dsig_h (+ da_add), dl_h = a_h (da_h - sum_c a_h da_h)
 // scale and dbeta_h = sum_c dl_h by wave shuffles; dqt_h = sum_c dl_h x_c one output column per lane.
 template <int DM>
-__global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args p) {
+__global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args p, int cp) {
   using lanes::f32x4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int XP = DM + 1, kMaxC = gfwd::kMaxC;
+  constexpr int XP = DM + 1;
   const int n = p.n_agents, N = p.N, D = p.D, F = p.F, C = p.C, H = kH;
   const int W = H * (D + 5);
   const int64_t g = blockIdx.x;
   float* X = lds;                          // [N][XP]
   float* G = X + (size_t)N * XP;           // [n][W] dxcat rows
-  float* Wb = G + (size_t)n * W;           // per wave: dl [kMaxC][kH] | S [kMaxC]
+  float* Wb = G + (size_t)n * W;           // per wave: dl [cp][kH] | S [cp] (cp = C rounded to 4)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < N * D; e += 256) {
     const int r = e / D, d = e - r * D;
@@ -2489,8 +2489,8 @@ __global__ __launch_bounds__(256) void attn_bwd_graph_kernel(dgppo_gnn_attn_args
   }
   for (int e = threadIdx.x; e < n * W; e += 256) G[e] = p.dxcat[g * n * W + e];
   __syncthreads();
-  float* Aw = Wb + wave * kMaxC * (kH + 1);
-  int* S = reinterpret_cast<int*>(Aw + kMaxC * kH);
+  float* Aw = Wb + wave * cp * (kH + 1);
+  int* S = reinterpret_cast<int*>(Aw + cp * kH);
   for (int i = wave; i < n; i += 4) {
     const int64_t row = g * n + i;
     const float* gv = G + i * W;  // dxbar (H D) | debar (4 H) | dsig (H)
@@ -2849,7 +2849,7 @@ void gbwd32_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
 }
 
 size_t gbwd_lds_floats(const dgppo_gnn_attn_args* p) {
-  return (size_t)p->N * (8 + 1) + (size_t)p->n_agents * kH * (p->D + 5) + 4 * (size_t)gfwd::kMaxC * (kH + 1);
+  return (size_t)p->N * (8 + 1) + (size_t)p->n_agents * kH * (p->D + 5) + 4 * (size_t)((p->C + 3) & ~3) * (kH + 1);
 }
 
 bool gbwd_ok(const dgppo_gnn_attn_args* p) {
@@ -2864,7 +2864,7 @@ bool gbwd_ok(const dgppo_gnn_attn_args* p) {
 void gbwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const size_t bytes = gbwd_lds_floats(p) * sizeof(float);
   if (bytes > 64 * 1024) allow_lds((const void*)attn_bwd_graph_kernel<8>);
-  hipLaunchKernelGGL(attn_bwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p);
+  hipLaunchKernelGGL(attn_bwd_graph_kernel<8>, dim3((unsigned)p->G), dim3(256), bytes, s, *p, (p->C + 3) & ~3);
 }
 
 // on-the-fly rows in the graph-form forward: -1 = unset (DGPPO_ATTN_GRAPH_OTF, default 1), else 0 / 1
