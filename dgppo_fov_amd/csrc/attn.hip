@@ -2314,12 +2314,14 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
     // on-the-fly senders of this row get consecutive slots of the wave buffer (clamped: the host enables the mode
     // only when a receiver has at most `slots` of them)
     int slot[2];
+    bool overflow = false;  // more on-the-fly senders than slots: the row's outputs become NaN (loud, not silent)
     {
       const bool f0 = otf && sv[0] >= ns, f1 = otf && sv[1] >= ns;
       const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
       const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
       slot[0] = __popcll(m0 & below);
       slot[1] = __popcll(m0) + __popcll(m1 & below);
+      overflow = __popcll(m0) + __popcll(m1) > slots && otf;
 #pragma unroll
       for (int u = 0; u < 2; ++u) slot[u] = slot[u] < slots ? slot[u] : (slots > 0 ? slots - 1 : 0);
     }
@@ -2425,6 +2427,7 @@ __global__ __launch_bounds__(256) void attn_fwd_graph_kernel(dgppo_gnn_attn_args
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] += __shfl_xor(acc[j], 32, 64);
+      if (overflow) acc = f32x4{NAN, NAN, NAN, NAN};
       if (half == 0) {
         float* o = p.xcat + row * W;
         if (kind == 0) {
@@ -2881,7 +2884,10 @@ gfwd::Plan gfwd_plan(const dgppo_gnn_attn_args* p) {
   }
   const int otf = g_graph_otf;
   const int n = p->n_agents, ns = 2 * n, slots = p->C - ns;
-  if (otf && p->D > 8 && (p->D & 3) == 0 && p->xa && p->pre_W && p->D0 <= kD0 && ns < p->N && slots >= 1 &&
+  // the Spread layout only: N = 2n + n k + 1 nodes and C = 2n + k candidates (every agent, every goal, the
+  // receiver's own k hits), so a receiver has at most C - 2n candidates past the staged rows
+  const bool spread_layout = n > 0 && p->N > ns + 1 && (p->N - 1 - ns) % n == 0 && p->C == ns + (p->N - 1 - ns) / n;
+  if (otf && spread_layout && p->D > 8 && (p->D & 3) == 0 && p->xa && p->pre_W && p->D0 <= kD0 && slots >= 1 &&
       slots <= gfwd::kMaxSlots)
     pl = gfwd::Plan{ns, (p->C + 3) & ~3, slots};
   return pl;
