@@ -4,18 +4,19 @@ one JSON: per run the eval curve every 50 updates (reward, cost, unsafe_frac on 
 det rollout, the det-rollout Qh targets and costs, train-rollout unsafe fraction / act_drift, entropy), plus
 milestones: the first update from which the eval unsafe_frac stays <= 0.1 for 10 consecutive evals, and windowed
 means over the last 5000 updates.
-  python scripts/long_summary.py gpurun_out/long profiles/r04_learning_long.json"""
+  python scripts/long_summary.py gpurun_out/long profiles/r04_learning_long.json [ENV]"""
 import glob
 import json
 import os
 import sys
 
 root, out_path = sys.argv[1], sys.argv[2]
+ENV = sys.argv[3] if len(sys.argv) > 3 else "LidarSpread"
 KEYS = ("eval/safe_data", "Vh/mean_h0", "Vh/mean_h1", "Vh/det_mean_h0", "Vh/det_mean_h1", "Vh/det_target_mean_h0",
         "Vh/det_target_mean_h1", "det/cost_mean_h0", "det/cost_mean_h1", "train/unsafe_frac", "train/act_drift",
         "train/reward", "policy/entropy", "policy/clip_frac", "Vl/loss", "Vh/loss_Vh")
 runs = {}
-for run in sorted(glob.glob(os.path.join(root, "LidarSpread", "*", "seed*"))):
+for run in sorted(glob.glob(os.path.join(root, ENV, "*", "seed*"))):
     algo = os.path.basename(os.path.dirname(run))
     rows = [json.loads(x) for x in open(os.path.join(run, "log.jsonl"))]
     ev = [r for r in rows if "eval/reward" in r]
@@ -37,7 +38,7 @@ for run in sorted(glob.glob(os.path.join(root, "LidarSpread", "*", "seed*"))):
                               "eval_unsafe_frac": mean([c[3] for c in tail])},
         "eval_at_0": curve[0], "eval_curve_keys": ["update", "eval/reward", "eval/cost", "eval/unsafe_frac"],
         "eval_curve": curve, "diag_keys": ["update"] + list(KEYS), "diag_every_50": diag}
-out = {"what": "README quickstart (python train.py --env LidarSpread --algo <algo> -n 3 --obs 3; reference defaults: "
+out = {"what": f"README quickstart (python train.py --env {ENV} --algo <algo> -n 3 --obs 3; reference defaults: "
                "128 envs, batch 16384, --steps 200000 CBF schedule, eval every 50 updates on 32 envs), resumed across "
                "gpurun calls (train.py --resume, bit-exact host RNG / Adam state)",
        "runs": runs}
