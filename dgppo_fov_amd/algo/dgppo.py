@@ -162,6 +162,7 @@ class DGPPO:
         self.init_Vl_rnn_state = torch.zeros((rnn_layers, 1, self.n_carries, 64), device=dev)
         self._engines = {}
         self._capturing = False
+        self._flat_reduce = False  # one flat gradient all-reduce per minibatch (the minibatch-graph path), not buckets
         self.trace: Optional[dict] = None  # set to {} to record update intermediates (parity tests)
         self.key = np.random.default_rng(seed)
         self.np_rng = np.random.default_rng(seed)
@@ -416,11 +417,14 @@ class DGPPO:
         waits for every bucket and scales by 1/world before clip + Adam (same result as one flat
         all-reduce: each bucket is reduced exactly once).  Not while a minibatch graph is being captured: the
         graph path all-reduces the whole gradient buffer eagerly between its two replays."""
-        if self.world > 1 and not self._capturing:
+        if self.world > 1 and not self._capturing and not self._flat_reduce:
             pending.append(dist.all_reduce(net.ps.grad, op=dist.ReduceOp.SUM, async_op=True))
 
     def _finish_reduce(self, pending: list):
         if self.world > 1 and not self._capturing:
+            if self._flat_reduce:  # the graph path's eager first minibatch: the same flat all-reduce as its replays
+                self._allreduce_grads()
+                return
             for w in pending:
                 w.wait()
             pending.clear()
@@ -473,9 +477,13 @@ class DGPPO:
         """Replay the minibatch step from captured hipGraphs: no parity trace, no phase timing, equal minibatch
         sizes, concurrent streams on; by default for small minibatches only (at the bench config, 16384 samples, the
         update is GPU-bound and it measured 230.3 vs 229.4 ms; config 4's 2048-sample rank minibatches: 92.3 ->
-        54.6 ms per update, profiles/r04_config4_strong.jsonl).  Bit-identical to the eager step.  Two graphs per
-        minibatch -- the gradient passes, then clip + Adam -- with the multi-GPU gradient all-reduce issued eagerly
-        between the two replays (no collective inside a captured graph)."""
+        54.6 ms per update, profiles/r04_config4_strong.jsonl).  Two graphs per minibatch -- the gradient passes,
+        then clip + Adam -- with the multi-GPU gradient all-reduce issued eagerly between the two replays (no
+        collective inside a captured graph).  On this path every minibatch, the eager first one included, reduces the
+        whole gradient buffer with ONE flat all-reduce (`_flat_reduce`), so the replays repeat the eager step's
+        arithmetic exactly on any number of ranks; the eager path's per-net buckets sum the same values, which is
+        bit-identical at two ranks and can differ in the last bit from three on (ring order follows the chunking).
+        tests/test_distributed_gpu.py::test_two_rank_minibatch_graphs_match_eager runs both paths on two ranks."""
         if "_mbg" not in self.__dict__:
             self._mbg = None
         if self.trace is not None or ph.on or len({len(b) for b in batches}) != 1 or self._aux_streams(2) is None:
@@ -651,6 +659,7 @@ class DGPPO:
             assert T % L == 0, "jnp.array(jnp.array_split(...)) in the reference needs rnn_step | T"
             env_ids = self._env_ids(batches)
             graph_ok = self._mb_graph_ok(batches, ph, T)
+            self._flat_reduce = graph_ok
             for k, bi in enumerate(batches):
                 envs = next(env_ids)
                 args = (rollout, det, A, Ql, Qh_det, len(bi), T, L)
@@ -669,6 +678,7 @@ class DGPPO:
                         envs=bi.copy(), grad=self._mb_grad, vl_loss=vl_loss.clone(), vh_loss=vh_loss.clone(),
                         stats=stats.clone(), before=self._mb_before["p"], m_before=self._mb_before["m"],
                         v_before=self._mb_before["v"], state_before=self._mb_before["s"]))
+            self._flat_reduce = False
             info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
                     "Vh/loss_Vh": vh_loss, "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
             safe = safe_cnt.sum()

@@ -75,13 +75,15 @@ class Trainer:
     # ---- resumable state (params + optimiser + RNG; the reference saves params only) ----------
     STATE_FILE = "trainer_state.json"
 
-    def save_state(self, step: int):
-        """models/<step>/ (params + Adam moments + counters, algo.save) and trainer_state.json: the next
-        step and every host RNG the loop draws from, so load_state() continues the exact sequence."""
+    def save_state(self, next_step: int):
+        """models/<next_step>/ (params + Adam moments + counters, algo.save) and trainer_state.json: the next
+        step and every host RNG the loop draws from, so load_state() continues the exact sequence.  The model
+        directory keeps the periodic saves' meaning, models/<k> = the state BEFORE update k (so a stop never
+        overwrites an earlier save with other parameters, and models/0 stays the initial parameters)."""
         if not self.save_log:
             return
-        self.algo.save(self.model_dir, step)
-        st = {"next_step": step + 1, "update_steps": self.update_steps, "model_step": step,
+        self.algo.save(self.model_dir, next_step)
+        st = {"next_step": next_step, "update_steps": self.update_steps, "model_step": next_step,
               "trainer_rng": self.rng.bit_generator.state, "algo_key": self.algo.key.bit_generator.state,
               "algo_np_rng": self.algo.np_rng.bit_generator.state}
         tmp = os.path.join(self.log_dir, self.STATE_FILE + ".tmp")
@@ -100,12 +102,24 @@ class Trainer:
         self.start_step, self.update_steps = st["next_step"], st["update_steps"]
         return st
 
+    def _out_of_time(self, start_time: float) -> bool:
+        """The --max-minutes stop decision, taken by rank 0 and broadcast, so every rank stops at the same step
+        (a rank that stopped on its own clock would leave the others blocked in the gradient all-reduce)."""
+        if self.max_minutes is None:
+            return False
+        stop = time() - start_time > 60.0 * float(self.max_minutes)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            flag = [bool(stop)]
+            dist.broadcast_object_list(flag, src=0)
+            stop = bool(flag[0])
+        return stop
+
     def train(self):
         start_time = time()
         test_key = int(self.seed)
         for step in range(self.start_step, self.steps + 1):
-            if self.max_minutes is not None and time() - start_time > 60.0 * float(self.max_minutes):
-                self.save_state(step - 1)
+            if self._out_of_time(start_time):
+                self.save_state(step)
                 print(f"> stopping after {time() - start_time:.0f}s at step {step} (resume with --resume)", flush=True)
                 return False
             if step % self.eval_interval == 0 and self.rank == 0:
@@ -124,7 +138,7 @@ class Trainer:
                 self._log({"step": self.update_steps, **update_info, **self._read_stats(train_stats)})
             self.update_steps += 1
         if self.max_minutes is not None:
-            self.save_state(self.steps)
+            self.save_state(self.steps + 1)
         return True
 
     def _train_stats(self, rollouts):

@@ -25,7 +25,34 @@ def host(r):
                 dones=r.dones.cpu().clone(), log_pis=None if r.log_pis is None else r.log_pis.cpu().clone())
 
 
+def graph_mode(out, knob):
+    """Two collect + update iterations of 2 minibatches each with the parity trace OFF and DGPPO_UPDATE_GRAPH=knob
+    (1: minibatch hipGraph replays with the eager flat all-reduce between them, 0: eager per-net buckets); saves
+    the parameters and Adam state of every net."""
+    os.environ["DGPPO_UPDATE_GRAPH"] = knob
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    env = make_env(ENV, N, num_obs=OBS, max_step=T, device=dev)
+    algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                     action_dim=env.action_dim, n_agents=N, batch_size=B_LOCAL * T * world // 2, rnn_step=L,
+                     train_steps=100, seed=1, device=dev)
+    for it in range(2):
+        roll = algo.collect(algo.params, 7 + it, n_env=B_LOCAL)
+        algo.update(roll, it)
+    torch.cuda.synchronize()
+    assert (algo._mbg is not None) == (knob == "1")
+    torch.save({k: dict(p=o.ps.flat.cpu().clone(), m=o.m.cpu().clone(), v=o.v.cpu().clone(),
+                        state=o.state.cpu().clone()) for k, o in algo.opt.items()},
+               os.path.join(out, f"graph{knob}_rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main(out, algo_name="dgppo"):
+    if algo_name.startswith("graph"):
+        return graph_mode(out, algo_name[5:])
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")

@@ -25,6 +25,36 @@ def _cat(parts, dev):
     return torch.cat([p.to(dev) for p in parts], 0)
 
 
+def _run_ranks(tmp_path, mode, world=2):
+    port = 29700 + (os.getpid() + 7 * len(mode)) % 200
+    procs = []
+    for r in range(world):
+        envv = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                    MASTER_PORT=str(port))
+        envv.pop("DGPPO_UPDATE_GRAPH", None)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_update_worker.py"), str(tmp_path),
+                                       mode], env=envv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        out, _ = p.communicate(timeout=150)
+        assert p.returncode == 0, out.decode()[-3000:]
+
+
+def test_two_rank_minibatch_graphs_match_eager(cuda, tmp_path):
+    """the minibatch-hipGraph path with two ranks and the parity trace off (two updates of two
+    minibatches: the eager first minibatch, its capture, one replay with the eager all-reduce between the two
+    graphs) against the eager per-net-bucket path -- parameters and Adam state bit-identical, and identical across
+    the ranks."""
+    _run_ranks(tmp_path, "graph1")
+    _run_ranks(tmp_path, "graph0")
+    ld = lambda k, r: torch.load(os.path.join(tmp_path, f"graph{k}_rank{r}.pt"), weights_only=True)  # noqa: E731
+    g1, e1, g1b = ld("1", 0), ld("0", 0), ld("1", 1)
+    for net in g1:
+        for f in ("p", "m", "v", "state"):
+            assert torch.equal(g1[net][f], g1b[net][f]), (net, f, "ranks differ")
+            assert torch.equal(g1[net][f], e1[net][f]), (net, f, "graph replay vs eager")
+    assert not torch.equal(g1["policy"]["m"], torch.zeros_like(g1["policy"]["m"]))
+
+
 @pytest.mark.parametrize("algo_name", ["dgppo", "informarl_lagr"])
 def test_two_rank_update_equals_single_process_union(cuda, tmp_path, algo_name):
     """informarl_lagr adds the sharded multiplier step (per-rank delta, one all-reduce, same relu step on

@@ -60,3 +60,48 @@ def test_train_then_test_entry_points(cuda, tmp_path, monkeypatch, capsys, eid, 
     row = open(os.path.join(run, "test_log.csv")).read().strip().split(",")
     assert len(row) == 7 and row[0] == str(n + 1) and row[1] == "5" and row[2] == "16" and row[4] == str(obs + 1)
     assert 0.0 <= float(row[5]) <= 100.0
+
+
+def test_resume_continues_the_exact_sequence(cuda, tmp_path, monkeypatch):
+    """a run stopped by --max-minutes after 2 updates and continued with --resume ends with the same
+    parameters, Adam moments / counts and update log as the same run trained in one go (models/<k> = the state
+    before update k; the final resumable state is models/<steps + 1>)."""
+    import torch
+
+    train_py = _entry("train")
+    from dgppo_fov_amd.trainer import trainer as trainer_mod
+
+    base = ["train.py", "--env", "LidarSpread", "-n", "3", "--algo", "dgppo", "--obs", "2", "--steps", "3",
+            "--n-env-train", "8", "--batch-size", "256", "--n-env-test", "4", "--eval-interval", "2",
+            "--save-interval", "100", "--max-minutes", "1000"]
+
+    def run(log_dir, extra=()):
+        monkeypatch.setattr(sys, "argv", base + ["--log-dir", str(log_dir)] + list(extra))
+        return train_py.main()
+
+    run(tmp_path / "once")
+    calls = {"n": 0}
+
+    def stop_at_step_2(self, start_time):  # the stop check runs once at the top of every step
+        calls["n"] += 1
+        return calls["n"] == 3
+
+    with monkeypatch.context() as m:
+        m.setattr(trainer_mod.Trainer, "_out_of_time", stop_at_step_2)
+        run(tmp_path / "split")
+    (split,) = glob.glob(os.path.join(str(tmp_path / "split"), "LidarSpread", "dgppo", "seed0_*"))
+    st = json.load(open(os.path.join(split, "trainer_state.json")))
+    assert st["next_step"] == 2 and sorted(os.listdir(os.path.join(split, "models"))) == ["0", "2"]
+    with pytest.raises(SystemExit):  # a resume with other hyperparameters is refused
+        run(tmp_path / "split", ["--resume", split, "--lr-actor", "1e-4"])
+    run(tmp_path / "split", ["--resume", split])
+    (once,) = glob.glob(os.path.join(str(tmp_path / "once"), "LidarSpread", "dgppo", "seed0_*"))
+    for net in ("actor", "Vl", "Vh"):
+        a = torch.load(os.path.join(once, "models", "4", f"{net}.pt"), weights_only=True)
+        b = torch.load(os.path.join(split, "models", "4", f"{net}.pt"), weights_only=True)
+        for k in ("params", "m", "v", "state"):
+            assert torch.equal(a[k], b[k]), (net, k)
+    strip = lambda rows: [{k: v for k, v in r.items() if not k.startswith("time")} for r in rows]  # noqa: E731
+    la = strip([json.loads(x) for x in open(os.path.join(once, "log.jsonl"))])
+    lb = strip([json.loads(x) for x in open(os.path.join(split, "log.jsonl"))])
+    assert la == lb

@@ -5,14 +5,37 @@ Multi-GPU (env-sharded, RCCL gradient all-reduce): `python -m torch.distributed.
 `--batch-size` is scaled by the world size (same minibatch count per update)."""
 import argparse
 import datetime
+import json
 import os
 
 import numpy as np
 import yaml
 
 
+# flags a resumed run may change; every other flag must match the run it continues (train_args.json)
+RESUME_FREE = ("resume", "max_minutes", "log_interval", "gpu", "debug", "log_dir", "name")
+
+
+def check_resume_args(args, log_dir):
+    """--resume continues a run with ITS hyperparameters: refuse a command line whose flags differ from the ones the
+    run started with (saved as train_args.json next to config.yaml), except the resume-only flags."""
+    path = os.path.join(log_dir, "train_args.json")
+    if not os.path.exists(path):
+        print(f"> warning: {path} missing (run started before it was written); flags not checked")
+        return
+    with open(path) as f:
+        saved = json.load(f)
+    cur = vars(args)
+    diff = {k: (saved[k], cur.get(k)) for k in saved if k not in RESUME_FREE and saved[k] != cur.get(k)}
+    if diff:
+        raise SystemExit("--resume: flags differ from the run's own (saved, given): " +
+                         ", ".join(f"{k}={v[0]!r} vs {v[1]!r}" for k, v in sorted(diff.items())))
+
+
 def train(args):
     print(f"> Running train.py {args}")
+    if args.resume:
+        check_resume_args(args, args.resume.rstrip("/"))
     if args.gpu is not None:
         os.environ["CUDA_VISIBLE_DEVICES"] = str(args.gpu)
         print(f"> Using GPU: {args.gpu}")
@@ -79,6 +102,8 @@ def train(args):
         with open(f"{log_dir}/config.yaml", "w") as f:
             yaml.safe_dump(vars(args), f)
             yaml.safe_dump(algo.config, f)
+        with open(f"{log_dir}/train_args.json", "w") as f:
+            json.dump(vars(args), f)
     done = trainer.train()
     if world > 1:
         dist.destroy_process_group()
