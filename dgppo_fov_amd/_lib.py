@@ -218,6 +218,13 @@ class GnnAttnArgs(ctypes.Structure):
     ]
 
 
+class GnnLayerArgs(ctypes.Structure):  # ABI 11 dgppo_gnn_layer_args
+    _fields_ = [
+        ("a", GnnAttnArgs), ("QBW", c_f32p), ("qb", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p), ("bu", c_f32p),
+        ("Y", c_f32p),
+    ]
+
+
 class TanhNormalArgs(ctypes.Structure):
     _fields_ = [
         ("rows", ctypes.c_int64),
@@ -307,12 +314,14 @@ SIGNATURES = {
     "dgppo_lagr_advantages": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _I32, _I32, _I32, _I32, _V]),
     "dgppo_lagr_update": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _I64, _I32, _I32, _F32, _F32, _V]),
     "dgppo_gather_env_steps": (ctypes.c_int, [ctypes.POINTER(GatherField), _I32, _V, _I32, _I32, _V]),
+    "dgppo_gnn_layer_supported": (ctypes.c_int, [ctypes.POINTER(GnnLayerArgs)]),
+    "dgppo_gnn_layer_fwd": (ctypes.c_int, [ctypes.POINTER(GnnLayerArgs), ctypes.c_void_p]),
 }
 
 _LIB = None
 
 
-ABI_VERSION = 10  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 11  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

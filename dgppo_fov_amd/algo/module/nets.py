@@ -76,8 +76,8 @@ class ActorNet(_Net):
         self.scale_hid.load_flax(d["ScaleHid"]), self.mean.load_flax(d["OutputDenseMean"])
         self.std.load_flax(d["OutputDenseStdTrans"])
 
-    def _trunk(self, g: GraphBatch):
-        z, gc = self.gnn.fwd(g)
+    def _trunk(self, g: GraphBatch, keep=True):
+        z, gc = self.gnn.fwd(g, keep=keep)
         y, hc = self.head.fwd(z)
         return y, (gc, hc)
 
@@ -151,7 +151,7 @@ class ActorNet(_Net):
             fa.action, fa.log_pi = K._p(action), K._p(log_pi)
             K._chk(_lib.load().dgppo_policy_step(ctypes.byref(fa), _lib.stream_handle(dev)), "dgppo_policy_step")
             return action, log_pi, h2
-        y, _ = self._trunk(g)
+        y, _ = self._trunk(g, keep=False)
         feat, h2, _ = self.gru.fwd(y, h, h_out=h_out)
         _, mu, sr = self._outputs(feat)
         action = action_out if action_out is not None else torch.empty((rows, self.A), device=h.device)
@@ -235,7 +235,7 @@ class VlNet(_Net):
     def graph_means(self, g: GraphBatch, out=None):
         """The GNN part of the value: the agent mean of the last GNN layer's agent rows, (G, 64) (graphs are
         independent here; seq_fwd's sequence structure starts after it)."""
-        z, _ = self.gnn.fwd(g)
+        z, _ = self.gnn.fwd(g, keep=False)
         zm = out if out is not None else torch.empty((g.G, 64), device=g.nodes.device)
         K.agent_mean_fwd(z, zm, g.G, self.n, 64, self.n * 64)
         return zm
@@ -251,7 +251,7 @@ class VlNet(_Net):
             z = gc = None
         else:
             n = self.n
-            z, gc = self.gnn.fwd(g)  # (G*n, 64)
+            z, gc = self.gnn.fwd(g, keep=keep_cache)  # (G*n, 64)
             zm = torch.empty((G, 64), device=dev)
             K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
         y, hc = self.head.fwd(zm)
@@ -299,7 +299,7 @@ class VhNet(_Net):
     def fwd(self, g: GraphBatch, h: torch.Tensor, keep_cache=True):
         """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, W): (G*n, n_cost)."""
         rows = g.G * self.n
-        z, gc = self.gnn.fwd(g)
+        z, gc = self.gnn.fwd(g, keep=keep_cache)
         y, hc = self.head.fwd(z)
         h2, _, rc = self.gru.fwd(y, h)
         out = self.out.fwd(h2, rows)
@@ -349,7 +349,7 @@ class VhGlobalNet(_Net):
         n, dev = self.n, g.nodes.device
         G = S * L
         rows = G * n
-        z, gc = self.gnn.fwd(g)  # (rows, 64)
+        z, gc = self.gnn.fwd(g, keep=keep_cache)  # (rows, 64)
         zm = torch.empty((G, 64), device=dev)
         K.agent_mean_fwd(z, zm, G, n, 64, n * 64)
         W0 = self.head.d0.W()

@@ -33,6 +33,9 @@ from . import kernels as K
 # LayerNorm + ReLU of the MLP heads and the GNN layers' ReLU backward fused into the neighbouring GEMMs' epilogues
 # (gemm epi 1-3, ABI 9); DGPPO_FUSE_LN=0 runs the separate layernorm64 / relu_bwd kernels (A/B, parity tests)
 FUSE_LN = os.environ.get("DGPPO_FUSE_LN", "1") == "1"
+# one GraphTransformer layer forward as ONE kernel ([qt | beta] GEMM + attention + message / update GEMMs, ABI 11
+# dgppo_gnn_layer_fwd) where it applies; DGPPO_FUSED_LAYER=0 runs the unfused chain (A/B, parity tests)
+FUSED_LAYER = os.environ.get("DGPPO_FUSED_LAYER", "1") == "1"
 
 
 # ---- parameter space ------------------------------------------------------------------------
@@ -665,13 +668,54 @@ class GraphTransformer:
         K.gemm(Waug, self.v("bk"), QBW, D + 1, 1, F, lda=H * F, sa=F, ldb=1, sb=F, ldc=W, sc=1, c_off=H * D, batch=H)
         return QBW
 
-    def fwd(self, g: "GraphBatch", xa=None, pre=None, xfull=None):
+    def _fused_fwd(self, g: "GraphBatch", xa, pre, keep: bool):
+        """The layer through dgppo_gnn_layer_fwd (one kernel), or None where it does not apply.  keep: also write
+        [qt | beta], attn and xcat for the backward (else Y only, forward-only passes)."""
+        if xa is not None and pre is None:
+            return None
+        G, n, D, F, H, C = g.G, g.n, self.D, self.F, self.H, g.C
+        R, W = G * n, H * D + H
+        dev = g.nodes.device
+        if xa is None:
+            x, x_gs, D0, pre_W, pre_b = g.nodes, g.N * g.nodes.shape[2], 0, None, None
+        else:
+            raw, cols = g.sender_raw
+            if cols is not None:
+                return None
+            x, x_gs, D0, pre_W, pre_b = raw, g.N * raw.shape[2], raw.shape[2], pre.v("Wu"), pre.v("bu")
+        QBW = self.qb_weights()
+        Y = torch.empty((R, F), device=dev)
+        kw = dict(dims=[G, g.N, g.E, n, D, F, H, C, D0], cand=g.cand, receivers=g.receivers, senders=g.senders,
+                  sidx=g.sidx, x=x, x_gstride=x_gs, ef=g.edges_head, ef_gstride=g.E * 4, scale=1.0 / math.sqrt(F),
+                  xa=xa, xa_gstride=n * D, pre_W=pre_W, pre_b=pre_b, QBW=QBW, Wcat=self.v("Wcat"), Wu=self.v("Wu"),
+                  bu=self.v("bu"), Y=Y)
+        if not ops.gnn_layer_supported(**kw):
+            return None
+        QB = attn = xcat = None
+        if keep:
+            QB = torch.empty((R, W), device=dev)
+            attn = torch.empty((R, H, C), device=dev)
+            xcat = torch.empty((R, H * (D + 5)), device=dev)
+        o = kw
+        torch.ops.dgppo.gnn_layer_fwd(o["dims"], o["cand"], o["receivers"], o["senders"], o["sidx"], o["x"],
+                                      o["x_gstride"], o["ef"], o["ef_gstride"], o["scale"], o["xa"], o["xa_gstride"],
+                                      o["pre_W"], o["pre_b"], o["QBW"], o["Wcat"], o["Wu"], o["bu"], Y, QB, attn, xcat)
+        return Y, ((xa, pre, QBW, QB, attn, xcat, None, Y, None) if keep else None)
+
+    def fwd(self, g: "GraphBatch", xa=None, pre=None, xfull=None, keep=True):
         """One layer on the graph batch.  xa None: senders read the raw nodes (G, N, D) (first layer);
         else xa (G*n, D) holds the agents' rows and the never-receiving nodes are `pre`'s
         Dense_4 + ReLU of their raw rows (agent mode); xfull (G, N, D): every node's row given
         (GNN layers past the second).  Returns Y (G*n, F) = the agents' outputs (only agents
         receive, so only their rows feed the next layer's queries) and the cache.
-        Edge columns past the first 4 add (sum_c attn * efx) @ Wex to the messages (edge_wsum)."""
+        Edge columns past the first 4 add (sum_c attn * efx) @ Wex to the messages (edge_wsum).
+        keep=False: forward only (the fused kernel then skips the backward's intermediates; cache None)."""
+        self.last_fused = False  # which path the last call took (tests)
+        if FUSED_LAYER and xfull is None and not self.EX:
+            out = self._fused_fwd(g, xa, pre, keep)
+            if out is not None:
+                self.last_fused = True
+                return out
         G, N, n = g.G, g.N, g.n
         D, F, H, C = self.D, self.F, self.H, g.C
         dev = g.nodes.device
@@ -693,7 +737,7 @@ class GraphTransformer:
             K.gemm(xcx, self.v("Wex"), M, R, F, H * self.EX, alpha=1.0 / H, beta=1.0)
         Y = torch.empty((R, F), device=dev)
         K.gemm(A, self.v("Wu"), Y, R, F, D, bias=self.v("bu"), addend=M, relu=True, **akw)
-        return Y, (xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull)
+        return Y, ((xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull) if keep else None)
 
     def _rows_in(self, g: "GraphBatch", xa, xfull):
         """The receiving agents' input rows as a GEMM operand: (tensor, row-grouping kwargs)."""
@@ -907,7 +951,7 @@ class GNN:
         K.gemm(Z, L.v("Wu"), out, rows, L.F, L.D, bias=L.v("bu"), relu=True)
         return out
 
-    def fwd(self, g: GraphBatch):
+    def fwd(self, g: GraphBatch, keep=True):
         """Layer 0 reads the raw nodes, layer 1 runs in agent mode (never-receivers' layer-1 rows recomputed
         from the raw rows in the kernel).  Layers l >= 2 (deeper stacks than the reference's defaults) read
         materialised rows X_l (G, N, D): the agents' rows are the previous layer's outputs, every other
@@ -918,17 +962,17 @@ class GNN:
         Zs = [g.nodes.reshape(G * N, g.nodes.shape[2])] if len(self.layers) > 2 else None
         for i, L in enumerate(self.layers):
             if i == 0:
-                Y, c = L.fwd(g)
+                Y, c = L.fwd(g, keep=keep)
             elif i == 1:
-                Y, c = L.fwd(g, xa=Y, pre=self.layers[0])
+                Y, c = L.fwd(g, xa=Y, pre=self.layers[0], keep=keep)
             else:
                 while len(Zs) <= i:
                     Zs.append(self._lift(Zs[-1], len(Zs) - 1, G * N))
                 X = Zs[i].view(G, N, L.D).clone()
                 X[:, :n] = Y.view(G, n, L.D)
-                Y, c = L.fwd(g, xfull=X)
+                Y, c = L.fwd(g, xfull=X, keep=keep)
             caches.append(c)
-        return Y, (caches, Zs)
+        return Y, ((caches, Zs) if keep else None)
 
     def bwd(self, caches, dZ, g: GraphBatch, top_masked=False):
         """top_masked: dZ already carries the last layer's ReLU gate (fused into its producer's GEMM)."""

@@ -287,6 +287,42 @@ def gnn_attn_partial_blocks(dims, cand, receivers, senders, sidx, x, x_gstride, 
     return int(_lib.load().dgppo_gnn_attn_partial_blocks(ctypes.byref(a)))
 
 
+# ---- one GraphTransformer layer forward as one kernel (ABI 11) -------------------------------------------
+def _layer_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride, pre_W,
+                  pre_b, QBW, Wcat, Wu, bu, Y, qb=None, attn=None, xcat=None) -> _lib.GnnLayerArgs:
+    la = _lib.GnnLayerArgs()
+    la.a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, None, None, None, scale, xa,
+                        xa_gstride, pre_W, pre_b)
+    la.a.attn, la.a.xcat = _p(attn), _p(xcat)
+    la.QBW, la.qb, la.Wcat, la.Wu, la.bu, la.Y = _p(QBW), _p(qb), _p(Wcat), _p(Wu), _p(bu), _p(Y)
+    return la
+
+
+def gnn_layer_supported(**kw) -> bool:
+    """Whether dgppo_gnn_layer_fwd covers this layer call (host query; same keyword arguments as gnn_layer_fwd)."""
+    return bool(_lib.load().dgppo_gnn_layer_supported(ctypes.byref(_layer_struct(**kw))))
+
+
+@torch.library.custom_op("dgppo::gnn_layer_fwd", mutates_args=("Y", "qb", "attn", "xcat"))
+def gnn_layer_fwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
+                  x_gstride: int, ef: Tensor, ef_gstride: int, scale: float, xa: Optional[Tensor], xa_gstride: int,
+                  pre_W: Optional[Tensor], pre_b: Optional[Tensor], QBW: Tensor, Wcat: Tensor, Wu: Tensor, bu: Tensor,
+                  Y: Tensor, qb: Optional[Tensor], attn: Optional[Tensor], xcat: Optional[Tensor]) -> None:
+    """One GraphTransformer layer forward (dims as gnn_attn_fwd): Y (G*n, F) = relu(xcat Wcat / H + x_i Wu + bu) with
+    the attention of gnn_attn_fwd in between and [qt | beta] = [x_i 1] QBW, all in one kernel; qb, attn and xcat are
+    optional outputs for the backward (nn/layers.py GraphTransformer.fwd)."""
+    _lib.require_gpu(Y.device, "dgppo::gnn_layer_fwd")
+    la = _layer_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride, pre_W,
+                       pre_b, QBW, Wcat, Wu, bu, Y, qb, attn, xcat)
+    _lib.check(_lib.load().dgppo_gnn_layer_fwd(ctypes.byref(la), _stream(Y)), "dgppo_gnn_layer_fwd")
+
+
+@gnn_layer_fwd.register_fake
+def _gnn_layer_fwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride,
+                        pre_W, pre_b, QBW, Wcat, Wu, bu, Y, qb, attn, xcat) -> None:
+    return None
+
+
 # ---- GAE, clip + Adam ------------------------------------------------------------------------------------
 @torch.library.custom_op("dgppo::gae", mutates_args=("Qh", "Ql"))
 def gae(hs: Tensor, l: Tensor, Vh: Tensor, Vl: Tensor, Qh: Tensor, Ql: Tensor, gamma: float, lam: float) -> None:

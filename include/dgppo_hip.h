@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 10  /* 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 11  /* 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -316,6 +316,29 @@ int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, int32_t E, co
                            const int32_t* receivers, const int32_t* senders, int32_t* sidx, void* stream);
 int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* args, void* stream);
 int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* args, void* stream);
+/* ABI 11: one GraphTransformer layer forward as ONE kernel (dgppo/nn/gnn.py:78-117: Dense_0 / Dense_1 queries and
+ * keys, segment softmax over each receiving agent's incoming edges, Dense_2 / Dense_3 messages, Dense_4 update and
+ * ReLU), replacing the [qt | beta] GEMM, dgppo_gnn_attn_fwd and the two message / update GEMMs of the layer:
+ *   [qt | beta] = [x_i 1] QBW,   xcat = attention over the candidates (as dgppo_gnn_attn_fwd),
+ *   Y = relu(xcat Wcat / H + x_i Wu + bu)
+ * with x_i the receiving agent's input row (full mode: node i of x; agent mode: row i of xa).  Each workgroup
+ * stages whole graphs (raw / agent rows, never-receivers' relu(x_raw pre_W + pre_b) computed once per node) in
+ * LDS with coalesced loads, so the per-candidate reads are LDS reads.  `a` carries the graph and the sender mode
+ * exactly as for dgppo_gnn_attn_fwd (sidx required; a.q / a.qt / a.beta are not read); a.attn, a.xcat and qb are
+ * OPTIONAL outputs (what dgppo_gnn_attn_bwd and the weight gradients read; NULL in forward-only passes).  Scope:
+ * H = 3, C <= 32, n <= 16, F <= 64, 4-wide edges; full mode with D <= 8, or agent mode with D = 32, D0 <= 8 and
+ * pre_W (dgppo_gnn_layer_supported; otherwise use the unfused chain). */
+typedef struct dgppo_gnn_layer_args {
+  dgppo_gnn_attn_args a;
+  const float* QBW;                  /* (D+1, H*D + H): [x 1] QBW = [qt | beta] (Q-free query-key products) */
+  float* qb;                         /* optional out (G*n, H*D + H) [qt | beta] rows */
+  const float* Wcat;                 /* (H*(D+5), F) = [Wv (H*D); We (H*4); bv (H)] per head */
+  const float* Wu; const float* bu;  /* Dense_4: (D, F), (F) */
+  float* Y;                          /* (G*n, F) */
+} dgppo_gnn_layer_args;
+int dgppo_gnn_layer_supported(const dgppo_gnn_layer_args* args);
+int dgppo_gnn_layer_fwd(const dgppo_gnn_layer_args* args, void* stream);
+
 /* Edge features wider than 4 (LidarOmniTarget's 10-wide edges, lidar_omni_target.py edge_dim): the attention
  * kernels see columns 0..3, the remaining EX columns efx (G, E, EX) go through these two.
  *   edge_wsum: out[r, h*EX + j] = sum_c attn[r, h, c] * efx[g, cand[i][c], j] over sidx[r][c] >= 0
