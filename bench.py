@@ -267,7 +267,8 @@ def read_mfma_pmc():
                 "window_executed_tflops": d["total_mfma_tflops_over_window"],
                 "window_frac_of_peak": round(d["total_mfma_tflops_over_window"] / FP32_MFMA_PEAK_TFLOPS, 4),
                 "update_window_ms": None if "update_window_s" not in d else round(d["update_window_s"] * 1e3, 2),
-                "update_mfma_tflop": d.get("update_mfma_tflop"), "src_sha256": d.get("src_sha256")}
+                "update_mfma_tflop": d.get("update_mfma_tflop"), "update_valu_fp32_tflop": d.get("update_valu_fp32_tflop"),
+                "valu_calibration": d.get("valu_calibration"), "src_sha256": d.get("src_sha256")}
     except Exception:
         return None
 
@@ -352,6 +353,17 @@ def ppo_bench(env, dev, world, rank, iters, strong=False):
             executed = {"achieved": round(ach, 2), "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                         "tflop_per_update": pmc["update_mfma_tflop"], "profile_update_ms_traced": pmc["update_window_ms"],
                         "src_sha256": live}
+            if pmc.get("update_valu_fp32_tflop") is not None:
+                # fp32 MFMA runs at the fp32 VALU rate on gfx950 (157.3 TF either way), so the executed fp32 work of
+                # both pipes over the update time is the utilisation of the one fp32 roof
+                tf = pmc["update_mfma_tflop"] + pmc["update_valu_fp32_tflop"]
+                executed_fp32 = {"achieved": round(tf / t_upd, 2), "frac": round(tf / t_upd / FP32_MFMA_PEAK_TFLOPS, 4),
+                                 "tflop_per_update": round(tf, 4), "mfma_tflop": pmc["update_mfma_tflop"],
+                                 "valu_tflop": pmc["update_valu_fp32_tflop"],
+                                 "counters": "SQ_INSTS_VALU_MFMA_MOPS_F32 x 512 + SQ_INSTS_VALU_FLOPS_FP32(_TRANS) "
+                                             "calibrated on known elementwise work (valu_calibration)",
+                                 "valu_calibration": pmc.get("valu_calibration")}
+                executed["executed_fp32"] = executed_fp32
     upd_tf = UPDATE_TFLOP_PER_4096_ENVS * (B_PER_GPU / 4096) * world + ROLLOUT_TFLOP_PER_4096_ENVS / 2 * (
         B_PER_GPU / 4096) * world  # the update runs the deterministic rollout too
     return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),
@@ -359,7 +371,10 @@ def ppo_bench(env, dev, world, rank, iters, strong=False):
             "update_roofline": {"bound": "mfma", "algorithmic_tflop": round(upd_tf, 2),
                                 "achieved": round(upd_tf / t_upd, 2), "peak": FP32_MFMA_PEAK_TFLOPS * world,
                                 "unit": "TFLOP/s", "frac": round(upd_tf / t_upd / (FP32_MFMA_PEAK_TFLOPS * world), 4),
-                                "flops_source": "SURVEY.md 8(d): 22.1 TF per update + 2.65 TF det-rollout inference",
+                                "frac_kind": "algorithmic (node-level projection formulation, SURVEY.md 8(d)), not a "
+                                             "utilisation: the executed work is executed_mfma / executed_fp32",
+                                "flops_source": "SURVEY.md 8(d) minimal node-level formulation: 22.1 TF per update + "
+                                                "2.65 TF det-rollout inference",
                                 "executed_mfma": executed},
             "collect_ms": round(t_col * 1e3, 2),
             "collect_env_steps_per_s": round(B_PER_GPU * T * world / t_col, 1),

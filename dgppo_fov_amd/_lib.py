@@ -218,11 +218,24 @@ class GnnAttnArgs(ctypes.Structure):
     ]
 
 
+class GnnValueTail(ctypes.Structure):  # ABI 11 dgppo_gnn_value_tail
+    _fields_ = [
+        ("W0", c_f32p), ("b0", c_f32p), ("ln0_s", c_f32p), ("ln0_b", c_f32p),
+        ("W1", c_f32p), ("b1", c_f32p), ("ln1_s", c_f32p), ("ln1_b", c_f32p),
+        ("Wi", c_f32p), ("bi", c_f32p), ("Wh", c_f32p), ("bhn", c_f32p), ("Wo", c_f32p), ("bo", c_f32p),
+        ("h_in", c_f32p), ("out", c_f32p), ("n_out", ctypes.c_int32), ("on", ctypes.c_int32),
+    ]
+
+
 class GnnLayerArgs(ctypes.Structure):  # ABI 11 dgppo_gnn_layer_args
     _fields_ = [
         ("a", GnnAttnArgs), ("QBW", c_f32p), ("qb", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p), ("bu", c_f32p),
-        ("Y", c_f32p),
+        ("Y", c_f32p), ("zmean", c_f32p), ("tail", GnnValueTail),
     ]
+
+
+class GnnLayerBwdArgs(ctypes.Structure):  # ABI 11 dgppo_gnn_layer_bwd_args
+    _fields_ = [("a", GnnAttnArgs), ("dY", c_f32p), ("QBW", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p), ("mask", c_f32p)]
 
 
 class TanhNormalArgs(ctypes.Structure):
@@ -316,6 +329,9 @@ SIGNATURES = {
     "dgppo_gather_env_steps": (ctypes.c_int, [ctypes.POINTER(GatherField), _I32, _V, _I32, _I32, _V]),
     "dgppo_gnn_layer_supported": (ctypes.c_int, [ctypes.POINTER(GnnLayerArgs)]),
     "dgppo_gnn_layer_fwd": (ctypes.c_int, [ctypes.POINTER(GnnLayerArgs), ctypes.c_void_p]),
+    "dgppo_gnn_layer_bwd_supported": (ctypes.c_int, [ctypes.POINTER(GnnLayerBwdArgs)]),
+    "dgppo_gnn_layer_bwd_partial_blocks": (ctypes.c_int64, [ctypes.POINTER(GnnLayerBwdArgs)]),
+    "dgppo_gnn_layer_bwd": (ctypes.c_int, [ctypes.POINTER(GnnLayerBwdArgs), ctypes.c_void_p]),
 }
 
 _LIB = None

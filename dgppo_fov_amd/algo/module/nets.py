@@ -235,8 +235,10 @@ class VlNet(_Net):
     def graph_means(self, g: GraphBatch, out=None):
         """The GNN part of the value: the agent mean of the last GNN layer's agent rows, (G, 64) (graphs are
         independent here; seq_fwd's sequence structure starts after it)."""
-        z, _ = self.gnn.fwd(g, keep=False)
         zm = out if out is not None else torch.empty((g.G, 64), device=g.nodes.device)
+        if self.gnn.fwd_epilogue(g, zmean=zm) is not None:  # the mean in the last layer's kernel (Y never stored)
+            return zm
+        z, _ = self.gnn.fwd(g, keep=False)
         K.agent_mean_fwd(z, zm, g.G, self.n, 64, self.n * 64)
         return zm
 
@@ -297,8 +299,18 @@ class VhNet(_Net):
         self.out.load_flax(d["out"])
 
     def fwd(self, g: GraphBatch, h: torch.Tensor, keep_cache=True):
-        """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, W): (G*n, n_cost)."""
+        """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, W): (G*n, n_cost).  Forward only
+        (keep_cache False): GNN, head, GRU step and output Dense in one kernel where it applies (the prepass)."""
         rows = g.G * self.n
+        if not keep_cache and self.gru.simple and len(self.gnn.layers) == 1 and h.shape[1] == 64:
+            out = torch.empty((rows, self.n_cost), device=h.device)
+            hd, cell = self.head, self.gru.cells[0]
+            v = self.ps.view
+            tail_w = [hd.d0.W(), hd.d0.b(), v(hd.ln0.name + ".scale"), v(hd.ln0.name + ".bias"), hd.d1.W(), hd.d1.b(),
+                      v(hd.ln1.name + ".scale"), v(hd.ln1.name + ".bias"), cell.v("Wi"), cell.v("bi"), cell.v("Wh"),
+                      cell.v("bhn"), self.out.W(), self.out.b()]
+            if self.gnn.fwd_epilogue(g, tail=(tail_w, h if h.is_contiguous() else h.contiguous(), out)) is not None:
+                return out, None
         z, gc = self.gnn.fwd(g, keep=keep_cache)
         y, hc = self.head.fwd(z)
         h2, _, rc = self.gru.fwd(y, h)

@@ -42,16 +42,33 @@ struct Lay {
   static constexpr int XP = DM + 4;                               // staged node row pitch (12 / 36 floats)
   static constexpr int HS = DM;                                   // per-head stride of a qt row
   static constexpr int QP = 3 * HS + 4;                           // qt row: qt_h at h*HS, beta_h at 3*HS + h
-  static constexpr int XCP = ((3 * (DM + 5) + 3) / 4) * 4 + 4;    // xcat tile pitch (44 / 116)
+  // xcat tile pitch (44 / 132): at DM = 32 a row also hosts its half-wave's 32 (a, sender) pairs (128 floats) for
+  // the LDS-loop weighted sums; 132 = 4 mod 64 spreads the 16 rows stage 5's MFMA A reads touch over the banks
+  static constexpr int XCP = DM == 32 ? 132 : ((3 * (DM + 5) + 3) / 4) * 4 + 4;
 };
+
+constexpr int kYP = 68;  // Y / carry tile pitch (64 + 4)
 
 struct Carve {
-  int rx, qt, pre;  // float offsets: node rows at 0 | raw rows / xcat tile | qt rows | pre_W, pre_b
-  size_t floats;
+  // float offsets: node rows at 0 | raw rows / xcat tile | qt rows | pre_W, pre_b | Y tile (zmean, tail) | tail
+  // carries [16][kYP] | tail LayerNorm parameters [4][64] | per-wave pair weights [4][64] float4 (LDS-loop sums)
+  int rx, qt, pre, yt, hb, lnp, pa;
+  int floats;
 };
 
+// weighted sums xbar_h = sum_c a_hc x_c (and the backward's dqt) by an LDS loop over the candidates (one lane per
+// output column) instead of transposed DPP reductions: DGPPO_LAYER_WSUM=lds|dpp.  Default dpp: the LDS loop measured
+// slower (forward 241 vs 216 us per D = 32 call, backward 690 vs 668 us)
+static bool wsum_lds() {
+  static const bool v = [] {
+    const char* e = getenv("DGPPO_LAYER_WSUM");
+    return e && e[0] == 'l';
+  }();
+  return v;
+}
+
 template <int DM>
-Carve carve(int gpb, int N, bool agent) {
+Carve carve(int gpb, int N, bool agent, bool ytile, bool tail, bool wsl = wsum_lds()) {
   using L = Lay<DM>;
   Carve c;
   const int xs = gpb * N * L::XP;
@@ -60,7 +77,18 @@ Carve carve(int gpb, int N, bool agent) {
   c.rx = (xs + 3) & ~3;
   c.qt = c.rx + ((raw > xct ? raw : xct) + 3) / 4 * 4;
   c.pre = c.qt + kRows * L::QP;
-  c.floats = (size_t)c.pre + (agent ? kD0 * 32 + 32 : 0);
+  int o = c.pre + (agent ? kD0 * 32 + 32 : 0);
+  // the Y tile reuses the xcat tile when that is wide enough (read by stage 5's MFMAs, then a barrier)
+  c.yt = (ytile || tail) ? (L::XCP >= kYP ? c.rx : o) : 0;
+  if ((ytile || tail) && L::XCP < kYP) o += kRows * kYP;
+  c.hb = tail ? o : 0;
+  o += tail ? kRows * kYP : 0;
+  c.lnp = tail ? o : 0;
+  o += tail ? 4 * 64 : 0;
+  const bool pa_own = wsl && L::XCP < 128;  // else the pairs live in the xcat tile's rows
+  c.pa = pa_own ? o : 0;
+  o += pa_own ? 4 * 64 * 4 : 0;
+  c.floats = o;
   return c;
 }
 
@@ -68,9 +96,56 @@ __device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int DM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void gnn_layer_fwd_kernel(
-    dgppo_gnn_layer_args p, int gpb, int o_rx, int o_qt, int o_pre) {
+// LayerNorm(64) (eps 1e-6) + ReLU in place over the 16 rows of a [16][kYP] tile: 8 lanes per row (threads 0..127;
+// the others return), flax's mean / E[x^2] - mean^2 form as the GEMM epilogue computes it
+__device__ __forceinline__ void ln_relu64(float* Y, const float* scale, const float* bias) {
+  if (threadIdx.x >= kRows * 8) return;
+  const int r = threadIdx.x >> 3, q = threadIdx.x & 7;
+  float v[8];
+  float s = 0.0f, s2 = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = Y[r * kYP + q * 8 + j];
+    s += v[j];
+    s2 += v[j] * v[j];
+  }
+#pragma unroll
+  for (int o = 4; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  const float mean = s / 64.0f;
+  float var = s2 / 64.0f - mean * mean;
+  var = var > 0.0f ? var : 0.0f;
+  const float rstd = 1.0f / sqrtf(var + 1e-6f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = q * 8 + j;
+    const float o = ((v[j] - mean) * rstd) * scale[col] + bias[col];
+    Y[r * kYP + col] = o > 0.0f ? o : 0.0f;
+  }
+}
+
+// acc (16 rows x the wave's 16 columns 16 ct + (lane & 15)) = A (LDS tile [16][lda], K = 64) @ W (64 x ldw, global,
+// columns 16 ct ..); every B operand loaded before the first MFMA
+__device__ __forceinline__ f32x4 dense64(const float* A, int lda, const float* W, int ldw, int ct, int N) {
+  const int lane = threadIdx.x & 63, i16 = lane & 15, kq = lane >> 4;
+  const int col = 16 * ct + i16;
+  float b[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) b[ks] = col < N ? W[(4 * ks + kq) * ldw + col] : 0.0f;
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) acc = mma(A[i16 * lda + 4 * ks + kq], b[ks], acc);
+  return acc;
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+template <int DM, bool TAIL, bool WSL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 4, 8))) void gnn_layer_fwd_kernel(
+    dgppo_gnn_layer_args p, int gpb, Carve cv) {
+  const int o_rx = cv.rx, o_qt = cv.qt, o_pre = cv.pre;
   using L = Lay<DM>;
   constexpr int XP = L::XP, HS = L::HS, QP = L::QP, XCP = L::XCP;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -141,29 +216,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
           f32x4{v0 > 0.0f ? v0 : 0.0f, v1 > 0.0f ? v1 : 0.0f, v2 > 0.0f ? v2 : 0.0f, v3 > 0.0f ? v3 : 0.0f};
     }
   }
-  // ---- stage 3: [qt | beta] = [x_i 1] QBW (16 x (D+1) x W) on MFMA; reads only the receivers' rows (stage 1)
+  // ---- stage 3: [qt | beta] = [x_i 1] QBW (16 x (D+1) x W) on MFMA; reads only the receivers' rows (stage 1).
+  // Every B operand of the wave's (at most two) column tiles is loaded before the first MFMA: one L2 round trip
+  // instead of one per k-step.
   {
+    constexpr int KS = (DM + 4) / 4;  // k-steps over D + 1 <= DM + 1 rows
     const bool ract = i16 < nrec;
     const int gl = ract ? i16 / n : 0, il = ract ? i16 - gl * n : 0;
     const float* arow = xs + (gl * N + il) * XP;
-    const int ntile = (W + 15) >> 4, ksteps = (D + 4) >> 2;
-    for (int ct = wave; ct < ntile; ct += 4) {
-      const int col = 16 * ct + i16;
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int ks = 0; ks < ksteps; ++ks) {
-        const int k = 4 * ks + kq;
-        const float av = !ract ? 0.0f : (k < D ? arow[k] : (k == D ? 1.0f : 0.0f));
-        const float bv = (k <= D && col < W) ? p.QBW[k * W + col] : 0.0f;
-        acc = mma(av, bv, acc);
-      }
-      if (col < W) {
-        const int dst = col < kH * D ? (col / D) * HS + (col % D) : kH * HS + (col - kH * D);
+    const int ntile = (W + 15) >> 4;
+    float bq[2][KS];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * kq + i;
-          if (r < nrec) {
-            qts[r * QP + dst] = acc[i];
-            if (p.qb) p.qb[(row0 + r) * W + col] = acc[i];
+    for (int t = 0; t < 2; ++t) {
+      const int col = 16 * (wave + 4 * t) + i16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = 4 * ks + kq;
+        bq[t][ks] = (k <= D && col < W) ? p.QBW[k * W + col] : 0.0f;
+      }
+    }
+    float aq[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 4 * ks + kq;
+      aq[ks] = !ract ? 0.0f : (k < D ? arow[k] : (k == D ? 1.0f : 0.0f));
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ct = wave + 4 * t;
+      if (ct < ntile) {
+        const int col = 16 * ct + i16;
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = mma(aq[ks], bq[t][ks], acc);
+        if (col < W) {
+          const int dst = col < kH * D ? (col / D) * HS + (col % D) : kH * HS + (col - kH * D);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * kq + i;
+            if (r < nrec) {
+              qts[r * QP + dst] = acc[i];
+              if (p.qb) p.qb[(row0 + r) * W + col] = acc[i];
+            }
           }
         }
       }
@@ -221,19 +315,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       }
       float* o = a.xcat ? a.xcat + row * WX : nullptr;
       float* ot = xc + rl * XCP;
+      if constexpr (WSL) {
+        // xbar_h[d] = sum_c a_hc x_c[d]: the row's (a, sender) pairs through the wave's LDS slots, lane c of the
+        // half-wave owns column d = c and walks the candidates (sender row reads: consecutive columns of one row)
+        // the half-wave's 32 slots: its own xcat row (written only after the loop) or, for narrow rows, a region
+        f32x4* pr = XCP >= 128 ? (f32x4*)ot : (f32x4*)(lds + cv.pa) + wave * 64 + slot * 32;
+        pr[c] = f32x4{aw[0], aw[1], aw[2], __int_as_float(ok ? gl * N + s : -1)};
+        lanes::wave_sync();
+        const int d = c < D ? c : 0;
+        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 8
+        for (int cc = 0; cc < 32; ++cc) {
+          if (cc < C) {
+            const f32x4 P = pr[cc];
+            const int node = __float_as_int(P[3]);
+            const float xv = node >= 0 ? xs[node * XP + d] : 0.0f;
+            s0 += P[0] * xv;
+            s1 += P[1] * xv;
+            s2 += P[2] * xv;
+          }
+        }
+        if (active && c < D) {
+          ot[c] = s0, ot[D + c] = s1, ot[2 * D + c] = s2;
+          if (o) o[c] = s0, o[D + c] = s1, o[2 * D + c] = s2;
+        }
+        lanes::wave_sync();  // the slots are rewritten next sub-round
+      } else {
 #pragma unroll
-      for (int h = 0; h < kH; ++h) {
-        float v[DM];
+        for (int h = 0; h < kH; ++h) {
+          float v[DM];
 #pragma unroll
-        for (int d = 0; d < DM; ++d) v[d] = aw[h] * x[d];
-        int cnt;
-        const int base = lanes::treduce32(v, cnt);
+          for (int dd = 0; dd < DM; ++dd) v[dd] = aw[h] * x[dd];
+          int cnt;
+          const int base = lanes::treduce32(v, cnt);
 #pragma unroll
-        for (int j = 0; j < lanes::tr_final<DM>(); ++j) {
-          const int q = base + j;
-          if (active && j < cnt && q < D) {
-            ot[h * D + q] = v[j];
-            if (o) o[h * D + q] = v[j];
+          for (int j = 0; j < lanes::tr_final<DM>(); ++j) {
+            const int q = base + j;
+            if (active && j < cnt && q < D) {
+              ot[h * D + q] = v[j];
+              if (o) o[h * D + q] = v[j];
+            }
           }
         }
       }
@@ -262,41 +383,130 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
   __syncthreads();
 
-  // ---- stage 5: Y = relu(xcat Wcat / H + x_i Wu + bu) on MFMA (16 x 111 x F and 16 x D x F), a wave per 16 columns
+  // ---- stage 5: Y = relu(xcat Wcat / H + x_i Wu + bu) on MFMA (16 x 3(D+5) x F and 16 x D x F), a wave per 16
+  // columns; the wave's B operands are all loaded before its first MFMA (one L2 round trip).  Y goes to global
+  // memory and / or the Y tile (forward-only epilogues)
+  const bool ytile = TAIL || p.zmean != nullptr;
+  float* yt = lds + cv.yt;
   {
+    constexpr int KM = (3 * (DM + 5) + 3) / 4, KU = DM / 4;
     const int WX = kH * (D + 5);
-    const bool ract = i16 < nrec;
-    const int gl = ract ? i16 / n : 0, il = ract ? i16 - gl * n : 0;
-    const float* arow = xs + (gl * N + il) * XP;
-    const float* xrow = xc + i16 * XCP;
-    const int nct = (F + 15) >> 4;
-    for (int ct = wave; ct < nct; ct += 4) {
-      const int col = 16 * ct + i16;
-      const bool cok = col < F;
-      f32x4 am = {0.0f, 0.0f, 0.0f, 0.0f}, au = {0.0f, 0.0f, 0.0f, 0.0f};
-      const int km = (WX + 3) >> 2;
-      for (int ks = 0; ks < km; ++ks) {
+    const int ct = wave;
+    const int col = 16 * ct + i16;
+    const bool cok = col < F;
+    f32x4 yv = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (16 * ct < F) {
+      float bm[KM], bu4[KU];
+#pragma unroll
+      for (int ks = 0; ks < KM; ++ks) {
         const int k = 4 * ks + kq;
-        const float av = (ract && k < WX) ? xrow[k] : 0.0f;
-        const float bv = (cok && k < WX) ? p.Wcat[k * F + col] : 0.0f;
-        am = mma(av, bv, am);
+        bm[ks] = (cok && k < WX) ? p.Wcat[k * F + col] : 0.0f;
       }
-      const int ku = (D + 3) >> 2;
-      for (int ks = 0; ks < ku; ++ks) {
+#pragma unroll
+      for (int ks = 0; ks < KU; ++ks) {
         const int k = 4 * ks + kq;
-        const float av = (ract && k < D) ? arow[k] : 0.0f;
-        const float bv = (cok && k < D) ? p.Wu[k * F + col] : 0.0f;
-        au = mma(av, bv, au);
+        bu4[ks] = (cok && k < D) ? p.Wu[k * F + col] : 0.0f;
       }
       const float bias = cok ? p.bu[col] : 0.0f;
+      const bool ract = i16 < nrec;
+      const int gl = ract ? i16 / n : 0, il = ract ? i16 - gl * n : 0;
+      const float* arow = xs + (gl * N + il) * XP;
+      const float* xrow = xc + i16 * XCP;
+      f32x4 am = {0.0f, 0.0f, 0.0f, 0.0f}, au = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < KM; ++ks) {
+        const int k = 4 * ks + kq;
+        am = mma((ract && k < WX) ? xrow[k] : 0.0f, bm[ks], am);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KU; ++ks) {
+        const int k = 4 * ks + kq;
+        au = mma((ract && k < D) ? arow[k] : 0.0f, bu4[ks], au);
+      }
       const float inv_h = 1.0f / (float)kH;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * kq + i;
-        if (r < nrec && cok) {
-          const float y = (au[i] + bias) + am[i] * inv_h;
-          p.Y[(row0 + r) * F + col] = y > 0.0f ? y : 0.0f;
-        }
+        const float y = (au[i] + bias) + am[i] * inv_h;
+        yv[i] = y > 0.0f ? y : 0.0f;
+        if (p.Y && r < nrec && cok) p.Y[(row0 + r) * F + col] = yv[i];
+      }
+    }
+    if (ytile) {
+      __syncthreads();  // the Y tile may alias the xcat tile the MFMAs above read
+      if (16 * ct < F && cok)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) yt[(4 * kq + i) * kYP + col] = yv[i];
+      __syncthreads();
+    }
+  }
+  // ---- zmean: per-graph mean of the agent rows (agents in order, then / n)
+  if (p.zmean) {
+    for (int t = tid; t < ng * F; t += 256) {
+      const int g = t / F, f = t - g * F;
+      float sacc = 0.0f;
+      for (int i = 0; i < n; ++i) sacc += yt[(g * n + i) * kYP + f];
+      p.zmean[(g0 + g) * F + f] = sacc / n;
+    }
+  }
+  // ---- value-net tail (forward only): MLP head -> GRUCell(h_in) -> Dense(n_out)
+  if constexpr (TAIL) {
+    const dgppo_gnn_value_tail& tl = p.tail;
+    float* hb = lds + cv.hb;
+    float* lnp = lds + cv.lnp;
+    for (int t = tid; t < kRows * 64; t += 256) {
+      const int r = t >> 6, f = t & 63;
+      hb[r * kYP + f] = r < nrec ? tl.h_in[(row0 + r) * 64 + f] : 0.0f;
+    }
+    {
+      const int q = tid >> 6;
+      const float* src = q == 0 ? tl.ln0_s : q == 1 ? tl.ln0_b : q == 2 ? tl.ln1_s : tl.ln1_b;
+      lnp[tid] = src[tid & 63];
+    }
+    __syncthreads();
+    const int col = 16 * wave + i16;
+    // head: two Dense(64) + LayerNorm + ReLU, in place in the Y tile
+#pragma unroll 1
+    for (int l = 0; l < 2; ++l) {
+      const f32x4 acc = dense64(yt, kYP, l == 0 ? tl.W0 : tl.W1, 64, wave, 64);
+      const float b = (l == 0 ? tl.b0 : tl.b1)[col];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) yt[(4 * kq + i) * kYP + col] = acc[i] + b;
+      __syncthreads();
+      ln_relu64(yt, lnp + 128 * l, lnp + 128 * l + 64);
+      __syncthreads();
+    }
+    // GRU: wave w's column tiles w, w+4, w+8 = the r, z, n gates of hidden columns 16w .. 16w+15
+    f32x4 gi[3], gh[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      gi[t] = dense64(yt, kYP, tl.Wi, 192, wave + 4 * t, 192);
+      gh[t] = dense64(hb, kYP, tl.Wh, 192, wave + 4 * t, 192);
+    }
+    const float bir = tl.bi[col], biz = tl.bi[64 + col], bin = tl.bi[128 + col], bhn = tl.bhn[col];
+    float hn[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * kq + i;
+      const float rg = sigm(gi[0][i] + bir + gh[0][i]);
+      const float zg = sigm(gi[1][i] + biz + gh[1][i]);
+      const float ng2 = tanhf(gi[2][i] + bin + rg * (gh[2][i] + bhn));
+      hn[i] = (1.0f - zg) * ng2 + zg * hb[r * kYP + col];
+    }
+    __syncthreads();  // every wave has read hb
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * kYP + col] = hn[i];
+    __syncthreads();
+    // output Dense (64 -> n_out <= 16): wave 0
+    if (wave == 0) {
+      const f32x4 acc = dense64(hb, kYP, tl.Wo, tl.n_out, 0, tl.n_out);
+      const bool ok = i16 < tl.n_out;
+      const float b = ok ? tl.bo[i16] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * kq + i;
+        if (ok && r < nrec) tl.out[(row0 + r) * tl.n_out + i16] = acc[i] + b;
       }
     }
   }
@@ -304,9 +514,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 
 bool supported(const dgppo_gnn_layer_args* p) {
   const dgppo_gnn_attn_args& a = p->a;
+  const bool tail = p->tail.on != 0;
   if (a.H != kH || a.C < 1 || a.C > 32 || a.n_agents < 1 || a.n_agents > kRows || a.F < 1 || a.F > 64 || !a.sidx ||
-      !a.cand || !a.x || !a.ef || !p->QBW || !p->Wcat || !p->Wu || !p->bu || !p->Y || a.G < 0 || a.N < a.n_agents)
+      !a.cand || !a.x || !a.ef || !p->QBW || !p->Wcat || !p->Wu || !p->bu || a.G < 0 || a.N < a.n_agents)
     return false;
+  if (!p->Y && !p->zmean && !tail) return false;
+  if (tail) {
+    const dgppo_gnn_value_tail& t = p->tail;
+    if (a.xa || a.F != 64 || p->Y || p->qb || a.attn || a.xcat || p->zmean || t.n_out < 1 || t.n_out > 16 || !t.W0 ||
+        !t.b0 || !t.ln0_s || !t.ln0_b || !t.W1 || !t.b1 || !t.ln1_s || !t.ln1_b || !t.Wi || !t.bi || !t.Wh || !t.bhn ||
+        !t.Wo || !t.bo || !t.h_in || !t.out)
+      return false;
+  }
   if (((uintptr_t)a.ef & 15) || (a.ef_gstride & 3)) return false;
   if (a.xa == nullptr) {
     if (a.D < 1 || a.D > 8 || a.pre_W) return false;
@@ -315,8 +534,9 @@ bool supported(const dgppo_gnn_layer_args* p) {
     if (((uintptr_t)a.xa & 15) || (a.xa_gstride & 3)) return false;
   }
   const int gpb = kRows / a.n_agents;
-  const Carve c = a.xa ? carve<32>(gpb, a.N, true) : carve<8>(gpb, a.N, false);
-  return c.floats * sizeof(float) <= 64 * 1024;
+  const bool yt = p->zmean != nullptr;
+  const Carve c = a.xa ? carve<32>(gpb, a.N, true, yt, false) : carve<8>(gpb, a.N, false, yt, tail);
+  return (size_t)c.floats * sizeof(float) <= 64 * 1024;
 }
 
 }  // namespace
@@ -332,14 +552,522 @@ extern "C" int dgppo_gnn_layer_fwd(const dgppo_gnn_layer_args* p, void* stream) 
   const int gpb = kRows / a.n_agents;
   const unsigned grid = (unsigned)((a.G + gpb - 1) / gpb);
   hipStream_t s = (hipStream_t)stream;
+  const bool yt = p->zmean != nullptr, tail = p->tail.on != 0, wsl = wsum_lds();
+  const size_t b32 = (size_t)carve<32>(gpb, a.N, true, yt, false).floats * sizeof(float);
+  const size_t b8 = (size_t)carve<8>(gpb, a.N, false, yt, tail).floats * sizeof(float);
+#define GL_LAUNCH(DMv, TAILv, WSLv, bytes)                                                                        \
+  hipLaunchKernelGGL((gnn_layer_fwd_kernel<DMv, TAILv, WSLv>), dim3(grid), dim3(256), bytes, s, *p, gpb,          \
+                     carve<DMv>(gpb, a.N, DMv == 32, yt, TAILv))
   if (a.xa) {
-    const Carve c = carve<32>(gpb, a.N, true);
-    hipLaunchKernelGGL(gnn_layer_fwd_kernel<32>, dim3(grid), dim3(256), c.floats * sizeof(float), s, *p, gpb, c.rx,
-                       c.qt, c.pre);
+    if (wsl) GL_LAUNCH(32, false, true, b32);
+    else GL_LAUNCH(32, false, false, b32);
+  } else if (tail) {
+    if (wsl) GL_LAUNCH(8, true, true, b8);
+    else GL_LAUNCH(8, true, false, b8);
   } else {
-    const Carve c = carve<8>(gpb, a.N, false);
-    hipLaunchKernelGGL(gnn_layer_fwd_kernel<8>, dim3(grid), dim3(256), c.floats * sizeof(float), s, *p, gpb, c.rx,
-                       c.qt, c.pre);
+    if (wsl) GL_LAUNCH(8, false, true, b8);
+    else GL_LAUNCH(8, false, false, b8);
+  }
+#undef GL_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// ================================================================================================================
+// Backward (dgppo_gnn_layer_bwd): the row-block attention backward (attn.hip attn_bwd2r: softmax backward, dqt by
+// transposed DPP reductions, sender gradients, the never-receivers' Dense_4 gradient as MFMA [x_raw | 1]^T dz over
+// 16-pair chunks) on graphs staged in LDS as in the forward, with the GEMMs on each side in the kernel:
+//   prologue  dxcat = dY Wcat^T / H            (16 x 64 x 111 on MFMA; the unfused chain's dxcat GEMM + HBM trip)
+//   epilogue  dxa = agent senders' gradients + dY Wu^T + [dqt | dbeta] QBW[:D]^T, ReLU mask   (two GEMMs)
+// A persistent workgroup walks blocks of gpb = 16 / n whole graphs.  The agent senders' gradients of each
+// sub-round's 8 receiving rows go to an LDS image and are folded into the block's dxa accumulator in fixed
+// receiver order after each sub-round; the pre-gradient accumulators are combined over waves in fixed order into
+// one partial row per workgroup.  Deterministic, no atomics.
+// ================================================================================================================
+namespace dgppo {
+namespace {
+namespace lb {
+constexpr int kPS = 44;  // pre-gradient chunk staging row: dz (0..31) | x_raw (32..39) | 1 (40)
+template <int DM>
+struct Lay {
+  // GP: a dxcat row, then the row's [dqt | dbeta]; at DM = 32 wide enough (132 >= 128) to host the half-wave's
+  // 32 (dl, sender) pairs of the LDS-loop dqt sums in between
+  static constexpr int XP = DM + 4, HS = DM, QP = 3 * HS + 4, GP = DM == 32 ? 132 : 3 * HS + 16;
+};
+struct Carve {
+  int raw, qt, gs, img, acc, stg, pre, pa;
+  int floats;
+};
+template <int DM>
+Carve carve(int gpb, int N, int n, int F) {
+  using L = Lay<DM>;
+  constexpr bool agent = DM == 32;
+  Carve c;
+  int o = (gpb * N * L::XP + 3) & ~3;
+  c.raw = o;
+  o += agent ? gpb * N * kD0 : 0;
+  c.qt = o;
+  o += kRows * L::QP;
+  c.gs = o;
+  o += kRows * L::GP;
+  c.img = o;  // dY tile [16][F + 4] for the dxcat GEMM, then the agent-sender image [8][n][DM]
+  const int dz = kRows * (F + 4), im = agent ? 8 * n * DM : 0;
+  o += ((dz > im ? dz : im) + 3) & ~3;
+  c.acc = o;
+  o += agent ? kRows * DM : 0;
+  c.stg = o;  // per wave [16][kPS]; the epilogue's [2][16][32] partial products afterwards
+  o += agent ? 4 * 16 * kPS : 0;
+  c.pre = o;
+  o += agent ? kD0 * 32 + 32 : 0;
+  const bool pa_own = wsum_lds() && L::GP < 128;  // else the pair slots live in the gs rows
+  c.pa = pa_own ? o : 0;
+  o += pa_own ? 4 * 64 * 4 : 0;
+  c.floats = o;
+  return c;
+}
+template <int DM>
+int64_t grid_cap() {
+  return DM == 32 ? 512 : 2048;  // resident workgroups: 2 per CU at the DM = 32 carve (~65 KB of LDS)
+}
+}  // namespace lb
+
+template <int DM, bool WSL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 2 : 4, 8))) void gnn_layer_bwd_kernel(
+    dgppo_gnn_layer_bwd_args p, int gpb, int64_t nblk, lb::Carve cv) {
+  using L = lb::Lay<DM>;
+  constexpr int XP = L::XP, HS = L::HS, QP = L::QP, GP = L::GP, kPS = lb::kPS;
+  constexpr bool agent = DM == 32;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const dgppo_gnn_attn_args& a = p.a;
+  float* xs = lds;                // [gpb * N][XP]
+  float* raw = lds + cv.raw;      // agent mode: raw rows [gpb * N][8]
+  float* qts = lds + cv.qt;       // [16][QP]: qt_h (HS stride) | beta_h at 3 HS + h
+  float* gs = lds + cv.gs;        // [16][GP]: dxcat (dxbar_h HS stride | debar 3HS.. | dsig 3HS+12..); then [dqt | dbeta]
+  float* img = lds + cv.img;      // dY tile [16][F + 4]; then the agent-sender image [8][n][DM]
+  float* dxacc = lds + cv.acc;    // [16][DM] the block's dxa rows
+  float* stg = lds + cv.stg;      // per wave [16][kPS]
+  float* preW = lds + cv.pre;     // [8][32] | pre_b [32]
+  float* preb = preW + kD0 * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int slot = lane >> 5, cc = lane & 31;
+  const int n = a.n_agents, N = a.N, D = a.D, F = a.F, C = a.C;
+  const int W = kH * D + kH, WX = kH * (D + 5), FP = F + 4;
+  const int64_t qld = a.qt_ld ? a.qt_ld : W;
+  const bool want_dxa = agent && a.dxa != nullptr;
+  const bool want_pre = agent && a.dpre_part != nullptr;
+  if constexpr (agent) {
+    const int k = tid >> 5, d = tid & 31;
+    preW[tid] = k < a.D0 ? a.pre_W[k * D + d] : 0.0f;
+    if (tid < 32) preb[tid] = a.pre_b[tid];
+  }
+  f32x4 gacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // [x_raw | 1]^T dz
+  float* ws = stg + wave * 16 * kPS;
+  const int TQ = (D + 3) >> 2;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t g0 = blk * gpb;
+    const int ng = (int)((int64_t)a.G - g0 < gpb ? (int64_t)a.G - g0 : gpb);
+    const int nrec = ng * n;
+    const int64_t row0 = g0 * n;
+    // ---- stage 1: graphs, [qt | beta] rows, dY rows into LDS; dxcat tile and dxa accumulator cleared
+    if constexpr (agent) {
+      const int D0 = a.D0;
+      for (int t = tid; t < ng * N * kD0; t += 256) {
+        const int node = t >> 3, k = t & 7;
+        const int g = node / N, j = node - g * N;
+        raw[t] = k < D0 ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D0 + k] : 0.0f;
+      }
+      for (int t = tid; t < nrec * (DM / 4); t += 256) {
+        const int r = t / (DM / 4), q = t - r * (DM / 4);
+        const int g = r / n, i = r - g * n;
+        *(f32x4*)(xs + (g * N + i) * XP + 4 * q) =
+            *(const f32x4*)(a.xa + (g0 + g) * a.xa_gstride + (int64_t)i * D + 4 * q);
+      }
+      for (int t = tid; t < kRows * DM; t += 256) dxacc[t] = 0.0f;
+    } else {
+      for (int t = tid; t < ng * N * XP; t += 256) {
+        const int node = t / XP, k = t - node * XP;
+        const int g = node / N, j = node - g * N;
+        xs[t] = k < D ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D + k] : 0.0f;
+      }
+    }
+    for (int t = tid; t < kRows * QP; t += 256) {
+      const int r = t / QP, k = t - r * QP;
+      int src = -1;
+      if (k < kH * HS) {
+        const int h = k / HS, d = k - h * HS;
+        src = d < D ? h * D + d : -1;
+      } else if (k - kH * HS < kH) {
+        src = kH * D + (k - kH * HS);
+      }
+      qts[t] = (r < nrec && src >= 0) ? a.qt[(row0 + r) * qld + src] : 0.0f;
+    }
+    for (int t = tid; t < kRows * F; t += 256) {
+      const int r = t / F, f = t - r * F;
+      img[r * FP + f] = r < nrec ? p.dY[(row0 + r) * F + f] : 0.0f;
+    }
+    for (int t = tid; t < kRows * GP; t += 256) gs[t] = 0.0f;
+    __syncthreads();
+    // ---- stage 2: never-receivers' rows (agent mode; the forward's order of operations) and dxcat = dY Wcat^T / H
+    if constexpr (agent) {
+      const int nn = N - n;
+      for (int t = tid; t < ng * nn * (DM / 4); t += 256) {
+        const int q = t & (DM / 4 - 1), rr = t / (DM / 4);
+        const int g = rr / nn, j = n + rr - g * nn;
+        const float* xr = raw + (g * N + j) * kD0;
+        const f32x4 b = *(const f32x4*)(preb + 4 * q);
+        float v0 = b[0], v1 = b[1], v2 = b[2], v3 = b[3];
+#pragma unroll
+        for (int k = 0; k < kD0; ++k) {
+          const float xk = xr[k];
+          const f32x4 w = *(const f32x4*)(preW + k * 32 + 4 * q);
+          v0 += xk * w[0];
+          v1 += xk * w[1];
+          v2 += xk * w[2];
+          v3 += xk * w[3];
+        }
+        *(f32x4*)(xs + (g * N + j) * XP + 4 * q) =
+            f32x4{v0 > 0.0f ? v0 : 0.0f, v1 > 0.0f ? v1 : 0.0f, v2 > 0.0f ? v2 : 0.0f, v3 > 0.0f ? v3 : 0.0f};
+      }
+    }
+    {
+      constexpr int KS = 16;  // k-steps over F <= 64
+      const int ntile = (WX + 15) >> 4;
+      float bq[2][KS];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int col = 16 * (wave + 4 * t) + i16;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k = 4 * ks + kq;
+          bq[t][ks] = (k < F && col < WX) ? p.Wcat[(int64_t)col * F + k] : 0.0f;
+        }
+      }
+      float aq[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = 4 * ks + kq;
+        aq[ks] = k < F ? img[i16 * FP + k] : 0.0f;
+      }
+      const float inv_h = 1.0f / (float)kH;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ct = wave + 4 * t;
+        if (ct < ntile) {
+          const int col = 16 * ct + i16;
+          f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) acc = mma(aq[ks], bq[t][ks], acc);
+          if (col < WX) {
+            const int dst = col < kH * D ? (col / D) * HS + (col % D) : kH * HS + (col - kH * D);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gs[(4 * kq + i) * GP + dst] = acc[i] * inv_h;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- stage 3: the pairs, two sub-rounds of 8 receiving rows
+#pragma unroll 1
+    for (int sr = 0; sr < 2; ++sr) {
+      const int rl = 2 * wave + 8 * sr + slot, lr = rl - 8 * sr;
+      const bool active = rl < nrec;
+      const int64_t row = row0 + rl;
+      const int gl = active ? rl / n : 0;
+      const int i = active ? rl - gl * n : 0;
+      if (want_dxa) {
+        for (int e = lane; e < 2 * n * DM; e += 64) img[2 * wave * n * DM + e] = 0.0f;
+        lanes::wave_sync();
+      }
+      int s = -1, e = 0;
+      if (active && cc < C) {
+        e = a.cand[i * C + cc];
+        s = a.sidx[row * C + cc];
+      }
+      const bool ok = s >= 0;
+      float av[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) av[h] = ok ? a.attn[(row * kH + h) * C + cc] : 0.0f;
+      f32x4 ef = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (ok) ef = *(const f32x4*)(a.ef + (g0 + gl) * a.ef_gstride + (int64_t)e * 4);
+      float x[DM];
+      {
+        const float* xr = xs + (gl * N + (ok ? s : 0)) * XP;
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q) {
+          const f32x4 v = ok ? *(const f32x4*)(xr + 4 * q) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          x[4 * q] = v[0], x[4 * q + 1] = v[1], x[4 * q + 2] = v[2], x[4 * q + 3] = v[3];
+        }
+      }
+      const bool viapre = agent && ok && s >= n;
+      // ---- softmax backward
+      const float* gv = gs + rl * GP;
+      float dl[kH], dbeta[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        float da = 0.0f;
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q)
+          if (q < TQ) {
+            const f32x4 gq = ((const f32x4*)(gv + HS * h))[q];
+            da += x[4 * q] * gq[0] + x[4 * q + 1] * gq[1] + x[4 * q + 2] * gq[2] + x[4 * q + 3] * gq[3];
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) da += gv[3 * HS + 4 * h + j] * ef[j];
+        da += gv[3 * HS + 12 + h];
+        da = ok ? da : 0.0f;
+        const float dot = lanes::sum32(av[h] * da);
+        dl[h] = ok ? av[h] * (da - dot) * a.scale : 0.0f;
+        dbeta[h] = lanes::sum32(dl[h]);
+      }
+      // ---- dqt_h = sum_c dl_h x_c (DPP form: transposed reductions now, stored after the sender gradients have
+      // read this row's dxcat; LDS form: an LDS loop over the candidates once the row is free)
+      constexpr int TF = lanes::tr_final<DM>();
+      float dqv[kH][TF];
+      int dq_base = 0, dq_cnt = 0;
+      if constexpr (!WSL) {
+#pragma unroll
+        for (int h = 0; h < kH; ++h) {
+          float v[DM];
+#pragma unroll
+          for (int d = 0; d < DM; ++d) v[d] = dl[h] * x[d];
+          dq_base = lanes::treduce32(v, dq_cnt);
+#pragma unroll
+          for (int j = 0; j < TF; ++j) dqv[h][j] = v[j];
+        }
+      }
+      // ---- sender gradient of this pair: sum_h a_h dxbar_h + dl_h qt_h
+      f32x4 cq[DM / 4];
+      const float* qt = qts + rl * QP;
+#pragma unroll
+      for (int q = 0; q < DM / 4; ++q) {
+        cq[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (q < TQ)
+#pragma unroll
+          for (int h = 0; h < kH; ++h)
+            cq[q] += av[h] * ((const f32x4*)(gv + HS * h))[q] + dl[h] * ((const f32x4*)(qt + HS * h))[q];
+      }
+      lanes::wave_sync();  // every lane of the row has read its dxcat row: it becomes the row's [dqt | dbeta]
+      {
+        float* o = a.dqt + row * (a.dqt_ld ? a.dqt_ld : (int64_t)kH * D);
+        float* ot = gs + rl * GP;
+        if constexpr (WSL) {
+          f32x4* pr = GP >= 128 ? (f32x4*)ot : (f32x4*)(lds + cv.pa) + wave * 64 + slot * 32;
+          pr[cc] = f32x4{dl[0], dl[1], dl[2], __int_as_float(ok ? gl * N + s : -1)};
+          lanes::wave_sync();
+          const int d = cc < D ? cc : 0;
+          float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 8
+          for (int k = 0; k < 32; ++k) {
+            if (k < C) {
+              const f32x4 P = pr[k];
+              const int node = __float_as_int(P[3]);
+              const float xv = node >= 0 ? xs[node * XP + d] : 0.0f;
+              s0 += P[0] * xv;
+              s1 += P[1] * xv;
+              s2 += P[2] * xv;
+            }
+          }
+          lanes::wave_sync();  // the pair slots are read: the row becomes [dqt | dbeta]
+          if (active && cc < D) {
+            o[cc] = s0, o[D + cc] = s1, o[2 * D + cc] = s2;
+            ot[cc] = s0, ot[D + cc] = s1, ot[2 * D + cc] = s2;
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < kH; ++h)
+#pragma unroll
+            for (int j = 0; j < TF; ++j) {
+              const int q = dq_base + j;
+              if (active && j < dq_cnt && q < D) {
+                o[h * D + q] = dqv[h][j];
+                ot[h * D + q] = dqv[h][j];
+              }
+            }
+        }
+        if (active && cc < kH) {
+          const float b = cc == 0 ? dbeta[0] : cc == 1 ? dbeta[1] : dbeta[2];
+          a.dbeta[row * (a.dbeta_ld ? a.dbeta_ld : kH) + cc] = b;
+          ot[kH * D + cc] = b;
+        }
+      }
+      if (want_dxa && ok && s < n) {
+        float* dst = img + (lr * n + s) * DM;
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q)
+          if (q < TQ) ((f32x4*)dst)[q] = cq[q];
+      }
+      // ---- never-receivers' Dense_4 gradient: gacc[ct] += [x_raw | 1]^T dz over 16-pair chunks
+      if (want_pre) {
+        float xraw[kD0];
+        {
+          const float* xr = raw + (gl * N + (viapre ? s : 0)) * kD0;
+#pragma unroll
+          for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? xr[k] : 0.0f;
+        }
+#pragma unroll 1
+        for (int ch = 0; ch < 4; ++ch) {
+          if (kq == ch) {
+            float* sp = ws + i16 * kPS;
+#pragma unroll
+            for (int q = 0; q < DM / 4; ++q) {
+              f32x4 dz;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) dz[j] = (viapre && x[4 * q + j] > 0.0f) ? cq[q][j] : 0.0f;
+              ((f32x4*)sp)[q] = dz;
+            }
+            ((f32x4*)(sp + 32))[0] = f32x4{xraw[0], xraw[1], xraw[2], xraw[3]};
+            ((f32x4*)(sp + 32))[1] = f32x4{xraw[4], xraw[5], xraw[6], xraw[7]};
+            sp[40] = viapre ? 1.0f : 0.0f;
+          }
+          lanes::wave_sync();
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const int pp = 4 * ks + kq;
+            const float av2 = i16 <= kD0 ? ws[pp * kPS + 32 + i16] : 0.0f;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) gacc[ct] = mma(av2, ws[pp * kPS + 16 * ct + i16], gacc[ct]);
+          }
+          lanes::wave_sync();
+        }
+      }
+      if (want_dxa) {
+        __syncthreads();
+        // fold this sub-round's image into the block's dxa rows: target (graph gl, agent j), receivers i ascending
+        for (int t = tid; t < nrec * DM; t += 256) {
+          const int r = t / DM, d = t - r * DM;
+          const int g = r / n, j = r - g * n;
+          float acc = dxacc[t];
+          for (int ii = 0; ii < n; ++ii) {
+            const int src = g * n + ii - 8 * sr;
+            if (src >= 0 && src < 8) acc += img[(src * n + j) * DM + d];
+          }
+          dxacc[t] = acc;
+        }
+        __syncthreads();
+      }
+    }
+    // ---- stage 4: dxa = (senders' image + dY Wu^T) + [dqt | dbeta] QBW[:D]^T, mask -> global (agent mode)
+    if (want_dxa) {
+      __syncthreads();  // every row's [dqt | dbeta] is in gs
+      constexpr int KS = 25;  // k-steps over max(F, W) <= 99
+      const int ct = wave & 1, part = wave >> 1;
+      const int col = 16 * ct + i16;
+      const int K = part == 0 ? F : W;
+      float bv[KS], avv[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = 4 * ks + kq;
+        bv[ks] = k >= K ? 0.0f : (part == 0 ? p.Wu[(int64_t)col * F + k] : p.QBW[(int64_t)col * W + k]);
+        avv[ks] = (k >= K || i16 >= nrec) ? 0.0f : (part == 0 ? p.dY[(row0 + i16) * F + k] : gs[i16 * GP + k]);
+      }
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mma(avv[ks], bv[ks], acc);
+      float* px = stg + part * 512;
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) px[(4 * kq + ii) * 32 + col] = acc[ii];
+      __syncthreads();
+      for (int t = tid; t < nrec * DM; t += 256) {
+        const int r = t / DM, d = t - r * DM;
+        float v = dxacc[t] + stg[r * 32 + d];
+        v = v + stg[512 + r * 32 + d];
+        if (p.mask) v = p.mask[(row0 + r) * DM + d] > 0.0f ? v : 0.0f;
+        a.dxa[(row0 + r) * DM + d] = v;
+      }
+    }
+    __syncthreads();
+  }
+  if (want_pre) {  // fixed-order combine of the 4 waves' accumulators -> this workgroup's partial row
+    float* red = stg;
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            float* dst = red + (4 * kq + ii) * 33 + 16 * ct + i16;
+            *dst = (w == 0 ? 0.0f : *dst) + gacc[ct][ii];
+          }
+      }
+      __syncthreads();
+    }
+    const int PK = a.D0 * D + D;
+    for (int o = tid; o < PK; o += 256) {
+      const int m = o < a.D0 * D ? o / D : kD0;
+      const int d = o < a.D0 * D ? o - m * D : o - a.D0 * D;
+      a.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * 33 + d];
+    }
+  }
+}
+
+bool bwd_supported(const dgppo_gnn_layer_bwd_args* p) {
+  const dgppo_gnn_attn_args& a = p->a;
+  if (a.H != kH || a.C < 1 || a.C > 32 || a.n_agents < 1 || a.n_agents > kRows || a.F < 1 || a.F > 64 || !a.sidx ||
+      !a.cand || !a.x || !a.ef || !a.qt || !a.attn || !a.dqt || !a.dbeta || !p->dY || !p->Wcat || a.G < 0 ||
+      a.N < a.n_agents || a.da_add || a.dx || a.dq)
+    return false;
+  if (((uintptr_t)a.ef & 15) || (a.ef_gstride & 3)) return false;
+  const int W = kH * a.D + kH;
+  if (a.qt_ld != 0 && a.qt_ld != W) return false;
+  if (a.xa == nullptr) {
+    if (a.D < 1 || a.D > 8 || a.pre_W || a.dxa || a.dpre_part) return false;
+  } else {
+    if (a.D != 32 || a.D0 < 1 || a.D0 > kD0 || !a.pre_W || !a.pre_b) return false;
+    if (((uintptr_t)a.xa & 15) || a.xa_gstride != (int64_t)a.n_agents * 32) return false;
+    if (a.dxa && (a.dxa_gstride != (int64_t)a.n_agents * 32 || !p->Wu || !p->QBW)) return false;
+  }
+  const int gpb = kRows / a.n_agents;
+  const lb::Carve c = a.xa ? lb::carve<32>(gpb, a.N, a.n_agents, a.F) : lb::carve<8>(gpb, a.N, a.n_agents, a.F);
+  return (size_t)c.floats * sizeof(float) <= 80 * 1024;
+}
+
+int64_t bwd_grid(const dgppo_gnn_layer_bwd_args* p, int64_t* nblk) {
+  const int gpb = kRows / p->a.n_agents;
+  *nblk = ((int64_t)p->a.G + gpb - 1) / gpb;
+  const int64_t cap = p->a.xa ? lb::grid_cap<32>() : lb::grid_cap<8>();
+  return *nblk < cap ? *nblk : cap;
+}
+
+}  // namespace
+}  // namespace dgppo
+
+extern "C" int dgppo_gnn_layer_bwd_supported(const dgppo_gnn_layer_bwd_args* p) {
+  return p && dgppo::bwd_supported(p) ? 1 : 0;
+}
+
+extern "C" int64_t dgppo_gnn_layer_bwd_partial_blocks(const dgppo_gnn_layer_bwd_args* p) {
+  if (!p || !dgppo::bwd_supported(p)) return 0;
+  int64_t nblk;
+  return dgppo::bwd_grid(p, &nblk);
+}
+
+extern "C" int dgppo_gnn_layer_bwd(const dgppo_gnn_layer_bwd_args* p, void* stream) {
+  using namespace dgppo;
+  if (!p || !bwd_supported(p)) return DGPPO_EINVAL;
+  const dgppo_gnn_attn_args& a = p->a;
+  if (a.G == 0) return 0;
+  const int gpb = kRows / a.n_agents;
+  int64_t nblk;
+  const unsigned grid = (unsigned)bwd_grid(p, &nblk);
+  hipStream_t s = (hipStream_t)stream;
+  if (a.xa) {
+    const lb::Carve c = lb::carve<32>(gpb, a.N, a.n_agents, a.F);
+    const size_t bytes = (size_t)c.floats * sizeof(float);
+    if (wsum_lds()) {
+      if (bytes > 64 * 1024) allow_lds((const void*)gnn_layer_bwd_kernel<32, true>);
+      hipLaunchKernelGGL((gnn_layer_bwd_kernel<32, true>), dim3(grid), dim3(256), bytes, s, *p, gpb, nblk, c);
+    } else {
+      if (bytes > 64 * 1024) allow_lds((const void*)gnn_layer_bwd_kernel<32, false>);
+      hipLaunchKernelGGL((gnn_layer_bwd_kernel<32, false>), dim3(grid), dim3(256), bytes, s, *p, gpb, nblk, c);
+    }
+  } else {
+    const lb::Carve c = lb::carve<8>(gpb, a.N, a.n_agents, a.F);
+    if (wsum_lds())
+      hipLaunchKernelGGL((gnn_layer_bwd_kernel<8, true>), dim3(grid), dim3(256), (size_t)c.floats * sizeof(float), s,
+                         *p, gpb, nblk, c);
+    else
+      hipLaunchKernelGGL((gnn_layer_bwd_kernel<8, false>), dim3(grid), dim3(256), (size_t)c.floats * sizeof(float), s,
+                         *p, gpb, nblk, c);
   }
   return (int)hipGetLastError();
 }

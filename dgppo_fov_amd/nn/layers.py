@@ -36,6 +36,10 @@ FUSE_LN = os.environ.get("DGPPO_FUSE_LN", "1") == "1"
 # one GraphTransformer layer forward as ONE kernel ([qt | beta] GEMM + attention + message / update GEMMs, ABI 11
 # dgppo_gnn_layer_fwd) where it applies; DGPPO_FUSED_LAYER=0 runs the unfused chain (A/B, parity tests)
 FUSED_LAYER = os.environ.get("DGPPO_FUSED_LAYER", "1") == "1"
+# the fused layer BACKWARD (dgppo_gnn_layer_bwd: dxcat GEMM + attention backward + d xa GEMMs in one kernel) is
+# measured slower than attn_bwd2r + its GEMMs (668 vs ~516 us per D = 32 call at 2 workgroups per CU);
+# DGPPO_FUSED_LAYER_BWD=1 selects it (A/B, parity tests)
+FUSED_LAYER_BWD = os.environ.get("DGPPO_FUSED_LAYER_BWD", "0") == "1"
 
 
 # ---- parameter space ------------------------------------------------------------------------
@@ -668,9 +672,12 @@ class GraphTransformer:
         K.gemm(Waug, self.v("bk"), QBW, D + 1, 1, F, lda=H * F, sa=F, ldb=1, sb=F, ldc=W, sc=1, c_off=H * D, batch=H)
         return QBW
 
-    def _fused_fwd(self, g: "GraphBatch", xa, pre, keep: bool):
+    def _fused_fwd(self, g: "GraphBatch", xa, pre, keep: bool, zmean=None, tail=None):
         """The layer through dgppo_gnn_layer_fwd (one kernel), or None where it does not apply.  keep: also write
-        [qt | beta], attn and xcat for the backward (else Y only, forward-only passes)."""
+        [qt | beta], attn and xcat for the backward (else Y only, forward-only passes).  Forward-only epilogues (keep
+        False): zmean (G, F) receives the per-graph agent mean of Y, and Y is not written; tail = (weights in
+        ops.TAIL_FIELDS order, carries (G*n, 64), out (G*n, n_out)) runs the value head after the layer (the return
+        value is then (out, None))."""
         if xa is not None and pre is None:
             return None
         G, n, D, F, H, C = g.G, g.n, self.D, self.F, self.H, g.C
@@ -684,11 +691,12 @@ class GraphTransformer:
                 return None
             x, x_gs, D0, pre_W, pre_b = raw, g.N * raw.shape[2], raw.shape[2], pre.v("Wu"), pre.v("bu")
         QBW = self.qb_weights()
-        Y = torch.empty((R, F), device=dev)
+        Y = torch.empty((R, F), device=dev) if (zmean is None and tail is None) else None
+        tail_w, tail_h, tail_out = tail if tail is not None else ([], None, None)
         kw = dict(dims=[G, g.N, g.E, n, D, F, H, C, D0], cand=g.cand, receivers=g.receivers, senders=g.senders,
                   sidx=g.sidx, x=x, x_gstride=x_gs, ef=g.edges_head, ef_gstride=g.E * 4, scale=1.0 / math.sqrt(F),
                   xa=xa, xa_gstride=n * D, pre_W=pre_W, pre_b=pre_b, QBW=QBW, Wcat=self.v("Wcat"), Wu=self.v("Wu"),
-                  bu=self.v("bu"), Y=Y)
+                  bu=self.v("bu"), Y=Y, zmean=zmean, tail_w=tail_w, tail_h=tail_h, tail_out=tail_out)
         if not ops.gnn_layer_supported(**kw):
             return None
         QB = attn = xcat = None
@@ -699,7 +707,12 @@ class GraphTransformer:
         o = kw
         torch.ops.dgppo.gnn_layer_fwd(o["dims"], o["cand"], o["receivers"], o["senders"], o["sidx"], o["x"],
                                       o["x_gstride"], o["ef"], o["ef_gstride"], o["scale"], o["xa"], o["xa_gstride"],
-                                      o["pre_W"], o["pre_b"], o["QBW"], o["Wcat"], o["Wu"], o["bu"], Y, QB, attn, xcat)
+                                      o["pre_W"], o["pre_b"], o["QBW"], o["Wcat"], o["Wu"], o["bu"], Y, QB, attn, xcat,
+                                      zmean, list(tail_w), tail_h, tail_out)
+        if tail is not None:
+            return tail_out, None
+        if zmean is not None:
+            return zmean, None
         return Y, ((xa, pre, QBW, QB, attn, xcat, None, Y, None) if keep else None)
 
     def fwd(self, g: "GraphBatch", xa=None, pre=None, xfull=None, keep=True):
@@ -746,6 +759,79 @@ class GraphTransformer:
         x = xfull if xfull is not None else g.nodes
         return x, dict(lda=self.D, a_grp=g.n, a_gs=g.N * self.D)
 
+    def _fused_bwd(self, cache, dY, g: "GraphBatch", mask_dxa: bool):
+        """dgppo_gnn_layer_bwd (dxcat GEMM + attention backward + the d xa GEMMs in one kernel) where it applies:
+        returns (True, d xa or None) after every gradient of the layer is accumulated, or (False, None)."""
+        xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull = cache
+        if (not FUSED_LAYER or not FUSED_LAYER_BWD or xfull is not None or self.EX or QB is None or
+                (xa is not None and pre is None)):
+            return False, None
+        G, n, D, F, H, C = g.G, g.n, self.D, self.F, self.H, g.C
+        R, WQ = G * n, H * D + H
+        dev = dY.device
+        if xa is None:
+            x, x_gs, D0, pre_W, pre_b = g.nodes, g.N * g.nodes.shape[2], 0, None, None
+        else:
+            raw, cols = g.sender_raw
+            if cols is not None:
+                return False, None
+            x, x_gs, D0, pre_W, pre_b = raw, g.N * raw.shape[2], raw.shape[2], pre.v("Wu"), pre.v("bu")
+        dQB = torch.empty((R, WQ), device=dev)
+        dXa = torch.empty((R, D), device=dev) if xa is not None else None
+        mask = xa if (xa is not None and mask_dxa) else None
+        head = [[G, g.N, g.E, n, D, F, H, C, D0], g.cand, g.receivers, g.senders, g.sidx, x, x_gs, g.edges_head, g.E * 4,
+                1.0 / math.sqrt(F), xa, n * D, pre_W, pre_b, QB, attn, dY, QBW, self.v("Wcat"), self.v("Wu"), mask]
+        PK = D0 * D + D
+        nb = ops.gnn_layer_bwd_plan(*head, dQB, dXa, QB if pre is not None else None)  # (any non-null dpre probe)
+        if nb == 0:
+            return False, None
+        part = K.workspace(nb * PK, dev, "attn_pre") if (xa is not None and pre is not None) else None
+        torch.ops.dgppo.gnn_layer_bwd(*head, dQB, dXa, part)
+        if part is not None:
+            self._pre_grads(pre, g, part, nb, PK, D0)
+        K.gemm(xcat, dY, self.v("Wcat", True), H * (D + 5), F, R, ta=True, lda=H * (D + 5), alpha=1.0 / H, beta=1.0)
+        A, akw = self._rows_in(g, xa, None)
+        self._qfree_grads(A, akw, dQB, R)
+        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
+        return True, dXa
+
+    def _pre_grads(self, pre, g, part, nb, PK, D0):
+        """Sum the per-workgroup [Wu (D0 x D) | bu (D)] partial rows of the pre layer (Wu rows = the raw columns used)."""
+        D, dev = self.D, part.device
+        cols = g.sender_raw[1]
+        ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
+        nw = D0 * D
+        if ob == ow + nw and cols is None:
+            K.colsum(part, nb, PK, pre.ps.grad[ow:ow + PK], beta=1.0)
+        else:
+            tmp = torch.empty(PK, device=dev)
+            K.colsum(part, nb, PK, tmp)
+            if cols is None:
+                pre.ps.grad[ow:ow + nw].add_(tmp[:nw])
+            else:
+                pre.v("Wu", True).index_add_(0, cols, tmp[:nw].view(D0, D))
+            pre.ps.grad[ob:ob + D].add_(tmp[nw:])
+
+    def _qfree_grads(self, A, akw, dQB, R):
+        """Q-free parameter gradients: Gaug = [x 1]^T [dqt | dbeta] ((D+1) x (HD+H)), one pass over the rows; then,
+        per head, with Waug_h = [Wq_h; bq_h] ((D+1) x F):
+          [dWq_h; dbq_h] += Gaug[:, hD:(h+1)D] Wkt_h^T + Gaug[:, HD+h] bk_h^T
+          dWkt_h += Waug_h^T Gaug[:, hD:(h+1)D],   dbk_h += Waug_h^T Gaug[:, HD+h]
+        (q_h = x Wq_h + bq_h is affine in the layer input, so every sum over rows of q collapses into Gaug)"""
+        D, F, H = self.D, self.F, self.H
+        HD, WQ = H * D, H * D + H
+        Gaug = torch.empty((D + 1, WQ), device=dQB.device)
+        K.gemm(A, dQB, Gaug, D, WQ, R, ta=True, bias_grad=Gaug[D], **akw)
+        Waug, dWaug = self._aug("Wq", "bq"), self._aug("Wq", "bq", grad=True)
+        K.gemm(Gaug, self.v("Wkt"), dWaug, D + 1, F, D, lda=WQ, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
+               batch=H, beta=1.0)
+        K.gemm(Gaug, self.v("bk"), dWaug, D + 1, F, 1, lda=WQ, a_off=HD, sa=1, ldb=F, sb=F, ldc=H * F, sc=F,
+               batch=H, beta=1.0)
+        K.gemm(Waug, Gaug, self.v("Wkt", True), F, D, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, sb=D, ldc=D,
+               sc=F * D, batch=H, beta=1.0)
+        K.gemm(Waug, Gaug, self.v("bk", True), F, 1, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, b_off=HD, sb=1,
+               ldc=1, sc=F, batch=H, beta=1.0)
+
     def bwd(self, cache, dY, g: "GraphBatch", masked=False, mask_dxa=False):
         """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, d xfull (G, N, D)
         when every node's row was given, else None; accumulates this layer's grads and, in agent mode
@@ -762,6 +848,10 @@ class GraphTransformer:
         A, akw = self._rows_in(g, xa, xfull)
         if not masked:
             K.relu_bwd_(dY, Y)  # dY := dZ
+        done, dXa = self._fused_bwd(cache, dY, g, mask_dxa)
+        self.last_fused_bwd = done
+        if done:
+            return dXa
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
         K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)
@@ -785,36 +875,9 @@ class GraphTransformer:
         torch.ops.dgppo.gnn_attn_bwd(**args, attn=attn, dxcat=dxcat, da_add=da_add, dqt=dQB, dq=None,
                                      dbeta=dQB[:, HD:], dxa=dXa, dxa_gstride=n * D, dpre_part=part, dqt_ld=WQ,
                                      dbeta_ld=WQ, dx=dXf, dx_gstride=N * D)
-        if part is not None:  # partial rows are [Wu (D0 x D) | bu (D)] of pre (Wu rows = the raw columns used)
-            cols = g.sender_raw[1]
-            ow, ob = pre.ps.offsets[pre.name + ".Wu"], pre.ps.offsets[pre.name + ".bu"]
-            nw = args["dims"][8] * D
-            if ob == ow + nw and cols is None:
-                K.colsum(part, nb, PK, pre.ps.grad[ow:ow + PK], beta=1.0)
-            else:
-                tmp = torch.empty(PK, device=dev)
-                K.colsum(part, nb, PK, tmp)
-                if cols is None:
-                    pre.ps.grad[ow:ow + nw].add_(tmp[:nw])
-                else:
-                    pre.v("Wu", True).index_add_(0, cols, tmp[:nw].view(args["dims"][8], D))
-                pre.ps.grad[ob:ob + D].add_(tmp[nw:])
-        # Q-free parameter gradients: Gaug = [x 1]^T [dqt | dbeta] ((D+1) x (HD+H)), one pass over the rows;
-        # then, per head, with Waug_h = [Wq_h; bq_h] ((D+1) x F):
-        #   [dWq_h; dbq_h] += Gaug[:, hD:(h+1)D] Wkt_h^T + Gaug[:, HD+h] bk_h^T
-        #   dWkt_h += Waug_h^T Gaug[:, hD:(h+1)D],   dbk_h += Waug_h^T Gaug[:, HD+h]
-        # (q_h = x Wq_h + bq_h is affine in the layer input, so every sum over rows of q collapses into Gaug)
-        Gaug = torch.empty((D + 1, WQ), device=dev)
-        K.gemm(A, dQB, Gaug, D, WQ, R, ta=True, bias_grad=Gaug[D], **akw)
-        Waug, dWaug = self._aug("Wq", "bq"), self._aug("Wq", "bq", grad=True)
-        K.gemm(Gaug, self.v("Wkt"), dWaug, D + 1, F, D, lda=WQ, sa=D, tb=True, ldb=D, sb=F * D, ldc=H * F, sc=F,
-               batch=H, beta=1.0)
-        K.gemm(Gaug, self.v("bk"), dWaug, D + 1, F, 1, lda=WQ, a_off=HD, sa=1, ldb=F, sb=F, ldc=H * F, sc=F,
-               batch=H, beta=1.0)
-        K.gemm(Waug, Gaug, self.v("Wkt", True), F, D, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, sb=D, ldc=D,
-               sc=F * D, batch=H, beta=1.0)
-        K.gemm(Waug, Gaug, self.v("bk", True), F, 1, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, b_off=HD, sb=1,
-               ldc=1, sc=F, batch=H, beta=1.0)
+        if part is not None:
+            self._pre_grads(pre, g, part, nb, PK, args["dims"][8])
+        self._qfree_grads(A, akw, dQB, R)
         K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
         if dXa is not None:
             K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
@@ -950,6 +1013,22 @@ class GNN:
         out = torch.empty((rows, L.F), device=Z.device)
         K.gemm(Z, L.v("Wu"), out, rows, L.F, L.D, bias=L.v("bu"), relu=True)
         return out
+
+    def fwd_epilogue(self, g: GraphBatch, zmean=None, tail=None):
+        """Forward only, with the last layer's fused epilogue (GraphTransformer._fused_fwd: zmean = the agent mean of
+        its output, tail = the value head): the epilogue's output, or None where the fused kernels do not cover the
+        stack (the caller then runs fwd() and the unfused head)."""
+        if not FUSED_LAYER or len(self.layers) > 2:
+            return None
+        Y = None
+        for i, L in enumerate(self.layers):
+            last = i == len(self.layers) - 1
+            kw = dict(zmean=zmean, tail=tail) if last else {}
+            out = L._fused_fwd(g, Y if i else None, self.layers[0] if i else None, False, **kw)
+            if out is None or L.EX:
+                return None
+            Y = out[0]
+        return Y
 
     def fwd(self, g: GraphBatch, keep=True):
         """Layer 0 reads the raw nodes, layer 1 runs in agent mode (never-receivers' layer-1 rows recomputed

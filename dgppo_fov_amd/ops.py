@@ -288,13 +288,23 @@ def gnn_attn_partial_blocks(dims, cand, receivers, senders, sidx, x, x_gstride, 
 
 
 # ---- one GraphTransformer layer forward as one kernel (ABI 11) -------------------------------------------
+TAIL_FIELDS = ("W0", "b0", "ln0_s", "ln0_b", "W1", "b1", "ln1_s", "ln1_b", "Wi", "bi", "Wh", "bhn", "Wo", "bo")
+
+
 def _layer_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride, pre_W,
-                  pre_b, QBW, Wcat, Wu, bu, Y, qb=None, attn=None, xcat=None) -> _lib.GnnLayerArgs:
+                  pre_b, QBW, Wcat, Wu, bu, Y, qb=None, attn=None, xcat=None, zmean=None, tail_w=(), tail_h=None,
+                  tail_out=None) -> _lib.GnnLayerArgs:
     la = _lib.GnnLayerArgs()
     la.a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, None, None, None, scale, xa,
                         xa_gstride, pre_W, pre_b)
     la.a.attn, la.a.xcat = _p(attn), _p(xcat)
     la.QBW, la.qb, la.Wcat, la.Wu, la.bu, la.Y = _p(QBW), _p(qb), _p(Wcat), _p(Wu), _p(bu), _p(Y)
+    la.zmean = _p(zmean)
+    if tail_out is not None:
+        for name, t in zip(TAIL_FIELDS, tail_w):
+            setattr(la.tail, name, _p(t))
+        la.tail.h_in, la.tail.out = _p(tail_h), _p(tail_out)
+        la.tail.n_out, la.tail.on = int(tail_out.shape[-1]), 1
     return la
 
 
@@ -303,23 +313,70 @@ def gnn_layer_supported(**kw) -> bool:
     return bool(_lib.load().dgppo_gnn_layer_supported(ctypes.byref(_layer_struct(**kw))))
 
 
-@torch.library.custom_op("dgppo::gnn_layer_fwd", mutates_args=("Y", "qb", "attn", "xcat"))
+@torch.library.custom_op("dgppo::gnn_layer_fwd", mutates_args=("Y", "qb", "attn", "xcat", "zmean", "tail_out"))
 def gnn_layer_fwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
                   x_gstride: int, ef: Tensor, ef_gstride: int, scale: float, xa: Optional[Tensor], xa_gstride: int,
                   pre_W: Optional[Tensor], pre_b: Optional[Tensor], QBW: Tensor, Wcat: Tensor, Wu: Tensor, bu: Tensor,
-                  Y: Tensor, qb: Optional[Tensor], attn: Optional[Tensor], xcat: Optional[Tensor]) -> None:
+                  Y: Optional[Tensor], qb: Optional[Tensor], attn: Optional[Tensor], xcat: Optional[Tensor],
+                  zmean: Optional[Tensor], tail_w: List[Tensor], tail_h: Optional[Tensor],
+                  tail_out: Optional[Tensor]) -> None:
     """One GraphTransformer layer forward (dims as gnn_attn_fwd): Y (G*n, F) = relu(xcat Wcat / H + x_i Wu + bu) with
     the attention of gnn_attn_fwd in between and [qt | beta] = [x_i 1] QBW, all in one kernel; qb, attn and xcat are
-    optional outputs for the backward (nn/layers.py GraphTransformer.fwd)."""
-    _lib.require_gpu(Y.device, "dgppo::gnn_layer_fwd")
+    optional outputs for the backward (nn/layers.py GraphTransformer.fwd).  Forward-only epilogues: zmean (G, F) the
+    per-graph agent mean of Y; tail_out (G*n, n_out) the value head after the layer (MLP -> GRU(tail_h) -> Dense,
+    weights tail_w in TAIL_FIELDS order)."""
+    dev = (Y if Y is not None else zmean if zmean is not None else tail_out).device
+    _lib.require_gpu(dev, "dgppo::gnn_layer_fwd")
     la = _layer_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride, pre_W,
-                       pre_b, QBW, Wcat, Wu, bu, Y, qb, attn, xcat)
-    _lib.check(_lib.load().dgppo_gnn_layer_fwd(ctypes.byref(la), _stream(Y)), "dgppo_gnn_layer_fwd")
+                       pre_b, QBW, Wcat, Wu, bu, Y, qb, attn, xcat, zmean, tail_w, tail_h, tail_out)
+    _lib.check(_lib.load().dgppo_gnn_layer_fwd(ctypes.byref(la), _lib.stream_handle(dev)), "dgppo_gnn_layer_fwd")
 
 
 @gnn_layer_fwd.register_fake
 def _gnn_layer_fwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride,
-                        pre_W, pre_b, QBW, Wcat, Wu, bu, Y, qb, attn, xcat) -> None:
+                        pre_W, pre_b, QBW, Wcat, Wu, bu, Y, qb, attn, xcat, zmean, tail_w, tail_h, tail_out) -> None:
+    return None
+
+
+def _layer_bwd_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride, pre_W,
+                      pre_b, qb, attn, dY, QBW, Wcat, Wu, mask, dqb, dxa, dpre_part) -> _lib.GnnLayerBwdArgs:
+    la = _lib.GnnLayerBwdArgs()
+    la.a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, None, qb, None, scale, xa,
+                        xa_gstride, pre_W, pre_b)
+    W = int(dims[6]) * int(dims[4]) + int(dims[6])
+    la.a.qt_ld, la.a.dqt_ld, la.a.dbeta_ld = W, W, W
+    la.a.attn, la.a.dqt = _p(attn), _p(dqb)
+    la.a.dbeta = (_p(dqb) + 4 * int(dims[6]) * int(dims[4])) if dqb is not None else None
+    la.a.dxa, la.a.dxa_gstride, la.a.dpre_part = _p(dxa), int(dims[3]) * int(dims[4]), _p(dpre_part)
+    la.dY, la.QBW, la.Wcat, la.Wu, la.mask = _p(dY), _p(QBW), _p(Wcat), _p(Wu), _p(mask)
+    return la
+
+
+def gnn_layer_bwd_plan(*args) -> int:
+    """Rows of the dpre_part workspace gnn_layer_bwd writes (0: the fused backward does not cover the call)."""
+    la = _layer_bwd_struct(*args)
+    lib = _lib.load()
+    return int(lib.dgppo_gnn_layer_bwd_partial_blocks(ctypes.byref(la))) if lib.dgppo_gnn_layer_bwd_supported(
+        ctypes.byref(la)) else 0
+
+
+@torch.library.custom_op("dgppo::gnn_layer_bwd", mutates_args=("dqb", "dxa", "dpre_part"))
+def gnn_layer_bwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
+                  x_gstride: int, ef: Tensor, ef_gstride: int, scale: float, xa: Optional[Tensor], xa_gstride: int,
+                  pre_W: Optional[Tensor], pre_b: Optional[Tensor], qb: Tensor, attn: Tensor, dY: Tensor, QBW: Tensor,
+                  Wcat: Tensor, Wu: Tensor, mask: Optional[Tensor], dqb: Tensor, dxa: Optional[Tensor],
+                  dpre_part: Optional[Tensor]) -> None:
+    """Backward of gnn_layer_fwd's attention and dense layers given dY (ReLU gate applied): dqb = [dqt | dbeta] rows,
+    in agent mode dxa (overwritten; ReLU-masked by `mask`) and the pre-layer partial rows (nn/layers.py)."""
+    _lib.require_gpu(dY.device, "dgppo::gnn_layer_bwd")
+    la = _layer_bwd_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride,
+                           pre_W, pre_b, qb, attn, dY, QBW, Wcat, Wu, mask, dqb, dxa, dpre_part)
+    _lib.check(_lib.load().dgppo_gnn_layer_bwd(ctypes.byref(la), _stream(dY)), "dgppo_gnn_layer_bwd")
+
+
+@gnn_layer_bwd.register_fake
+def _gnn_layer_bwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride,
+                        pre_W, pre_b, qb, attn, dY, QBW, Wcat, Wu, mask, dqb, dxa, dpre_part) -> None:
     return None
 
 

@@ -328,16 +328,54 @@ int dgppo_gnn_attn_bwd(const dgppo_gnn_attn_args* args, void* stream);
  * OPTIONAL outputs (what dgppo_gnn_attn_bwd and the weight gradients read; NULL in forward-only passes).  Scope:
  * H = 3, C <= 32, n <= 16, F <= 64, 4-wide edges; full mode with D <= 8, or agent mode with D = 32, D0 <= 8 and
  * pre_W (dgppo_gnn_layer_supported; otherwise use the unfused chain). */
+/* Forward-only epilogues of the value networks (forward passes whose intermediates nobody reads):
+ *   zmean (G, F): the per-graph mean of Y over its n agent rows (VlNet's agent mean, value.py:35-37, summed over
+ *         the agents in order then divided by n, as dgppo_agent_mean_fwd); Y may then be NULL;
+ *   tail (tail.on = 1, F = 64): DecRStateFn's head after a 1-layer GNN (value.py:67-79, dgppo.py:83-95): MLP
+ *         (Dense(64) + LayerNorm + ReLU x 2) -> GRUCell(64) fed the carries h_in -> Dense(n_out), written to
+ *         tail.out (G*n, n_out <= 16); Y, qb, a.attn and a.xcat must then be NULL. */
+typedef struct dgppo_gnn_value_tail {
+  const float* W0; const float* b0; const float* ln0_s; const float* ln0_b;  /* head Dense_0 (64 x 64), LayerNorm_0 */
+  const float* W1; const float* b1; const float* ln1_s; const float* ln1_b;  /* head Dense_1, LayerNorm_1 */
+  const float* Wi; const float* bi; const float* Wh; const float* bhn;      /* GRUCell: (64, 192) [r|z|n], (192), (64, 192), (64) */
+  const float* Wo; const float* bo;                                         /* output Dense (64, n_out), (n_out) */
+  const float* h_in;                                                        /* (G*n, 64) carries */
+  float* out;                                                               /* (G*n, n_out) */
+  int32_t n_out, on;
+} dgppo_gnn_value_tail;
 typedef struct dgppo_gnn_layer_args {
   dgppo_gnn_attn_args a;
   const float* QBW;                  /* (D+1, H*D + H): [x 1] QBW = [qt | beta] (Q-free query-key products) */
   float* qb;                         /* optional out (G*n, H*D + H) [qt | beta] rows */
   const float* Wcat;                 /* (H*(D+5), F) = [Wv (H*D); We (H*4); bv (H)] per head */
   const float* Wu; const float* bu;  /* Dense_4: (D, F), (F) */
-  float* Y;                          /* (G*n, F) */
+  float* Y;                          /* (G*n, F) (NULL allowed with zmean or the tail) */
+  float* zmean;                      /* optional out (G, F) */
+  dgppo_gnn_value_tail tail;
 } dgppo_gnn_layer_args;
 int dgppo_gnn_layer_supported(const dgppo_gnn_layer_args* args);
 int dgppo_gnn_layer_fwd(const dgppo_gnn_layer_args* args, void* stream);
+
+/* ABI 11: the backward of dgppo_gnn_layer_fwd's attention and of the two dense layers around it as ONE kernel,
+ * given dY = dL/dY with the layer's ReLU gate applied: dxcat = dY Wcat^T / H (in the kernel, never stored), the
+ * softmax / attention backward of dgppo_gnn_attn_bwd (a.dqt, a.dbeta written, [dqt | dbeta] rows with a.dqt_ld /
+ * a.dbeta_ld), the never-receivers' pre_W / pre_b gradient partials (a.dpre_part, one row of D0*D + D per
+ * workgroup: dgppo_gnn_layer_bwd_partial_blocks rows; sum them with dgppo_colsum) and, in agent mode with a.dxa,
+ *   dxa = (sum of the agent senders' gradients) + dY Wu^T + [dqt | dbeta] QBW[:D]^T, then dxa *= (mask > 0)
+ * (OVERWRITTEN, not accumulated; mask = the previous layer's ReLU output, or NULL).  a.qt = the forward's
+ * [qt | beta] rows (a.qt_ld = H*D + H); a.attn = the forward's attention.  The weight gradients (xcat^T dY,
+ * [x 1]^T [dqt | dbeta], x^T dY) stay GEMMs.  Same scope as dgppo_gnn_layer_fwd (dgppo_gnn_layer_bwd_supported). */
+typedef struct dgppo_gnn_layer_bwd_args {
+  dgppo_gnn_attn_args a;
+  const float* dY;    /* (G*n, F) */
+  const float* QBW;   /* (D+1, H*D + H) */
+  const float* Wcat;  /* (H*(D+5), F) */
+  const float* Wu;    /* (D, F) */
+  const float* mask;  /* optional (G*n, D) */
+} dgppo_gnn_layer_bwd_args;
+int dgppo_gnn_layer_bwd_supported(const dgppo_gnn_layer_bwd_args* args);
+int64_t dgppo_gnn_layer_bwd_partial_blocks(const dgppo_gnn_layer_bwd_args* args);
+int dgppo_gnn_layer_bwd(const dgppo_gnn_layer_bwd_args* args, void* stream);
 
 /* Edge features wider than 4 (LidarOmniTarget's 10-wide edges, lidar_omni_target.py edge_dim): the attention
  * kernels see columns 0..3, the remaining EX columns efx (G, E, EX) go through these two.

@@ -69,6 +69,35 @@ if marks:
     out["update_mfma_tflop"] = round(uf / 1e12, 4)
     out["update_executed_tflops"] = round(uf / uspan / 1e12, 2)
     out["update_frac_of_peak"] = round(uf / uspan / PEAK, 4)
+# VALU fp32 flops (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS), calibrated on the known elementwise work of valu_calib.py
+# (torch.mul: 1 flop per element, torch.addcmul: 2), so `counter / per_flop` = executed fp32 VALU flops
+cal = glob.glob(os.path.join(root, "calib", "**", "*counter_collection.csv"), recursive=True)
+per_flop = None
+if cal:
+    crow = list(csv.DictReader(open(cal[0])))
+    got = defaultdict(float)
+    for r in crow:
+        if r["Counter_Name"] == "SQ_INSTS_VALU_FLOPS_FP32":
+            k = "mul" if "MulFunctor" in r["Kernel_Name"] else ("addcmul" if "addcmul" in r["Kernel_Name"] else None)
+            if k:
+                got[k] += float(r["Counter_Value"])
+    n_el = float(1 << 24) * 2  # two launches each
+    if got.get("mul"):
+        per_flop = got["mul"] / n_el
+        out["valu_calibration"] = {"mul_counter_per_element": round(got["mul"] / n_el, 4),
+                                   "addcmul_counter_per_element": round(got.get("addcmul", 0.0) / n_el, 4),
+                                   "counter_per_flop": round(per_flop, 4)}
+if marks and per_flop:
+    vf = sum(float(r["Counter_Value"]) for r in prow if r["Counter_Name"] in
+             ("SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS") and d_mark is not None
+             and int(r["Dispatch_Id"]) > d_mark) / per_flop
+    out["update_valu_fp32_tflop"] = round(vf / 1e12, 4)
+    out["update_executed_fp32_tflop"] = round((uf + vf) / 1e12, 4)
+    out["update_executed_fp32_frac_of_peak"] = round((uf + vf) / uspan / PEAK, 4)
+for fam in out["families"]:
+    v = pmc[fam].get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) + pmc[fam].get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0)
+    if per_flop and v:
+        out["families"][fam]["valu_fp32_tflop"] = round(v / per_flop / 1e12, 4)
 # the build the profile measured: bench.py quotes the executed-MFMA figure only for the same sources (a hash of
 # dgppo_fov_amd/csrc/* and include/dgppo_hip.h -- a rebuild of the same sources is the same build)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

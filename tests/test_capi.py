@@ -55,6 +55,8 @@ def _c_layout(struct, fields):
                                             (_lib.GemmArgs, "dgppo_gemm_args"),
                                             (_lib.GnnAttnArgs, "dgppo_gnn_attn_args"),
                                             (_lib.GnnLayerArgs, "dgppo_gnn_layer_args"),
+                                            (_lib.GnnValueTail, "dgppo_gnn_value_tail"),
+                                            (_lib.GnnLayerBwdArgs, "dgppo_gnn_layer_bwd_args"),
                                             (_lib.TanhNormalArgs, "dgppo_tanh_normal_args"),
                                             (_lib.GaeArgs, "dgppo_gae_args"),
                                             (_lib.AdvArgs, "dgppo_adv_args"),

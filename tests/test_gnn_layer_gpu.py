@@ -80,3 +80,65 @@ def test_fused_layer_falls_back_outside_its_scope(cuda, eid, n, obs):
     actor = ActorNet(env.node_dim, n, cuda, seed=3, edge_dim=env.edge_dim, action_dim=env.action_dim)
     Y, c = actor.gnn.layers[0].fwd(g)
     assert not actor.gnn.layers[0].last_fused and c is not None
+
+
+def _grads(net, g, dz, fused):
+    old, oldb = layers.FUSED_LAYER, layers.FUSED_LAYER_BWD
+    layers.FUSED_LAYER = layers.FUSED_LAYER_BWD = fused
+    try:
+        net.ps.zero_grad()
+        z, c = net.gnn.fwd(g)
+        net.gnn.bwd(c, dz.clone(), g)
+        for L in net.gnn.layers:
+            assert L.last_fused_bwd == fused, "fused backward not taken" if fused else "unfused backward expected"
+        torch.cuda.synchronize()
+        return net.ps.grad.clone()
+    finally:
+        layers.FUSED_LAYER, layers.FUSED_LAYER_BWD = old, oldb
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("LidarSpread", 3, 2), ("MPESpread", 3, 3),
+                                       ("LidarBicycleTarget", 8, 3), ("LidarSpread", 5, 1)])
+def test_fused_layer_backward_matches_unfused_chain(cuda, eid, n, obs):
+    """dgppo_gnn_layer_bwd (dxcat GEMM + attention backward + d xa GEMMs in one kernel): every GNN parameter
+    gradient of the 2-layer actor GNN (agent-mode second layer: pre-layer partials, the previous layer's ReLU
+    mask, agent-sender sums) and the 1-layer Vh GNN within fp32 rounding of the unfused chain."""
+    env, g = _batch(cuda, eid, n, obs)
+    gen = torch.Generator(device=cuda).manual_seed(5)
+    for net in (ActorNet(env.node_dim, n, cuda, seed=3, edge_dim=env.edge_dim),
+                VhNet(env.node_dim, n, env.n_cost, cuda, seed=4, edge_dim=env.edge_dim)):
+        dz = torch.randn((g.G * n, 64), device=cuda, generator=gen) * 1e-2
+        gf, gu = _grads(net, g, dz, True), _grads(net, g, dz, False)
+        for name, shape, _ in net.ps.entries:
+            if not name.startswith("gnn."):
+                continue
+            o = net.ps.offsets[name]
+            k = int(np.prod(shape))
+            a, b = gf[o:o + k].double().cpu(), gu[o:o + k].double().cpu()
+            scale = b.abs().max().item()
+            assert (a - b).abs().max().item() <= 2e-5 * scale + 1e-9, f"{eid} {name}: {(a - b).abs().max().item():.3e} vs {scale:.3e}"
+
+
+@pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("MPESpread", 3, 3), ("LidarBicycleTarget", 8, 3),
+                                       ("LidarSpread", 3, 2)])
+def test_forward_only_epilogues_match_unfused(cuda, eid, n, obs):
+    """The prepass's forward-only passes: VlNet's agent means from the last layer's kernel (zmean, Y never stored) and
+    VhNet's whole get_Vh (layer + MLP head + GRU step + output Dense, one kernel) against the unfused chain."""
+    from dgppo_fov_amd.algo.module.nets import VlNet
+
+    env, g = _batch(cuda, eid, n, obs)
+    vl = VlNet(env.node_dim, n, cuda, seed=6, edge_dim=env.edge_dim)
+    vh = VhNet(env.node_dim, n, env.n_cost, cuda, seed=4, edge_dim=env.edge_dim)
+    h = torch.randn((g.G * n, 64), device=cuda, generator=torch.Generator(device=cuda).manual_seed(2)) * 0.5
+    zf = vl.graph_means(g)
+    vf, cf = vh.fwd(g, h, keep_cache=False)
+    assert cf is None
+    old = layers.FUSED_LAYER
+    layers.FUSED_LAYER = False
+    try:
+        zu = vl.graph_means(g)
+        vu, _ = vh.fwd(g, h, keep_cache=False)
+    finally:
+        layers.FUSED_LAYER = old
+    _close(zf, zu, f"{eid} Vl agent means")
+    _close(vf, vu, f"{eid} Vh", rtol=1e-4, atol=1e-5)
