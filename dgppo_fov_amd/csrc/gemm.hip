@@ -746,14 +746,17 @@ constexpr int kWWaves = 8;
 constexpr int kWMaxChunks = 256;
 constexpr int kWMinRows = 512;
 
-__host__ __device__ inline int wgrad_chunks(int64_t K, int min_rows = kWMinRows) {
+__host__ __device__ inline int wgrad_chunks(int64_t K, int min_rows = kWMinRows, int max_chunks = kWMaxChunks) {
   int64_t c = (K + min_rows - 1) / min_rows;
-  if (c > kWMaxChunks) c = kWMaxChunks;
+  if (c > max_chunks) c = max_chunks;
   return c < 1 ? 1 : (int)c;
 }
 
-// workspace layout: [batch][chunk][M*N + N]
-template <int MT, int NT>
+// workspace layout: [batch][chunk][M*N + N]; U row pairs of loads in flight per wave.  FLAT (no row grouping on A or
+// B): every load unconditional -- the row clamped into the chunk, the column into the matrix, out-of-range values
+// zeroed by a select -- so a row pair's loads issue back to back; with grouping each load sits behind a branch and
+// a 64-bit division (row_off64), which made the loop issue-bound (SALU ~ VALU instructions, PMC)
+template <int MT, int NT, int U, bool FLAT>
 __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
   constexpr int CP = NT * 32 + 1;
@@ -786,20 +789,47 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
   for (int mt = 0; mt < MT; ++mt) mok[mt] = m0 + mt * 32 + i < M;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) nok[nt] = n0 + nt * 32 + i < N;
+  int mcol[MT], ncol[NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) mcol[mt] = mok[mt] ? m0 + mt * 32 + i : 0;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) ncol[nt] = nok[nt] ? n0 + nt * 32 + i : 0;
   // row pairs (2q, 2q+1) of the chunk, interleaved over the waves; lane half h takes row 2q + h
-  constexpr int U = 2;  // row pairs in flight per wave
   for (int64_t k0 = r0 + 2 * wave; k0 < r1; k0 += 2 * kWWaves * U) {
     float a[U][MT], bb[U][NT];
+    if constexpr (FLAT) {  // every load of the U row pairs first, then the selects (one wait for all of them)
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {
+        const int64_t k = k0 + 2 * kWWaves * u + h;
+        const int64_t kc = k < r1 ? k : r0;
+        const float* Ar = A + kc * p.lda;
+        const float* Br = B + kc * p.ldb;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[u][mt] = Ar[mcol[mt]];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = Br[ncol[nt]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool kok = k0 + 2 * kWWaves * u + h < r1;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? a[u][mt] : 0.0f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? bb[u][nt] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (FLAT ? 0 : U); ++u) {
       const int64_t k = k0 + 2 * kWWaves * u + h;
       const bool kok = k < r1;
-      const float* Ar = A + (kok ? row_off64(k, p.lda, p.a_grp, p.a_gstride) : 0) + m0 + i;
-      const float* Br = B + (kok ? row_off64(k, p.ldb, p.b_grp, p.b_gstride) : 0) + n0 + i;
+      {
+        const float* Ar = A + (kok ? row_off64(k, p.lda, p.a_grp, p.a_gstride) : 0) + m0 + i;
+        const float* Br = B + (kok ? row_off64(k, p.ldb, p.b_grp, p.b_gstride) : 0) + n0 + i;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? Ar[mt * 32] : 0.0f;
+        for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? Ar[mt * 32] : 0.0f;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? Br[nt * 32] : 0.0f;
+        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? Br[nt * 32] : 0.0f;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -921,6 +951,20 @@ int wgrad_max_acc() {
   static int v = env_knob("DGPPO_WGRAD_MAXACC", 4);
   return v;
 }
+// row chunks (workgroups along K; 256 = one 512-thread workgroup per CU) and row pairs in flight per wave (2 / 4)
+int wgrad_max_chunks() {
+  static int v = env_knob("DGPPO_WGRAD_MAXCHUNKS", 256);
+  return v;
+}
+int wgrad_unroll() {  // default 4 with the branch-free loads: M64 N192 66.9 -> 64.2 us, update 179.8 -> 178.6 ms
+  static int v = env_knob("DGPPO_WGRAD_U", 4);
+  return v == 4 ? 4 : 2;
+}
+// the branch-free loads of ungrouped operands (DGPPO_WGRAD_FLAT=0 keeps the guarded loads: A/B)
+int wgrad_flat() {
+  static int v = env_knob("DGPPO_WGRAD_FLAT", 1);
+  return v;
+}
 
 GemmPath gemm_path(const dgppo_gemm_args* p) {
   if (p->trans_a && !p->trans_b && p->N <= 192 && p->M <= 4096 && !p->bias && !p->addend && !p->relu)
@@ -958,14 +1002,21 @@ template <int MT, int NT>
 void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
   const int gm = (p->M + MT * 32 - 1) / (MT * 32), gn = (p->N + NT * 32 - 1) / (NT * 32);
   const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
-  hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT>), dim3(chunks, gm * gn, p->batch), dim3(512), lds, s, *p,
-                     chunks, gn);
+  const dim3 grid(chunks, gm * gn, p->batch);
+  const bool flat = p->a_grp <= 0 && p->b_grp <= 0 && wgrad_flat();
+  if (wgrad_unroll() == 4 && MT * NT <= 4) {
+    if (flat) hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 4, true>), grid, dim3(512), lds, s, *p, chunks, gn);
+    else hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 4, false>), grid, dim3(512), lds, s, *p, chunks, gn);
+  } else {
+    if (flat) hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 2, true>), grid, dim3(512), lds, s, *p, chunks, gn);
+    else hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 2, false>), grid, dim3(512), lds, s, *p, chunks, gn);
+  }
 }
 
 int launch_wgrad(const dgppo_gemm_args* p, hipStream_t s) {
   int MT, NT;
   wgrad_shape(p->M, p->N, &MT, &NT);
-  const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows());
+  const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows(), wgrad_max_chunks());
   if (chunks > 1 && !p->workspace) return DGPPO_EINVAL;
 #define DG_W(a, b) \
   if (MT == a && NT == b) { launch_wgrad_t<a, b>(p, chunks, s); goto launched; }
@@ -1117,7 +1168,7 @@ extern "C" int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* p) {
   if (!p) return 0;
   switch (gemm_path(p)) {
     case kPathWgrad: {
-      const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows());
+      const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows(), wgrad_max_chunks());
       return chunks > 1 ? (int64_t)chunks * p->batch * ((int64_t)p->M * p->N + p->N) : 0;
     }
     case kPathRows:
