@@ -752,10 +752,11 @@ __host__ __device__ inline int wgrad_chunks(int64_t K, int min_rows = kWMinRows,
   return c < 1 ? 1 : (int)c;
 }
 
-// workspace layout: [batch][chunk][M*N + N]; U row pairs of loads in flight per wave.  FLAT (no row grouping on A or
-// B): every load unconditional -- the row clamped into the chunk, the column into the matrix, out-of-range values
-// zeroed by a select -- so a row pair's loads issue back to back; with grouping each load sits behind a branch and
-// a 64-bit division (row_off64), which made the loop issue-bound (SALU ~ VALU instructions, PMC)
+// workspace layout: [batch][chunk][M*N + N]; U row pairs of loads in flight per wave.  Every load is unconditional --
+// the row clamped into the chunk, the column into the matrix, out-of-range values zeroed by a select -- so a row
+// pair's loads issue back to back (guarded loads each sat behind a branch and a 64-bit row division, which made the
+// loop issue-bound: SALU ~ VALU instructions, PMC); FLAT (no row grouping) addresses rows as k * ld, grouped rows
+// with 32-bit arithmetic.
 template <int MT, int NT, int U, bool FLAT>
 __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
@@ -797,13 +798,14 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
   // row pairs (2q, 2q+1) of the chunk, interleaved over the waves; lane half h takes row 2q + h
   for (int64_t k0 = r0 + 2 * wave; k0 < r1; k0 += 2 * kWWaves * U) {
     float a[U][MT], bb[U][NT];
-    if constexpr (FLAT) {  // every load of the U row pairs first, then the selects (one wait for all of them)
+    if constexpr (true) {  // every load of the U row pairs first, then the selects (one wait for all of them)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t k = k0 + 2 * kWWaves * u + h;
         const int64_t kc = k < r1 ? k : r0;
-        const float* Ar = A + kc * p.lda;
-        const float* Br = B + kc * p.ldb;
+        // grouped rows: 32-bit row arithmetic (K < 2^31), one division per row instead of row_off64's 64-bit one
+        const float* Ar = A + (FLAT ? kc * p.lda : row_off((int)kc, p.lda, p.a_grp, p.a_gstride));
+        const float* Br = B + (FLAT ? kc * p.ldb : row_off((int)kc, p.ldb, p.b_grp, p.b_gstride));
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) a[u][mt] = Ar[mcol[mt]];
 #pragma unroll
@@ -819,7 +821,7 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
       }
     }
 #pragma unroll
-    for (int u = 0; u < (FLAT ? 0 : U); ++u) {
+    for (int u = 0; u < 0; ++u) {  // (the guarded form, kept for reference: no longer instantiated)
       const int64_t k = k0 + 2 * kWWaves * u + h;
       const bool kok = k < r1;
       {
@@ -960,11 +962,7 @@ int wgrad_unroll() {  // default 4 with the branch-free loads: M64 N192 66.9 -> 
   static int v = env_knob("DGPPO_WGRAD_U", 4);
   return v == 4 ? 4 : 2;
 }
-// the branch-free loads of ungrouped operands (DGPPO_WGRAD_FLAT=0 keeps the guarded loads: A/B)
-int wgrad_flat() {
-  static int v = env_knob("DGPPO_WGRAD_FLAT", 1);
-  return v;
-}
+
 
 GemmPath gemm_path(const dgppo_gemm_args* p) {
   if (p->trans_a && !p->trans_b && p->N <= 192 && p->M <= 4096 && !p->bias && !p->addend && !p->relu)
@@ -1003,7 +1001,7 @@ void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
   const int gm = (p->M + MT * 32 - 1) / (MT * 32), gn = (p->N + NT * 32 - 1) / (NT * 32);
   const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
   const dim3 grid(chunks, gm * gn, p->batch);
-  const bool flat = p->a_grp <= 0 && p->b_grp <= 0 && wgrad_flat();
+  const bool flat = p->a_grp <= 0 && p->b_grp <= 0;
   if (wgrad_unroll() == 4 && MT * NT <= 4) {
     if (flat) hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 4, true>), grid, dim3(512), lds, s, *p, chunks, gn);
     else hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 4, false>), grid, dim3(512), lds, s, *p, chunks, gn);
@@ -1013,7 +1011,12 @@ void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
   }
 }
 
-int launch_wgrad(const dgppo_gemm_args* p, hipStream_t s) {
+int launch_wgrad(const dgppo_gemm_args* p0, hipStream_t s) {
+  // a grouping whose group stride is grp rows is the plain row layout: drop it (the flat kernel's addressing)
+  dgppo_gemm_args q = *p0;
+  if (q.a_grp > 0 && q.a_gstride == (int64_t)q.a_grp * q.lda) q.a_grp = 0;
+  if (q.b_grp > 0 && q.b_gstride == (int64_t)q.b_grp * q.ldb) q.b_grp = 0;
+  const dgppo_gemm_args* p = &q;
   int MT, NT;
   wgrad_shape(p->M, p->N, &MT, &NT);
   const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows(), wgrad_max_chunks());

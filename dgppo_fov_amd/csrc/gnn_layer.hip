@@ -598,13 +598,13 @@ struct Carve {
   int floats;
 };
 template <int DM>
-Carve carve(int gpb, int N, int n, int F) {
+Carve carve(int gpb, int N, int n, int F, bool stage) {
   using L = Lay<DM>;
   constexpr bool agent = DM == 32;
   Carve c;
-  int o = (gpb * N * L::XP + 3) & ~3;
+  int o = stage ? (gpb * N * L::XP + 3) & ~3 : 0;
   c.raw = o;
-  o += agent ? gpb * N * kD0 : 0;
+  o += (agent && stage) ? gpb * N * kD0 : 0;
   c.qt = o;
   o += kRows * L::QP;
   c.gs = o;
@@ -618,21 +618,31 @@ Carve carve(int gpb, int N, int n, int F) {
   o += agent ? 4 * 16 * kPS : 0;
   c.pre = o;
   o += agent ? kD0 * 32 + 32 : 0;
-  const bool pa_own = wsum_lds() && L::GP < 128;  // else the pair slots live in the gs rows
+  const bool pa_own = stage && wsum_lds() && L::GP < 128;  // else the pair slots live in the gs rows
   c.pa = pa_own ? o : 0;
   o += pa_own ? 4 * 64 * 4 : 0;
   c.floats = o;
   return c;
 }
+// staging the graphs (STAGE) or gathering per lane as attn_bwd2r does (the default: 3 workgroups per CU)
+static bool bwd_stage() {
+  static const bool v = [] {
+    const char* e = getenv("DGPPO_LAYER_BWD_STAGE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 template <int DM>
-int64_t grid_cap() {
-  return DM == 32 ? 512 : 2048;  // resident workgroups: 2 per CU at the DM = 32 carve (~65 KB of LDS)
+int64_t grid_cap(bool stage) {
+  // resident workgroups: 2 per CU at the staged DM = 32 carve (~65 KB of LDS), 3 at the gather carve (~37 KB, VGPRs)
+  return DM == 32 ? (stage ? 512 : 768) : 2048;
 }
 }  // namespace lb
 
-template <int DM, bool WSL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 2 : 4, 8))) void gnn_layer_bwd_kernel(
-    dgppo_gnn_layer_bwd_args p, int gpb, int64_t nblk, lb::Carve cv) {
+template <int DM, bool WSL, bool STAGE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? (STAGE ? 2 : 3) : 4, 8))) void
+gnn_layer_bwd_kernel(dgppo_gnn_layer_bwd_args p, int gpb, int64_t nblk, lb::Carve cv) {
+  static_assert(STAGE || !WSL, "the LDS-loop sums read the staged rows");
   using L = lb::Lay<DM>;
   constexpr int XP = L::XP, HS = L::HS, QP = L::QP, GP = L::GP, kPS = lb::kPS;
   constexpr bool agent = DM == 32;
@@ -668,15 +678,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 
     const int ng = (int)((int64_t)a.G - g0 < gpb ? (int64_t)a.G - g0 : gpb);
     const int nrec = ng * n;
     const int64_t row0 = g0 * n;
-    // ---- stage 1: graphs, [qt | beta] rows, dY rows into LDS; dxcat tile and dxa accumulator cleared
+    // ---- stage 1: graphs (STAGE), [qt | beta] rows, dY rows into LDS; dxcat tile and dxa accumulator cleared
     if constexpr (agent) {
       const int D0 = a.D0;
-      for (int t = tid; t < ng * N * kD0; t += 256) {
+      for (int t = tid; t < (STAGE ? ng * N * kD0 : 0); t += 256) {
         const int node = t >> 3, k = t & 7;
         const int g = node / N, j = node - g * N;
         raw[t] = k < D0 ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D0 + k] : 0.0f;
       }
-      for (int t = tid; t < nrec * (DM / 4); t += 256) {
+      for (int t = tid; t < (STAGE ? nrec * (DM / 4) : 0); t += 256) {
         const int r = t / (DM / 4), q = t - r * (DM / 4);
         const int g = r / n, i = r - g * n;
         *(f32x4*)(xs + (g * N + i) * XP + 4 * q) =
@@ -684,7 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 
       }
       for (int t = tid; t < kRows * DM; t += 256) dxacc[t] = 0.0f;
     } else {
-      for (int t = tid; t < ng * N * XP; t += 256) {
+      for (int t = tid; t < (STAGE ? ng * N * XP : 0); t += 256) {
         const int node = t / XP, k = t - node * XP;
         const int g = node / N, j = node - g * N;
         xs[t] = k < D ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D + k] : 0.0f;
@@ -708,7 +718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 
     for (int t = tid; t < kRows * GP; t += 256) gs[t] = 0.0f;
     __syncthreads();
     // ---- stage 2: never-receivers' rows (agent mode; the forward's order of operations) and dxcat = dY Wcat^T / H
-    if constexpr (agent) {
+    if constexpr (agent && STAGE) {
       const int nn = N - n;
       for (int t = tid; t < ng * nn * (DM / 4); t += 256) {
         const int q = t & (DM / 4 - 1), rr = t / (DM / 4);
@@ -790,15 +800,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 
       f32x4 ef = {0.0f, 0.0f, 0.0f, 0.0f};
       if (ok) ef = *(const f32x4*)(a.ef + (g0 + gl) * a.ef_gstride + (int64_t)e * 4);
       float x[DM];
-      {
+      float xg[kD0];  // the gather form's raw row of a never-receiving sender (its pre-gradient operand)
+      const bool viapre = agent && ok && s >= n;
+      if constexpr (STAGE) {
         const float* xr = xs + (gl * N + (ok ? s : 0)) * XP;
 #pragma unroll
         for (int q = 0; q < DM / 4; ++q) {
           const f32x4 v = ok ? *(const f32x4*)(xr + 4 * q) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
           x[4 * q] = v[0], x[4 * q + 1] = v[1], x[4 * q + 2] = v[2], x[4 * q + 3] = v[3];
         }
+      } else if (!agent || !viapre) {  // node rows (full mode) / agent senders' layer input rows (attn_bwd2r's gathers)
+        const float* xr = agent ? a.xa + (g0 + gl) * a.xa_gstride + (int64_t)(ok ? s : 0) * D
+                                : a.x + (g0 + gl) * a.x_gstride + (int64_t)(ok ? s : 0) * D;
+#pragma unroll
+        for (int d = 0; d < DM; ++d) x[d] = (ok && d < D) ? xr[d] : 0.0f;
+      } else {  // never-receiving sender: relu(x_raw pre_W + pre_b), attn_bwd2r's order of operations
+        const float* xr = a.x + (g0 + gl) * a.x_gstride + (int64_t)s * a.D0;
+#pragma unroll
+        for (int k = 0; k < kD0; ++k) xg[k] = k < a.D0 ? xr[k] : 0.0f;
+#pragma unroll
+        for (int q = 0; q < DM / 4; ++q) {
+          const f32x4 b = *(const f32x4*)(preb + 4 * q);
+          x[4 * q] = b[0], x[4 * q + 1] = b[1], x[4 * q + 2] = b[2], x[4 * q + 3] = b[3];
+        }
+#pragma unroll
+        for (int k = 0; k < kD0; ++k)
+#pragma unroll
+          for (int q = 0; q < DM / 4; ++q) {
+            const f32x4 w = *(const f32x4*)(preW + k * 32 + 4 * q);
+            x[4 * q] += xg[k] * w[0];
+            x[4 * q + 1] += xg[k] * w[1];
+            x[4 * q + 2] += xg[k] * w[2];
+            x[4 * q + 3] += xg[k] * w[3];
+          }
+#pragma unroll
+        for (int d = 0; d < DM; ++d) x[d] = x[d] > 0.0f ? x[d] : 0.0f;
       }
-      const bool viapre = agent && ok && s >= n;
       // ---- softmax backward
       const float* gv = gs + rl * GP;
       float dl[kH], dbeta[kH];
@@ -899,10 +936,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? 
       // ---- never-receivers' Dense_4 gradient: gacc[ct] += [x_raw | 1]^T dz over 16-pair chunks
       if (want_pre) {
         float xraw[kD0];
-        {
+        if constexpr (STAGE) {
           const float* xr = raw + (gl * N + (viapre ? s : 0)) * kD0;
 #pragma unroll
           for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? xr[k] : 0.0f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? xg[k] : 0.0f;
         }
 #pragma unroll 1
         for (int ch = 0; ch < 4; ++ch) {
@@ -1017,14 +1057,16 @@ bool bwd_supported(const dgppo_gnn_layer_bwd_args* p) {
     if (a.dxa && (a.dxa_gstride != (int64_t)a.n_agents * 32 || !p->Wu || !p->QBW)) return false;
   }
   const int gpb = kRows / a.n_agents;
-  const lb::Carve c = a.xa ? lb::carve<32>(gpb, a.N, a.n_agents, a.F) : lb::carve<8>(gpb, a.N, a.n_agents, a.F);
+  const bool st = lb::bwd_stage();
+  const lb::Carve c =
+      a.xa ? lb::carve<32>(gpb, a.N, a.n_agents, a.F, st) : lb::carve<8>(gpb, a.N, a.n_agents, a.F, st);
   return (size_t)c.floats * sizeof(float) <= 80 * 1024;
 }
 
 int64_t bwd_grid(const dgppo_gnn_layer_bwd_args* p, int64_t* nblk) {
   const int gpb = kRows / p->a.n_agents;
   *nblk = ((int64_t)p->a.G + gpb - 1) / gpb;
-  const int64_t cap = p->a.xa ? lb::grid_cap<32>() : lb::grid_cap<8>();
+  const int64_t cap = p->a.xa ? lb::grid_cap<32>(lb::bwd_stage()) : lb::grid_cap<8>(lb::bwd_stage());
   return *nblk < cap ? *nblk : cap;
 }
 
@@ -1050,24 +1092,23 @@ extern "C" int dgppo_gnn_layer_bwd(const dgppo_gnn_layer_bwd_args* p, void* stre
   int64_t nblk;
   const unsigned grid = (unsigned)bwd_grid(p, &nblk);
   hipStream_t s = (hipStream_t)stream;
+  const bool st = lb::bwd_stage(), wsl = st && wsum_lds();
+  const lb::Carve c = a.xa ? lb::carve<32>(gpb, a.N, a.n_agents, a.F, st) : lb::carve<8>(gpb, a.N, a.n_agents, a.F, st);
+  const size_t bytes = (size_t)c.floats * sizeof(float);
+#define GLB_LAUNCH(DMv, WSLv, STv)                                                                              \
+  do {                                                                                                          \
+    if (bytes > 64 * 1024) allow_lds((const void*)gnn_layer_bwd_kernel<DMv, WSLv, STv>);                       \
+    hipLaunchKernelGGL((gnn_layer_bwd_kernel<DMv, WSLv, STv>), dim3(grid), dim3(256), bytes, s, *p, gpb, nblk, c); \
+  } while (0)
   if (a.xa) {
-    const lb::Carve c = lb::carve<32>(gpb, a.N, a.n_agents, a.F);
-    const size_t bytes = (size_t)c.floats * sizeof(float);
-    if (wsum_lds()) {
-      if (bytes > 64 * 1024) allow_lds((const void*)gnn_layer_bwd_kernel<32, true>);
-      hipLaunchKernelGGL((gnn_layer_bwd_kernel<32, true>), dim3(grid), dim3(256), bytes, s, *p, gpb, nblk, c);
-    } else {
-      if (bytes > 64 * 1024) allow_lds((const void*)gnn_layer_bwd_kernel<32, false>);
-      hipLaunchKernelGGL((gnn_layer_bwd_kernel<32, false>), dim3(grid), dim3(256), bytes, s, *p, gpb, nblk, c);
-    }
+    if (!st) GLB_LAUNCH(32, false, false);
+    else if (wsl) GLB_LAUNCH(32, true, true);
+    else GLB_LAUNCH(32, false, true);
   } else {
-    const lb::Carve c = lb::carve<8>(gpb, a.N, a.n_agents, a.F);
-    if (wsum_lds())
-      hipLaunchKernelGGL((gnn_layer_bwd_kernel<8, true>), dim3(grid), dim3(256), (size_t)c.floats * sizeof(float), s,
-                         *p, gpb, nblk, c);
-    else
-      hipLaunchKernelGGL((gnn_layer_bwd_kernel<8, false>), dim3(grid), dim3(256), (size_t)c.floats * sizeof(float), s,
-                         *p, gpb, nblk, c);
+    if (!st) GLB_LAUNCH(8, false, false);
+    else if (wsl) GLB_LAUNCH(8, true, true);
+    else GLB_LAUNCH(8, false, true);
   }
+#undef GLB_LAUNCH
   return (int)hipGetLastError();
 }
