@@ -26,6 +26,10 @@ from ... import _lib
 from ...nn import kernels as K
 from ...nn.layers import FUSE_LN, GNN, Dense, GraphBatch, MLPHead, ParamSpace, RNNStack
 
+# the whole forward-only get_Vh in the GNN layer's kernel (its value-head tail): measured slower than the layer kernel +
+# the unfused head GEMMs (418 vs ~334 us per 131k agent rows: every 16-row workgroup reloads the head / GRU weights
+# from L2), so off unless DGPPO_VH_TAIL=1
+VH_TAIL = os.environ.get("DGPPO_VH_TAIL", "0") == "1"
 STD_DEV_INIT_INV = math.log(math.exp(0.5) - 1.0)  # TanhNormal.std_dev_init_inv (policy.py:54-59)
 STD_DEV_MIN = 1e-5
 
@@ -302,7 +306,7 @@ class VhNet(_Net):
         """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, W): (G*n, n_cost).  Forward only
         (keep_cache False): GNN, head, GRU step and output Dense in one kernel where it applies (the prepass)."""
         rows = g.G * self.n
-        if not keep_cache and self.gru.simple and len(self.gnn.layers) == 1 and h.shape[1] == 64:
+        if VH_TAIL and not keep_cache and self.gru.simple and len(self.gnn.layers) == 1 and h.shape[1] == 64:
             out = torch.empty((rows, self.n_cost), device=h.device)
             hd, cell = self.head, self.gru.cells[0]
             v = self.ps.view

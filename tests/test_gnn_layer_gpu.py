@@ -130,8 +130,14 @@ def test_forward_only_epilogues_match_unfused(cuda, eid, n, obs):
     vl = VlNet(env.node_dim, n, cuda, seed=6, edge_dim=env.edge_dim)
     vh = VhNet(env.node_dim, n, env.n_cost, cuda, seed=4, edge_dim=env.edge_dim)
     h = torch.randn((g.G * n, 64), device=cuda, generator=torch.Generator(device=cuda).manual_seed(2)) * 0.5
+    from dgppo_fov_amd.algo.module import nets
+
     zf = vl.graph_means(g)
-    vf, cf = vh.fwd(g, h, keep_cache=False)
+    old_tail, nets.VH_TAIL = nets.VH_TAIL, True
+    try:
+        vf, cf = vh.fwd(g, h, keep_cache=False)
+    finally:
+        nets.VH_TAIL = old_tail
     assert cf is None
     old = layers.FUSED_LAYER
     layers.FUSED_LAYER = False
