@@ -1730,7 +1730,8 @@ constexpr int kPS = 44;  // chunk staging row: dz (0..31) | x_raw (32..39) | 1 (
 template <int DM>
 size_t lds_floats(int n, int D) {
   using L = bwd2::Lay<DM>;
-  return (size_t)bwd2::kRows * (L::QP + L::GP) + kD0 * 32 + 32 + 4 * 16 * kPS + (size_t)bwd2::kRows * n * D;
+  return (size_t)bwd2::kRows * (L::QP + L::GP) + kD0 * 32 + 32 + 4 * 16 * kPS + (size_t)bwd2::kRows * n * D +
+         4 * 256;
 }
 }  // namespace bwd2r
 
@@ -1750,6 +1751,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
   float* preb = preW + kD0 * 32;    // [32]
   float* stg = preb + 32;           // per wave [16][kPS]: pre-gradient chunk staging
   float* cbi = stg + 4 * 16 * kPS;  // [rows][n][D] agent-sender contributions
+  int* pse = reinterpret_cast<int*>(cbi + bwd2::kRows * p.n_agents * p.D);  // [2 sub-rounds][s, e][256]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, kq = lane >> 4;
   const int slot = lane >> 5, c = lane & 31;
@@ -1768,26 +1770,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
   f32x4 gacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // [x_raw | 1]^T dz
   float* ws = stg + wave * 16 * kPS;
   const int TQ = (D + 3) >> 2, W = H * (D + 5);
+  // A block's staged rows (qt, dxcat) and its pairs' senders / candidates are loaded into registers with every
+  // load issued before the first use: one memory round trip per block (a runtime-bounded staging loop waits for
+  // each load before its LDS store: 13 round trips per block at DM = 32; attn_bwd2r<32> 405 -> 380 us).  Issuing
+  // the next block's loads before this block's epilogue instead spilled at DM = 32 and measured slower (579 us).
+  static_assert(kSR == 2, "two sub-rounds per block");
+  constexpr int NQS = (kRows * 3 * HS + 255) / 256, NGS = (kRows * kGP + 255) / 256, NXS = (kRows * DM + 255) / 256;
+  float qv[NQS], gw[NGS];
+  int sv[kSR], ev[kSR];
+  // (tid: threadIdx.x behind an empty asm, so that the per-lane index math below is redone per block instead of
+  // being hoisted out of the block loop as 64-bit addresses that then spill)
+  auto load_block = [&](int64_t b, int tid) {
+    const int64_t bg0 = b * gpb;
+    const int bnrec = (int)((int64_t)p.G - bg0 < gpb ? (int64_t)p.G - bg0 : gpb) * n;
+    const int64_t brow0 = bg0 * n;
+    const int32_t* sb = p.sidx + brow0 * C;
+    const float* qb = p.qt + brow0 * qt_ld(p);
+    const float* xb = p.dxcat + brow0 * W;
+    const int qld = (int)qt_ld(p);
+#pragma unroll
+    for (int sr = 0; sr < kSR; ++sr) {
+      const int rl = 2 * (tid >> 6) + 8 * sr + ((tid >> 5) & 1), cc = tid & 31;
+      const bool act = rl < bnrec;
+      const int i = act ? rl - (rl / n) * n : 0;
+      int s = -1, e = 0;
+      if (act && cc < C) {
+        e = p.cand[i * C + cc];
+        s = sb[rl * C + cc];
+      }
+      sv[sr] = s;
+      ev[sr] = e;
+    }
+#pragma unroll
+    for (int k = 0; k < NQS; ++k) {
+      const int e = tid + 256 * k;
+      const int r = e / (3 * HS), kk = e - r * (3 * HS), h = kk / HS, d = kk - h * HS;
+      qv[k] = (e < kRows * 3 * HS && r < bnrec && d < D) ? qb[r * qld + h * D + d] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < NGS; ++k) {
+      const int e = tid + 256 * k;
+      const int r = e / kGP, kk = e - r * kGP;
+      int src = -1;
+      if (kk < 3 * HS) src = (kk % HS) < D ? (kk / HS) * D + (kk % HS) : -1;
+      else if (kk < 3 * HS + 12) src = H * D + (kk - 3 * HS);
+      else if (kk < 3 * HS + 15) src = H * D + 4 * H + (kk - 3 * HS - 12);
+      gw[k] = (e < kRows * kGP && r < bnrec && src >= 0) ? xb[r * W + src] : 0.0f;
+    }
+  };
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    load_block(blk, tid);
     const int64_t g0 = blk * gpb;
     const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
     const int nrec = ng * n;
     const int64_t row0 = g0 * n;
-    // ---- block staging: qt rows, dxcat rows (split at aligned offsets), agent image cleared
-    for (int e = threadIdx.x; e < kRows * 3 * HS; e += 256) {
-      const int r = e / (3 * HS), k = e - r * (3 * HS), h = k / HS, d = k - h * HS;
-      qts[r * kQP + k] = (r < nrec && d < D) ? p.qt[(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
+    // ---- block staging from the registers: qt rows, dxcat rows (split at aligned offsets), agent image cleared
+#pragma unroll
+    for (int k = 0; k < NQS; ++k) {
+      const int e = tid + 256 * k;
+      const int r = e / (3 * HS), kk = e - r * (3 * HS);
+      if (e < kRows * 3 * HS) qts[r * kQP + kk] = qv[k];
     }
-    for (int e = threadIdx.x; e < kRows * kGP; e += 256) {
-      const int r = e / kGP, k = e - r * kGP;
-      int src = -1;
-      if (k < 3 * HS) src = (k % HS) < D ? (k / HS) * D + (k % HS) : -1;
-      else if (k < 3 * HS + 12) src = H * D + (k - 3 * HS);
-      else if (k < 3 * HS + 15) src = H * D + 4 * H + (k - 3 * HS - 12);
-      gs[e] = (r < nrec && src >= 0) ? p.dxcat[(row0 + r) * W + src] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < NGS; ++k) {
+      const int e = tid + 256 * k;
+      if (e < kRows * kGP) gs[e] = gw[k];
     }
     if (want_dxa)
       for (int e = threadIdx.x; e < kRows * n * D; e += 256) cbi[e] = 0.0f;
+#pragma unroll
+    for (int sr = 0; sr < kSR; ++sr) {  // (through LDS: 4 fewer registers live across the sub-rounds)
+      pse[(2 * sr) * 256 + tid] = sv[sr];
+      pse[(2 * sr + 1) * 256 + tid] = ev[sr];
+    }
     __syncthreads();
 #pragma unroll 1
     for (int sr = 0; sr < kSR; ++sr) {
@@ -1796,13 +1853,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
       const int64_t row = row0 + rl;
       // ---- the pair: sender, edge, attention, sender row
       const int gl = active ? rl / n : 0;
-      const int i = active ? rl - gl * n : 0;
       const int64_t g = g0 + gl;
-      int s = -1, e = 0;
-      if (active && c < C) {
-        e = p.cand[i * C + c];
-        s = p.sidx[row * C + c];
-      }
+      const int s = pse[(2 * sr) * 256 + tid], e = pse[(2 * sr + 1) * 256 + tid];
       const bool ok = s >= 0;
       float av[kH];
 #pragma unroll
@@ -1946,16 +1998,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
         }
       }
     }
+    // the agent rows' current d xa (the epilogue adds this block's sums to them)
+    float dxv[NXS];
+#pragma unroll
+    for (int k = 0; k < NXS; ++k) {
+      const int e = tid + 256 * k;
+      const int gl = e / (n * D), jd = e - gl * (n * D);
+      dxv[k] = (want_dxa && e < nrec * D) ? p.dxa[(g0 + gl) * p.dxa_gstride + jd] : 0.0f;
+    }
     __syncthreads();
     if (want_dxa) {  // agent j of graph gl: sum over its receivers i in order
-      for (int e = threadIdx.x; e < nrec * D; e += 256) {
-        const int gl = e / (n * D), jd = e - gl * (n * D), j = jd / D, d = jd - j * D;
-        float acc = 0.0f;
-        for (int i = 0; i < n; ++i) acc += cbi[((gl * n + i) * n + j) * D + d];
-        p.dxa[(g0 + gl) * p.dxa_gstride + j * D + d] += acc;
+#pragma unroll
+      for (int k = 0; k < NXS; ++k) {
+        const int e = tid + 256 * k;
+        if (e < nrec * D) {
+          const int gl = e / (n * D), jd = e - gl * (n * D), j = jd / D, d = jd - j * D;
+          float acc = 0.0f;
+          for (int i = 0; i < n; ++i) acc += cbi[((gl * n + i) * n + j) * D + d];
+          p.dxa[(g0 + gl) * p.dxa_gstride + jd] = dxv[k] + acc;
+        }
       }
-      __syncthreads();
     }
+    __syncthreads();  // the sub-rounds' staging reads and the image sums are done before the next block's writes
   }
   if (want_pre) {  // fixed-order combine of the 4 waves' accumulators -> this workgroup's partial row
     float* red = stg;  // [16][33] (the staging area is free now)
@@ -2028,9 +2092,8 @@ void bwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
     const void* fn = v == 0 ? (const void*)attn_bwd2r_kernel<8>
                             : (v == 1 ? (const void*)attn_bwd2r_kernel<16> : (const void*)attn_bwd2r_kernel<32>);
     if (bytes > 64 * 1024) allow_lds(fn);
-    if (v == 0) hipLaunchKernelGGL(attn_bwd2r_kernel<8>, dim3(grid), dim3(256), bytes, s, *p, nblk);
-    else if (v == 1) hipLaunchKernelGGL(attn_bwd2r_kernel<16>, dim3(grid), dim3(256), bytes, s, *p, nblk);
-    else hipLaunchKernelGGL(attn_bwd2r_kernel<32>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(dgppo_gnn_attn_args, int64_t)>(const_cast<void*>(fn)), dim3(grid),
+                       dim3(256), bytes, s, *p, nblk);
     return;
   }
   const size_t bytes = (v == 0   ? bwd2::lds_floats<8>(p->n_agents, p->D)

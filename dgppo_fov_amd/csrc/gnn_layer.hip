@@ -49,6 +49,20 @@ struct Lay {
 
 constexpr int kYP = 68;  // Y / carry tile pitch (64 + 4)
 
+// dst[t] = ld(t) for t = tid, tid + 256, .. < total, U loads in flight per lane: a plain runtime-bounded copy loop
+// waits for each global load before its LDS store (one memory round trip per 256 elements)
+template <int U, class Ld>
+__device__ __forceinline__ void stage_copy(float* dst, int total, int tid, Ld ld) {
+  for (int t0 = tid; t0 < total; t0 += 256 * U) {
+    float v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = t0 + 256 * j < total ? ld(t0 + 256 * j) : 0.0f;
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (t0 + 256 * j < total) dst[t0 + 256 * j] = v[j];
+  }
+}
+
 struct Carve {
   // float offsets: node rows at 0 | raw rows / xcat tile | qt rows | pre_W, pre_b | Y tile (zmean, tail) | tail
   // carries [16][kYP] | tail LayerNorm parameters [4][64] | per-wave pair weights [4][64] float4 (LDS-loop sums)
@@ -168,6 +182,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
   // ---- stage 1: the block's graphs into LDS (coalesced), qt rows cleared
   if constexpr (agent) {
     const int D0 = a.D0;
+    // (one load per iteration: batching these loads -- eight in flight, or a float4 copy -- measured no faster
+    // here, and the extra paths cost the kernel's later phases ~10%, 220 -> 242 us; DGPPO_LAYER_STAGE A/B)
     for (int t = tid; t < ng * N * kD0; t += 256) {
       const int node = t >> 3, k = t & 7;
       const int g = node / N, j = node - g * N;
@@ -184,10 +200,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
       if (tid < 32) preb[tid] = a.pre_b[tid];
     }
   } else {
-    for (int t = tid; t < ng * N * XP; t += 256) {
-      const int node = t / XP, k = t - node * XP;
-      const int g = node / N, j = node - g * N;
-      xs[t] = k < D ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D + k] : 0.0f;
+    const float* xb = a.x + g0 * a.x_gstride;
+    if (a.x_gstride == (int64_t)N * D) {
+      stage_copy<8>(xs, ng * N * XP, tid, [&](int t) {
+        const int node = t / XP, k = t - node * XP;
+        return k < D ? xb[node * D + k] : 0.0f;
+      });
+    } else {
+      const int xg = (int)a.x_gstride;
+      stage_copy<8>(xs, ng * N * XP, tid, [&](int t) {
+        const int node = t / XP, k = t - node * XP;
+        const int g = node / N, j = node - g * N;
+        return k < D ? xb[g * xg + j * D + k] : 0.0f;
+      });
     }
   }
   for (int t = tid; t < kRows * QP; t += 256) qts[t] = 0.0f;
