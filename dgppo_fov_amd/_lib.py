@@ -238,6 +238,19 @@ class GnnLayerBwdArgs(ctypes.Structure):  # ABI 11 dgppo_gnn_layer_bwd_args
     _fields_ = [("a", GnnAttnArgs), ("dY", c_f32p), ("QBW", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p), ("mask", c_f32p)]
 
 
+ADAM_MAX_NETS = 4  # include/dgppo_hip.h DGPPO_ADAM_MAX_NETS
+
+
+class AdamNet(ctypes.Structure):  # ABI 12 dgppo_adam_net
+    _fields_ = [("param", c_f32p), ("grad", c_f32p), ("m", c_f32p), ("v", c_f32p), ("n", ctypes.c_int64),
+                ("state", c_f32p), ("lr", ctypes.c_float), ("max_norm", ctypes.c_float)]
+
+
+class AdamMultiArgs(ctypes.Structure):  # ABI 12 dgppo_adam_multi_args
+    _fields_ = [("n_nets", ctypes.c_int32), ("eps", ctypes.c_float), ("b1", ctypes.c_double), ("b2", ctypes.c_double),
+                ("workspace", c_f32p), ("net", AdamNet * ADAM_MAX_NETS)]
+
+
 class TanhNormalArgs(ctypes.Structure):
     _fields_ = [
         ("rows", ctypes.c_int64),
@@ -322,6 +335,8 @@ SIGNATURES = {
     "dgppo_dgppo_advantages": (ctypes.c_int, [ctypes.POINTER(AdvArgs), ctypes.c_void_p]),
     "dgppo_grad_norm": (ctypes.c_int, [_V, _I64, _V, _V, _V]),
     "dgppo_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, _V, _F32, ctypes.c_double, ctypes.c_double, _F32, _F32, _V]),
+    "dgppo_adam_multi_workspace_floats": (ctypes.c_int64, []),
+    "dgppo_adam_multi": (ctypes.c_int, [_V, _V]),
     "dgppo_normal": (ctypes.c_int, [_V, _I64, _V, ctypes.c_uint64, ctypes.c_uint64, _V]),
     "dgppo_clip_min0": (ctypes.c_int, [_V, _V, _I64, _V]),
     "dgppo_lagr_advantages": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _I32, _I32, _I32, _I32, _V]),
@@ -337,7 +352,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 11  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 12  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

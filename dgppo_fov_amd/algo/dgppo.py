@@ -64,6 +64,11 @@ def PHASE_EVENTS() -> bool:
     return os.environ.get("DGPPO_PHASE_EVENTS", "0") == "1"
 
 
+def ADAM_MULTI() -> bool:
+    """The three nets' clip + Adam steps in two launches (dgppo_adam_multi) instead of four per net (default on)."""
+    return os.environ.get("DGPPO_ADAM_MULTI", "1") == "1"
+
+
 def FORCE_SAFE() -> bool:
     """Learning-dynamics ablation (scripts/learn_ablate.sh): treat every sample as inside the safe set."""
     return os.environ.get("DGPPO_DEBUG_FORCE_SAFE", "0") == "1"
@@ -525,7 +530,14 @@ class DGPPO:
         return out
 
     def _mb_apply(self):
-        for name in ("Vl", "Vh", "policy"):
+        """clip + finite check + Adam of the three nets: two launches for all three (dgppo_adam_multi, bit-identical
+        to the per-net grad_norm + adam pairs; DGPPO_ADAM_MULTI=0 runs the pairs)."""
+        names = ("Vl", "Vh", "policy")
+        if ADAM_MULTI() and self.device.type == "cuda":
+            K.adam_multi([(o.ps.flat, o.ps.grad, o.m, o.v, o.state, o.lr, o.max_norm)
+                          for o in (self.opt[k] for k in names)])
+            return
+        for name in names:
             self.opt[name].step()
 
     def _mb_body(self, envs, rollout, det, A, Ql, Qh_det, Bm, T, L, ph, apply=True):

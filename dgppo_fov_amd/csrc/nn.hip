@@ -677,6 +677,68 @@ __global__ void adam_count_kernel(float* state) {
   if (threadIdx.x == 0 && state[1] == 0.0f) state[2] += 1.0f;
 }
 
+// ---- several nets' grad_norm + adam in two launches (dgppo_adam_multi): blockIdx.y = net.  The partials, the
+// norm (wave 0 of every workgroup redoes norm_final_kernel's sums over the same partials) and the update are
+// norm_final / adam_kernel's arithmetic, so the results are bit-identical to the per-net launches.
+constexpr int kAdamParts = 512;  // = kLossBlocks: partial blocks per net
+struct AdamMultiDev {
+  dgppo_adam_multi_args a;
+  float omb1, omb2;
+};
+__global__ __launch_bounds__(256) void sumsq_multi_kernel(AdamMultiDev d) {
+  const dgppo_adam_net& t = d.a.net[blockIdx.y];
+  float* part = d.a.workspace + (int64_t)blockIdx.y * kAdamParts * 8;
+  float v[2] = {0.0f, 0.0f};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < t.n; i += (int64_t)gridDim.x * 256) {
+    const float x = t.grad[i];
+    v[0] += x * x;
+    v[1] += isfinite(x) ? 0.0f : 1.0f;
+  }
+  block_sums(v, 2, part);
+  // the step count before this update, read by every workgroup of the second kernel (workgroup 0 rewrites state)
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.a.workspace[(int64_t)DGPPO_ADAM_MAX_NETS * kAdamParts * 8 + blockIdx.y] = t.state[2];
+}
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMultiDev d) {
+  const dgppo_adam_net& t = d.a.net[blockIdx.y];
+  const float* part = d.a.workspace + (int64_t)blockIdx.y * kAdamParts * 8;
+  __shared__ float nrm[2];
+  if (threadIdx.x < 64) {
+    float s = 0.0f, nf = 0.0f;
+    for (int b = threadIdx.x; b < kAdamParts; b += 64) {
+      s += part[b * 8 + 0];
+      nf += part[b * 8 + 1];
+    }
+    s = wave_sum(s);
+    nf = wave_sum(nf);
+    if (threadIdx.x == 0) {
+      nrm[0] = sqrtf(s);
+      nrm[1] = nf;
+    }
+  }
+  __syncthreads();
+  const float gnorm = nrm[0], nf = nrm[1];
+  const float count = d.a.workspace[(int64_t)DGPPO_ADAM_MAX_NETS * kAdamParts * 8 + blockIdx.y];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    t.state[0] = gnorm;
+    t.state[1] = nf;
+    if (nf == 0.0f) t.state[2] = count + 1.0f;
+  }
+  if (nf != 0.0f) return;  // apply_if_finite: skip the whole update
+  const float b1 = (float)d.a.b1, b2 = (float)d.a.b2, max_norm = t.max_norm, lr = t.lr, eps = d.a.eps;
+  const float c = fmaxf(max_norm, gnorm);
+  const float tt = count + 1.0f;
+  const float bc1 = 1.0f - powf(b1, tt);
+  const float bc2 = 1.0f - powf(b2, tt);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < t.n; i += (int64_t)gridDim.x * 256) {
+    const float g = (t.grad[i] / c) * max_norm;
+    const float mi = b1 * t.m[i] + d.omb1 * g;
+    const float vi = b2 * t.v[i] + d.omb2 * (g * g);
+    t.m[i] = mi;
+    t.v[i] = vi;
+    t.param[i] = t.param[i] - lr * ((mi / bc1) / (sqrtf(vi / bc2) + eps));
+  }
+}
+
 // ---- Philox normals (Box-Muller, noise.h) ----------------------------------------------------------
 __global__ __launch_bounds__(256) void normal_kernel(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t seed,
                                                      uint64_t stream_id) {
@@ -1038,6 +1100,28 @@ extern "C" int dgppo_adam(float* param, const float* grad, float* m, float* v, i
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, DG_STREAM(stream), param, grad, m, v, n, state, lr,
                      (float)b1, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, max_norm);
   hipLaunchKernelGGL(adam_count_kernel, dim3(1), dim3(64), 0, DG_STREAM(stream), state);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t dgppo_adam_multi_workspace_floats(void) {
+  return (int64_t)DGPPO_ADAM_MAX_NETS * kAdamParts * 8 + DGPPO_ADAM_MAX_NETS;
+}
+
+extern "C" int dgppo_adam_multi(const dgppo_adam_multi_args* a, void* stream) {
+  if (!a || a->n_nets < 1 || a->n_nets > DGPPO_ADAM_MAX_NETS || !a->workspace) return DGPPO_EINVAL;
+  int64_t nmax = 0;
+  for (int k = 0; k < a->n_nets; ++k) {
+    const dgppo_adam_net& t = a->net[k];
+    if (t.n < 0 || !t.param || !t.grad || !t.m || !t.v || !t.state) return DGPPO_EINVAL;
+    nmax = t.n > nmax ? t.n : nmax;
+  }
+  static_assert(kAdamParts == kLossBlocks, "the per-net partials are dgppo_grad_norm's");
+  AdamMultiDev d;
+  d.a = *a;
+  d.omb1 = (float)(1.0 - a->b1);  // (1 - b) formed in double and rounded once, as dgppo_adam
+  d.omb2 = (float)(1.0 - a->b2);
+  hipLaunchKernelGGL(sumsq_multi_kernel, dim3(kAdamParts, a->n_nets), dim3(256), 0, DG_STREAM(stream), d);
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(grid_for(nmax), a->n_nets), dim3(256), 0, DG_STREAM(stream), d);
   return (int)hipGetLastError();
 }
 

@@ -216,6 +216,23 @@ def adam(param, grad, m, v, state, lr, b1=0.9, b2=0.999, eps=1e-8, max_norm=2.0)
     torch.ops.dgppo.adam(param, grad, m, v, state, float(lr), float(b1), float(b2), float(eps), float(max_norm))
 
 
+def adam_multi(nets, b1=0.9, b2=0.999, eps=1e-8):
+    """grad_norm + adam (the pair above) for up to 4 nets in two launches, bit-identical to the per-net calls:
+    nets = [(param, grad, m, v, state, lr, max_norm), ...] (dgppo_adam_multi, ABI 12)."""
+    lib = _lib.load()
+    a = _lib.AdamMultiArgs()
+    a.n_nets, a.eps, a.b1, a.b2 = len(nets), float(eps), float(b1), float(b2)
+    if not 1 <= len(nets) <= _lib.ADAM_MAX_NETS:
+        raise ValueError(f"{len(nets)} nets (1..{_lib.ADAM_MAX_NETS})")
+    param0 = nets[0][0]
+    a.workspace = _p(workspace(lib.dgppo_adam_multi_workspace_floats(), param0.device, "adam_multi"))
+    for k, (param, grad, m, v, state, lr, max_norm) in enumerate(nets):
+        t = a.net[k]
+        t.param, t.grad, t.m, t.v, t.state = _p(param), _p(grad), _p(m), _p(v), _p(state)
+        t.n, t.lr, t.max_norm = int(param.numel()), float(lr), float(max_norm)
+    _chk(lib.dgppo_adam_multi(ctypes.byref(a), _stream(param0)), "dgppo_adam_multi")
+
+
 def normal_(out, seed=0, stream_id=0, seed_tensor=None):
     _chk(_lib.load().dgppo_normal(_p(out), int(out.numel()), _p(seed_tensor), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                   int(stream_id) & 0xFFFFFFFFFFFFFFFF, _stream(out)), "dgppo_normal")

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 11  /* 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 12  /* 12: dgppo_adam_multi (the clipped Adam steps of several nets in two launches); 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -586,6 +586,32 @@ int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace
  * `(1 - decay) * g` does (ABI 3) */
 int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, double b1,
                double b2, float eps, float max_norm, void* stream);
+
+/* The grad_norm + adam pair of up to DGPPO_ADAM_MAX_NETS nets (each its own parameters, state, lr and clip norm) in
+ * TWO launches instead of four per net (ABI 12): the sum-of-squares / non-finite partials of every net, then one
+ * kernel whose workgroups each finish their net's norm from the partials (the arithmetic of dgppo_grad_norm's
+ * second kernel) and apply the clipped Adam step; workgroup 0 of each net writes its state.  Every value is
+ * bit-identical to dgppo_grad_norm + dgppo_adam per net.  workspace: dgppo_adam_multi_workspace_floats() floats. */
+#define DGPPO_ADAM_MAX_NETS 4
+typedef struct dgppo_adam_net {
+  float* param;
+  const float* grad;
+  float* m;
+  float* v;
+  int64_t n;
+  float* state; /* [global norm, non-finite count, adam step] */
+  float lr;
+  float max_norm;
+} dgppo_adam_net;
+typedef struct dgppo_adam_multi_args {
+  int32_t n_nets;
+  float eps;
+  double b1, b2;
+  float* workspace;
+  dgppo_adam_net net[DGPPO_ADAM_MAX_NETS];
+} dgppo_adam_multi_args;
+int64_t dgppo_adam_multi_workspace_floats(void);
+int dgppo_adam_multi(const dgppo_adam_multi_args* a, void* stream);
 
 /* InforMARL-Lagr (dgppo/algo/informarl_lagr.py:125-309): y = max(x, 0) (the GAE's clipped costs, :196);
  * the merged advantage A = -norm_t(Ql - Vl) - mean_h(lagr norm_t(Qh - Vh)) with Ah = norm_t(Qh - Vh) out

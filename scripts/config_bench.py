@@ -29,7 +29,10 @@ CONFIGS = [
     # 2048 samples per rank (batch 2048 here gives the per-rank plan: 32 minibatches of 16 envs; no all-reduce)
     ("LidarBicycleTarget n8 o3 x512/GPU (config 4 strong share, 2048-sample rank minibatch)", "LidarBicycleTarget", 8,
      3, 512, 2048),
-    ("LidarSpread n32 o8 x1024/GPU (8192 envs over 8 GPUs)", "LidarSpread", 32, 8, 1024),
+    # config 5's share: 8192 envs over 8 GPUs = 1024 per GPU; minibatch_plan at world 8 gives each rank 64 minibatches
+    # of 2048 samples (batch 2048 here reproduces that per-rank plan on one GPU; no all-reduce)
+    ("LidarSpread n32 o8 x1024/GPU (config 5 share, 64 x 2048-sample rank minibatches)", "LidarSpread", 32, 8, 1024,
+     2048),
     ("LidarOmniTarget n8 o3 x4096", "LidarOmniTarget", 8, 3, 4096),
     # env variants (no BASELINE config names them): same per-GPU shapes as their base envs
     ("LidarLine n6 o3 x4096 (variant; n = 8 does not fit the landmarks in the default area)", "LidarLine", 6, 3, 4096),

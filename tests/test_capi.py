@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.dgppo_abi_version() == 11
+    assert lib.dgppo_abi_version() == 12
     assert b"gfx950" in lib.dgppo_build_info()
 
 
@@ -62,6 +62,8 @@ def _c_layout(struct, fields):
                                             (_lib.AdvArgs, "dgppo_adv_args"),
                                             (_lib.GruSeqArgs, "dgppo_gru_seq_args"),
                                             (_lib.GtLayer, "dgppo_gt_layer"),
+                                            (_lib.AdamNet, "dgppo_adam_net"),
+                                            (_lib.AdamMultiArgs, "dgppo_adam_multi_args"),
                                             (_lib.PolicyStepArgs, "dgppo_policy_step_args")])
 def test_ctypes_mirror_matches_c_layout(pystruct, cname):
     names = [f[0] for f in pystruct._fields_]

@@ -72,8 +72,7 @@ def _trajectory(cuda, eid, n, obs, K_UPD=5, perturb=None):
     algo, env = _algo(cuda, eid, n, obs, T, batch=2 * T, L=L)  # 2 envs per minibatch -> 4 minibatches
     nets = (("Vl", algo.Vl), ("Vh", algo.Vh), ("policy", algo.actor))
     if perturb is not None:
-        for name, opt in algo.opt.items():
-            opt.step = _counting_step(opt, name, algo, perturb)
+        algo._mb_apply = _counting_apply(algo, perturb)
     fallbacks = []
     for it in range(K_UPD):
         algo._traj_it = it
@@ -207,16 +206,18 @@ def _trajectory(cuda, eid, n, obs, K_UPD=5, perturb=None):
     return fallbacks
 
 
-def _counting_step(opt, name, algo, perturb):
-    """opt.step wrapped so perturb(algo, name, update, minibatch) runs before each minibatch's Adam step."""
-    orig = opt.step
-    opt._mb = -1
+def _counting_apply(algo, perturb):
+    """algo._mb_apply wrapped so perturb(algo, opt, name, update, minibatch) runs for every net before each minibatch's
+    clip + Adam launch (the per-net pairs or the multi-net kernel read each optimiser's lr at that point)."""
+    orig = algo._mb_apply
+    algo._mb_count = -1
 
-    def step():
-        opt._mb += 1
-        perturb(algo, opt, name, getattr(algo, "_traj_it", 0), opt._mb % 4)
+    def apply():
+        algo._mb_count += 1
+        for name, opt in algo.opt.items():
+            perturb(algo, opt, name, getattr(algo, "_traj_it", 0), algo._mb_count % 4)
         orig()
-    return step
+    return apply
 
 
 @pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 3, 2), ("MPETarget", 2, 0)])
