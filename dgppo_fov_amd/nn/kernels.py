@@ -13,6 +13,7 @@ import torch
 from .. import _lib, ops  # noqa: F401  (ops registers torch.ops.dgppo.*)
 
 _WS = {}
+_WS_KEPT = []  # replaced workspace buffers (see workspace)
 
 
 def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
@@ -21,7 +22,13 @@ def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
     key = (str(device), slot, _lib.stream_handle(device))
     t = _WS.get(key)
     if t is None or t.numel() < nfloats:
-        t = torch.empty(max(int(nfloats), 1024), dtype=torch.float32, device=device)
+        # a replaced buffer is never freed: a captured hipGraph (minibatch replay, rollout engines) may still hold
+        # its address, and once its memory went back to the allocator a replay would write into whatever reuses it
+        # (or fault, if the pool was released); growth at least doubles, so the kept buffers stay below the final size
+        old = t.numel() if t is not None else 0
+        if t is not None:
+            _WS_KEPT.append(t)
+        t = torch.empty(max(int(nfloats), 2 * old, 1024), dtype=torch.float32, device=device)
         _WS[key] = t
     return t
 
