@@ -587,7 +587,9 @@ int dgppo_grad_norm(const float* grad, int64_t n, float* state, float* workspace
 int dgppo_adam(float* param, const float* grad, float* m, float* v, int64_t n, float* state, float lr, double b1,
                double b2, float eps, float max_norm, void* stream);
 
-/* The grad_norm + adam pair of up to DGPPO_ADAM_MAX_NETS nets (each its own parameters, state, lr and clip norm) in
+/* Replaces the per-train-state compute_norm_and_clip + apply_if_finite(adam) of DGPPO.update_inner's three updates
+ * (trainer/utils.py:105-118, dgppo.py:275-289) in one call.
+ * The grad_norm + adam pair of up to DGPPO_ADAM_MAX_NETS nets (each its own parameters, state, lr and clip norm) in
  * TWO launches instead of four per net (ABI 12): the sum-of-squares / non-finite partials of every net, then one
  * kernel whose workgroups each finish their net's norm from the partials (the arithmetic of dgppo_grad_norm's
  * second kernel) and apply the clipped Adam step; workgroup 0 of each net writes its state.  Every value is
