@@ -41,6 +41,11 @@ __device__ __forceinline__ float clampf_nan(float x, float lo, float hi) {
   x = x < lo ? lo : x;
   return x > hi ? hi : x;
 }
+// clampf_nan for a NONZERO constant bound pair: IEEE maximum / minimum (v_maximum3 / v_minimum3, NaN-propagating)
+// give the same value for every x (no signed-zero tie with a nonzero bound), NaN payload aside
+__device__ __forceinline__ float clampk(float x, float lo, float hi) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, lo), hi);
+}
 __device__ __forceinline__ float min_nan(float a, float b) {
   // jnp.min / jnp.minimum semantics: NaN wins
   return (a != a || a < b) ? a : b;
@@ -920,6 +925,25 @@ __device__ __forceinline__ bool rect_inside0(const float* rec, float px, float p
 // per ray with an LDS atomic min on an order-preserving encoding (NaN wins, as jnp.min).
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"  // branch-free predicates on purpose
 constexpr int kOmniSD = 7, kOmniED = 10, kOmniNC = 5;  // LidarOmniTarget state / edge width, costs
+// 16-byte state rows (SD = 4) stored one float4 per lane instead of one dword per lane and column (A/B builds:
+// -DDGPPO_ENV_ST4=0 restores the dword stores)
+#ifndef DGPPO_ENV_ST4
+#define DGPPO_ENV_ST4 1
+#endif
+// hit ranks of the non-miss rays against their row's compacted non-miss keys (-DDGPPO_ENV_CRANK=1) instead of all
+// 32 keys: 100 fewer instructions per step, but the runtime-bounded loop waits for each key load (the unrolled
+// 32-key loop has all 16 in flight) -- LidarSpread episode 1.34 vs 1.25-1.27 ms, so off by default
+#ifndef DGPPO_ENV_CRANK
+#define DGPPO_ENV_CRANK 0
+#endif
+// the persistent rollout's env index wave-uniform for the bicycle engine (-DDGPPO_ENV_UNI=0: per-lane everywhere, the
+// round-5 form; =2: uniform for every engine).  Episode A/B (4096 envs, same box, 3 runs each): bicycle 1.306-1.316
+// vs 1.341-1.352 ms uniform vs per-lane; LidarSpread 1.249-1.269 vs 1.240-1.255 and Omni 1.926-1.945 vs
+// 1.889-1.894, so only the bicycle engine takes it
+#ifndef DGPPO_ENV_UNI
+#define DGPPO_ENV_UNI 1
+#endif
+
 namespace wv {
 constexpr int NA = 8, NR = 32, NK = 8;
 constexpr float kCullMargin = 0.01f;
@@ -938,11 +962,17 @@ __device__ __forceinline__ float dpp(float v) {
 __device__ __forceinline__ float rlf(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
-// min_nan over each 8-lane group: quad xor 1, xor 2, row_half_mirror
+// minimum over each 8-lane group of values that are >= +0 or NaN (norms and squared norms): quad xor 1, xor 2,
+// row_half_mirror.  v_minimum3_f32 (IEEE minimum: NaN-propagating) equals min_nan on such values but for the NaN
+// payload; every lane of the three patterns reads a valid lane, so the moves need no old-value initialisation
+template <int CTRL>
+__device__ __forceinline__ float dppb(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
 __device__ __forceinline__ float min8(float v) {
-  v = min_nan(v, dpp<0xB1>(v));
-  v = min_nan(v, dpp<0x4E>(v));
-  return min_nan(v, dpp<0x141>(v));
+  v = __builtin_elementwise_minimum(v, dppb<0xB1>(v));
+  v = __builtin_elementwise_minimum(v, dppb<0x4E>(v));
+  return __builtin_elementwise_minimum(v, dppb<0x141>(v));
 }
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1114,6 +1144,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   constexpr int AD = OMNI ? 3 : 2;   // action width
   constexpr int ED = OMNI ? 10 : 4;  // edge width
   constexpr int XS = 16 * SD - 64;   // agent + goal state floats past the first 64
+  constexpr bool ST4 = SD == 4 && DGPPO_ENV_ST4;  // state rows stored as one float4 per lane
   using C = Carve<SD, O>;
   constexpr int N = C::N, ND = C::ND, pad = N - 1;
   constexpr int n_ag = GOAL == DGPPO_GOAL_SPREAD ? NA * NA : NA;
@@ -1138,8 +1169,8 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
 
   // ---- A: every global load first (unconditional, clamped addresses), then stage in LDS -------
   const float3 araw = LOAD ? wave_action<AD>(io, env, gj) : pre;
-  const float a0 = clampf_nan(araw.x, -1.0f, 1.0f), a1 = clampf_nan(araw.y, -1.0f, 1.0f);
-  const float aw = OMNI ? clampf_nan(araw.z, -1000.0f, 1000.0f) : 0.0f;  // omni alpha
+  const float a0 = clampk(araw.x, -1.0f, 1.0f), a1 = clampk(araw.y, -1.0f, 1.0f);
+  const float aw = OMNI ? clampk(araw.z, -1000.0f, 1000.0f) : 0.0f;  // omni alpha
   float hcx, hcy;
   if constexpr (LOAD) {
     const float* st = io.states + env * io.states_stride;
@@ -1232,11 +1263,24 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   if (!pc && lane < O * 8) lds[C::evec + lane] = ev;  // (persistent: staged once with the constants)
   const float an = norm2(a0, a1);
   const float a2 = an * an;
-  float daa = norm2(cix - x[0], ciy - x[1]);
-  if (gi == gj) daa = daa + 1e6f;
-  const float dga = GOAL == DGPPO_GOAL_SPREAD ? norm2(gix - x[0], giy - x[1]) : norm2(gix - cix, giy - ciy);
-  float dh;
+  // Lidar / bicycle: the agent, hit and goal distance minima of agent gi over squared norms, then ONE sqrtf for all
+  // three (lane (gi, 0): agents, (gi, 1): hits, (gi, >= 2): goals).  sqrtf is correctly rounded and monotone, so
+  // sqrtf(min x) == min sqrtf(x) (NaN either way).  The agent-agent diagonal is sqrtf(0) + 1e6 = 1e6 or NaN (the
+  // row minus itself): it enters the squared minimum as +inf / NaN and the 1e6 after the sqrtf
+  float dmin = 0.0f;
+  if constexpr (!OMNI) {
+    float saa = sq2(cix - x[0], ciy - x[1]);
+    if (gi == gj) saa = saa == 0.0f ? __builtin_inff() : __builtin_nanf("");
+    const float sga = GOAL == DGPPO_GOAL_SPREAD ? sq2(gix - x[0], giy - x[1]) : sq2(gix - cix, giy - ciy);
+    const float sh = sq2(hcx - cix, hcy - ciy);
+    const float maa = min8(saa), mh = min8(sh), mg = min8(sga);
+    dmin = sqrtf(gj == 0 ? maa : (gj == 1 ? mh : mg));
+  }
+  float daa = 0.0f, dga = 0.0f, dh = 0.0f;
   if constexpr (OMNI) {
+    daa = norm2(cix - x[0], ciy - x[1]);
+    if (gi == gj) daa = daa + 1e6f;
+    dga = norm2(gix - cix, giy - ciy);
     // every agent's current hits and the origin row (see oracle get_cost_omni): minimum of the squared
     // norms, one sqrtf after it (sqrtf is correctly rounded and monotone, so sqrtf(min x) == min sqrtf(x);
     // NaN propagates through min_nan either way)
@@ -1248,10 +1292,8 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       d2 = min_nan(d2, sq2(hv.x - cix, hv.y - ciy));
     }
     dh = sqrtf(d2);
-  } else {
-    dh = norm2(hcx - cix, hcy - ciy);
   }
-  const float md = min8(daa), dg = min8(dga), mo = min8(dh);
+  const float md = OMNI ? min8(daa) : 0.0f, dg = OMNI ? min8(dga) : 0.0f, mo = OMNI ? min8(dh) : 0.0f;
 
   ENV_STAMP(1);
   // ---- C: cost (lanes j < 2 of group i, 5 for omni), reward (lane 0) -------------------------
@@ -1273,7 +1315,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     const int q = gj < kOmniNC ? gj : 0;
     float v = q == 0 ? cq[0] : (q == 1 ? cq[1] : (q == 2 ? cq[2] : (q == 3 ? cq[3] : cq[4])));
     v = v <= 0.0f ? v - 0.1f : v + 0.1f;
-    v = clampf_nan(v, -1.0f, 1.0f);
+    v = clampk(v, -1.0f, 1.0f);
     if (!REBUILD && st_live & (gj < kOmniNC)) io.cost[env * io.cost_stride + kOmniNC * gi + gj] = v;
     const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
     const float w2 = aw * aw, o2 = x[6] * x[6];
@@ -1296,19 +1338,17 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       io.reward[env * io.reward_stride] = r;
     }
   } else {
-    float c0 = cfg.c_agent_cost - md;
-    float c1 = cfg.c_obs_cost - mo;
-    c0 = c0 <= 0.0f ? c0 - 0.5f : c0 + 0.5f;
-    c1 = c1 <= 0.0f ? c1 - 0.5f : c1 + 0.5f;
-    c0 = clampf_nan(c0, -1.0f, 1.0f);
-    c1 = clampf_nan(c1, -1.0f, 1.0f);
-    if (!REBUILD && st_live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = gj == 0 ? c0 : c1;
-    const float far = dg > cfg.dist2goal ? 1.0f : 0.0f;
+    // lane (gi, 0): the agent cost c_agent - min(d_aa), lane (gi, 1): the obstacle cost c_obs - min(d_hit)
+    float c = gj == 0 ? cfg.c_agent_cost - min_nan(dmin, 1e6f) : cfg.c_obs_cost - dmin;
+    c = c <= 0.0f ? c - 0.5f : c + 0.5f;
+    c = clampk(c, -1.0f, 1.0f);
+    if (!REBUILD && st_live & (gj < 2)) io.cost[env * io.cost_stride + 2 * gi + gj] = c;
+    const float far = dmin > cfg.dist2goal ? 1.0f : 0.0f;  // (read at lanes (i, 2): the goal distance)
     float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      sd_ = sd_ + rlf(dg, 8 * i);
-      sf = sf + rlf(far, 8 * i);
+      sd_ = sd_ + rlf(dmin, 8 * i + 2);
+      sf = sf + rlf(far, 8 * i + 2);
       sa = sa + rlf(a2, i);  // lane i holds agent j = i
     }
     if (!REBUILD && st_live & (lane == 0)) {
@@ -1331,7 +1371,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   int32_t* ro = io.receivers + env * io.edge_index_stride;
   int32_t* sno = io.senders + env * io.edge_index_stride;
   // edge rows as vector stores: the launchers send only 16-byte (4-wide) / 8-byte (10-wide) aligned edge
-  // buffers here (wave_edges_aligned); a runtime fallback branch would let the compiler merge both
+  // buffers here (wave_bufs_aligned); a runtime fallback branch would let the compiler merge both
   // paths into 4-byte stores
   auto put = [&](int e, float f0, float f1, float f2, float f3, int rv, int sv) {
     reinterpret_cast<float4*>(eo)[e] = make_float4(f0, f1, f2, f3);
@@ -1502,16 +1542,25 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       const float v = c < SD ? sv : (c == SD + 2 ? (r < NA ? 1.0f : 0.0f) : (c == SD + 1 ? (r < NA ? 0.0f : 1.0f) : 0.0f));
       if (idx < 16 * ND) no[idx] = v;
     }
+    if constexpr (ST4) {
+      // 16-byte state rows (SD = 4): lane r < 16 stores row r, lane 16 the pad row, one float4 each (the launchers
+      // send only 16-byte aligned state buffers here: wave_bufs_aligned)
+      const int rs = lane < 16 ? lane : 0;
+      const float4 v = *reinterpret_cast<const float4*>(rs < NA ? nxt + rs * SD : goal + (rs - NA) * SD);
+      if (lane <= 16)
+        reinterpret_cast<float4*>(so)[lane < 16 ? lane : pad] = lane < 16 ? v : make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
+    } else {
 #pragma unroll
-    for (int k = 0; k < (16 * SD + 63) / 64; ++k) {
-      const int idx = lane + 64 * k;
-      const int r = idx / SD, c = idx - (idx / SD) * SD;
-      const int rs = r < 16 ? r : 15;
-      const float v = (rs < NA ? nxt + rs * SD : goal + (rs - NA) * SD)[c];
-      if (idx < 16 * SD) so[idx] = v;
+      for (int k = 0; k < (16 * SD + 63) / 64; ++k) {
+        const int idx = lane + 64 * k;
+        const int r = idx / SD, c = idx - (idx / SD) * SD;
+        const int rs = r < 16 ? r : 15;
+        const float v = (rs < NA ? nxt + rs * SD : goal + (rs - NA) * SD)[c];
+        if (idx < 16 * SD) so[idx] = v;
+      }
+      if (lane < SD) so[pad * SD + lane] = -1.0f;
     }
     if (lane < ND) no[pad * ND + lane] = 0.0f;
-    if (lane < SD) so[pad * SD + lane] = -1.0f;
   }
   uint32_t* alpha = reinterpret_cast<uint32_t*>(lds + C::alpha);
   reinterpret_cast<uint4*>(alpha)[lane] = make_uint4(kEncMiss, kEncMiss, kEncMiss, kEncMiss);
@@ -1591,6 +1640,16 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
   int* olist = reinterpret_cast<int*>(lds + C::olist);
   const float isin = ((in_mask >> (8 * gi)) & 0xFFull) ? 1.0f : 0.0f;
   int n_other = 0;
+  // CRANK: each agent row keeps only its non-miss keys, compacted and padded with all-ones keys, and a non-miss ray
+  // is ranked against that list (mrow = the longest row, wave-uniform) plus, for a NaN alpha, every miss of its row
+  // (misses sort after every number and before NaN); a miss never ranks before a number, so the ranks are the
+  // full row's.  Alphas here are >= +0, 1e6 or NaN, so the key's high word is the alpha bits (NaN -> all ones).
+  static_assert(NA * C::key_stride + NA <= C::uni_size, "row counts fit behind the keys");
+  int* rowcnt = reinterpret_cast<int*>(lds + C::uni + NA * C::key_stride);
+  int mrow = 0;
+  auto key_pos = [](float a, int r) {
+    return ((uint64_t)(a != a ? 0xFFFFFFFFu : __float_as_uint(a)) << 32) | (uint32_t)r;
+  };
   {
     const uint4 e4 = reinterpret_cast<const uint4*>(alpha + gi * NR)[gj];
     const float4 rA = reinterpret_cast<const float4*>(rays)[2 * gj], rB = reinterpret_cast<const float4*>(rays)[2 * gj + 1];
@@ -1599,6 +1658,7 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     float av[4], hx[4], hy[4];
     bool miss[4];
     uint32_t sm[4];
+    uint64_t obq[4];
     int hf = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1608,12 +1668,37 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       hx[q] = sxi + (ex - sxi) * av[q];
       hy[q] = syi + (ey - syi) * av[q];
       sm[q] = (uint32_t)(__ballot(miss[q]) >> (8 * gi)) & 0xFFu;
+      obq[q] = __ballot(!miss[q]);
       hf += __builtin_popcount((uint32_t)(__ballot(!miss[q] & (av[q] == av[q])) >> (8 * gi)) & 0xFFu);
     }
     uint64_t* krow = keys + gi * (C::key_stride / 2);
-    reinterpret_cast<ulonglong2*>(krow)[2 * gj] = make_ulonglong2(sort_key(av[0], 4 * gj), sort_key(av[1], 4 * gj + 1));
-    reinterpret_cast<ulonglong2*>(krow)[2 * gj + 1] = make_ulonglong2(sort_key(av[2], 4 * gj + 2), sort_key(av[3], 4 * gj + 3));
     const uint32_t below = (1u << gj) - 1u;
+    if constexpr (DGPPO_ENV_CRANK) {
+      const ulonglong2 ones = make_ulonglong2(~0ull, ~0ull);
+      reinterpret_cast<ulonglong2*>(krow)[2 * gj] = ones;
+      reinterpret_cast<ulonglong2*>(krow)[2 * gj + 1] = ones;
+      int pos = 0, rc = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t nm = (uint32_t)(obq[q] >> (8 * gi)) & 0xFFu;
+        pos += __builtin_popcount(nm & below);
+        rc += __builtin_popcount(nm);
+      }
+      wave_sync();  // every lane's padding before any compacted key
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!miss[q]) krow[pos] = key_pos(av[q], 4 * gj + q);
+        pos += miss[q] ? 0 : 1;
+      }
+      if (gj == 0) rowcnt[gi] = rc;
+      // the longest row: max of the two groups of each 16-lane row, then of the four rows
+      const int m2 = max(rc, __builtin_amdgcn_mov_dpp(rc, 0x128, 0xf, 0xf, true));  // row_ror:8
+      mrow = max(max(__builtin_amdgcn_readlane(m2, 0), __builtin_amdgcn_readlane(m2, 16)),
+                 max(__builtin_amdgcn_readlane(m2, 32), __builtin_amdgcn_readlane(m2, 48)));
+    } else {
+      reinterpret_cast<ulonglong2*>(krow)[2 * gj] = make_ulonglong2(sort_key(av[0], 4 * gj), sort_key(av[1], 4 * gj + 1));
+      reinterpret_cast<ulonglong2*>(krow)[2 * gj + 1] = make_ulonglong2(sort_key(av[2], 4 * gj + 2), sort_key(av[3], 4 * gj + 3));
+    }
     int cnt = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) cnt += __builtin_popcount(sm[q] & below);
@@ -1625,9 +1710,8 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
         hits[(gi * NK + rank) * 2 + 1] = hy[q];
       }
       cnt += (sm[q] >> gj) & 1u;
-      const uint64_t obq = __ballot(!miss[q]);
-      if (!miss[q]) olist[n_other + mbcnt(obq)] = gi * NR + 4 * gj + q;
-      n_other += __popcll(obq);
+      if (!miss[q]) olist[n_other + mbcnt(obq[q])] = gi * NR + 4 * gj + q;
+      n_other += __popcll(obq[q]);
     }
   }
   wave_sync();
@@ -1637,16 +1721,26 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     const int v = olist[t];  // past n_other: stale words (olist is followed by the key region)
     const int i = (v >> 5) & 7, r = v & 31;
     const uint64_t* krow = keys + i * (C::key_stride / 2);
-    const uint64_t key = krow[r];
     const float a = dec_alpha(alpha[i * NR + r]) * (((in_mask >> (8 * i)) & 0xFFull) ? 0.0f : 1.0f);
     const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
     const float2 rd = reinterpret_cast<const float2*>(rays)[r];
     int rank = 0;
+    if constexpr (DGPPO_ENV_CRANK) {
+      const uint64_t key = key_pos(a, r);
+      for (int j = 0; j < mrow; j += 2) {
+        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(krow + j);
+        rank += kk.x < key ? 1 : 0;
+        rank += kk.y < key ? 1 : 0;
+      }
+      if (a != a) rank += NR - rowcnt[i];
+    } else {
+      const uint64_t key = krow[r];
 #pragma unroll
-    for (int j = 0; j < NR; j += 2) {
-      const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(krow + j);
-      rank += kk.x < key ? 1 : 0;
-      rank += kk.y < key ? 1 : 0;
+      for (int j = 0; j < NR; j += 2) {
+        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(krow + j);
+        rank += kk.x < key ? 1 : 0;
+        rank += kk.y < key ? 1 : 0;
+      }
     }
     if ((t < n_other) & (rank < NK)) {
       const float ex = sx + rd.x, ey = sy + rd.y;
@@ -1672,8 +1766,10 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
     float* ss = sn + 64 * ND;    // (64, SD) hit state rows [x, y, 0..]
 #pragma unroll
     for (int c = 0; c < ND; ++c) sn[lane * ND + c] = c == 0 ? hl.x : (c == 1 ? hl.y : (c == SD ? 1.0f : 0.0f));
+    if constexpr (!ST4) {
 #pragma unroll
-    for (int c = 0; c < SD; ++c) ss[lane * SD + c] = c == 0 ? hl.x : (c == 1 ? hl.y : 0.0f);
+      for (int c = 0; c < SD; ++c) ss[lane * SD + c] = c == 0 ? hl.x : (c == 1 ? hl.y : 0.0f);
+    }
     wave_sync();
     if (st_live) {
       if constexpr (ED == 4) reinterpret_cast<float4*>(eo)[e] = make_float4(f0, f1, 0.0f, 0.0f);
@@ -1683,8 +1779,12 @@ __device__ __forceinline__ void wave_body(const dgppo_env_cfg& cfg, const dgppo_
       float* sdst = so + 16 * SD;
 #pragma unroll
       for (int k = 0; k < ND; ++k) nd[64 * k + lane] = sn[64 * k + lane];
+      if constexpr (ST4) {
+        reinterpret_cast<float4*>(sdst)[lane] = make_float4(hl.x, hl.y, 0.0f, 0.0f);
+      } else {
 #pragma unroll
-      for (int k = 0; k < SD; ++k) sdst[64 * k + lane] = ss[64 * k + lane];
+        for (int k = 0; k < SD; ++k) sdst[64 * k + lane] = ss[64 * k + lane];
+      }
     }
     if constexpr (ED != 4) {
       wave_sync();  // (in-order LDS: the reads above are done before these writes)
@@ -1762,7 +1862,11 @@ __global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(4))) v
   constexpr int AD = ENGINE == DGPPO_ENGINE_OMNI ? 3 : 2;
   constexpr int APS = NA * AD, KC = 16, PER = KC * APS / 64;  // action floats per step / per lane and chunk
   static_assert(PER * 64 == KC * APS, "chunk = whole lanes");
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, gj = lane & 7;
+  // the wave index as a wave-uniform (SGPR) value: the env's output base pointers then live in SGPRs and every store
+  // takes the SGPR-base + 32-bit lane offset form (one address VGPR per lane, no 64-bit address arithmetic per store)
+  const int lane = threadIdx.x & 63, gj = lane & 7;
+  constexpr bool UNI = DGPPO_ENV_UNI == 2 || (DGPPO_ENV_UNI == 1 && ENGINE == DGPPO_ENGINE_BICYCLE);
+  const int wid = UNI ? (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) : (int)(threadIdx.x >> 6);
   const int64_t env_raw = (int64_t)blockIdx.x * WPG + wid;
   const int64_t env = env_raw < g0.n_env ? env_raw : g0.n_env - 1;
   float* acts = smem + WPG * wv::Carve<SD, O>::total + wid * (KC * APS);
@@ -3070,7 +3174,8 @@ extern "C" int dgppo_env_set_step_kernel(int mode) {
   return prev;
 }
 
-static bool wave_edges_aligned(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges);
+static bool wave_bufs_aligned(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges,
+                              const float* states, int64_t states_stride, int64_t t_states);
 
 extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
@@ -3094,7 +3199,7 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
   }
   const bool wave_shape = lidar && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR && cfg->top_k == wv::NK &&
                           cfg->n_obs == 3 && wave_step_enabled() &&
-                          wave_edges_aligned(cfg, io->edges, io->edges_stride, 0);
+                          wave_bufs_aligned(cfg, io->edges, io->edges_stride, 0, io->out_states, io->out_states_stride, 0);
   if (cfg->engine == DGPPO_ENGINE_OMNI && wave_shape) {
     const size_t sh = 4 * sizeof(float) * wv::Carve<kOmniSD, 3>::total;
     hipLaunchKernelGGL((wv::lidar_step_wave_kernel<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD, 3>),
@@ -3130,18 +3235,24 @@ extern "C" int dgppo_env_step(const dgppo_env_cfg* cfg, const dgppo_env_step_io*
   return (int)hipGetLastError();
 }
 
-// the wave kernels store edge rows as float4 (4-wide) / float2 (LidarOmniTarget's 10-wide): the edge buffer,
-// its per-env stride and (rollouts) its per-step stride must keep that alignment, else the generic kernels run
-static bool wave_edges_aligned(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges) {
+// the wave kernels store edge rows as float4 (4-wide) / float2 (LidarOmniTarget's 10-wide) and 4-wide state rows
+// as float4: those buffers, their per-env strides and (rollouts) their per-step strides must keep that alignment,
+// else the generic kernels run
+static bool wave_bufs_aligned(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges,
+                              const float* states, int64_t states_stride, int64_t t_states) {
   const int64_t q = cfg->engine == DGPPO_ENGINE_OMNI ? 2 : 4;
-  return (reinterpret_cast<uintptr_t>(edges) % (uintptr_t)(4 * q)) == 0 && edges_stride % q == 0 && t_edges % q == 0;
+  const bool e = (reinterpret_cast<uintptr_t>(edges) % (uintptr_t)(4 * q)) == 0 && edges_stride % q == 0 && t_edges % q == 0;
+  const bool st4 = DGPPO_ENV_ST4 && cfg->state_dim == 4;
+  const bool s = !st4 || ((reinterpret_cast<uintptr_t>(states) % 16u) == 0 && states_stride % 4 == 0 && t_states % 4 == 0);
+  return e && s;
 }
 
-static bool wave_config(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges) {
+static bool wave_config(const dgppo_env_cfg* cfg, const float* edges, int64_t edges_stride, int64_t t_edges,
+                        const float* states, int64_t states_stride, int64_t t_states) {
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   return lidar && cfg->variant == DGPPO_VARIANT_NONE && cfg->n_agents == wv::NA && cfg->n_rays == wv::NR &&
          cfg->top_k == wv::NK && cfg->n_obs == 3 && wave_step_enabled() &&
-         wave_edges_aligned(cfg, edges, edges_stride, t_edges);
+         wave_bufs_aligned(cfg, edges, edges_stride, t_edges, states, states_stride, t_states);
 }
 
 // the initial graph of sampled agent / goal rows and obstacles: the wave step kernel in REBUILD mode, in place
@@ -3174,7 +3285,8 @@ static void launch_rebuild(const dgppo_env_cfg* cfg, const dgppo_env_step_io& st
 extern "C" int dgppo_env_reset_states(const dgppo_env_cfg* cfg, const dgppo_env_reset_io* io, void* stream) {
   if (validate(cfg) || !io || io->n_env < 0) return DGPPO_EINVAL;
   if (vmas::is_vmas(cfg)) return vmas::reset(cfg, io, stream);  // the full reset (graph 0 included)
-  if (!wave_config(cfg, io->edges, io->edges_stride, 0)) return dgppo_env_reset(cfg, io, stream);
+  if (!wave_config(cfg, io->edges, io->edges_stride, 0, io->out_states, io->out_states_stride, 0))
+    return dgppo_env_reset(cfg, io, stream);
   if (io->n_env == 0) return 0;
   if (!io->out_states || !io->obstacles) return DGPPO_EINVAL;
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k, true);
@@ -3245,7 +3357,7 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
   const bool lidar = cfg->engine != DGPPO_ENGINE_MPE && cfg->n_obs > 0;
   if (lidar && (!io.obstacles || !io.ray_dirs)) return DGPPO_EINVAL;
   const hipStream_t s = (hipStream_t)stream;
-  if (wave_config(cfg, io.edges, io.edges_stride, r->t_edges)) {
+  if (wave_config(cfg, io.edges, io.edges_stride, r->t_edges, io.out_states, io.out_states_stride, r->t_states)) {
     const bool spread = cfg->goal_mode == DGPPO_GOAL_SPREAD;
     if (cfg->engine == DGPPO_ENGINE_OMNI) launch_rollout<DGPPO_ENGINE_OMNI, DGPPO_GOAL_TARGET, kOmniSD>(*cfg, *r, s);
     else if (cfg->engine == DGPPO_ENGINE_BICYCLE && spread) launch_rollout<DGPPO_ENGINE_BICYCLE, DGPPO_GOAL_SPREAD, 5>(*cfg, *r, s);
@@ -3256,7 +3368,8 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
   }
   // other configs: rebuild_first: a states-only reset (dgppo_env_reset_states) left graph 0 unbuilt when the
   // wave kernels took it (a misaligned per-step stride sends the rollout here)
-  if (r->rebuild_first && wave_config(cfg, io.edges, io.edges_stride, 0)) launch_rebuild(cfg, io, s);
+  if (r->rebuild_first && wave_config(cfg, io.edges, io.edges_stride, 0, io.out_states, io.out_states_stride, 0))
+    launch_rebuild(cfg, io, s);
   // the workgroup-per-env shapes: one persistent launch for all T steps (DGPPO_ENV_BLOCK_ROLLOUT=0: T launches)
   static const bool block_rollout = [] {
     const char* e = getenv("DGPPO_ENV_BLOCK_ROLLOUT");
@@ -3314,7 +3427,7 @@ extern "C" int dgppo_env_reset(const dgppo_env_cfg* cfg, const dgppo_env_reset_i
   const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,
                  cfg->engine != DGPPO_ENGINE_MPE);
   const size_t shmem = ((size_t)cv.total + 2 * kSampTab) * sizeof(float);  // + the sampler's candidate table
-  const bool wave = wave_config(cfg, io->edges, io->edges_stride, 0);
+  const bool wave = wave_config(cfg, io->edges, io->edges_stride, 0, io->out_states, io->out_states_stride, 0);
   if (!wave) {
     dispatch_reset(*cfg, *io, shmem, s, 0);
     return (int)hipGetLastError();
