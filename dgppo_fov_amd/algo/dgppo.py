@@ -69,6 +69,14 @@ def ADAM_MULTI() -> bool:
     return os.environ.get("DGPPO_ADAM_MULTI", "1") == "1"
 
 
+def WGRAD_SIDE() -> bool:
+    """Each net's weight-gradient GEMMs on a side stream of its pass's stream (K.wgrad_side), off the dX chain.
+    Off by default: bit-identical (tests/test_update_gpu.py) but slower at the bench config, 172.5-173.6 vs
+    170.0 ms per update (six streams over GPU_MAX_HW_QUEUES = 4 hardware queues), config 4's share 43.9-44.0 vs
+    44.1-44.4 ms (its captured minibatches keep the inline order: side streams under capture crashed capture_end)."""
+    return os.environ.get("DGPPO_WGRAD_SIDE", "0") == "1"
+
+
 def FORCE_SAFE() -> bool:
     """Learning-dynamics ablation (scripts/learn_ablate.sh): treat every sample as inside the safe set."""
     return os.environ.get("DGPPO_DEBUG_FORCE_SAFE", "0") == "1"
@@ -466,6 +474,18 @@ class DGPPO:
             main.wait_stream(st)
         return out
 
+    def _wgrad_sides(self):
+        """Three side streams (one per concurrent pass) for the weight-gradient GEMMs, or Nones (serial streams,
+        phase profiling, or DGPPO_WGRAD_SIDE=0)."""
+        if not WGRAD_SIDE() or self._aux_streams(2) is None:
+            return [None, None, None]
+        if getattr(self, "_capturing", False) and os.environ.get("DGPPO_WGRAD_SIDE_GRAPH", "0") != "1":
+            return [None, None, None]  # captured minibatches keep the inline order (side streams crashed capture_end)
+        ws = getattr(self, "_wside", None)
+        if ws is None:
+            ws = self._wside = [torch.cuda.Stream(self.device) for _ in range(3)]
+        return ws
+
     def _buf(self, name: str, shape) -> torch.Tensor:
         """Update scratch that keeps its address from update to update (the captured minibatch graph reads it)."""
         bufs = self.__dict__.setdefault("_bufs", {})
@@ -563,6 +583,7 @@ class DGPPO:
         tgt = tgt.view(Bm * S_per_env, L)
         acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
         pending = []
+        side = self._wgrad_sides()  # (policy, Vl, Vh): weight gradients off each backward's dX chain
 
         def vl_job():  # update_Vl (informarl.py:357-385)
             v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
@@ -570,7 +591,8 @@ class DGPPO:
             loss = torch.empty(1, device=dev)
             K.l2_loss(v, tgt, dv, loss)
             ph.mark("Vl_fwd")
-            self.Vl.seq_bwd(cache, dv)
+            with K.wgrad_side(side[1]):
+                self.Vl.seq_bwd(cache, dv)
             self._start_reduce(self.Vl, pending)  # the bucket's all-reduce overlaps the other passes
             ph.mark("Vl_bwd")
             return loss
@@ -581,7 +603,8 @@ class DGPPO:
             loss = torch.empty(1, device=dev)
             K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)
             ph.mark("Vh_fwd")
-            self.Vh.bwd(cache, dvh)
+            with K.wgrad_side(side[2]):
+                self.Vh.bwd(cache, dvh)
             self._start_reduce(self.Vh, pending)
             ph.mark("Vh_bwd")
             return loss
@@ -593,7 +616,8 @@ class DGPPO:
             st = torch.empty(4, device=dev)
             K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, st)
             ph.mark("pi_fwd")
-            self.actor.eval_seq_bwd(cache, dlp, dent)
+            with K.wgrad_side(side[0]):
+                self.actor.eval_seq_bwd(cache, dlp, dent)
             self._start_reduce(self.actor, pending)
             ph.mark("pi_bwd")
             return st

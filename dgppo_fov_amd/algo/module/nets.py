@@ -395,10 +395,10 @@ class VhGlobalNet(_Net):
         dy0 = hd.d1.bwd(y0, dh1, rows)
         dh0 = hd.ln0.bwd(c0, dy0)  # d(head Dense_0 output) (rows, 64)
         W0, dW0 = hd.d0.W(), hd.d0.W(True)
-        K.gemm(z, dh0, dW0[:64], 64, 64, rows, ta=True, beta=1.0, bias_grad=hd.d0.b(True))
+        K.gemm(z, dh0, dW0[:64], 64, 64, rows, ta=True, beta=1.0, bias_grad=hd.d0.b(True), side=True)
         sm = torch.empty((G, 64), device=dev)  # per-graph mean of dh0; the agent SUM is n x it
         K.agent_mean_fwd(dh0, sm, G, n, 64, n * 64)
-        K.gemm(zm, sm, dW0[64:], 64, 64, G, ta=True, alpha=float(n), beta=1.0)
+        K.gemm(zm, sm, dW0[64:], 64, 64, G, ta=True, alpha=float(n), beta=1.0, side=True)
         # dz = dh0 W[:64]^T + (sum_agents dh0) W[64:]^T / n  (the mean's backward), one GEMM with a per-graph addend
         dzm = torch.empty((G, 64), device=dev)
         K.gemm(sm, W0[64:], dzm, G, 64, 64, tb=True, ldb=64)

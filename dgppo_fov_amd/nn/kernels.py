@@ -33,6 +33,23 @@ def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
     return t
 
 
+def on_side(fn, *hold):
+    """fn() on the current stream's wgrad_side stream when one is active (forked after everything enqueued so far;
+    `hold` stays referenced until the join), else inline.  For a group of parameter-gradient launches whose
+    temporaries are allocated inside fn (then on the side stream's own pool)."""
+    if _SIDE:
+        cur = torch.cuda.current_stream()
+        ent = _SIDE.get(cur.cuda_stream)
+        if ent is not None:
+            st, held = ent
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                r = fn()
+            held.append(hold)
+            return r
+    return fn()
+
+
 def _p(t, off=0):
     return 0 if t is None else int(t.data_ptr()) + 4 * int(off)
 
@@ -47,17 +64,65 @@ def _chk(rc, what):
 
 GEMM_LOG = None  # set to a list to record (M, N, K, batch, ta, tb, split_k, has_bias) per launch
 
+# weight-gradient GEMMs off the dX chain: current stream handle -> (side stream, inputs held until the join)
+_SIDE = {}
+
+
+class wgrad_side:
+    """Inside this context, gemm(..., side=True) weight-gradient calls issued on the current stream run on `side`
+    instead: the side stream first waits for everything enqueued so far on the current stream (the GEMM's inputs),
+    the inputs are held until the exit, where the current stream waits for the side stream (so their memory returns
+    to the allocator only once a later reuse on the current stream is ordered after the side work; record_stream is
+    not used: the allocator's deferred events crashed hipGraph capture_end).  The chain of dX GEMMs / attention backward no longer waits for each layer's dW GEMM and
+    its chunk reduction.  Only calls whose output is a parameter gradient that nothing on the current stream touches
+    before the exit take side=True; they stay in issue order on the one side stream.  side=None: a no-op."""
+
+    def __init__(self, side):
+        self.side = side
+
+    def __enter__(self):
+        if self.side is not None:
+            self.main = torch.cuda.current_stream(self.side.device)
+            self.key = self.main.cuda_stream
+            _SIDE[self.key] = (self.side, [])
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is not None:
+            _, held = _SIDE.pop(self.key, (None, []))
+            # join only a side stream that was forked here: under hipGraph capture an unforked side stream is not
+            # capturing, and waiting on an event recorded outside the capture broke capture_end
+            if held:
+                self.main.wait_stream(self.side)
+            held.clear()
+        return False
+
 
 def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
          a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
          bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
-         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None, mask=None, ld_mask=None, ln=None):
+         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None, mask=None, ld_mask=None, ln=None,
+         side=False):
     """C = alpha op(A) op(B) + beta C + bias + addend (see dgppo_gemm).  Element offsets/strides.
     bias_grad (ta only): bias_grad = alpha colsum(B) + beta bias_grad, fused into the dW GEMM.
     mask: C = mask > 0 ? result : 0 (the ReLU backward fused into the epilogue, ABI 9 epi 1).
     ln: LayerNorm(64) + ReLU epilogue (epi 2 / 3): dict(mode="fwd" | "bwd", scale, bias, h, mean, rstd,
     dscale, dbias) -- fwd writes h (pre-LN rows), mean, rstd and C = y; bwd reads h, mean, rstd, writes C = dx and
-    accumulates dscale / dbias (per-workgroup partials summed by dgppo_colsum)."""
+    accumulates dscale / dbias (per-workgroup partials summed by dgppo_colsum).
+    side (ta only): run on the wgrad_side stream of the current stream, if one is active."""
+    if side and _SIDE:
+        ent = _SIDE.get(torch.cuda.current_stream(C.device).cuda_stream)
+        if ent is not None:
+            st, held = ent
+            st.wait_stream(torch.cuda.current_stream(C.device))
+            with torch.cuda.stream(st):
+                gemm(A, B, C, M, N, K, ta=ta, tb=tb, lda=lda, ldb=ldb, ldc=ldc, batch=batch, sa=sa, sb=sb, sc=sc,
+                     a_off=a_off, b_off=b_off, c_off=c_off, a_grp=a_grp, a_gs=a_gs, b_grp=b_grp, b_gs=b_gs,
+                     c_grp=c_grp, c_gs=c_gs, bias=bias, addend=addend, add_off=add_off, ld_add=ld_add,
+                     add_grp=add_grp, add_gs=add_gs, alpha=alpha, beta=beta, relu=relu, split_k=split_k,
+                     bias_grad=bias_grad, mask=mask, ld_mask=ld_mask, ln=ln)
+            held.append((A, B))
+            return
     lib = _lib.load()
     _lib.require_gpu(C.device, "gemm")
     g = _lib.GemmArgs()

@@ -160,7 +160,7 @@ class Dense:
     def bwd(self, x, dy, rows, need_dx=True, dx_out=None, accumulate=False, mask=None, ln=None):
         """dW, db += ...; returns dx.  mask: dx = mask > 0 ? dx : 0 (the input's ReLU backward, fused into the dx
         GEMM); ln: the LayerNorm + ReLU backward of the layer that produced x (GEMM epilogue epi 3)."""
-        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0, bias_grad=self.b(True))
+        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0, bias_grad=self.b(True), side=True)
         if not need_dx:
             return None
         dx = dx_out if dx_out is not None else torch.empty((rows, self.d_in), device=dy.device)
@@ -336,14 +336,16 @@ class GRUCell:
         part = K.workspace(nb * H, dev, "gru_bhn")
         K.gru_seq(False, Q, L, n, gi, self.v("Wh"), self.v("bhn"), h0, hs, dhs=dhs, dgi=dgi, dgh=dgh, dh0=dh0,
                   dbhn_part=part)
-        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0, bias_grad=self.v("bi", True))
+        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0, bias_grad=self.v("bi", True),
+               side=True)
         S = Q // n
         if L > 1:  # h_{t-1} of step t >= 1 is hs of step t-1: row-grouped per sequence, B shifted by n rows
             K.gemm(hs, dgh, self.v("Wh", True), H, 3 * H, S * (L - 1) * n, ta=True, lda=H, a_grp=(L - 1) * n,
-                   a_gs=L * n * H, ldb=3 * H, b_off=n * 3 * H, b_grp=(L - 1) * n, b_gs=L * n * 3 * H, beta=1.0)
+                   a_gs=L * n * H, ldb=3 * H, b_off=n * 3 * H, b_grp=(L - 1) * n, b_gs=L * n * 3 * H, beta=1.0,
+                   side=True)
         if h0 is not None:  # step 0 uses the initial carries
             K.gemm(h0, dgh, self.v("Wh", True), H, 3 * H, Q, ta=True, lda=H, ldb=3 * H, b_grp=n,
-                   b_gs=L * n * 3 * H, beta=1.0)
+                   b_gs=L * n * 3 * H, beta=1.0, side=True)
         K.colsum(part, nb, H, self.v("bhn", True), beta=1.0)
         dx = None
         if need_dx:
@@ -453,8 +455,8 @@ class LSTMCell:
         dWh, db = self.v("Wh", True), self.v("b", True)
         for j in (0, 2 * H):  # two 2H-column halves: the weight-gradient kernel (fused bias colsum) takes N <= 192
             K.gemm(hprev, dGf, dWh, H, 2 * H, L * Q, ta=True, ldb=4 * H, b_off=j, ldc=4 * H, c_off=j, beta=1.0,
-                   bias_grad=db[j:j + 2 * H])
-        K.gemm(xt, dGf, self.v("Wi", True), self.d_in, 4 * H, L * Q, ta=True, beta=1.0)
+                   bias_grad=db[j:j + 2 * H], side=True)
+        K.gemm(xt, dGf, self.v("Wi", True), self.d_in, 4 * H, L * Q, ta=True, beta=1.0, side=True)
         dx = None
         if need_dx:
             dxt = torch.empty((L * Q, self.d_in), device=dev)
@@ -789,10 +791,11 @@ class GraphTransformer:
         torch.ops.dgppo.gnn_layer_bwd(*head, dQB, dXa, part)
         if part is not None:
             self._pre_grads(pre, g, part, nb, PK, D0)
-        K.gemm(xcat, dY, self.v("Wcat", True), H * (D + 5), F, R, ta=True, lda=H * (D + 5), alpha=1.0 / H, beta=1.0)
+        K.gemm(xcat, dY, self.v("Wcat", True), H * (D + 5), F, R, ta=True, lda=H * (D + 5), alpha=1.0 / H, beta=1.0,
+               side=True)
         A, akw = self._rows_in(g, xa, None)
-        self._qfree_grads(A, akw, dQB, R)
-        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
+        K.on_side(lambda: self._qfree_grads(A, akw, dQB, R), A, dQB)  # parameter gradients only
+        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), side=True, **akw)
         return True, dXa
 
     def _pre_grads(self, pre, g, part, nb, PK, D0):
@@ -828,9 +831,9 @@ class GraphTransformer:
         K.gemm(Gaug, self.v("bk"), dWaug, D + 1, F, 1, lda=WQ, a_off=HD, sa=1, ldb=F, sb=F, ldc=H * F, sc=F,
                batch=H, beta=1.0)
         K.gemm(Waug, Gaug, self.v("Wkt", True), F, D, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, sb=D, ldc=D,
-               sc=F * D, batch=H, beta=1.0)
+               sc=F * D, batch=H, beta=1.0, side=True)
         K.gemm(Waug, Gaug, self.v("bk", True), F, 1, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, b_off=HD, sb=1,
-               ldc=1, sc=F, batch=H, beta=1.0)
+               ldc=1, sc=F, batch=H, beta=1.0, side=True)
 
     def bwd(self, cache, dY, g: "GraphBatch", masked=False, mask_dxa=False):
         """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, d xfull (G, N, D)
@@ -854,13 +857,13 @@ class GraphTransformer:
             return dXa
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
-        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)
+        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0, side=True)
         da_add = None
         if self.EX:
             WX = H * self.EX
             dxx = torch.empty((R, WX), device=dev)
             K.gemm(dY, self.v("Wex"), dxx, R, WX, F, tb=True, ldb=F, alpha=1.0 / H)
-            K.gemm(xcx, dY, self.v("Wex", True), WX, F, R, ta=True, lda=WX, alpha=1.0 / H, beta=1.0)
+            K.gemm(xcx, dY, self.v("Wex", True), WX, F, R, ta=True, lda=WX, alpha=1.0 / H, beta=1.0, side=True)
             da_add = torch.empty((R, H, C), device=dev)
             K.edge_da(G, n, C, H, self.EX, g.E, dxx, g.cand, g.sidx, g.edges_x, da_add)
         dQB = torch.empty((R, WQ), device=dev)  # [dqt | dbeta]
@@ -877,8 +880,8 @@ class GraphTransformer:
                                      dbeta_ld=WQ, dx=dXf, dx_gstride=N * D)
         if part is not None:
             self._pre_grads(pre, g, part, nb, PK, args["dims"][8])
-        self._qfree_grads(A, akw, dQB, R)
-        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
+        K.on_side(lambda: self._qfree_grads(A, akw, dQB, R), A, dQB)  # parameter gradients only
+        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), side=True, **akw)
         if dXa is not None:
             K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
             K.gemm(dQB, QBW, dXa, R, D, WQ, tb=True, ldb=WQ, beta=1.0,  # d[qt | beta] / dx = QBW[:D]^T

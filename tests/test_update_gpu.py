@@ -323,3 +323,39 @@ def test_update_graph_replay_matches_eager(cuda, monkeypatch):
         assert d0.keys() == d1.keys()
         for k in d0:
             assert d0[k] == d1[k] or (np.isnan(d0[k]) and np.isnan(d1[k])), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("eid,n,obs,graph", [("LidarSpread", 3, 2, "0"), ("LidarSpread", 3, 2, "1"),
+                                             ("LidarBicycleTarget", 3, 2, "0")])
+def test_update_wgrad_side_streams_match_inline(cuda, monkeypatch, eid, n, obs, graph):
+    """Each net's weight-gradient GEMMs on a side stream of its pass's stream (DGPPO_WGRAD_SIDE=1, K.wgrad_side)
+    give bit-identical parameters, Adam state and info to the inline order (=0), eager and graph-replayed
+    minibatches, over two updates: the same kernels accumulate each gradient in the same order."""
+    B, T = 8, 32
+
+    def run(flag):
+        monkeypatch.setenv("DGPPO_WGRAD_SIDE", flag)
+        monkeypatch.setenv("DGPPO_UPDATE_GRAPH", graph)
+        env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
+        algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                         action_dim=env.action_dim, n_agents=n, batch_size=64, rnn_step=16, train_steps=100, seed=5,
+                         device=cuda)
+        infos = []
+        for it in range(2):
+            r = algo.collect(algo.params, 21 + it, n_env=B)
+            infos.append(algo.update(r, it))
+        torch.cuda.synchronize()
+        return algo, infos
+
+    a0, i0 = run("0")
+    a1, i1 = run("1")
+    assert getattr(a0, "_wside", None) is None and a1._wside is not None  # the side streams really ran
+    for name in ("Vl", "Vh", "policy"):
+        o0, o1 = a0.opt[name], a1.opt[name]
+        assert torch.equal(o0.ps.flat, o1.ps.flat), name
+        assert torch.equal(o0.m, o1.m) and torch.equal(o0.v, o1.v) and torch.equal(o0.state, o1.state), name
+    for d0, d1 in zip(i0, i1):
+        assert d0.keys() == d1.keys()
+        for k in d0:
+            assert d0[k] == d1[k] or (np.isnan(d0[k]) and np.isnan(d1[k])), k
