@@ -2252,6 +2252,23 @@ __device__ int sample_phase(const Rng& rng, uint32_t& count, uint32_t count0, co
   }
 }
 
+// max{x : sqrtf(x) <= r} (-1 when no x >= 0 qualifies): sqrtf is correctly rounded and monotone, so for a squared
+// norm x (>= +0, +inf or NaN) `sqrtf(x) <= r` is `x <= T` exactly (NaN compares false either way).  Found by ulp
+// steps from fl(r * r), within a few ulps of T.
+__device__ float sq_le_threshold(float r) {
+  if (!(r >= 0.0f)) return -1.0f;
+  if (r == __builtin_inff()) return __builtin_inff();
+  float T = r * r;
+  if (T == __builtin_inff()) T = 3.40282347e38f;
+  for (int i = 0; i < 16 && !(sqrtf(T) <= r); ++i) T = __uint_as_float(__float_as_uint(T) - 1u);
+  for (int i = 0; i < 16; ++i) {
+    const float U = __uint_as_float(__float_as_uint(T) + 1u);
+    if (!(sqrtf(U) <= r)) break;
+    T = U;
+  }
+  return T;
+}
+
 __device__ void node_goal_rng_wave(Rng& rng, const float* tab, float side, int n, float min_dist, float r_in,
                                    const float* obst, int O, float* pos, float* gl) {
   constexpr int kMaxIter = 1024;
@@ -2283,20 +2300,23 @@ __device__ void node_goal_rng_wave(Rng& rng, const float* tab, float side, int n
     inobs[q] = __ballot(inside_any(obst, O, tx[q], ty[q], r_in));
     oob[q] = __ballot(tx[q] < 0.0f || ty[q] < 0.0f || tx[q] > side || ty[q] > side);
   }
+  // `norm2(..) <= min_dist` on the squared norms (sq_le_threshold; NaN iff the squared norm is NaN): no root per
+  // candidate and placed point
+  const float t_le = sq_le_threshold(min_dist);
   auto origin_only = [&]() {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float d = norm2(0.0f - tx[q], 0.0f - ty[q]);
-      nearA[q] = nearG[q] = __ballot(d <= min_dist);
-      nanA[q] = nanG[q] = __ballot(d != d);
+      const float x = sq2(0.0f - tx[q], 0.0f - ty[q]);
+      nearA[q] = nearG[q] = __ballot(x <= t_le);
+      nanA[q] = nanG[q] = __ballot(x != x);
     }
   };
   auto add_point = [&](uint64_t (&near)[4], uint64_t (&nan)[4], float px, float py) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float d = norm2(px - tx[q], py - ty[q]);
-      near[q] |= __ballot(d <= min_dist);
-      nan[q] |= __ballot(d != d);
+      const float x = sq2(px - tx[q], py - ty[q]);
+      near[q] |= __ballot(x <= t_le);
+      nan[q] |= __ballot(x != x);
     }
   };
   auto phase = [&](bool goals, const float* pts, const uint64_t (&near)[4], const uint64_t (&nan)[4], float& ox,
