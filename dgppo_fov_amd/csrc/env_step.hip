@@ -1945,6 +1945,210 @@ __global__ __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu(4))) v
 #endif
 }
 
+
+// ---- MPE, n = 3 agents, 3 obstacles (BASELINE config 2): persistent rollout, a wave per env ------------------
+// The workgroup-per-env block kernel spends each step on generic task loops between five barrier phases; at 1024
+// envs one wave sits on each SIMD, so every phase's latency is exposed.  Here one 64-lane wave owns one env for the
+// whole episode with fixed lane roles, the same fp32 arithmetic as block_step / write_graph_mpe (bit-identical,
+// tests/test_rollout_gpu.py):
+//   lanes 0..2       agent q's dynamics + clip (mpe/base.py:129-135), its next row into LDS
+//   quads 0..2       agent i vs agent j = lane & 3 (the eye * 1e6 diagonal added after the root, mpe/base.py:173-176)
+//   quads 3..5       goal g vs agent a (SPREAD: every a, goal g's nearest agent; TARGET: a = g only)
+//   quads 6..8       agent i vs obstacle o (mpe/base.py:179-181)
+//   lanes 36..38     ||a_i|| (get_reward's action norm)
+// one sqrtf for all of them, the row minima as 2-step quad reductions (v_minimum3: NaN-propagating like min_nan,
+// equal values on these >= +0 norms), costs on lanes 0..5, the reward on lane 0 from readlanes in the reference's
+// order, then graph t + 1 (70 node floats, 40 state floats, 27 / 21 edges) from LDS rows with per-lane constant
+// roles.  Agent rows double-buffer in LDS by step parity; actions arrive clipped in KC-step chunks (as the Lidar
+// wave kernel: a chunk's load waits once for the store drain before it, not once per step).
+namespace mpew {
+constexpr int NA = 3, NO = 3, SD = 4, ND = SD + 3, N = 2 * NA + NO + 1, PAD = N - 1, KC = 32;
+constexpr int A0 = 0, GL = A0 + 2 * NA * SD, OB = GL + NA * SD, ACT = OB + NO * SD;  // LDS floats per wave
+constexpr int TOTAL = ACT + KC * 2 * NA;                                                  // 48 + 192 = 240
+static_assert((KC * 2 * NA) % 64 == 0, "a chunk is whole lanes");
+
+template <int GOAL>
+__global__ __launch_bounds__(256) void mpe_rollout_wave_kernel(dgppo_env_cfg cfg, dgppo_env_rollout_io r) {
+  constexpr bool SPREAD = GOAL == DGPPO_GOAL_SPREAD;
+  constexpr int NAG = SPREAD ? NA * NA : NA, E = NA * NA + NAG + NA * NO;
+  constexpr int PER = KC * 2 * NA / 64;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const dgppo_env_step_io& g0 = r.step;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+  const int64_t env_raw = (int64_t)blockIdx.x * 4 + wid;
+  if (env_raw >= g0.n_env) return;  // no workgroup barrier in this kernel: a surplus wave just leaves
+  const int64_t env = env_raw;
+  float* lds = smem + wid * TOTAL;
+  // graph 0's state rows: agents -> agent slot 0, goals -> GL, obstacles -> OB (2n + O rows)
+  {
+    const float* st = g0.states + env * g0.states_stride;
+    const float v = st[lane < 36 ? lane : 0];
+    if (lane < 36) lds[lane < NA * SD ? A0 + lane : GL + (lane - NA * SD)] = v;
+  }
+  wv::wave_sync();
+  // per-lane roles (constant over the episode)
+  const int q4 = lane >> 2, c4 = lane & 3;
+  bool dvalid = lane < 36 && c4 < 3;
+  if (!SPREAD && q4 >= 3 && q4 < 6) dvalid = dvalid && c4 == 0;
+  const bool diag = q4 < 3 && c4 == q4;
+  const bool anorm = lane >= 36 && lane < 39;
+  // operand rows (x, y) of the lane's distance: (cur?, offset)
+  int oa, ob;
+  bool ca, cb;
+  if (q4 < 3) {
+    ca = true, oa = q4 * SD, cb = true, ob = (c4 < 3 ? c4 : 0) * SD;
+  } else if (q4 < 6) {
+    const int gj = q4 - 3, ai = SPREAD ? (c4 < 3 ? c4 : 0) : gj;
+    ca = false, oa = GL + gj * SD, cb = true, ob = ai * SD;
+  } else {
+    const int i = q4 < 9 ? q4 - 6 : 0;
+    ca = true, oa = i * SD, cb = false, ob = OB + (c4 < 3 ? c4 : 0) * SD;
+  }
+  const int ag = lane < 3 ? lane : (anorm ? lane - 36 : 0);  // the agent whose action this lane reads
+  // graph roles: node floats idx = lane + 64 k (k = 0, 1), state floats idx = lane, edge e = lane
+  int nr[2], nc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = lane + 64 * k;
+    nr[k] = idx / ND;
+    nc[k] = idx - nr[k] * ND;
+  }
+  const int sr = lane >> 2, sc = lane & 3;
+  int ei = 0, ej = 0, ekind = 0;  // kind 0 agent-agent, 1 agent-goal, 2 agent-obstacle
+  if (lane < NA * NA) {
+    ei = lane / NA, ej = lane - ei * NA, ekind = 0;
+  } else if (lane < NA * NA + NAG) {
+    const int qq = lane - NA * NA;
+    ei = SPREAD ? qq / NA : qq, ej = SPREAD ? qq - ei * NA : qq, ekind = 1;
+  } else if (lane < E) {
+    const int qq = lane - NA * NA - NAG;
+    ei = qq / NO, ej = qq - ei * NO, ekind = 2;
+  }
+  // actions: chunks of KC steps, the next chunk in registers one chunk ahead
+  const float* act0 = g0.action + env * g0.action_stride;
+  float* acts = lds + ACT;
+  auto load_chunk = [&](int t0, float (&v)[PER]) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = lane * PER + j, st = idx / (2 * NA), kk = idx - st * (2 * NA);
+      const int ts = t0 + st < r.T ? t0 + st : r.T - 1;
+      v[j] = act0[(int64_t)ts * r.t_action + kk];
+    }
+  };
+  float cv[PER];
+  if (r.T > 0) load_chunk(0, cv);
+  float* const nodes_e = g0.nodes + env * g0.nodes_stride;
+  float* const edges_e = g0.edges + env * g0.edges_stride;
+  float* const states_e = g0.out_states + env * g0.out_states_stride;
+  int32_t* const recv_e = g0.receivers + env * g0.edge_index_stride;
+  int32_t* const send_e = g0.senders + env * g0.edge_index_stride;
+  float* const reward_e = g0.reward + env * g0.reward_stride;
+  float* const cost_e = g0.cost + env * g0.cost_stride;
+#pragma clang loop unroll(disable)
+  for (int t = 0; t < r.T; ++t) {
+    const int tc = t % KC;
+    if (tc == 0) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) acts[lane * PER + j] = clampf_nan(cv[j], -1.0f, 1.0f);
+      wv::wave_sync();
+      if (t + KC < r.T) load_chunk(t + KC, cv);
+    }
+    const int cur = (t & 1) * NA * SD, nxt = NA * SD - cur;
+    // ---- dynamics (lanes 0..2) and the action norms (lanes 36..38)
+    const float2 a = *reinterpret_cast<const float2*>(acts + tc * 2 * NA + 2 * ag);
+    const float4 x = *reinterpret_cast<const float4*>(lds + A0 + cur + ag * SD);
+    float y[SD];
+    y[0] = x.z * cfg.dt + x.x;
+    y[1] = x.w * cfg.dt + x.y;
+    y[2] = (a.x * 10.0f) * cfg.dt + x.z;
+    y[3] = (a.y * 10.0f) * cfg.dt + x.w;
+#pragma unroll
+    for (int c = 0; c < SD; ++c) y[c] = clampf_nan(y[c], cfg.state_lo[c], cfg.state_hi[c]);
+    if (lane < NA) *reinterpret_cast<float4*>(lds + A0 + nxt + lane * SD) = make_float4(y[0], y[1], y[2], y[3]);
+    // ---- distances on the current rows, one root for every lane
+    const float2 pa = *reinterpret_cast<const float2*>(lds + oa + (ca ? cur : 0));
+    const float2 pb = *reinterpret_cast<const float2*>(lds + ob + (cb ? cur : 0));
+    const float sq = anorm ? sq2(a.x, a.y) : sq2(pa.x - pb.x, pa.y - pb.y);
+    float v = sqrtf(sq);
+    if (diag) v = v + 1e6f;
+    float m = dvalid ? v : __builtin_inff();
+    m = __builtin_elementwise_minimum(m, wv::dppb<0xB1>(m));
+    m = __builtin_elementwise_minimum(m, wv::dppb<0x4E>(m));
+    // ---- costs (lane 2 i + h) and reward (lane 0), mpe/base.py:164-191 / get_reward
+    float md[NA], dg[NA], mo[NA], a2[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      md[i] = wv::rlf(m, 4 * i);
+      dg[i] = wv::rlf(m, 12 + 4 * i);
+      mo[i] = wv::rlf(m, 24 + 4 * i);
+      const float an = wv::rlf(v, 36 + i);
+      a2[i] = an * an;
+    }
+    {
+      const int ci = lane >> 1;
+      const float mdi = ci == 0 ? md[0] : (ci == 1 ? md[1] : md[2]);
+      const float moi = ci == 0 ? mo[0] : (ci == 1 ? mo[1] : mo[2]);
+      float c = (lane & 1) == 0 ? cfg.c_agent_cost - mdi : cfg.c_obs_cost - moi;
+      c = c <= 0.0f ? c - 0.5f : c + 0.5f;
+      c = c < -1.0f ? -1.0f : c;  // jnp.clip(cost, a_min=-1.0)
+      if (lane < 2 * NA) cost_e[t * r.t_cost + lane] = c;
+    }
+    if (lane == 0) {
+      float sd_ = 0.0f, sf = 0.0f, sa = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        sd_ = sd_ + dg[i];
+        sf = sf + (dg[i] > cfg.dist2goal ? 1.0f : 0.0f);
+        sa = sa + a2[i];
+      }
+      const float nn = (float)NA;
+      float rw = 0.0f - (sd_ / nn) * 0.01f;
+      rw = rw - (sf / nn) * 0.001f;
+      rw = rw - (sa / nn) * 0.0001f;
+      reward_e[t * r.t_reward] = rw;
+    }
+    wv::wave_sync();  // next agent rows visible
+    // ---- graph t + 1 (write_graph_mpe)
+    float* no = nodes_e + (int64_t)(t + 1) * r.t_nodes;
+    float* so = states_e + (int64_t)(t + 1) * r.t_states;
+    float* eo = edges_e + (int64_t)(t + 1) * r.t_edges;
+    int32_t* ro = recv_e + (int64_t)(t + 1) * r.t_index;
+    int32_t* sno = send_e + (int64_t)(t + 1) * r.t_index;
+    auto row_off = [&](int rr) {
+      return rr < NA ? A0 + nxt + rr * SD : (rr < 2 * NA ? GL + (rr - NA) * SD : (rr < PAD ? OB + (rr - 2 * NA) * SD : A0 + nxt));
+    };
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int rr = nr[k], c = nc[k];
+      const float xv = lds[row_off(rr) + (c < SD ? c : 0)];
+      const int hot = rr < NA ? SD + 2 : (rr < 2 * NA ? SD + 1 : SD);
+      const float val = rr == PAD ? 0.0f : (c < SD ? xv : (c == hot ? 1.0f : 0.0f));
+      if (lane + 64 * k < N * ND) no[lane + 64 * k] = val;
+    }
+    {
+      const float xv = lds[row_off(sr) + sc];
+      if (lane < N * SD) so[lane] = sr == PAD ? -1.0f : xv;
+    }
+    {
+      const float4 si = *reinterpret_cast<const float4*>(lds + A0 + nxt + ei * SD);
+      const float4 sj = *reinterpret_cast<const float4*>(
+          lds + (ekind == 0 ? A0 + nxt + ej * SD : (ekind == 1 ? GL + ej * SD : OB + ej * SD)));
+      const float f0 = si.x - sj.x, f1 = si.y - sj.y, f2 = si.z - sj.z, f3 = si.w - sj.w;
+      const float d2 = sq2(si.x - sj.x, si.y - sj.y);
+      bool msk;
+      if (ekind == 0) msk = ei == ej ? ((d2 == 0.0f) & (cfg.c_self_dist < cfg.comm_radius)) : (d2 < cfg.t2_comm);
+      else msk = ekind == 1 ? true : (d2 < cfg.t2_comm);
+      const int sv0 = ekind == 0 ? ej : (ekind == 1 ? NA + ej : 2 * NA + ej);
+      if (lane < E) {
+        reinterpret_cast<float4*>(eo)[lane] = make_float4(f0, f1, f2, f3);
+        ro[lane] = msk ? ei : PAD;
+        sno[lane] = msk ? sv0 : PAD;
+      }
+    }
+  }
+}
+}  // namespace mpew
 }  // namespace wv
 
 // ---- LidarOmniTarget (dgppo/env/lidar_env/lidar_omni_target.py) --------------------------------
@@ -3395,6 +3599,23 @@ extern "C" int dgppo_env_rollout(const dgppo_env_cfg* cfg, const dgppo_env_rollo
     const char* e = getenv("DGPPO_ENV_BLOCK_ROLLOUT");
     return !(e && atoi(e) == 0);
   }();
+  // MPE n = 3 with 3 obstacles (BASELINE config 2): the wave-per-env persistent rollout (graph 0 is loaded: the MPE
+  // reset always builds it); DGPPO_MPE_WAVE=0 or the block step kernels forced keep the workgroup-per-env kernel
+  static const bool mpe_wave = [] {
+    const char* e = getenv("DGPPO_MPE_WAVE");
+    return !(e && atoi(e) == 0);
+  }();
+  if (block_rollout && mpe_wave && r->T > 0 && cfg->engine == DGPPO_ENGINE_MPE && cfg->variant == DGPPO_VARIANT_NONE &&
+      cfg->n_agents == wv::mpew::NA && cfg->n_obs == wv::mpew::NO && wave_step_enabled() &&
+      (reinterpret_cast<uintptr_t>(io.edges) % 16u) == 0 && io.edges_stride % 4 == 0 && r->t_edges % 4 == 0) {
+    const size_t sh = 4 * sizeof(float) * wv::mpew::TOTAL;
+    const dim3 grid((unsigned)((io.n_env + 3) / 4));
+    if (cfg->goal_mode == DGPPO_GOAL_SPREAD)
+      hipLaunchKernelGGL((wv::mpew::mpe_rollout_wave_kernel<DGPPO_GOAL_SPREAD>), grid, dim3(256), sh, s, *cfg, *r);
+    else
+      hipLaunchKernelGGL((wv::mpew::mpe_rollout_wave_kernel<DGPPO_GOAL_TARGET>), grid, dim3(256), sh, s, *cfg, *r);
+    return (int)hipGetLastError();
+  }
   if (block_rollout && r->T > 0 && cfg->variant == DGPPO_VARIANT_NONE && cfg->engine != DGPPO_ENGINE_OMNI &&
       cfg->n_agents <= 32) {  // (2 n actions per step staged one per thread of a >= 64-thread workgroup)
     const Carve cv(cfg->n_agents, cfg->state_dim, cfg->n_obs, cfg->n_rays, cfg->top_k,

@@ -178,7 +178,7 @@ def test_policy_rollout_lanes_bit_exact(cuda, env_id, graph):
 
 @pytest.mark.parametrize("eid,n,obs,B", [("LidarSpread", 8, 3, 255), ("LidarTarget", 8, 3, 64),
                                          ("LidarBicycleTarget", 8, 3, 130), ("LidarOmniTarget", 8, 3, 97),
-                                         ("MPESpread", 3, 3, 33), ("LidarSpread", 4, 2, 20),
+                                         ("MPESpread", 3, 3, 33), ("MPETarget", 3, 3, 29), ("LidarSpread", 4, 2, 20),
                                          # the workgroup-per-env persistent kernel (env_rollout_block_kernel)
                                          ("MPETarget", 3, 0, 17), ("LidarTarget", 2, 0, 11),
                                          ("LidarBicycleTarget", 2, 1, 7), ("LidarSpread", 32, 8, 5)])
@@ -248,6 +248,34 @@ def test_block_persistent_rollout_matches_wave_steps(cuda):
             gen.manual_seed(3)
             eng.actions.uniform_(-1.0, 1.0, generator=gen)
             eng.run(key=8)
+            torch.cuda.synchronize(cuda)
+            b = eng.buf
+            outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders, eng.rewards,
+                                                  eng.costs)])
+        finally:
+            lib.dgppo_env_set_step_kernel(prev)
+    for k, (x, y) in enumerate(zip(*outs)):
+        assert np.array_equal(x, y), k
+
+
+@pytest.mark.parametrize("eid", ["MPESpread", "MPETarget"])
+def test_mpe_wave_rollout_matches_block_rollout(cuda, eid):
+    """MPE n = 3 with 3 obstacles (BASELINE config 2) runs the wave-per-env persistent rollout
+    (wv::mpew::mpe_rollout_wave_kernel); with the workgroup-per-env kernels forced it runs the block persistent
+    rollout: the two agree bit for bit at the episode length, partial workgroups and out-of-range actions included."""
+    from dgppo_fov_amd import _lib
+    lib = _lib.load()
+    env = make_env(eid, 3, num_obs=3, device=cuda)
+    B, T = 45, 128
+    outs = []
+    for mode in (0, 1):
+        prev = lib.dgppo_env_set_step_kernel(mode)
+        try:
+            eng = RolloutEngine(env, B, T, cuda, fused=True)
+            gen = torch.Generator(device=cuda)
+            gen.manual_seed(13)
+            eng.actions.uniform_(-1.3, 1.3, generator=gen)
+            eng.run(key=31)
             torch.cuda.synchronize(cuda)
             b = eng.buf
             outs.append([x.cpu().numpy() for x in (b.nodes, b.edges, b.states, b.receivers, b.senders, eng.rewards,
