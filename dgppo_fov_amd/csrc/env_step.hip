@@ -497,8 +497,82 @@ __device__ __forceinline__ void lidar_scan(const D& d, const float* ray_dirs, fl
     __syncthreads();
     const int tot = n * R * O;
     const int lane = tid & 63;
+    // One-pass form (32 rays, every lane's (agent slot, obstacle) bits in one 64-bit mask): lane tid keeps ray
+    // r = tid & 31 and its ray constants in registers and tests agents i = (tid >> 5) + (nthr / 32) it against every
+    // obstacle; the survivors are compacted once by a workgroup prefix of the per-lane counts instead of one ballot +
+    // LDS atomic per 64 triples.  The item order differs, the alphas do not (atomicMin per (agent, ray)).  When the
+    // survivors exceed the list (adversarial inputs), the multi-round loop below runs instead.
+    const int slots = nthr >> 5, its = (n + slots - 1) / slots;
+    bool one_pass = R == 32 && (nthr & 31) == 0 && its * O <= 64 && nthr <= 1024;
+    if (one_pass) {
+      const int r = tid & 31, a0 = tid >> 5;
+      const float4 rc = rayc[r];
+      const float dx = rc.x, dy = rc.y, rlen2 = rc.z, rlen = rc.w;
+      uint64_t bits = 0ull;
 #pragma unroll 1
-    for (int t0 = 0; t0 < tot; t0 += cap) {
+      for (int it = 0; it < its; ++it) {
+        const int i = a0 + slots * it;
+        const bool ai = i < n;
+        const int ic = ai ? i : 0;
+        const float sx = nxt[ic * SD + 0], sy = nxt[ic * SD + 1];
+        const bool qok = (fabsf(sx) <= 2.0f) & (fabsf(sy) <= 2.0f);
+#pragma unroll 1
+        for (int o = 0; o < O; ++o) {
+          const float vx = obst[o * DGPPO_OBST_FIELDS] - sx, vy = obst[o * DGPPO_OBST_FIELDS + 1] - sy;
+          const float perp = vx * dy - vy * dx, proj = vx * dx + vy * dy;
+          const float Rl = (rho[o] + 0.01f) * rlen;
+          const bool miss = qok & ((fabsf(perp) > Rl) | (proj < -Rl) | (proj > rlen2 + Rl));
+          const bool keep = ai & (!miss | ((unsafe[o] >> r) & 1u));
+          bits |= (uint64_t)keep << (it * O + o);
+        }
+      }
+      // workgroup exclusive prefix of the per-lane counts: 7 ballots per wave, then the waves' totals in LDS
+      const int c = __popcll(bits);
+      int pre = 0, wtot = 0;
+#pragma unroll
+      for (int b = 0; b < 7; ++b) {
+        const uint64_t bb = __ballot((c >> b) & 1);
+        pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+        wtot += __popcll(bb) << b;
+      }
+      int* wsum = cnt + 1;  // (the 3 ints after the counter; nthr / 64 <= 3 waves used here, else the wave totals
+      const int wid = tid >> 6, nw = nthr >> 6;  //  go to the item list's tail, see below)
+      int* wt = nw <= 3 ? wsum : items + cv.dist_n - nw;
+      if (lane == 0) wt[wid] = wtot;
+      __syncthreads();
+      int base = 0, all = 0;
+      for (int w = 0; w < nw; ++w) {
+        const int v = wt[w];
+        base += w < wid ? v : 0;
+        all += v;
+      }
+      __syncthreads();  // every wave read the totals before any item (possibly over them) is written
+      const int capw = cv.dist_n - (nw <= 3 ? 0 : nw);
+      one_pass = all <= capw;
+      if (one_pass) {
+        int pos = base + pre;
+        while (bits) {
+          const int q = __builtin_ctzll(bits);
+          bits &= bits - 1ull;
+          const int it = q / O, o = q - it * O;
+          items[pos++] = (o << 16) | ((a0 + slots * it) * R + r);
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int j = tid; j < all; j += nthr) {
+          const int code = items[j], o = code >> 16, p = code & 0xFFFF, i = p / R, rr = p - (p / R) * R;
+          const float sx = nxt[i * SD + 0], sy = nxt[i * SD + 1];
+          const float4 rc2 = rayc[rr];
+          const float ex = sx + rc2.x;
+          const float ey = sy + rc2.y;
+          const float a = rect_raytrace(obst + o * DGPPO_OBST_FIELDS, evec + o * 8, sx, sy, sx - ex, sy - ey);
+          atomicMin(aenc + p, enc(a));
+        }
+        __syncthreads();
+      }
+    }
+#pragma unroll 1
+    for (int t0 = 0; t0 < (one_pass ? 0 : tot); t0 += cap) {
       const int t1 = t0 + cap < tot ? t0 + cap : tot;
 #pragma unroll 1
       for (int tb = t0; tb < t1; tb += nthr) {  // uniform trip count: every wave joins the ballots
