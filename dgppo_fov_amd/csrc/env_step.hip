@@ -192,19 +192,38 @@ __device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d
     }
     out.nodes[idx] = v;
   }
-  // states (N, SD); pad row is -1
+  // states (N, SD); pad row is -1.  4-wide rows into a 16-byte aligned buffer: one float4 per row and lane (the LDS
+  // rows are 16-byte aligned: Carve regions are), else one float per element
+  if (SD == 4 && (reinterpret_cast<uintptr_t>(out.states) & 15u) == 0) {
 #pragma unroll 1
-  for (int idx = tid; idx < N * SD; idx += nthr) {
-    const int r = idx / SD;
-    const int c = idx - r * SD;
-    float v;
-    if (r < n) v = nxt[r * SD + c];
-    else if (r < 2 * n) v = goal[(r - n) * SD + c];
-    else if (r < 2 * n + n_third) {
-      const int h = r - 2 * n;
-      v = mpe ? third[h * SD + c] : (c < 2 ? third[h * 2 + c] : 0.0f);
-    } else v = -1.0f;
-    out.states[idx] = v;
+    for (int r = tid; r < N; r += nthr) {
+      float4 v;
+      if (r < n) {
+        v = *reinterpret_cast<const float4*>(nxt + r * SD);
+      } else if (r < 2 * n) {
+        v = *reinterpret_cast<const float4*>(goal + (r - n) * SD);
+      } else if (r < 2 * n + n_third) {
+        const int h = r - 2 * n;
+        v = mpe ? *reinterpret_cast<const float4*>(third + h * SD) : make_float4(third[h * 2], third[h * 2 + 1], 0.0f, 0.0f);
+      } else {
+        v = make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
+      }
+      reinterpret_cast<float4*>(out.states)[r] = v;
+    }
+  } else {
+#pragma unroll 1
+    for (int idx = tid; idx < N * SD; idx += nthr) {
+      const int r = idx / SD;
+      const int c = idx - r * SD;
+      float v;
+      if (r < n) v = nxt[r * SD + c];
+      else if (r < 2 * n) v = goal[(r - n) * SD + c];
+      else if (r < 2 * n + n_third) {
+        const int h = r - 2 * n;
+        v = mpe ? third[h * SD + c] : (c < 2 ? third[h * 2 + c] : 0.0f);
+      } else v = -1.0f;
+      out.states[idx] = v;
+    }
   }
   // edges: [agent-agent n*n][agent-goal][agent-lidar n*k | agent-obstacle n*O]
   const int n_aa = n * n;
