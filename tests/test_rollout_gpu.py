@@ -211,7 +211,7 @@ def test_persistent_env_rollout_bit_exact(cuda, eid, n, obs, B, graph):
     ("MPESpread", 3, 3, 9, 128),     # T * 2n = 768 action floats: staged in LDS at kernel start
     ("MPESpread", 3, 3, 9, 700),     # 4200 > kActStage: per-step action prefetch from HBM
     ("LidarSpread", 32, 8, 3, 128),  # 8192 > kActStage (the default n = 32 episode): prefetch path
-    ("LidarSpread", 32, 8, 3, 24),   # 1536 fits kActStage, but 59 KB of carve + 6 KB > 64 KB: not staged
+    ("LidarSpread", 32, 8, 3, 24),   # 1536 fits kActStage and 37.3 KB of carve + 6 KB <= 64 KB: staged
 ])
 def test_persistent_block_rollout_action_staging_branches(cuda, eid, n, obs, B, T):
     """Both branches of the block persistent rollout's action staging (the host decides it from kActStage and
