@@ -108,8 +108,10 @@ def cpu_baseline_update():
     GraphTransformer, MLP, GRU, TanhNormal restated, every graph of the batch evaluated as one disjoint
     union graph as vmap does): update_Vl + update_Vh + update_policy forward + backward on a bounded
     sample of SAMPLE_ENVS envs x T steps, torch.set_num_threads(host cores), warm-up 3, median of 10.
-    Scaled to one update = 32 minibatches x (16,384 / sample graphs) x t_sample; the prepass (Vl / Vh
-    over the rollouts) and the deterministic rollout are NOT counted, so the CPU figure is optimistic."""
+    Scaled to one update = 32 minibatches x (16,384 / sample graphs) x t_sample, plus the prepass on the same
+    sample (forward only: the Vl scan and Vh on the rollout and the deterministic rollout's graphs) and the
+    deterministic rollout itself (actor mode + NumPy env step, T steps of the sample envs), both scaled by
+    B / SAMPLE_ENVS (median of 3 after 1 warm-up)."""
     import torch as th
 
     from oracle import env as O
@@ -120,7 +122,7 @@ def cpu_baseline_update():
     SAMPLE_ENVS, L = 2, RNN_STEP
     spec = O.Spec(ENV_ID, N_AGENTS, N_OBS)
     ag, gl, third = O.env_reset(spec, 3, SAMPLE_ENVS)
-    g = O.initial_graph(spec, ag, gl, third)
+    g = g0 = O.initial_graph(spec, ag, gl, third)
     rng = np.random.default_rng(2)
     seq = {k: [] for k in ("nodes", "edges", "receivers", "senders")}
     states = g["states"]
@@ -153,23 +155,45 @@ def cpu_baseline_update():
             lp, ent = R.actor_eval_seq(pa, graph, S, L, n, acts, eps)
             R.ppo_loss(lp, lp_old, adv, ent).backward()
 
+        def prepass_and_det():
+            pa, pl, ph = (R.to_t(x) for x in trees)
+            with th.no_grad():
+                R.vl_seq(pl, graph, S, L, n)
+                R.vh(ph, graph, h_act, n)  # the rollout's graphs
+                R.vh(ph, graph, h_act, n)  # the deterministic rollout's graphs (same shapes)
+                gd, h = g0, np.zeros((SAMPLE_ENVS, n, 64), np.float32)
+                for t in range(T):  # the deterministic rollout: actor mode + env step
+                    h2 = R.actor_carry(pa, gd, h, n)
+                    mu, _ = R.policy_dist(pa, h2)
+                    h = h2.numpy()
+                    gd = O.env_step(spec, gd["states"], third, th.tanh(mu).numpy())
+
         times = []
         for it in range(CPU_WARMUP + CPU_ITERS):
             t0 = time.perf_counter()
             one()
             if it >= CPU_WARMUP:
                 times.append(time.perf_counter() - t0)
+        times_pd = []
+        for it in range(1 + 3):
+            t0 = time.perf_counter()
+            prepass_and_det()
+            if it >= 1:
+                times_pd.append(time.perf_counter() - t0)
     finally:
         R.T64 = th.float64
     t_sample = float(np.median(times))
-    t_update = t_sample * (PPO_BATCH / G) * (B_PER_GPU * T // PPO_BATCH)
+    t_pd = float(np.median(times_pd))
+    t_update = t_sample * (PPO_BATCH / G) * (B_PER_GPU * T // PPO_BATCH) + t_pd * (B_PER_GPU / SAMPLE_ENVS)
     return {"value": round(1.0 / t_update, 6), "unit": "PPO-updates/s", "cores": P, "kind": "port",
-            "cpu": _cpu_model(), "sample_ms": round(t_sample * 1e3, 2),
+            "cpu": _cpu_model(), "sample_ms": round(t_sample * 1e3, 2), "prepass_det_sample_ms": round(t_pd * 1e3, 2),
             "sample": f"oracle/nets_t.py torch-CPU fp32 ({P} threads): Vl + Vh + policy forward+backward on "
                       f"{SAMPLE_ENVS} envs x T={T} LidarSpread n=8 graphs ({S} rnn_step-{L} chunks), warm-up "
                       f"{CPU_WARMUP}, median of {CPU_ITERS} = {t_sample * 1e3:.1f} ms; scaled x{PPO_BATCH // G} "
-                      f"to a 16,384-graph minibatch and x{B_PER_GPU * T // PPO_BATCH} minibatches per update "
-                      f"(prepass and deterministic rollout not counted)"}
+                      f"to a 16,384-graph minibatch and x{B_PER_GPU * T // PPO_BATCH} minibatches per update; "
+                      f"plus the prepass (Vl scan, Vh x2, forward) and the deterministic rollout (actor + env, "
+                      f"{T} steps) on the same {SAMPLE_ENVS} envs = {t_pd * 1e3:.1f} ms (median of 3), "
+                      f"x{B_PER_GPU // SAMPLE_ENVS}"}
 
 
 def cpu_baseline_rollout():
@@ -288,10 +312,9 @@ def source_sha256():
 
 
 PPO_BATCH, RNN_STEP = 16384, 16  # BASELINE.md synthetic-input plan (batch_size, rnn_step)
-# SURVEY.md §8(d) official algorithmic flops (minimal node-level projection formulation), LidarSpread n8
-# B4096: one PPO update (det rollout excluded: prepass + SGD, fwd+bwd = 3x fwd) and the two rollouts'
-# actor inference; MFMA% = flops / (t * 157.3 TF * n_gpu)
-UPDATE_TFLOP_PER_4096_ENVS, ROLLOUT_TFLOP_PER_4096_ENVS = 22.1, 5.3
+# the update's algorithmic flops: dgppo_fov_amd/utils/flops.py counts the per-receiver formulation the kernels
+# implement (DESIGN.md §4, §3.3 "Update flops"), not SURVEY.md §8(d)'s node-level count (22.1 TF + 2.65 TF det
+# rollout at this config, 4-5x more than the kernels need); fp32 MFMA and VALU share the 157.3 TF/s peak
 FP32_MFMA_PEAK_TFLOPS = 157.3
 
 
@@ -364,17 +387,22 @@ def ppo_bench(env, dev, world, rank, iters, strong=False):
                                              "calibrated on known elementwise work (valu_calibration)",
                                  "valu_calibration": pmc.get("valu_calibration")}
                 executed["executed_fp32"] = executed_fp32
-    upd_tf = UPDATE_TFLOP_PER_4096_ENVS * (B_PER_GPU / 4096) * world + ROLLOUT_TFLOP_PER_4096_ENVS / 2 * (
-        B_PER_GPU / 4096) * world  # the update runs the deterministic rollout too
+    from dgppo_fov_amd.utils.flops import update_flops
+
+    fl = update_flops(algo, env, B_PER_GPU, T)  # per rank; the deterministic rollout's actor inference included
+    upd_tf = fl["total"] * world / 1e12
     return {"updates_per_s": round(1.0 / t_upd, 4), "update_ms": round(t_upd * 1e3, 2),
             "update_ms_mean": round(t_upd_mean * 1e3, 2), "timing": f"median of {iters} iterations after 2 warm-up updates",
             "update_roofline": {"bound": "mfma", "algorithmic_tflop": round(upd_tf, 2),
                                 "achieved": round(upd_tf / t_upd, 2), "peak": FP32_MFMA_PEAK_TFLOPS * world,
                                 "unit": "TFLOP/s", "frac": round(upd_tf / t_upd / (FP32_MFMA_PEAK_TFLOPS * world), 4),
-                                "frac_kind": "algorithmic (node-level projection formulation, SURVEY.md 8(d)), not a "
-                                             "utilisation: the executed work is executed_mfma / executed_fp32",
-                                "flops_source": "SURVEY.md 8(d) minimal node-level formulation: 22.1 TF per update + "
-                                                "2.65 TF det-rollout inference",
+                                "frac_kind": "algorithmic: the per-receiver formulation the kernels implement "
+                                             "(dgppo_fov_amd/utils/flops.py, DESIGN.md 3.3); the hardware's executed "
+                                             "work is executed_mfma / executed_fp32",
+                                "flops_source": "utils/flops.py update_flops: " + ", ".join(
+                                    f"{k} {v / 1e12:.3f} TF" for k, v in fl["parts"].items()),
+                                "per_graph_fwd_mflop": fl["per_graph_fwd_mflop"],
+                                "survey_8d_node_level_tflop": round((22.1 + 2.65) * (B_PER_GPU / 4096) * world, 2),
                                 "executed_mfma": executed},
             "collect_ms": round(t_col * 1e3, 2),
             "collect_env_steps_per_s": round(B_PER_GPU * T * world / t_col, 1),

@@ -47,9 +47,10 @@ def minibatch_plan(n_env_local: int, T: int, world: int, batch_size: int, rng: n
     return np.array_split(idx, n_mb)
 
 
-def allreduce_mean_(t: torch.Tensor, world: int):
-    """In-place mean over ranks (one collective: SUM then scale; RCCL on GPUs, gloo on CPU)."""
-    if world > 1:
+def allreduce_mean_(t: torch.Tensor, world: int, force: bool = False):
+    """In-place mean over ranks (one collective: SUM then scale; RCCL on GPUs, gloo on CPU).  force: run the
+    collective on a one-rank group too (DGPPO_FORCE_ALLREDUCE, the RCCL path's world-size-1 test)."""
+    if world > 1 or force:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         t.mul_(1.0 / world)
     return t
@@ -67,14 +68,6 @@ def PHASE_EVENTS() -> bool:
 def ADAM_MULTI() -> bool:
     """The three nets' clip + Adam steps in two launches (dgppo_adam_multi) instead of four per net (default on)."""
     return os.environ.get("DGPPO_ADAM_MULTI", "1") == "1"
-
-
-def WGRAD_SIDE() -> bool:
-    """Each net's weight-gradient GEMMs on a side stream of its pass's stream (K.wgrad_side), off the dX chain.
-    Off by default: bit-identical (tests/test_update_gpu.py) but slower at the bench config, 172.5-173.6 vs
-    170.0 ms per update (six streams over GPU_MAX_HW_QUEUES = 4 hardware queues), config 4's share 43.9-44.0 vs
-    44.1-44.4 ms (its captured minibatches keep the inline order: side streams under capture crashed capture_end)."""
-    return os.environ.get("DGPPO_WGRAD_SIDE", "0") == "1"
 
 
 def FORCE_SAFE() -> bool:
@@ -147,6 +140,10 @@ class DGPPO:
         self.train_steps = int(train_steps)
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
+        # the gradient / safe-data collectives run when there are several ranks, or on a one-rank process group when
+        # DGPPO_FORCE_ALLREDUCE=1 (tests/test_distributed_gpu.py: RCCL's code path exercised on one GPU)
+        self._reduce = self.world > 1 or (os.environ.get("DGPPO_FORCE_ALLREDUCE", "0") == "1" and dist.is_available()
+                                          and dist.is_initialized())
 
         dev = self.device
         # RNN(GRUCell | LSTMCell, rnn_layers) or none (--no-rnn / --use-lstm / --rnn-layers, nn/rnn.py:10-30)
@@ -422,7 +419,7 @@ class DGPPO:
         return out
 
     def _allreduce_grads(self):
-        allreduce_mean_(self.grad_flat, self.world)
+        allreduce_mean_(self.grad_flat, self.world, self._reduce)
 
     def _start_reduce(self, net, pending: list):
         """Start the (sum) all-reduce of one net's gradient bucket as soon as its backward is done, so it
@@ -430,11 +427,11 @@ class DGPPO:
         waits for every bucket and scales by 1/world before clip + Adam (same result as one flat
         all-reduce: each bucket is reduced exactly once).  Not while a minibatch graph is being captured: the
         graph path all-reduces the whole gradient buffer eagerly between its two replays."""
-        if self.world > 1 and not self._capturing and not self._flat_reduce:
+        if self._reduce and not self._capturing and not self._flat_reduce:
             pending.append(dist.all_reduce(net.ps.grad, op=dist.ReduceOp.SUM, async_op=True))
 
     def _finish_reduce(self, pending: list):
-        if self.world > 1 and not self._capturing:
+        if self._reduce and not self._capturing:
             if self._flat_reduce:  # the graph path's eager first minibatch: the same flat all-reduce as its replays
                 self._allreduce_grads()
                 return
@@ -473,18 +470,6 @@ class DGPPO:
         for st in aux:
             main.wait_stream(st)
         return out
-
-    def _wgrad_sides(self):
-        """Three side streams (one per concurrent pass) for the weight-gradient GEMMs, or Nones (serial streams,
-        phase profiling, or DGPPO_WGRAD_SIDE=0)."""
-        if not WGRAD_SIDE() or self._aux_streams(2) is None:
-            return [None, None, None]
-        if getattr(self, "_capturing", False) and os.environ.get("DGPPO_WGRAD_SIDE_GRAPH", "0") != "1":
-            return [None, None, None]  # captured minibatches keep the inline order (side streams crashed capture_end)
-        ws = getattr(self, "_wside", None)
-        if ws is None:
-            ws = self._wside = [torch.cuda.Stream(self.device) for _ in range(3)]
-        return ws
 
     def _buf(self, name: str, shape) -> torch.Tensor:
         """Update scratch that keeps its address from update to update (the captured minibatch graph reads it)."""
@@ -530,7 +515,7 @@ class DGPPO:
         three nets' passes on their streams, (2) clip + finite check + Adam; replays copy each minibatch's ids into
         the buffer, replay (1), all-reduce the gradients eagerly when there are several ranks, replay (2)."""
         static_envs = envs.clone()
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        g1, g2 = K.hold_for_graph(torch.cuda.CUDAGraph()), K.hold_for_graph(torch.cuda.CUDAGraph())
         self._capturing = True
         try:
             with torch.cuda.graph(g1):
@@ -583,7 +568,6 @@ class DGPPO:
         tgt = tgt.view(Bm * S_per_env, L)
         acts, lp_old, adv = acts.view(-1, self._action_dim), lp_old.view(-1), adv.view(-1)
         pending = []
-        side = self._wgrad_sides()  # (policy, Vl, Vh): weight gradients off each backward's dX chain
 
         def vl_job():  # update_Vl (informarl.py:357-385)
             v, _, cache = self.Vl.seq_fwd(g, Bm * S_per_env, L)
@@ -591,8 +575,7 @@ class DGPPO:
             loss = torch.empty(1, device=dev)
             K.l2_loss(v, tgt, dv, loss)
             ph.mark("Vl_fwd")
-            with K.wgrad_side(side[1]):
-                self.Vl.seq_bwd(cache, dv)
+            self.Vl.seq_bwd(cache, dv)
             self._start_reduce(self.Vl, pending)  # the bucket's all-reduce overlaps the other passes
             ph.mark("Vl_bwd")
             return loss
@@ -603,8 +586,7 @@ class DGPPO:
             loss = torch.empty(1, device=dev)
             K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)
             ph.mark("Vh_fwd")
-            with K.wgrad_side(side[2]):
-                self.Vh.bwd(cache, dvh)
+            self.Vh.bwd(cache, dvh)
             self._start_reduce(self.Vh, pending)
             ph.mark("Vh_bwd")
             return loss
@@ -616,8 +598,7 @@ class DGPPO:
             st = torch.empty(4, device=dev)
             K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, st)
             ph.mark("pi_fwd")
-            with K.wgrad_side(side[0]):
-                self.actor.eval_seq_bwd(cache, dlp, dent)
+            self.actor.eval_seq_bwd(cache, dlp, dent)
             self._start_reduce(self.actor, pending)
             ph.mark("pi_bwd")
             return st
@@ -718,7 +699,7 @@ class DGPPO:
             info = {"Vl/loss": vl_loss, "Vl/max_target": tgt.max(), "Vl/min_target": tgt.min(),
                     "Vh/loss_Vh": vh_loss, "policy/stats": stats, "policy/log_pi_min": lp_old.min()}
             safe = safe_cnt.sum()
-            if self.world > 1:
+            if self._reduce:
                 dist.all_reduce(safe)
             info["eval/safe_data"] = safe / (B * self.world * T * n)
             # learning diagnostics (not reference metrics): per cost column, the mean Vh over the rollout's

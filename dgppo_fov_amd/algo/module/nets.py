@@ -306,6 +306,7 @@ class VhNet(_Net):
         """get_Vh (dgppo.py:128-134) on G graphs with the actor's carries h (G*n, W): (G*n, n_cost).  Forward only
         (keep_cache False): GNN, head, GRU step and output Dense in one kernel where it applies (the prepass)."""
         rows = g.G * self.n
+        self.last_tail = False  # True when the fused kernel's value-head tail produced the output (tests)
         if VH_TAIL and not keep_cache and self.gru.simple and len(self.gnn.layers) == 1 and h.shape[1] == 64:
             out = torch.empty((rows, self.n_cost), device=h.device)
             hd, cell = self.head, self.gru.cells[0]
@@ -314,6 +315,7 @@ class VhNet(_Net):
                       v(hd.ln1.name + ".scale"), v(hd.ln1.name + ".bias"), cell.v("Wi"), cell.v("bi"), cell.v("Wh"),
                       cell.v("bhn"), self.out.W(), self.out.b()]
             if self.gnn.fwd_epilogue(g, tail=(tail_w, h if h.is_contiguous() else h.contiguous(), out)) is not None:
+                self.last_tail = True
                 return out, None
         z, gc = self.gnn.fwd(g, keep=keep_cache)
         y, hc = self.head.fwd(z)
@@ -395,10 +397,10 @@ class VhGlobalNet(_Net):
         dy0 = hd.d1.bwd(y0, dh1, rows)
         dh0 = hd.ln0.bwd(c0, dy0)  # d(head Dense_0 output) (rows, 64)
         W0, dW0 = hd.d0.W(), hd.d0.W(True)
-        K.gemm(z, dh0, dW0[:64], 64, 64, rows, ta=True, beta=1.0, bias_grad=hd.d0.b(True), side=True)
+        K.gemm(z, dh0, dW0[:64], 64, 64, rows, ta=True, beta=1.0, bias_grad=hd.d0.b(True))
         sm = torch.empty((G, 64), device=dev)  # per-graph mean of dh0; the agent SUM is n x it
         K.agent_mean_fwd(dh0, sm, G, n, 64, n * 64)
-        K.gemm(zm, sm, dW0[64:], 64, 64, G, ta=True, alpha=float(n), beta=1.0, side=True)
+        K.gemm(zm, sm, dW0[64:], 64, 64, G, ta=True, alpha=float(n), beta=1.0)
         # dz = dh0 W[:64]^T + (sum_agents dh0) W[64:]^T / n  (the mean's backward), one GEMM with a per-graph addend
         dzm = torch.empty((G, 64), device=dev)
         K.gemm(sm, W0[64:], dzm, G, 64, 64, tb=True, ldb=64)

@@ -7,13 +7,23 @@ from __future__ import annotations
 
 import ctypes
 import math
+import weakref
 
 import torch
 
 from .. import _lib, ops  # noqa: F401  (ops registers torch.ops.dgppo.*)
 
 _WS = {}
-_WS_KEPT = []  # replaced workspace buffers (see workspace)
+_GRAPHS = weakref.WeakSet()  # captured hipGraphs still alive (registered by hold_for_graph before their capture)
+_WS_KEPT = []  # (replaced workspace buffer, weak references to the graphs alive when it was replaced)
+
+
+def hold_for_graph(g):
+    """Register a hipGraph (torch.cuda.CUDAGraph) BEFORE its capture starts: until it is garbage-collected, a
+    workspace buffer that is replaced by a larger one stays allocated, because the graph's kernels keep its
+    address (a replay would otherwise write into memory the allocator has handed to another tensor)."""
+    _GRAPHS.add(g)
+    return g
 
 
 def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
@@ -22,32 +32,15 @@ def workspace(nfloats: int, device, slot: str = "default") -> torch.Tensor:
     key = (str(device), slot, _lib.stream_handle(device))
     t = _WS.get(key)
     if t is None or t.numel() < nfloats:
-        # a replaced buffer is never freed: a captured hipGraph (minibatch replay, rollout engines) may still hold
-        # its address, and once its memory went back to the allocator a replay would write into whatever reuses it
-        # (or fault, if the pool was released); growth at least doubles, so the kept buffers stay below the final size
         old = t.numel() if t is not None else 0
-        if t is not None:
-            _WS_KEPT.append(t)
-        t = torch.empty(max(int(nfloats), 2 * old, 1024), dtype=torch.float32, device=device)
+        live = [weakref.ref(g) for g in _GRAPHS]
+        if t is not None and live:
+            _WS_KEPT.append((t, live))  # a live graph may hold its address: freed once every such graph is gone
+        _WS_KEPT[:] = [(b, refs) for b, refs in _WS_KEPT if any(r() is not None for r in refs)]
+        # with graphs alive growth doubles, so the kept buffers stay below the final size; otherwise exact
+        t = torch.empty(max(int(nfloats), 2 * old if live else 0, 1024), dtype=torch.float32, device=device)
         _WS[key] = t
     return t
-
-
-def on_side(fn, *hold):
-    """fn() on the current stream's wgrad_side stream when one is active (forked after everything enqueued so far;
-    `hold` stays referenced until the join), else inline.  For a group of parameter-gradient launches whose
-    temporaries are allocated inside fn (then on the side stream's own pool)."""
-    if _SIDE:
-        cur = torch.cuda.current_stream()
-        ent = _SIDE.get(cur.cuda_stream)
-        if ent is not None:
-            st, held = ent
-            st.wait_stream(cur)
-            with torch.cuda.stream(st):
-                r = fn()
-            held.append(hold)
-            return r
-    return fn()
 
 
 def _p(t, off=0):
@@ -64,65 +57,16 @@ def _chk(rc, what):
 
 GEMM_LOG = None  # set to a list to record (M, N, K, batch, ta, tb, split_k, has_bias) per launch
 
-# weight-gradient GEMMs off the dX chain: current stream handle -> (side stream, inputs held until the join)
-_SIDE = {}
-
-
-class wgrad_side:
-    """Inside this context, gemm(..., side=True) weight-gradient calls issued on the current stream run on `side`
-    instead: the side stream first waits for everything enqueued so far on the current stream (the GEMM's inputs),
-    the inputs are held until the exit, where the current stream waits for the side stream (so their memory returns
-    to the allocator only once a later reuse on the current stream is ordered after the side work; record_stream is
-    not used: the allocator's deferred events crashed hipGraph capture_end).  The chain of dX GEMMs / attention backward no longer waits for each layer's dW GEMM and
-    its chunk reduction.  Only calls whose output is a parameter gradient that nothing on the current stream touches
-    before the exit take side=True; they stay in issue order on the one side stream.  side=None: a no-op."""
-
-    def __init__(self, side):
-        self.side = side
-
-    def __enter__(self):
-        if self.side is not None:
-            self.main = torch.cuda.current_stream(self.side.device)
-            self.key = self.main.cuda_stream
-            _SIDE[self.key] = (self.side, [])
-        return self
-
-    def __exit__(self, *exc):
-        if self.side is not None:
-            _, held = _SIDE.pop(self.key, (None, []))
-            # join only a side stream that was forked here: under hipGraph capture an unforked side stream is not
-            # capturing, and waiting on an event recorded outside the capture broke capture_end
-            if held:
-                self.main.wait_stream(self.side)
-            held.clear()
-        return False
-
-
 def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
          a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
          bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
-         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None, mask=None, ld_mask=None, ln=None,
-         side=False):
+         alpha=1.0, beta=0.0, relu=False, split_k=None, bias_grad=None, mask=None, ld_mask=None, ln=None):
     """C = alpha op(A) op(B) + beta C + bias + addend (see dgppo_gemm).  Element offsets/strides.
     bias_grad (ta only): bias_grad = alpha colsum(B) + beta bias_grad, fused into the dW GEMM.
     mask: C = mask > 0 ? result : 0 (the ReLU backward fused into the epilogue, ABI 9 epi 1).
     ln: LayerNorm(64) + ReLU epilogue (epi 2 / 3): dict(mode="fwd" | "bwd", scale, bias, h, mean, rstd,
     dscale, dbias) -- fwd writes h (pre-LN rows), mean, rstd and C = y; bwd reads h, mean, rstd, writes C = dx and
-    accumulates dscale / dbias (per-workgroup partials summed by dgppo_colsum).
-    side (ta only): run on the wgrad_side stream of the current stream, if one is active."""
-    if side and _SIDE:
-        ent = _SIDE.get(torch.cuda.current_stream(C.device).cuda_stream)
-        if ent is not None:
-            st, held = ent
-            st.wait_stream(torch.cuda.current_stream(C.device))
-            with torch.cuda.stream(st):
-                gemm(A, B, C, M, N, K, ta=ta, tb=tb, lda=lda, ldb=ldb, ldc=ldc, batch=batch, sa=sa, sb=sb, sc=sc,
-                     a_off=a_off, b_off=b_off, c_off=c_off, a_grp=a_grp, a_gs=a_gs, b_grp=b_grp, b_gs=b_gs,
-                     c_grp=c_grp, c_gs=c_gs, bias=bias, addend=addend, add_off=add_off, ld_add=ld_add,
-                     add_grp=add_grp, add_gs=add_gs, alpha=alpha, beta=beta, relu=relu, split_k=split_k,
-                     bias_grad=bias_grad, mask=mask, ld_mask=ld_mask, ln=ln)
-            held.append((A, B))
-            return
+    accumulates dscale / dbias (per-workgroup partials summed by dgppo_colsum)."""
     lib = _lib.load()
     _lib.require_gpu(C.device, "gemm")
     g = _lib.GemmArgs()

@@ -160,7 +160,7 @@ class Dense:
     def bwd(self, x, dy, rows, need_dx=True, dx_out=None, accumulate=False, mask=None, ln=None):
         """dW, db += ...; returns dx.  mask: dx = mask > 0 ? dx : 0 (the input's ReLU backward, fused into the dx
         GEMM); ln: the LayerNorm + ReLU backward of the layer that produced x (GEMM epilogue epi 3)."""
-        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0, bias_grad=self.b(True), side=True)
+        K.gemm(x, dy, self.W(True), self.d_in, self.d_out, rows, ta=True, beta=1.0, bias_grad=self.b(True))
         if not need_dx:
             return None
         dx = dx_out if dx_out is not None else torch.empty((rows, self.d_in), device=dy.device)
@@ -336,16 +336,14 @@ class GRUCell:
         part = K.workspace(nb * H, dev, "gru_bhn")
         K.gru_seq(False, Q, L, n, gi, self.v("Wh"), self.v("bhn"), h0, hs, dhs=dhs, dgi=dgi, dgh=dgh, dh0=dh0,
                   dbhn_part=part)
-        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0, bias_grad=self.v("bi", True),
-               side=True)
+        K.gemm(x, dgi, self.v("Wi", True), self.d_in, 3 * H, rows, ta=True, beta=1.0, bias_grad=self.v("bi", True))
         S = Q // n
         if L > 1:  # h_{t-1} of step t >= 1 is hs of step t-1: row-grouped per sequence, B shifted by n rows
             K.gemm(hs, dgh, self.v("Wh", True), H, 3 * H, S * (L - 1) * n, ta=True, lda=H, a_grp=(L - 1) * n,
-                   a_gs=L * n * H, ldb=3 * H, b_off=n * 3 * H, b_grp=(L - 1) * n, b_gs=L * n * 3 * H, beta=1.0,
-                   side=True)
+                   a_gs=L * n * H, ldb=3 * H, b_off=n * 3 * H, b_grp=(L - 1) * n, b_gs=L * n * 3 * H, beta=1.0)
         if h0 is not None:  # step 0 uses the initial carries
             K.gemm(h0, dgh, self.v("Wh", True), H, 3 * H, Q, ta=True, lda=H, ldb=3 * H, b_grp=n,
-                   b_gs=L * n * 3 * H, beta=1.0, side=True)
+                   b_gs=L * n * 3 * H, beta=1.0)
         K.colsum(part, nb, H, self.v("bhn", True), beta=1.0)
         dx = None
         if need_dx:
@@ -455,8 +453,8 @@ class LSTMCell:
         dWh, db = self.v("Wh", True), self.v("b", True)
         for j in (0, 2 * H):  # two 2H-column halves: the weight-gradient kernel (fused bias colsum) takes N <= 192
             K.gemm(hprev, dGf, dWh, H, 2 * H, L * Q, ta=True, ldb=4 * H, b_off=j, ldc=4 * H, c_off=j, beta=1.0,
-                   bias_grad=db[j:j + 2 * H], side=True)
-        K.gemm(xt, dGf, self.v("Wi", True), self.d_in, 4 * H, L * Q, ta=True, beta=1.0, side=True)
+                   bias_grad=db[j:j + 2 * H])
+        K.gemm(xt, dGf, self.v("Wi", True), self.d_in, 4 * H, L * Q, ta=True, beta=1.0)
         dx = None
         if need_dx:
             dxt = torch.empty((L * Q, self.d_in), device=dev)
@@ -680,7 +678,7 @@ class GraphTransformer:
         False): zmean (G, F) receives the per-graph agent mean of Y, and Y is not written; tail = (weights in
         ops.TAIL_FIELDS order, carries (G*n, 64), out (G*n, n_out)) runs the value head after the layer (the return
         value is then (out, None))."""
-        if xa is not None and pre is None:
+        if (xa is not None and pre is None) or self.EX:
             return None
         G, n, D, F, H, C = g.G, g.n, self.D, self.F, self.H, g.C
         R, W = G * n, H * D + H
@@ -791,11 +789,10 @@ class GraphTransformer:
         torch.ops.dgppo.gnn_layer_bwd(*head, dQB, dXa, part)
         if part is not None:
             self._pre_grads(pre, g, part, nb, PK, D0)
-        K.gemm(xcat, dY, self.v("Wcat", True), H * (D + 5), F, R, ta=True, lda=H * (D + 5), alpha=1.0 / H, beta=1.0,
-               side=True)
+        K.gemm(xcat, dY, self.v("Wcat", True), H * (D + 5), F, R, ta=True, lda=H * (D + 5), alpha=1.0 / H, beta=1.0)
         A, akw = self._rows_in(g, xa, None)
-        K.on_side(lambda: self._qfree_grads(A, akw, dQB, R), A, dQB)  # parameter gradients only
-        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), side=True, **akw)
+        self._qfree_grads(A, akw, dQB, R)  # parameter gradients only
+        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
         return True, dXa
 
     def _pre_grads(self, pre, g, part, nb, PK, D0):
@@ -831,9 +828,9 @@ class GraphTransformer:
         K.gemm(Gaug, self.v("bk"), dWaug, D + 1, F, 1, lda=WQ, a_off=HD, sa=1, ldb=F, sb=F, ldc=H * F, sc=F,
                batch=H, beta=1.0)
         K.gemm(Waug, Gaug, self.v("Wkt", True), F, D, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, sb=D, ldc=D,
-               sc=F * D, batch=H, beta=1.0, side=True)
+               sc=F * D, batch=H, beta=1.0)
         K.gemm(Waug, Gaug, self.v("bk", True), F, 1, D + 1, ta=True, lda=H * F, sa=F, ldb=WQ, b_off=HD, sb=1,
-               ldc=1, sc=F, batch=H, beta=1.0, side=True)
+               ldc=1, sc=F, batch=H, beta=1.0)
 
     def bwd(self, cache, dY, g: "GraphBatch", masked=False, mask_dxa=False):
         """dY (G*n, F) is consumed (becomes dZ).  Returns d xa (G*n, D) in agent mode, d xfull (G, N, D)
@@ -857,13 +854,13 @@ class GraphTransformer:
             return dXa
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
-        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0, side=True)
+        K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)
         da_add = None
         if self.EX:
             WX = H * self.EX
             dxx = torch.empty((R, WX), device=dev)
             K.gemm(dY, self.v("Wex"), dxx, R, WX, F, tb=True, ldb=F, alpha=1.0 / H)
-            K.gemm(xcx, dY, self.v("Wex", True), WX, F, R, ta=True, lda=WX, alpha=1.0 / H, beta=1.0, side=True)
+            K.gemm(xcx, dY, self.v("Wex", True), WX, F, R, ta=True, lda=WX, alpha=1.0 / H, beta=1.0)
             da_add = torch.empty((R, H, C), device=dev)
             K.edge_da(G, n, C, H, self.EX, g.E, dxx, g.cand, g.sidx, g.edges_x, da_add)
         dQB = torch.empty((R, WQ), device=dev)  # [dqt | dbeta]
@@ -880,8 +877,8 @@ class GraphTransformer:
                                      dbeta_ld=WQ, dx=dXf, dx_gstride=N * D)
         if part is not None:
             self._pre_grads(pre, g, part, nb, PK, args["dims"][8])
-        K.on_side(lambda: self._qfree_grads(A, akw, dQB, R), A, dQB)  # parameter gradients only
-        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), side=True, **akw)
+        self._qfree_grads(A, akw, dQB, R)  # parameter gradients only
+        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
         if dXa is not None:
             K.gemm(dY, self.v("Wu"), dXa, R, D, F, tb=True, ldb=F, beta=1.0)
             K.gemm(dQB, QBW, dXa, R, D, WQ, tb=True, ldb=WQ, beta=1.0,  # d[qt | beta] / dx = QBW[:D]^T
@@ -1021,14 +1018,15 @@ class GNN:
         """Forward only, with the last layer's fused epilogue (GraphTransformer._fused_fwd: zmean = the agent mean of
         its output, tail = the value head): the epilogue's output, or None where the fused kernels do not cover the
         stack (the caller then runs fwd() and the unfused head)."""
-        if not FUSED_LAYER or len(self.layers) > 2:
+        # 10-wide edges (EX > 0) need the edge_wsum term the fused kernel does not add: decline before launching
+        if not FUSED_LAYER or len(self.layers) > 2 or any(L.EX for L in self.layers):
             return None
         Y = None
         for i, L in enumerate(self.layers):
             last = i == len(self.layers) - 1
             kw = dict(zmean=zmean, tail=tail) if last else {}
             out = L._fused_fwd(g, Y if i else None, self.layers[0] if i else None, False, **kw)
-            if out is None or L.EX:
+            if out is None:
                 return None
             Y = out[0]
         return Y

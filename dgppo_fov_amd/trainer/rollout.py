@@ -156,7 +156,7 @@ class RolloutEngine:
         """Record reset + T x (actor, step) into one hipGraph (after one eager warm-up run)."""
         self._run()
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
+        g = K.hold_for_graph(torch.cuda.CUDAGraph())
         with torch.cuda.graph(g):
             self._run()
         self._hip_graph = g

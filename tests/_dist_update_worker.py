@@ -25,15 +25,30 @@ def host(r):
                 dones=r.dones.cpu().clone(), log_pis=None if r.log_pis is None else r.log_pis.cpu().clone())
 
 
-def graph_mode(out, knob):
+def graph_mode(out, knob, backend="gloo"):
     """Two collect + update iterations of 2 minibatches each with the parity trace OFF and DGPPO_UPDATE_GRAPH=knob
     (1: minibatch hipGraph replays with the eager flat all-reduce between them, 0: eager per-net buckets); saves
-    the parameters and Adam state of every net."""
+    the parameters and Adam state of every net.  backend "nccl" (RCCL) at world size 1 forces the collectives
+    (DGPPO_FORCE_ALLREDUCE=1) and counts them; backend "none" runs without a process group (the no-reduce path)."""
     os.environ["DGPPO_UPDATE_GRAPH"] = knob
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
+    calls = []
+    if backend != "none":
+        if backend == "nccl":
+            os.environ["DGPPO_FORCE_ALLREDUCE"] = "1"
+            dist.init_process_group("nccl", device_id=dev)
+            real = dist.all_reduce
+
+            def counted(t, *a, **k):
+                calls.append(int(t.numel()))
+                return real(t, *a, **k)
+
+            dist.all_reduce = counted
+        else:
+            dist.init_process_group("gloo")
+    rank = dist.get_rank() if backend != "none" else 0
+    world = dist.get_world_size() if backend != "none" else 1
     env = make_env(ENV, N, num_obs=OBS, max_step=T, device=dev)
     algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
                      action_dim=env.action_dim, n_agents=N, batch_size=B_LOCAL * T * world // 2, rnn_step=L,
@@ -43,16 +58,24 @@ def graph_mode(out, knob):
         algo.update(roll, it)
     torch.cuda.synchronize()
     assert (algo._mbg is not None) == (knob == "1")
+    if backend == "nccl":
+        assert dist.get_backend() == "nccl" and algo._reduce and calls, calls
+        print(f"nccl all_reduce calls: {len(calls)} sizes {sorted(set(calls))}", flush=True)
+    tag = "" if backend == "gloo" else backend
     torch.save({k: dict(p=o.ps.flat.cpu().clone(), m=o.m.cpu().clone(), v=o.v.cpu().clone(),
                         state=o.state.cpu().clone()) for k, o in algo.opt.items()},
-               os.path.join(out, f"graph{knob}_rank{rank}.pt"))
-    dist.barrier()
-    dist.destroy_process_group()
+               os.path.join(out, f"{tag}graph{knob}_rank{rank}.pt"))
+    if backend != "none":
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main(out, algo_name="dgppo"):
     if algo_name.startswith("graph"):
         return graph_mode(out, algo_name[5:])
+    for backend in ("nccl", "none"):
+        if algo_name.startswith(backend + "graph"):
+            return graph_mode(out, algo_name[len(backend) + 5:], backend)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")

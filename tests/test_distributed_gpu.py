@@ -37,6 +37,7 @@ def _run_ranks(tmp_path, mode, world=2):
     for p in procs:
         out, _ = p.communicate(timeout=150)
         assert p.returncode == 0, out.decode()[-3000:]
+        print(out.decode()[-400:])
 
 
 def test_two_rank_minibatch_graphs_match_eager(cuda, tmp_path):
@@ -53,6 +54,22 @@ def test_two_rank_minibatch_graphs_match_eager(cuda, tmp_path):
             assert torch.equal(g1[net][f], g1b[net][f]), (net, f, "ranks differ")
             assert torch.equal(g1[net][f], e1[net][f]), (net, f, "graph replay vs eager")
     assert not torch.equal(g1["policy"]["m"], torch.zeros_like(g1["policy"]["m"]))
+
+
+def test_rccl_world1_reduce_paths_bit_identical(cuda, tmp_path):
+    """RCCL executed before any 8-GPU run.  A world-size-1 `nccl` (RCCL) process group with the
+    collectives forced on (DGPPO_FORCE_ALLREDUCE=1): the eager path's per-net bucketed async all-reduce + the
+    safe-data reduce, and the graph path's flat all-reduce issued eagerly between the two minibatch-graph replays.
+    Each is bit-identical to the same run without a process group (no reduce at all)."""
+    for mode in ("ncclgraph1", "ncclgraph0", "nonegraph1", "nonegraph0"):
+        _run_ranks(tmp_path, mode, world=1)
+    ld = lambda f: torch.load(os.path.join(tmp_path, f), weights_only=True)  # noqa: E731
+    for knob in ("0", "1"):
+        a, b = ld(f"ncclgraph{knob}_rank0.pt"), ld(f"nonegraph{knob}_rank0.pt")
+        for net in a:
+            for f in ("p", "m", "v", "state"):
+                assert torch.equal(a[net][f], b[net][f]), (knob, net, f)
+        assert not torch.equal(a["policy"]["m"], torch.zeros_like(a["policy"]["m"]))
 
 
 @pytest.mark.parametrize("algo_name", ["dgppo", "informarl_lagr"])

@@ -133,12 +133,14 @@ def test_forward_only_epilogues_match_unfused(cuda, eid, n, obs):
     from dgppo_fov_amd.algo.module import nets
 
     zf = vl.graph_means(g)
+    # the fused epilogues really ran (a silent None would compare the unfused chain with itself)
+    assert vl.gnn.fwd_epilogue(g, zmean=torch.empty_like(zf)) is not None
     old_tail, nets.VH_TAIL = nets.VH_TAIL, True
     try:
         vf, cf = vh.fwd(g, h, keep_cache=False)
     finally:
         nets.VH_TAIL = old_tail
-    assert cf is None
+    assert cf is None and vh.last_tail
     old = layers.FUSED_LAYER
     layers.FUSED_LAYER = False
     try:
@@ -148,3 +150,23 @@ def test_forward_only_epilogues_match_unfused(cuda, eid, n, obs):
         layers.FUSED_LAYER = old
     _close(zf, zu, f"{eid} Vl agent means")
     _close(vf, vu, f"{eid} Vh", rtol=1e-4, atol=1e-5)
+
+
+def test_forward_only_epilogue_declines_wide_edges(cuda):
+    """on 10-wide-edge envs (LidarOmniTarget) the fused epilogue declines BEFORE launching anything
+    (its kernel has no edge_wsum term), and the forward-only agent means equal the unfused chain's."""
+    from dgppo_fov_amd.algo.module.nets import VlNet
+
+    env, g = _batch(cuda, "LidarOmniTarget", 8, 3)
+    vl = VlNet(env.node_dim, 8, cuda, seed=6, edge_dim=env.edge_dim)
+    zm = torch.full((g.G, 64), 7.0, device=cuda)
+    assert vl.gnn.fwd_epilogue(g, zmean=zm) is None
+    assert bool((zm == 7.0).all())  # nothing was launched into zmean
+    zf = vl.graph_means(g)
+    old = layers.FUSED_LAYER
+    layers.FUSED_LAYER = False
+    try:
+        zu = vl.graph_means(g)
+    finally:
+        layers.FUSED_LAYER = old
+    assert torch.equal(zf, zu)

@@ -16,16 +16,19 @@ import yaml
 RESUME_FREE = ("resume", "max_minutes", "log_interval", "gpu", "debug", "log_dir", "name")
 
 
-def check_resume_args(args, log_dir):
+def check_resume_args(args, log_dir, world=None):
     """--resume continues a run with ITS hyperparameters: refuse a command line whose flags differ from the ones the
-    run started with (saved as train_args.json next to config.yaml), except the resume-only flags."""
+    run started with (saved as train_args.json next to config.yaml), except the resume-only flags.  The world size
+    (saved as "_world_size") scales the batch size and the env sharding, so a different one is refused too."""
     path = os.path.join(log_dir, "train_args.json")
     if not os.path.exists(path):
         print(f"> warning: {path} missing (run started before it was written); flags not checked")
         return
     with open(path) as f:
         saved = json.load(f)
-    cur = vars(args)
+    cur = dict(vars(args))
+    cur["_world_size"] = int(os.environ.get("WORLD_SIZE", "1")) if world is None else int(world)
+    saved.setdefault("_world_size", 1)  # runs saved before the world size was recorded ran on one GPU
     diff = {k: (saved[k], cur.get(k)) for k in saved if k not in RESUME_FREE and saved[k] != cur.get(k)}
     if diff:
         raise SystemExit("--resume: flags differ from the run's own (saved, given): " +
@@ -103,7 +106,7 @@ def train(args):
             yaml.safe_dump(vars(args), f)
             yaml.safe_dump(algo.config, f)
         with open(f"{log_dir}/train_args.json", "w") as f:
-            json.dump(vars(args), f)
+            json.dump(dict(vars(args), _world_size=world), f)
     done = trainer.train()
     if world > 1:
         dist.destroy_process_group()
