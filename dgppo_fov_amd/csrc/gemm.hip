@@ -752,17 +752,38 @@ __host__ __device__ inline int wgrad_chunks(int64_t K, int min_rows = kWMinRows,
   return c < 1 ? 1 : (int)c;
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const float* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float wg_load(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
 // workspace layout: [batch][chunk][M*N + N]; U row pairs of loads in flight per wave.  Every load is unconditional --
 // the row clamped into the chunk, the column into the matrix, out-of-range values zeroed by a select -- so a row
 // pair's loads issue back to back (guarded loads each sat behind a branch and a 64-bit row division, which made the
 // loop issue-bound: SALU ~ VALU instructions, PMC); FLAT (no row grouping) addresses rows as k * ld, grouped rows
 // with 32-bit arithmetic.
-template <int MT, int NT, int U, bool FLAT>
+template <int MT, int NT, int U, bool FLAT, bool PIPE>
 __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
   constexpr int CP = NT * 32 + 1;
-  const int c = blockIdx.x;
-  const int gm = blockIdx.y / ngroups_n, gn = blockIdx.y % ngroups_n;
+  // one 1-D grid of chunks x tile groups: the G tile groups of a chunk read the same rows (each its own columns),
+  // so they are dispatched back to back on ONE XCD (workgroups go round-robin over the 8 XCDs: linear id L runs on
+  // XCD L % 8) and the later groups' reads hit that XCD's L2 instead of HBM.  Needs chunks % 8 == 0 (the launcher
+  // rounds), else chunk-major order.
+  const int G = gridDim.x / chunks;
+  const int L = blockIdx.x;
+  int c, grp;
+  if ((chunks & 7) == 0) {
+    const int j = L >> 3;
+    c = 8 * (j / G) + (L & 7);
+    grp = j - (j / G) * G;
+  } else {
+    c = L / G;
+    grp = L - c * G;
+  }
+  const int gm = grp / ngroups_n, gn = grp % ngroups_n;
   const int b = blockIdx.z;
   const int m0 = gm * MT * 32, n0 = gn * NT * 32;
   const int M = p.M, N = p.N;
@@ -772,7 +793,7 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
   const int64_t r1 = r0 + rpc < K ? r0 + rpc : K;
   const float* A = p.A + (int64_t)b * p.stride_a;
   const float* B = p.B + (int64_t)b * p.stride_b;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = lane & 31, h = lane >> 5;
   const bool do_bias = p.bias_grad != nullptr && gm == 0;
   f32x16 acc[MT][NT];
@@ -795,43 +816,53 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
   for (int mt = 0; mt < MT; ++mt) mcol[mt] = mok[mt] ? m0 + mt * 32 + i : 0;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) ncol[nt] = nok[nt] ? n0 + nt * 32 + i : 0;
-  // row pairs (2q, 2q+1) of the chunk, interleaved over the waves; lane half h takes row 2q + h
-  for (int64_t k0 = r0 + 2 * wave; k0 < r1; k0 += 2 * kWWaves * U) {
-    float a[U][MT], bb[U][NT];
-    if constexpr (true) {  // every load of the U row pairs first, then the selects (one wait for all of them)
+  // row pairs (2q, 2q+1) of the chunk, interleaved over the waves; lane half h takes row 2q + h.  A stage = U row
+  // pairs: every load first (clamped, unconditional), then the selects and MFMAs (one wait for all of them)
+  // FLAT: each row pair is read through a buffer resource based at its first row (wave-uniform, SGPRs) with the
+  // lane's 32-bit offset (h * ld + column): no per-lane 64-bit addresses, and a row past the matrix end reads 0
+  int offA[MT], offB[NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) offA[mt] = 4 * (h * p.lda + mcol[mt]);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) offB[nt] = 4 * (h * p.ldb + ncol[nt]);
+  auto issue = [&](float (&a)[U][MT], float (&bb)[U][NT], int64_t kb) {
+    if constexpr (FLAT) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t k = k0 + 2 * kWWaves * u + h;
-        const int64_t kc = k < r1 ? k : r0;
-        // grouped rows: 32-bit row arithmetic (K < 2^31), one division per row instead of row_off64's 64-bit one
-        const float* Ar = A + (FLAT ? kc * p.lda : row_off((int)kc, p.lda, p.a_grp, p.a_gstride));
-        const float* Br = B + (FLAT ? kc * p.ldb : row_off((int)kc, p.ldb, p.b_grp, p.b_gstride));
+        const int64_t k0 = kb + 2 * kWWaves * u;  // wave-uniform
+        const int64_t ku = k0 < r1 ? k0 : r0;
+        const int64_t left = K - ku;
+        const int64_t ba = left * p.lda * 4, bbn = left * p.ldb * 4;
+        const auto ra = wg_rsrc(A + ku * p.lda, ba < 0x7FFFFFFF ? (int)ba : 0x7FFFFFFF);
+        const auto rb = wg_rsrc(B + ku * p.ldb, bbn < 0x7FFFFFFF ? (int)bbn : 0x7FFFFFFF);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) a[u][mt] = Ar[mcol[mt]];
+        for (int mt = 0; mt < MT; ++mt) a[u][mt] = wg_load(ra, offA[mt]);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = Br[ncol[nt]];
+        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = wg_load(rb, offB[nt]);
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool kok = k0 + 2 * kWWaves * u + h < r1;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? a[u][mt] : 0.0f;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? bb[u][nt] : 0.0f;
-      }
+      return;
     }
 #pragma unroll
-    for (int u = 0; u < 0; ++u) {  // (the guarded form, kept for reference: no longer instantiated)
-      const int64_t k = k0 + 2 * kWWaves * u + h;
-      const bool kok = k < r1;
-      {
-        const float* Ar = A + (kok ? row_off64(k, p.lda, p.a_grp, p.a_gstride) : 0) + m0 + i;
-        const float* Br = B + (kok ? row_off64(k, p.ldb, p.b_grp, p.b_gstride) : 0) + n0 + i;
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = kb + 2 * kWWaves * u + h;
+      const int64_t kc = k < r1 ? k : r0;
+      // grouped rows: 32-bit row arithmetic (K < 2^31), one division per row instead of row_off64's 64-bit one
+      const float* Ar = A + (FLAT ? kc * p.lda : row_off((int)kc, p.lda, p.a_grp, p.a_gstride));
+      const float* Br = B + (FLAT ? kc * p.ldb : row_off((int)kc, p.ldb, p.b_grp, p.b_gstride));
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? Ar[mt * 32] : 0.0f;
+      for (int mt = 0; mt < MT; ++mt) a[u][mt] = Ar[mcol[mt]];
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? Br[nt * 32] : 0.0f;
-      }
+      for (int nt = 0; nt < NT; ++nt) bb[u][nt] = Br[ncol[nt]];
+    }
+  };
+  auto consume = [&](float (&a)[U][MT], float (&bb)[U][NT], int64_t kb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool kok = kb + 2 * kWWaves * u + h < r1;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a[u][mt] = (kok && mok[mt]) ? a[u][mt] : 0.0f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bb[u][nt] = (kok && nok[nt]) ? bb[u][nt] : 0.0f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -843,6 +874,33 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
       if (do_bias)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) bs[nt] += bb[u][nt];
+    }
+  };
+  constexpr int64_t S = 2 * kWWaves * U;  // rows one stage advances
+  if constexpr (PIPE) {
+    // two register stages: the next stage's loads are in flight while this stage's MFMAs run (without it each
+    // stage waited for its own loads: the kernel was load-latency-bound, ~30% MFMA busy on M64 N192).  Same row
+    // order as the single-stage loop; a stage past the chunk end loads clamped rows and adds zeros.
+    float a0[U][MT], b0[U][NT], a1[U][MT], b1[U][NT];
+    int64_t kb = r0 + 2 * wave;
+    if (kb < r1) issue(a0, b0, kb);
+    for (; kb < r1; kb += 2 * S) {
+      issue(a1, b1, kb + S);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(a0, b0, kb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kb + S < r1) {
+        issue(a0, b0, kb + 2 * S);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(a1, b1, kb + S);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
+    for (int64_t k0 = r0 + 2 * wave; k0 < r1; k0 += S) {
+      float a[U][MT], bb[U][NT];
+      issue(a, bb, k0);
+      consume(a, bb, k0);
     }
   }
   // combine the 8 wave partials in LDS, fixed order
@@ -958,9 +1016,15 @@ int wgrad_max_chunks() {
   static int v = env_knob("DGPPO_WGRAD_MAXCHUNKS", 256);
   return v;
 }
+// two register stages in the wgrad loop (loads of the next U row pairs in flight under this stage's MFMAs);
+// DGPPO_WGRAD_PIPE=0: the single-stage loop
+int wgrad_pipe() {
+  static int v = env_knob("DGPPO_WGRAD_PIPE", 1);
+  return v;
+}
 int wgrad_unroll() {  // default 4 with the branch-free loads: M64 N192 66.9 -> 64.2 us, update 179.8 -> 178.6 ms
   static int v = env_knob("DGPPO_WGRAD_U", 4);
-  return v == 4 ? 4 : 2;
+  return v == 8 ? 8 : (v == 4 ? 4 : 2);
 }
 
 
@@ -973,6 +1037,12 @@ GemmPath gemm_path(const dgppo_gemm_args* p) {
     if (((p->K + 15) & ~15) * (32 * nt + 1) <= dgppo::kRowsLdsFloats) return kPathRows;
   }
   return kPathTile;
+}
+
+// row chunks of a wgrad call: whole groups of 8 above 8 (the kernel's XCD-aware order; fewer chunks, more rows each)
+int wgrad_chunk_count(int64_t K) {
+  int chunks = dgppo::wgrad_chunks(K, wgrad_min_rows(), wgrad_max_chunks());
+  return chunks > 8 ? (chunks & ~7) : chunks;
 }
 
 // (MT, NT) tile-group shape for the wgrad kernel: MT * NT <= 12 accumulators of 16 per lane
@@ -1000,15 +1070,31 @@ template <int MT, int NT>
 void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
   const int gm = (p->M + MT * 32 - 1) / (MT * 32), gn = (p->N + NT * 32 - 1) / (NT * 32);
   const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
-  const dim3 grid(chunks, gm * gn, p->batch);
+  const dim3 grid(chunks * gm * gn, 1, p->batch);
   const bool flat = p->a_grp <= 0 && p->b_grp <= 0;
-  if (wgrad_unroll() == 4 && MT * NT <= 4) {
-    if (flat) hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 4, true>), grid, dim3(512), lds, s, *p, chunks, gn);
-    else hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 4, false>), grid, dim3(512), lds, s, *p, chunks, gn);
+#define DG_WL(U, FL, PP) \
+  hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, U, FL, PP>), grid, dim3(512), lds, s, *p, chunks, gn)
+  const bool pipe = wgrad_pipe();
+  if (wgrad_unroll() == 8 && MT * NT <= 4 && flat && pipe) {
+    DG_WL(8, true, true);
+  } else if (wgrad_unroll() >= 4 && MT * NT <= 4) {
+    if (pipe) {
+      if (flat) DG_WL(4, true, true);
+      else DG_WL(4, false, true);
+    } else {
+      if (flat) DG_WL(4, true, false);
+      else DG_WL(4, false, false);
+    }
   } else {
-    if (flat) hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 2, true>), grid, dim3(512), lds, s, *p, chunks, gn);
-    else hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, 2, false>), grid, dim3(512), lds, s, *p, chunks, gn);
+    if (pipe) {
+      if (flat) DG_WL(2, true, true);
+      else DG_WL(2, false, true);
+    } else {
+      if (flat) DG_WL(2, true, false);
+      else DG_WL(2, false, false);
+    }
   }
+#undef DG_WL
 }
 
 int launch_wgrad(const dgppo_gemm_args* p0, hipStream_t s) {
@@ -1019,7 +1105,7 @@ int launch_wgrad(const dgppo_gemm_args* p0, hipStream_t s) {
   const dgppo_gemm_args* p = &q;
   int MT, NT;
   wgrad_shape(p->M, p->N, &MT, &NT);
-  const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows(), wgrad_max_chunks());
+  const int chunks = wgrad_chunk_count(p->K);
   if (chunks > 1 && !p->workspace) return DGPPO_EINVAL;
 #define DG_W(a, b) \
   if (MT == a && NT == b) { launch_wgrad_t<a, b>(p, chunks, s); goto launched; }
@@ -1171,7 +1257,7 @@ extern "C" int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* p) {
   if (!p) return 0;
   switch (gemm_path(p)) {
     case kPathWgrad: {
-      const int chunks = dgppo::wgrad_chunks(p->K, wgrad_min_rows(), wgrad_max_chunks());
+      const int chunks = wgrad_chunk_count(p->K);
       return chunks > 1 ? (int64_t)chunks * p->batch * ((int64_t)p->M * p->N + p->N) : 0;
     }
     case kPathRows:
