@@ -294,6 +294,8 @@ SIGNATURES = {
     "dgppo_env_reset_states": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvResetIO), ctypes.c_void_p]),
     "dgppo_env_rollout": (ctypes.c_int, [ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvRolloutIO), ctypes.c_void_p]),
     "dgppo_gemm_workspace_floats": (ctypes.c_int64, [ctypes.POINTER(GemmArgs)]),
+    "dgppo_gemm_wgrad_grouped_workspace_floats": (ctypes.c_int64, [ctypes.POINTER(GemmArgs), ctypes.c_int]),
+    "dgppo_gemm_wgrad_grouped": (ctypes.c_int, [ctypes.POINTER(GemmArgs), ctypes.c_int, c_f32p, ctypes.c_void_p]),
     "dgppo_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), ctypes.c_void_p]),
     "dgppo_gnn_attn_fwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
     "dgppo_gnn_attn_bwd": (ctypes.c_int, [ctypes.POINTER(GnnAttnArgs), ctypes.c_void_p]),
@@ -352,7 +354,7 @@ SIGNATURES = {
 _LIB = None
 
 
-ABI_VERSION = 12  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 13  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

@@ -70,6 +70,13 @@ def ADAM_MULTI() -> bool:
     return os.environ.get("DGPPO_ADAM_MULTI", "1") == "1"
 
 
+def DEFER_WGRAD() -> bool:
+    """Each net's weight-gradient GEMMs deferred to the end of its backward and launched as one grouped kernel
+    (K.defer_wgrad, dgppo_gemm_wgrad_grouped): bit-identical, fewer launches (DGPPO_DEFER_WGRAD=0: one launch pair
+    per GEMM)."""
+    return os.environ.get("DGPPO_DEFER_WGRAD", "1") == "1"
+
+
 def FORCE_SAFE() -> bool:
     """Learning-dynamics ablation (scripts/learn_ablate.sh): treat every sample as inside the safe set."""
     return os.environ.get("DGPPO_DEBUG_FORCE_SAFE", "0") == "1"
@@ -575,7 +582,8 @@ class DGPPO:
             loss = torch.empty(1, device=dev)
             K.l2_loss(v, tgt, dv, loss)
             ph.mark("Vl_fwd")
-            self.Vl.seq_bwd(cache, dv)
+            with K.defer_wgrad(dev, self.Vl.ps.grad, DEFER_WGRAD()):
+                self.Vl.seq_bwd(cache, dv)
             self._start_reduce(self.Vl, pending)  # the bucket's all-reduce overlaps the other passes
             ph.mark("Vl_bwd")
             return loss
@@ -586,7 +594,8 @@ class DGPPO:
             loss = torch.empty(1, device=dev)
             K.l2_loss(vh, qhd.view(-1, env.n_cost), dvh, loss)
             ph.mark("Vh_fwd")
-            self.Vh.bwd(cache, dvh)
+            with K.defer_wgrad(dev, self.Vh.ps.grad, DEFER_WGRAD()):
+                self.Vh.bwd(cache, dvh)
             self._start_reduce(self.Vh, pending)
             ph.mark("Vh_bwd")
             return loss
@@ -598,7 +607,8 @@ class DGPPO:
             st = torch.empty(4, device=dev)
             K.ppo_loss(lp, lp_old, adv, ent, self.clip_eps, self.coef_ent, dlp, dent, st)
             ph.mark("pi_fwd")
-            self.actor.eval_seq_bwd(cache, dlp, dent)
+            with K.defer_wgrad(dev, self.actor.ps.grad, DEFER_WGRAD()):
+                self.actor.eval_seq_bwd(cache, dlp, dent)
             self._start_reduce(self.actor, pending)
             ph.mark("pi_bwd")
             return st

@@ -764,17 +764,30 @@ __device__ __forceinline__ float wg_load(__amdgpu_buffer_rsrc_t r, int byte_off)
 // pair's loads issue back to back (guarded loads each sat behind a branch and a 64-bit row division, which made the
 // loop issue-bound: SALU ~ VALU instructions, PMC); FLAT (no row grouping) addresses rows as k * ld, grouped rows
 // with 32-bit arithmetic.
-template <int MT, int NT, int U, bool FLAT, bool PIPE>
-__global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
-  constexpr int CP = NT * 32 + 1;
-  // one 1-D grid of chunks x tile groups: the G tile groups of a chunk read the same rows (each its own columns),
-  // so they are dispatched back to back on ONE XCD (workgroups go round-robin over the 8 XCDs: linear id L runs on
-  // XCD L % 8) and the later groups' reads hit that XCD's L2 instead of HBM.  Needs chunks % 8 == 0 (the launcher
-  // rounds), else chunk-major order.
-  const int G = gridDim.x / chunks;
-  const int L = blockIdx.x;
-  int c, grp;
+// one wgrad problem of a grouped launch (dgppo_gemm_wgrad_grouped): the dgppo_gemm_args fields the kernel reads
+struct WgradEntry {
+  const float* A;
+  const float* B;
+  float* C;
+  float* bias_grad;
+  float* workspace;
+  int64_t lda, ldb, ldc, stride_a, stride_b, stride_c, a_gstride, b_gstride, c_gstride;
+  int32_t a_grp, b_grp, c_grp, M, N, K, batch, chunks, ngroups_n;
+  float alpha, beta;
+};
+constexpr int kWgradGroupMax = 12;
+struct WgradGroup {
+  int32_t n;
+  int32_t wg_begin[kWgradGroupMax + 1];   // workgroups of the wgrad kernel per entry (prefix)
+  int32_t red_begin[kWgradGroupMax + 1];  // 32-element blocks of the reduce kernel per entry (prefix)
+  WgradEntry e[kWgradGroupMax];
+};
+
+// chunk c and tile group grp of workgroup L of one problem (G tile groups): the G tile groups of a chunk read the
+// same rows (each its own columns), so they are dispatched back to back on ONE XCD (workgroups go round-robin over
+// the 8 XCDs: linear id L runs on XCD L % 8) and the later groups' reads hit that XCD's L2 instead of HBM.  Needs
+// chunks % 8 == 0 (the launcher rounds), else chunk-major order.
+__device__ __forceinline__ void wgrad_place(int L, int chunks, int G, int& c, int& grp) {
   if ((chunks & 7) == 0) {
     const int j = L >> 3;
     c = 8 * (j / G) + (L & 7);
@@ -783,8 +796,12 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
     c = L / G;
     grp = L - c * G;
   }
+}
+
+template <int MT, int NT, int U, bool FLAT, bool PIPE, class P>
+__device__ __forceinline__ void wgrad_body(const P& p, int chunks, int ngroups_n, int c, int grp, int b, float* red) {
+  constexpr int CP = NT * 32 + 1;
   const int gm = grp / ngroups_n, gn = grp % ngroups_n;
-  const int b = blockIdx.z;
   const int m0 = gm * MT * 32, n0 = gn * NT * 32;
   const int M = p.M, N = p.N;
   const int64_t K = p.K;
@@ -957,15 +974,46 @@ __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int 
   }
 }
 
+template <int MT, int NT, int U, bool FLAT, bool PIPE>
+__global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
+  int c, grp;
+  wgrad_place(blockIdx.x, chunks, gridDim.x / chunks, c, grp);
+  wgrad_body<MT, NT, U, FLAT, PIPE>(p, chunks, ngroups_n, c, grp, blockIdx.z, red);
+}
+
+// several wgrad problems in ONE launch (a network pass's weight gradients, deferred to the end of its backward):
+// workgroup -> (problem, batch entry, chunk, tile group) from the prefix table; per problem the same chunking,
+// tile order and fixed-order sums as its own launch, so every output is bit-identical to gemm_wgrad_kernel's
+template <int MT, int NT>
+__global__ __launch_bounds__(512) void gemm_wgrad_grouped_kernel(WgradGroup g) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int L = blockIdx.x;
+  int k = 0;
+  for (int q = 1; q < g.n; ++q) k = L >= g.wg_begin[q] ? q : k;
+  const WgradEntry& p = g.e[k];
+  const int G = ((p.M + MT * 32 - 1) / (MT * 32)) * p.ngroups_n;
+  const int per_b = p.chunks * G;
+  const int Lk = L - g.wg_begin[k];
+  const int b = Lk / per_b;
+  int c, grp;
+  wgrad_place(Lk - b * per_b, p.chunks, G, c, grp);
+  if (p.a_grp <= 0 && p.b_grp <= 0)
+    wgrad_body<MT, NT, 4, true, true>(p, p.chunks, p.ngroups_n, c, grp, b, red);
+  else
+    wgrad_body<MT, NT, 4, false, true>(p, p.chunks, p.ngroups_n, c, grp, b, red);
+}
+
 // chunk partials -> C / bias_grad: 32 output elements per block, 8 chunk subsets each (coalesced
 // over elements), combined in LDS in fixed order
-__global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int chunks) {
+template <class P>
+__device__ __forceinline__ void wgrad_reduce_body(const P& p, int chunks, int64_t blk) {
   __shared__ float red[8][33];
   const int64_t MN = (int64_t)p.M * p.N;
   const int64_t slab = MN + p.N;
   const int64_t total = slab * p.batch;
   const int j = threadIdx.x >> 5;
-  const int64_t t = (int64_t)blockIdx.x * 32 + (threadIdx.x & 31);
+  const int64_t t = blk * 32 + (threadIdx.x & 31);
   const int b = (int)(t / slab);
   const int64_t e = t - (int64_t)b * slab;
   const bool ok = t < total && (e < MN || p.bias_grad);
@@ -989,6 +1037,18 @@ __global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int 
     }
     *dst = p.alpha * v + (p.beta != 0.0f ? p.beta * *dst : 0.0f);
   }
+}
+
+__global__ __launch_bounds__(256) void gemm_wgrad_reduce(dgppo_gemm_args p, int chunks) {
+  wgrad_reduce_body(p, chunks, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void gemm_wgrad_grouped_reduce(WgradGroup g) {
+  const int L = blockIdx.x;
+  int k = 0;
+  for (int q = 1; q < g.n; ++q) k = L >= g.red_begin[q] ? q : k;
+  if (g.e[k].chunks <= 1) return;
+  wgrad_reduce_body(g.e[k], g.e[k].chunks, L - g.red_begin[k]);
 }
 
 }  // namespace dgppo
@@ -1293,6 +1353,70 @@ extern "C" int dgppo_gemm(const dgppo_gemm_args* p, void* stream) {
     const int64_t nb = (total + 255) / 256;
     const int blocks = (int)(nb < 4096 ? nb : 4096);
     hipLaunchKernelGGL(dgppo::gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, *p);
+  }
+  return (int)hipGetLastError();
+}
+
+// ---- grouped weight gradients (ABI 13) ---------------------------------------------------------------------------
+namespace {
+bool wgrad_grouped_ok(const dgppo_gemm_args* p) {
+  return p->M >= 1 && p->N >= 1 && p->K >= 0 && p->batch >= 1 && p->A && p->B && p->C && p->trans_a && !p->trans_b &&
+         gemm_path(p) == kPathWgrad && !p->epi;
+}
+int64_t wgrad_grouped_floats(const dgppo_gemm_args* p) {
+  const int chunks = wgrad_chunk_count(p->K);
+  return chunks > 1 ? (int64_t)chunks * p->batch * ((int64_t)p->M * p->N + p->N) : 0;
+}
+}  // namespace
+
+extern "C" int64_t dgppo_gemm_wgrad_grouped_workspace_floats(const dgppo_gemm_args* args, int n) {
+  if (!args || n < 0) return 0;
+  int64_t t = 0;
+  for (int k = 0; k < n; ++k) t += wgrad_grouped_floats(args + k);
+  return t;
+}
+
+extern "C" int dgppo_gemm_wgrad_grouped(const dgppo_gemm_args* args, int n, float* workspace, void* stream) {
+  if (!args || n < 0) return DGPPO_EINVAL;
+  for (int k = 0; k < n; ++k)
+    if (!wgrad_grouped_ok(args + k)) return DGPPO_EINVAL;
+  if (dgppo_gemm_wgrad_grouped_workspace_floats(args, n) > 0 && !workspace) return DGPPO_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int MT = 2, NT = 2;
+  const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
+  int64_t off = 0;
+  for (int k0 = 0; k0 < n; k0 += dgppo::kWgradGroupMax) {
+    dgppo::WgradGroup g{};
+    g.n = n - k0 < dgppo::kWgradGroupMax ? n - k0 : dgppo::kWgradGroupMax;
+    int64_t wg = 0, rb = 0;
+    for (int q = 0; q < g.n; ++q) {
+      const dgppo_gemm_args& a = args[k0 + q];
+      dgppo::WgradEntry& e = g.e[q];
+      e.A = a.A, e.B = a.B, e.C = a.C, e.bias_grad = a.bias_grad;
+      e.lda = a.lda, e.ldb = a.ldb, e.ldc = a.ldc;
+      e.stride_a = a.stride_a, e.stride_b = a.stride_b, e.stride_c = a.stride_c;
+      // a grouping whose group stride is grp rows is the plain row layout (the flat kernel's addressing)
+      e.a_grp = (a.a_grp > 0 && a.a_gstride == (int64_t)a.a_grp * a.lda) ? 0 : a.a_grp;
+      e.b_grp = (a.b_grp > 0 && a.b_gstride == (int64_t)a.b_grp * a.ldb) ? 0 : a.b_grp;
+      e.c_grp = a.c_grp;
+      e.a_gstride = a.a_gstride, e.b_gstride = a.b_gstride, e.c_gstride = a.c_gstride;
+      e.M = a.M, e.N = a.N, e.K = a.K, e.batch = a.batch;
+      e.alpha = a.alpha, e.beta = a.beta;
+      e.chunks = wgrad_chunk_count(a.K);
+      e.ngroups_n = (a.N + NT * 32 - 1) / (NT * 32);
+      const int G = ((a.M + MT * 32 - 1) / (MT * 32)) * e.ngroups_n;
+      e.workspace = e.chunks > 1 ? workspace + off : nullptr;
+      off += wgrad_grouped_floats(&a);
+      g.wg_begin[q] = (int32_t)wg;
+      g.red_begin[q] = (int32_t)rb;
+      wg += (int64_t)a.batch * e.chunks * G;
+      if (e.chunks > 1) rb += ((int64_t)a.batch * ((int64_t)a.M * a.N + a.N) + 31) / 32;
+    }
+    g.wg_begin[g.n] = (int32_t)wg;
+    g.red_begin[g.n] = (int32_t)rb;
+    if (wg > 0x7FFFFFFF || rb > 0x7FFFFFFF) return DGPPO_EINVAL;
+    hipLaunchKernelGGL((dgppo::gemm_wgrad_grouped_kernel<MT, NT>), dim3((unsigned)wg), dim3(512), lds, s, g);
+    if (rb > 0) hipLaunchKernelGGL(dgppo::gemm_wgrad_grouped_reduce, dim3((unsigned)rb), dim3(256), 0, s, g);
   }
   return (int)hipGetLastError();
 }

@@ -57,6 +57,111 @@ def _chk(rc, what):
 
 GEMM_LOG = None  # set to a list to record (M, N, K, batch, ta, tb, split_k, has_bias) per launch
 
+# weight-gradient GEMMs deferred to the end of a network pass's backward (defer_wgrad): current stream handle ->
+# [(GemmArgs copy, tensors held until the launch, (C start, C end), (bias start, bias end))]
+_DEFER = {}
+_DEFER_GRADS = {}  # stream handle -> [start, end) bytes of the parameter-gradient buffer deferred outputs must lie in
+DEFER_MAX = 64  # pending problems per stream before an early flush
+
+
+def _extent(t_ptr, rows, cols, ld, grp, gstride, batch=1, bstride=0):
+    """[start, end) byte range of a (rows, cols) float matrix at address t_ptr with row grouping (grp rows per group,
+    gstride floats between groups) and batch entries bstride floats apart."""
+    if rows <= 0 or cols <= 0:
+        return (t_ptr, t_ptr)
+    if grp > 0:
+        last = ((rows - 1) // grp) * gstride + (min(grp, rows) - 1) * ld
+    else:
+        last = (rows - 1) * ld
+    return (t_ptr, t_ptr + 4 * ((batch - 1) * bstride + last + cols))
+
+
+def _in_workspace(ptr, device) -> bool:
+    dev = str(device)
+    for (d, _, _), t in _WS.items():
+        if d == dev and t.data_ptr() <= ptr < t.data_ptr() + 4 * t.numel():
+            return True
+    for t, _ in _WS_KEPT:
+        if t.device == device and t.data_ptr() <= ptr < t.data_ptr() + 4 * t.numel():
+            return True
+    return False
+
+
+class defer_wgrad:
+    """Inside this context the weight-gradient GEMMs (gemm(..., ta=True) on the wgrad path) issued on the current
+    stream whose outputs (C and bias_grad) lie in `grads` -- the pass's parameter-gradient buffer -- are recorded
+    instead of launched, and launched together on exit: ONE grouped kernel + ONE partial reduction per 12 problems
+    (dgppo_gemm_wgrad_grouped, ABI 13) instead of two launches each, every output bit-identical.  Safe because
+    nothing reads a parameter gradient before the pass ends (a wgrad GEMM into a temporary, e.g. the Q-free
+    projections' [x 1]^T [dqt | dbeta] that the next GEMM reads, runs at once) and the recorded inputs are held (a
+    call whose A / B lives in a workspace slot, which later launches reuse, runs at once; one whose C / bias_grad
+    overlaps a pending problem's first flushes the pending ones, keeping the accumulation order).  on=False: a
+    no-op."""
+
+    def __init__(self, device, grads=None, on=True):
+        self.device, self.on = device, on and grads is not None and torch.device(device).type == "cuda"
+        self.grads = grads
+
+    def __enter__(self):
+        if self.on:
+            self.key = _lib.stream_handle(self.device)
+            self.prev = _DEFER.get(self.key)
+            _DEFER[self.key] = []
+            g = self.grads
+            _DEFER_GRADS[self.key] = (g.data_ptr(), g.data_ptr() + 4 * g.numel())
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            try:
+                if exc[0] is None:
+                    flush_wgrad(self.device, self.key)
+            finally:
+                _DEFER_GRADS.pop(self.key, None)
+                if self.prev is None:
+                    _DEFER.pop(self.key, None)
+                else:
+                    _DEFER[self.key] = self.prev
+        return False
+
+
+def flush_wgrad(device, key=None):
+    key = _lib.stream_handle(device) if key is None else key
+    pend = _DEFER.get(key)
+    if not pend:
+        return
+    lib = _lib.load()
+    n = len(pend)
+    arr = (_lib.GemmArgs * n)(*[e[0] for e in pend])
+    nws = lib.dgppo_gemm_wgrad_grouped_workspace_floats(arr, n)
+    ws = _p(workspace(nws, device, "wgrad_group")) if nws > 0 else None
+    _chk(lib.dgppo_gemm_wgrad_grouped(arr, n, ws, _lib.stream_handle(device)), "dgppo_gemm_wgrad_grouped")
+    pend.clear()
+
+
+def _try_defer(g, A, B, C, bias_grad, relu, bias, addend, mask, ln) -> bool:
+    """Record a weight-gradient GEMM in the current stream's defer_wgrad list (True) or leave it to run now."""
+    if not _DEFER or not (g.trans_a and not g.trans_b) or bias is not None or addend is not None or relu or \
+            mask is not None or ln is not None or g.N > 192 or g.M > 4096 or g.M < 1 or g.N < 1:
+        return False
+    key = _lib.stream_handle(C.device)
+    pend = _DEFER.get(key)
+    if pend is None or _in_workspace(g.A, C.device) or _in_workspace(g.B, C.device):
+        return False
+    cr = _extent(g.C, g.M, g.N, g.ldc, g.c_grp, g.c_gstride, g.batch, g.stride_c)
+    br = (g.bias_grad, g.bias_grad + 4 * g.N * g.batch) if g.bias_grad else (0, 0)
+    lo, hi = _DEFER_GRADS[key]
+    if not (lo <= cr[0] and cr[1] <= hi and (br[0] == br[1] or (lo <= br[0] and br[1] <= hi))):
+        return False  # not a parameter gradient: something later in the pass may read it
+    for _, _, c2, b2 in pend:
+        if any(x[0] < y[1] and y[0] < x[1] for x in (cr, br) for y in (c2, b2) if x[0] != x[1] and y[0] != y[1]):
+            flush_wgrad(C.device)  # (the overlapping accumulation keeps its order)
+            break
+    if len(pend) >= DEFER_MAX:
+        flush_wgrad(C.device)
+    pend.append((type(g).from_buffer_copy(g), (A, B, C, bias_grad), cr, br))
+    return True
+
 def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, batch=1, sa=0, sb=0, sc=0,
          a_off=0, b_off=0, c_off=0, a_grp=0, a_gs=0, b_grp=0, b_gs=0, c_grp=0, c_gs=0,
          bias=None, addend=None, add_off=0, ld_add=None, add_grp=0, add_gs=0,
@@ -99,6 +204,8 @@ def gemm(A, B, C, M, N, K, *, ta=False, tb=False, lda=None, ldb=None, ldc=None, 
             g.ln_part = _p(part)
     if GEMM_LOG is not None:
         GEMM_LOG.append((int(M), int(N), int(K), int(batch), int(ta), int(tb), int(split_k), bias is not None))
+    if _DEFER and _try_defer(g, A, B, C, bias_grad, relu, bias, addend, mask, ln):
+        return
     nws = lib.dgppo_gemm_workspace_floats(ctypes.byref(g))
     g.workspace = _p(workspace(nws, C.device, "gemm")) if nws > 0 else None
     _chk(lib.dgppo_gemm(ctypes.byref(g), _stream(C)), "dgppo_gemm")

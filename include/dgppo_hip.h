@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 12  /* 12: dgppo_adam_multi (the clipped Adam steps of several nets in two launches); 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 13  /* 13: dgppo_gemm_wgrad_grouped (a pass's weight gradients in one launch); 12: dgppo_adam_multi (the clipped Adam steps of several nets in two launches); 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -248,6 +248,14 @@ typedef struct dgppo_gemm_args {
 } dgppo_gemm_args;
 
 int64_t dgppo_gemm_workspace_floats(const dgppo_gemm_args* args);
+/* ABI 13: n weight-gradient GEMMs (each trans_a, !trans_b, on dgppo_gemm's weight-gradient path: N <= 192,
+ * M <= 4096, no bias / addend / relu / epi) in one launch plus one partial-reduction launch (per 12 problems),
+ * every output bit-identical to its own dgppo_gemm call -- a network pass's weight gradients deferred to the end
+ * of its backward (dgppo/algo/informarl.py:357-457 grads of one loss).  `workspace`: the floats
+ * dgppo_gemm_wgrad_grouped_workspace_floats(args, n) returns (their own region per problem).  The problems' C /
+ * bias_grad regions must not overlap one another. */
+int64_t dgppo_gemm_wgrad_grouped_workspace_floats(const dgppo_gemm_args* args, int n);
+int dgppo_gemm_wgrad_grouped(const dgppo_gemm_args* args, int n, float* workspace, void* stream);
 /* rows of ln_part an epi 3 call writes (its workgroup count; 0 when the call is not on the row-GEMM paths) */
 int64_t dgppo_gemm_partial_rows(const dgppo_gemm_args* args);
 int dgppo_gemm(const dgppo_gemm_args* args, void* stream);

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.dgppo_abi_version() == 12
+    assert lib.dgppo_abi_version() == 13
     assert b"gfx950" in lib.dgppo_build_info()
 
 

@@ -78,3 +78,30 @@ def test_wgrad_pipelined_loop_bit_identical(cuda, tmp_path):
     other = _child(tmp_path, "p0.pt", DGPPO_WGRAD_PIPE="0")
     for s, a, b in zip(SHAPES, mine, other):
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), s
+
+
+def test_grouped_wgrad_bit_identical_to_single_launches(cuda):
+    """dgppo_gemm_wgrad_grouped (K.defer_wgrad): the SHAPES problems in one grouped launch (batched entries, grouped
+    rows, bias gradients, beta 0 / 1) equal their single dgppo_gemm calls bit for bit."""
+    single = _results(cuda)
+    class everything:  # a "gradient buffer" spanning the address space
+        data_ptr = staticmethod(lambda: 0)
+        numel = staticmethod(lambda: 1 << 60)
+
+    with K.defer_wgrad(cuda, everything):
+        cases = [_case(cuda, M, N, R, grp, beta, 11 + k) for k, (M, N, R, grp, beta) in enumerate(SHAPES)]
+        assert len(K._DEFER[K._lib.stream_handle(cuda)]) == len(SHAPES)
+    torch.cuda.synchronize()
+    for s, a, (C, bg, _, _) in zip(SHAPES, single, cases):
+        assert torch.equal(a[0], C.cpu()) and torch.equal(a[1], bg.cpu()), s
+    # batched problems (batch = 3, strided C) through both paths
+    g = torch.Generator(device=cuda).manual_seed(5)
+    A = torch.randn((3, 5000, 40), device=cuda, generator=g)
+    B = torch.randn((3, 5000, 70), device=cuda, generator=g)
+    C0 = torch.randn((3, 40, 70), device=cuda, generator=g)
+    C1 = C0.clone()
+    K.gemm(A, B, C0, 40, 70, 5000, ta=True, batch=3, sa=5000 * 40, sb=5000 * 70, sc=40 * 70, beta=1.0)
+    with K.defer_wgrad(cuda, C1):
+        K.gemm(A, B, C1, 40, 70, 5000, ta=True, batch=3, sa=5000 * 40, sb=5000 * 70, sc=40 * 70, beta=1.0)
+        assert len(K._DEFER[K._lib.stream_handle(cuda)]) == 1
+    assert torch.equal(C0, C1)

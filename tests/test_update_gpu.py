@@ -380,3 +380,50 @@ def test_graph_replay_after_workspace_growth(cuda, monkeypatch):
         K.workspace(1 << 16, cuda, "growth_probe")
     for _, rs in K._WS_KEPT:
         assert any(r() is not None for r in rs)  # nothing is kept for graphs that are gone
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("eid,n,obs,graph", [("LidarSpread", 3, 2, "0"), ("LidarSpread", 3, 2, "1"),
+                                             ("LidarBicycleTarget", 3, 2, "0"), ("LidarOmniTarget", 3, 2, "0")])
+def test_update_grouped_wgrad_bit_identical(cuda, monkeypatch, eid, n, obs, graph):
+    """Each net's weight-gradient GEMMs deferred to the end of its backward and launched as one grouped kernel
+    (DGPPO_DEFER_WGRAD=1, K.defer_wgrad, dgppo_gemm_wgrad_grouped) give bit-identical parameters, Adam state and
+    info to one launch pair per GEMM (=0), eager and graph-replayed minibatches, over two updates."""
+    from dgppo_fov_amd.nn import kernels as K
+
+    B, T = 8, 32
+
+    def run(flag):
+        monkeypatch.setenv("DGPPO_DEFER_WGRAD", flag)
+        monkeypatch.setenv("DGPPO_UPDATE_GRAPH", graph)
+        env = make_env(eid, n, num_obs=obs, max_step=T, device=cuda)
+        algo = make_algo("dgppo", env=env, node_dim=env.node_dim, edge_dim=env.edge_dim, state_dim=env.state_dim,
+                         action_dim=env.action_dim, n_agents=n, batch_size=64, rnn_step=16, train_steps=100, seed=5,
+                         device=cuda)
+        infos = []
+        calls = []
+        real = K.flush_wgrad
+
+        def counting(device, key=None):
+            calls.append(len(K._DEFER.get(K._lib.stream_handle(device) if key is None else key) or ()))
+            return real(device, key)
+
+        monkeypatch.setattr(K, "flush_wgrad", counting)
+        for it in range(2):
+            r = algo.collect(algo.params, 21 + it, n_env=B)
+            infos.append(algo.update(r, it))
+        torch.cuda.synchronize()
+        monkeypatch.setattr(K, "flush_wgrad", real)
+        return algo, infos, calls
+
+    a0, i0, c0 = run("0")
+    a1, i1, c1 = run("1")
+    assert not any(c0) and sum(c1) > 0  # the grouped launches really ran
+    for name in ("Vl", "Vh", "policy"):
+        o0, o1 = a0.opt[name], a1.opt[name]
+        assert torch.equal(o0.ps.flat, o1.ps.flat), name
+        assert torch.equal(o0.m, o1.m) and torch.equal(o0.v, o1.v) and torch.equal(o0.state, o1.state), name
+    for d0, d1 in zip(i0, i1):
+        assert d0.keys() == d1.keys()
+        for k in d0:
+            assert d0[k] == d1[k] or (np.isnan(d0[k]) and np.isnan(d1[k])), k
