@@ -27,6 +27,7 @@
 
 #include "../../include/dgppo_hip.h"
 #include "lanes.h"
+#include "lds_attr.h"
 
 namespace dgppo {
 
@@ -920,22 +921,40 @@ __device__ __forceinline__ void wgrad_body(const P& p, int chunks, int ngroups_n
       consume(a, bb, k0);
     }
   }
-  // combine the 8 wave partials in LDS, fixed order
-  float* bred = red + MT * 32 * CP;
-  for (int w = 0; w < kWWaves; ++w) {
-    if (wave == w) {
+  // combine the 8 wave partials: a fixed pairwise tree over four LDS slabs ((w0 + w4) + (w2 + w6)) + ((w1 + w5) +
+  // (w3 + w7)), 3 rounds instead of 8 serial read-modify-write rounds; the total lands in slab 0
+  constexpr int SL = MT * 32 * CP;
+  float* bred = red + 4 * SL;
+  auto put = [&](float* dst) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float* dst = red + row * CP + nt * 32 + i;
-            *dst = (w == 0 ? 0.0f : *dst) + acc[mt][nt][r];
-          }
-    }
-    __syncthreads();
+        for (int r = 0; r < 16; ++r) dst[(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CP + nt * 32 + i] = acc[mt][nt][r];
+  };
+  auto add = [&](const float* src) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mt][nt][r] += src[(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CP + nt * 32 + i];
+  };
+  static_assert(kWWaves == 8, "tree over 8 waves");
+  if (wave >= 4) put(red + (wave - 4) * SL);
+  __syncthreads();
+  if (wave < 4) add(red + wave * SL);
+  __syncthreads();
+  if (wave == 2 || wave == 3) put(red + (wave - 2) * SL);
+  __syncthreads();
+  if (wave < 2) add(red + wave * SL);
+  __syncthreads();
+  if (wave == 1) put(red + SL);
+  __syncthreads();
+  if (wave == 0) {
+    add(red + SL);
+    put(red);
   }
   if (do_bias) {
 #pragma unroll
@@ -976,7 +995,7 @@ __device__ __forceinline__ void wgrad_body(const P& p, int chunks, int ngroups_n
 
 template <int MT, int NT, int U, bool FLAT, bool PIPE>
 __global__ __launch_bounds__(512) void gemm_wgrad_kernel(dgppo_gemm_args p, int chunks, int ngroups_n) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // 4 x [MT*32][NT*32 + 1] + colsum [2*kWWaves][NT*32]
   int c, grp;
   wgrad_place(blockIdx.x, chunks, gridDim.x / chunks, c, grp);
   wgrad_body<MT, NT, U, FLAT, PIPE>(p, chunks, ngroups_n, c, grp, blockIdx.z, red);
@@ -1129,11 +1148,14 @@ void wgrad_shape(int M, int N, int* MT, int* NT) {
 template <int MT, int NT>
 void launch_wgrad_t(const dgppo_gemm_args* p, int chunks, hipStream_t s) {
   const int gm = (p->M + MT * 32 - 1) / (MT * 32), gn = (p->N + NT * 32 - 1) / (NT * 32);
-  const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
+  const size_t lds = ((size_t)4 * MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
   const dim3 grid(chunks * gm * gn, 1, p->batch);
   const bool flat = p->a_grp <= 0 && p->b_grp <= 0;
-#define DG_WL(U, FL, PP) \
-  hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, U, FL, PP>), grid, dim3(512), lds, s, *p, chunks, gn)
+#define DG_WL(U, FL, PP)                                                                                       \
+  do {                                                                                                         \
+    if (lds > 64 * 1024) dgppo::allow_lds((const void*)dgppo::gemm_wgrad_kernel<MT, NT, U, FL, PP>);         \
+    hipLaunchKernelGGL((dgppo::gemm_wgrad_kernel<MT, NT, U, FL, PP>), grid, dim3(512), lds, s, *p, chunks, gn); \
+  } while (0)
   const bool pipe = wgrad_pipe();
   if (wgrad_unroll() == 8 && MT * NT <= 4 && flat && pipe) {
     DG_WL(8, true, true);
@@ -1383,7 +1405,7 @@ extern "C" int dgppo_gemm_wgrad_grouped(const dgppo_gemm_args* args, int n, floa
   if (dgppo_gemm_wgrad_grouped_workspace_floats(args, n) > 0 && !workspace) return DGPPO_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   constexpr int MT = 2, NT = 2;
-  const size_t lds = ((size_t)MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
+  const size_t lds = ((size_t)4 * MT * 32 * (NT * 32 + 1) + 2 * dgppo::kWWaves * NT * 32) * sizeof(float);
   int64_t off = 0;
   for (int k0 = 0; k0 < n; k0 += dgppo::kWgradGroupMax) {
     dgppo::WgradGroup g{};
@@ -1415,6 +1437,7 @@ extern "C" int dgppo_gemm_wgrad_grouped(const dgppo_gemm_args* args, int n, floa
     g.wg_begin[g.n] = (int32_t)wg;
     g.red_begin[g.n] = (int32_t)rb;
     if (wg > 0x7FFFFFFF || rb > 0x7FFFFFFF) return DGPPO_EINVAL;
+    if (lds > 64 * 1024) dgppo::allow_lds((const void*)dgppo::gemm_wgrad_grouped_kernel<MT, NT>);
     hipLaunchKernelGGL((dgppo::gemm_wgrad_grouped_kernel<MT, NT>), dim3((unsigned)wg), dim3(512), lds, s, g);
     if (rb > 0) hipLaunchKernelGGL(dgppo::gemm_wgrad_grouped_reduce, dim3((unsigned)rb), dim3(256), 0, s, g);
   }
