@@ -1725,6 +1725,9 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, i
 // layer's gradient [x_raw | 1]^T dz goes through the MFMA in four 16-pair chunks staged in a 2.8 KB
 // per-wave area (instead of a 64-pair image).  The agent-sender image and its fixed-order sums are the
 // same as the LDS form.
+#ifndef DGPPO_DIAG_BWD
+#define DGPPO_DIAG_BWD 0  // diagnostic builds only (time attribution, results invalid): 1 no pre transform, 2 no dqt, 4 no pre gradient
+#endif
 namespace bwd2r {
 constexpr int kPS = 44;  // chunk staging row: dz (0..31) | x_raw (32..39) | 1 (40)
 template <int DM>
@@ -1877,7 +1880,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
       float xraw[kD0];
 #pragma unroll
       for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? x[k < DM ? k : 0] : 0.0f;
-      if (viapre) {  // relu(x_raw pre_W + pre_b)
+      if (viapre && !(DGPPO_DIAG_BWD & 1)) {  // relu(x_raw pre_W + pre_b)
 #pragma unroll
         for (int q = 0; q < DM / 4; ++q) {
           const f32x4 b = *(const f32x4*)(preb + 4 * q);
@@ -1939,7 +1942,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
 #pragma unroll
         for (int j = 0; j < lanes::tr_final<DM>(); ++j) {
           const int q = base + j;
-          if (active && j < cnt && q < D) o[q] = v[j];
+          if (active && j < cnt && q < D && !(DGPPO_DIAG_BWD & 2)) o[q] = v[j];
         }
       }
       // ---- sender gradient of this pair: sum_h a_h dxbar_h + dl_h qt_h
@@ -1967,13 +1970,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
               if (4 * q + j < D) dst[4 * q + j] = cq[q][j];
         }
       }
-      // ---- pre layer gradient: gacc[ct] += [x_raw | 1]^T dz over the wave's pairs, 16-pair chunks (one DPP
-      // row of lanes each) staged in the wave's area
-      if (want_pre) {
+      // ---- pre layer gradient: gacc[ct] += [x_raw | 1]^T dz over the wave's pairs in 16-pair chunks staged in the
+      // wave's area.  Only the pairs whose sender went through the pre layer carry a nonzero dz (never-receivers:
+      // 16 of a receiver's 24 candidates at n = 8, 9 of 17 for own-goal envs), so they are compacted to the front
+      // (ballot rank) and the chunk loop runs over ceil(count / 16) chunks, not 4; the other lanes fill the last
+      // chunk's free slots with zero rows (lane l: chunk pos >> 4, slot pos & 15)
+      if (want_pre && !(DGPPO_DIAG_BWD & 4)) {
+        const uint64_t vb = __ballot(viapre);
+        const int nvia = __popcll(vb);
+        const int pos = viapre ? lanes::mbcnt64(vb) : nvia + lanes::mbcnt64(~vb);
+        const int nch = (nvia + 15) >> 4;
 #pragma unroll 1
-        for (int ch = 0; ch < 4; ++ch) {
-          if (kq == ch) {
-            float* sp = ws + i16 * kPS;
+        for (int ch = 0; ch < nch; ++ch) {
+          if ((pos >> 4) == ch) {
+            float* sp = ws + (pos & 15) * kPS;
 #pragma unroll
             for (int q = 0; q < DM / 4; ++q) {
               f32x4 dz;

@@ -97,6 +97,11 @@ __device__ __forceinline__ int treduce32(float (&v)[V], int& cnt) {
   return ((c & 8) ? H0 : 0) + ((c & 4) ? H1 : 0) + ((c & 2) ? H2 : 0) + ((c & 1) ? H3 : 0) + ((c & 16) ? H4 : 0);
 }
 
+// lanes below this one whose bit of m is set
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // LDS visibility among the lanes of one wave (no workgroup barrier)
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
