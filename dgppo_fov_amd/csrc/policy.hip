@@ -55,6 +55,9 @@ constexpr int kNarrowD0 = 8;
 #define POLICY_REG_WAVES 3
 #endif
 constexpr int kRegWaves = POLICY_REG_WAVES;
+#ifndef DGPPO_DIAG_POL
+#define DGPPO_DIAG_POL 0  // diagnostic builds only (time attribution, results invalid): 1 no layer-1 pre transform
+#endif
 // LDS pitches (floats); xs rows: x (0..31) | edge head (32..35) | extra edge columns (36..41)
 constexpr int kX0P = 13, kQTP = 100, kXCP = 132, kY0P = 36, kYP = 68, kXSP = 44;
 // work: per layer the (32 + 1) x 100 query-key matrix [QT_0 | QT_1 | QT_2 (32 cols each) | beta_0..2 | 0]
@@ -194,8 +197,12 @@ __device__ __forceinline__ void layer_load(LayerW<KQ, KC, KX, KU>& w, const dgpp
   bias_load(w.bu, ly.bu, ly.F);
 }
 
+// layer-1 features relu(x_raw Wu0 + bu0) of a workgroup's never-receiving nodes, computed once per node (MFMA) into
+// LDS when the group has at most kPreMax of them (LidarSpread n = 8: 2 graphs x 73 nodes); rows of 32 floats, each
+// row's float4 quads stored XOR-swizzled by (row & 7) so that lanes reading different rows spread over the banks
+constexpr int kPreMax = 160;
 struct Lds {
-  float *x0, *qt, *xc, *y0, *yb, *preW, *preb, *lnp, *outW, *att;
+  float *x0, *qt, *xc, *y0, *yb, *preW, *preb, *lnp, *outW, *att, *pre;
   int *psrc, *pedge;  // alias att: consumed before the first attention sub-round
   float* hb;          // aliases att: the carries are written there after the GNN
 };
@@ -205,7 +212,7 @@ constexpr int kAttPerWave = 2 * kCP * (kXSP + 4);
 constexpr int kAttReg = kRowsG * kYP > 2 * kRowsG * kCP ? kRowsG * kYP : 2 * kRowsG * kCP;
 constexpr size_t lds_floats(bool reg) {
   return (size_t)kRowsG * (kX0P + kQTP + kXCP + kY0P + kYP) + kMaxD0 * 32 + 32 + 4 * kHid + 2 * kHid * 4 + 8 +
-         (reg ? kAttReg : 4 * kAttPerWave);
+         (reg ? kAttReg + kPreMax * 32 : 4 * kAttPerWave);
 }
 
 __device__ __forceinline__ Lds carve(float* base) {
@@ -223,6 +230,7 @@ __device__ __forceinline__ Lds carve(float* base) {
   L.psrc = (int*)L.att;
   L.hb = L.att;
   L.pedge = L.psrc + kRowsG * kCP;
+  L.pre = L.att + kAttReg;  // (register form only)
   return L;
 }
 
@@ -451,7 +459,7 @@ __device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const 
 // are one transposed DPP reduction per head (lanes::treduce32), whose totals each lane writes to the
 // row's xcat.  No per-pair LDS staging: the workgroup's LDS is its row activations only, so more
 // workgroups are resident per CU, and the weighted sums need no LDS round trips.
-template <int DX, bool layer0, int MD0, int MEX, int KQ, int KC, int KX, int KU>
+template <int DX, bool layer0, int MD0, int MEX, int KQ, int KC, int KX, int KU, bool node_pre = false>
 __device__ __forceinline__ void gt_layer_reg(const dgppo_policy_step_args& p, const dgppo_gt_layer& ly,
                                              const PairG<MD0, MEX> (&pg)[kSR], const Lds& L, const float* qk,
                                              const float* A, int lda, float* out, int ldo, int nmag, int pk) {
@@ -496,6 +504,17 @@ __device__ __forceinline__ void gt_layer_reg(const dgppo_policy_step_args& p, co
         x[4 * q + 2] = v[2];
         x[4 * q + 3] = v[3];
       }
+    } else if constexpr (node_pre) {  // never-receiving sender: its row of the per-node table (masked pairs: node 0)
+      const int m = ok ? div_n(r, nmag) * (p.N - n) + (cur.s - n) : 0;
+      const float* src = L.pre + m * 32;
+#pragma unroll
+      for (int q = 0; q < DX / 4; ++q) {
+        const f32x4 v = *(const f32x4*)(src + 4 * (q ^ (m & 7)));
+        x[4 * q] = v[0];
+        x[4 * q + 1] = v[1];
+        x[4 * q + 2] = v[2];
+        x[4 * q + 3] = v[3];
+      }
     } else {  // never-receiving sender: relu(x_raw Wu0 + bu0) (masked pairs too; their weights are 0)
 #pragma unroll
       for (int q = 0; q < DX / 4; ++q) {
@@ -506,7 +525,7 @@ __device__ __forceinline__ void gt_layer_reg(const dgppo_policy_step_args& p, co
         x[4 * q + 3] = b[3];
       }
 #pragma unroll
-      for (int k = 0; k < MD0; ++k) {
+      for (int k = 0; k < (DGPPO_DIAG_POL ? 0 : MD0); ++k) {
         const float xk = cur.xr[k];
 #pragma unroll
         for (int q = 0; q < DX / 4; ++q) {
@@ -633,7 +652,10 @@ __device__ __forceinline__ void ln_relu64(float* Y, const float* scale, const fl
   }
 }
 
-template <int MD0, int MEX, bool REG>
+// NP: the per-node layer-1 pre-transform table (narrow register form, two layers, <= kPreMax never-receiving nodes
+// per group: the host picks this instantiation, node_pre_ok); its own instantiation, so that the raw sender rows die
+// after layer 0 instead of staying live through layer 1 for the per-lane fallback
+template <int MD0, int MEX, bool REG, bool NP = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG && MD0 <= kNarrowD0 ? kRegWaves : 1, 8))) void policy_step_kernel(dgppo_policy_step_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Lds L = carve(lds);
@@ -694,6 +716,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
     }
     if (threadIdx.x < 2 * A) L.outW[kHid * 2 * A + threadIdx.x] = threadIdx.x < A ? p.bm[threadIdx.x] : p.bsd[threadIdx.x - A];
   }
+  // raw rows of the group's never-receiving nodes (graph gl, node n + j -> table row gl (N - n) + j), staged in the
+  // xcat region (free until layer 0's attention) for the per-node layer-1 pre-transform
+  constexpr int kPreLd = kPreMax * kNarrowD0 / kThreads;
+  const int nnr = p.N - n;
+  constexpr bool node_pre = NP && REG && MD0 <= kNarrowD0;
+  float prv[kPreLd];
+  if constexpr (node_pre) {
+#pragma unroll
+    for (int u = 0; u < kPreLd; ++u) {
+      const int e = threadIdx.x + u * kThreads, m = e >> 3, k = e & 7;
+      const int gl = m / nnr, j = n + m - gl * nnr;
+      prv[u] = (gl < ng && k < p.D0) ? p.nodes[(g0 + gl) * p.nodes_gstride + (int64_t)j * p.D0 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kPreLd; ++u) L.xc[threadIdx.x + u * kThreads] = prv[u];
+  }
   const int tr = threadIdx.x >> 3, tq = threadIdx.x & 7;  // tail: row, action lane
   const bool nz_own = p.mode == 1 && tr < rows && tq < A;
   const float nz = (nz_own && p.noise) ? p.noise[(row0 + tr) * A + tq] : 0.0f;  // else drawn at the tail
@@ -716,6 +754,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
     }
   }
   __syncthreads();
+  // ---- the per-node layer-1 pre-transform: 16-node x 16-column tiles on MFMA, K = the raw width (<= 8) in two
+  // steps, bias as the accumulator's start, ReLU on the way to the swizzled table
+  if constexpr (node_pre) {
+    const int ntile = (gpg * nnr + 15) >> 4;
+    for (int t = wave; t < 2 * ntile; t += 4) {
+      const int tile = t >> 1, ct = t & 1;
+      const float b = L.preb[16 * ct + i16];
+      f32x4 acc = {b, b, b, b};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(L.xc[(16 * tile + i16) * kNarrowD0 + 4 * ks + kq],
+                                                   L.preW[(4 * ks + kq) * 32 + 16 * ct + i16], acc, 0, 0, 0);
+      const int col = 16 * ct + i16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 16 * tile + 4 * kq + i;
+        L.pre[m * 32 + 4 * ((col >> 2) ^ (m & 7)) + (col & 3)] = acc[i] > 0.0f ? acc[i] : 0.0f;
+      }
+    }
+  }
   // ---- level 3: every pair this lane attends over (kSR sub-rounds), kept in registers for both layers
   PairG<MD0, MEX> pg[kSR];
   {
@@ -732,8 +790,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
         p, p.layer[0], pg, L, p.work, L.x0, kX0P, two ? L.y0 : L.yb, two ? kY0P : kYP, nmag, 2);
     PROBE(4);
     if (two) {
-      gt_layer_reg<32, false, MD0, MEX, 8, 28, KX, 8>(p, p.layer[1], pg, L, p.work + kQKStride, L.y0, kY0P, L.yb, kYP,
-                                                     nmag, 5);
+      gt_layer_reg<32, false, MD0, MEX, 8, 28, KX, 8, node_pre>(p, p.layer[1], pg, L, p.work + kQKStride, L.y0, kY0P,
+                                                               L.yb, kYP, nmag, 5);
       PROBE(7);
     }
   }
@@ -953,16 +1011,19 @@ extern "C" int dgppo_policy_step(const dgppo_policy_step_args* p, void* stream) 
     const char* e = getenv("DGPPO_POLICY_ATTN");
     return !(e && strcmp(e, "lds") == 0);
   }();
+  const bool np = !wide && reg && p->n_layers == 2 && (int64_t)gpg * (p->N - p->n_agents) <= dgppo::kPreMax;
   const void* fn = wide ? (reg ? (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, true>
                                : (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, false>)
-                        : (reg ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>
-                               : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>);
+                        : (np ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true, true>
+                              : reg ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>
+                                    : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>);
   const size_t bytes = dgppo::lds_bytes(reg);
   if (bytes > 64 * 1024) dgppo::allow_lds(fn);
   const dim3 g((unsigned)grid), b(dgppo::kThreads);
   const hipStream_t s = (hipStream_t)stream;
   if (wide && reg) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, true>), g, b, bytes, s, *p);
   else if (wide) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, false>), g, b, bytes, s, *p);
+  else if (np) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true, true>), g, b, bytes, s, *p);
   else if (reg) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>), g, b, bytes, s, *p);
   else hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>), g, b, bytes, s, *p);
   return (int)hipGetLastError();
