@@ -156,6 +156,9 @@ __device__ __forceinline__ f32x4 dense64(const float* A, int lda, const float* W
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+#ifndef DGPPO_DIAG_FWD
+#define DGPPO_DIAG_FWD 0  // diagnostic builds only (time attribution, results invalid): 1 no staging loads, 2 no xbar
+#endif                    // reductions, 4 no [qt | beta] / message GEMMs, 8 no attn / xcat / qb stores
 template <int DM, bool TAIL, bool WSL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 4, 8))) void gnn_layer_fwd_kernel(
     dgppo_gnn_layer_args p, int gpb, Carve cv) {
@@ -187,12 +190,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
     for (int t = tid; t < ng * N * kD0; t += 256) {
       const int node = t >> 3, k = t & 7;
       const int g = node / N, j = node - g * N;
-      rx[t] = k < D0 ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D0 + k] : 0.0f;
+      rx[t] = (k < D0 && !(DGPPO_DIAG_FWD & 1)) ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D0 + k] : 0.0f;
     }
     for (int t = tid; t < nrec * (DM / 4); t += 256) {
       const int r = t / (DM / 4), q = t - r * (DM / 4);
       const int g = r / n, i = r - g * n;
-      *(f32x4*)(xs + (g * N + i) * XP + 4 * q) = *(const f32x4*)(a.xa + (g0 + g) * a.xa_gstride + (int64_t)i * D + 4 * q);
+      *(f32x4*)(xs + (g * N + i) * XP + 4 * q) = (DGPPO_DIAG_FWD & 1) ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : *(const f32x4*)(a.xa + (g0 + g) * a.xa_gstride + (int64_t)i * D + 4 * q);
     }
     {
       const int k = tid >> 5, d = tid & 31;
@@ -204,14 +207,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
     if (a.x_gstride == (int64_t)N * D) {
       stage_copy<8>(xs, ng * N * XP, tid, [&](int t) {
         const int node = t / XP, k = t - node * XP;
-        return k < D ? xb[node * D + k] : 0.0f;
+        return (k < D && !(DGPPO_DIAG_FWD & 1)) ? xb[node * D + k] : 0.0f;
       });
     } else {
       const int xg = (int)a.x_gstride;
       stage_copy<8>(xs, ng * N * XP, tid, [&](int t) {
         const int node = t / XP, k = t - node * XP;
         const int g = node / N, j = node - g * N;
-        return k < D ? xb[g * xg + j * D + k] : 0.0f;
+        return (k < D && !(DGPPO_DIAG_FWD & 1)) ? xb[g * xg + j * D + k] : 0.0f;
       });
     }
   }
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
         const int col = 16 * ct + i16;
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) acc = mma(aq[ks], bq[t][ks], acc);
+        for (int ks = 0; ks < ((DGPPO_DIAG_FWD & 4) ? 0 : KS); ++ks) acc = mma(aq[ks], bq[t][ks], acc);
         if (col < W) {
           const int dst = col < kH * D ? (col / D) * HS + (col % D) : kH * HS + (col - kH * D);
 #pragma unroll
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
             const int r = 4 * kq + i;
             if (r < nrec) {
               qts[r * QP + dst] = acc[i];
-              if (p.qb) p.qb[(row0 + r) * W + col] = acc[i];
+              if (p.qb && !(DGPPO_DIAG_FWD & 8)) p.qb[(row0 + r) * W + col] = acc[i];
             }
           }
         }
@@ -336,9 +339,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
         const float ex = ok ? expf(lg - mx) : 0.0f;
         const float sm = lanes::sum32(ex);
         aw[h] = ok ? ex / sm : 0.0f;
-        if (active && c < C && a.attn) a.attn[(row * kH + h) * C + c] = aw[h];
+        if (active && c < C && a.attn && !(DGPPO_DIAG_FWD & 8)) a.attn[(row * kH + h) * C + c] = aw[h];
       }
-      float* o = a.xcat ? a.xcat + row * WX : nullptr;
+      float* o = (a.xcat && !(DGPPO_DIAG_FWD & 8)) ? a.xcat + row * WX : nullptr;
       float* ot = xc + rl * XCP;
       if constexpr (WSL) {
         // xbar_h[d] = sum_c a_hc x_c[d]: the row's (a, sender) pairs through the wave's LDS slots, lane c of the
@@ -367,7 +370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
         lanes::wave_sync();  // the slots are rewritten next sub-round
       } else {
 #pragma unroll
-        for (int h = 0; h < kH; ++h) {
+        for (int h = 0; h < ((DGPPO_DIAG_FWD & 2) ? 0 : kH); ++h) {
           float v[DM];
 #pragma unroll
           for (int dd = 0; dd < DM; ++dd) v[dd] = aw[h] * x[dd];
@@ -439,12 +442,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
       const float* xrow = xc + i16 * XCP;
       f32x4 am = {0.0f, 0.0f, 0.0f, 0.0f}, au = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int ks = 0; ks < KM; ++ks) {
+      for (int ks = 0; ks < ((DGPPO_DIAG_FWD & 4) ? 0 : KM); ++ks) {
         const int k = 4 * ks + kq;
         am = mma((ract && k < WX) ? xrow[k] : 0.0f, bm[ks], am);
       }
 #pragma unroll
-      for (int ks = 0; ks < KU; ++ks) {
+      for (int ks = 0; ks < ((DGPPO_DIAG_FWD & 4) ? 0 : KU); ++ks) {
         const int k = 4 * ks + kq;
         au = mma((ract && k < D) ? arow[k] : 0.0f, bu4[ks], au);
       }
