@@ -234,10 +234,6 @@ class GnnLayerArgs(ctypes.Structure):  # ABI 11 dgppo_gnn_layer_args
     ]
 
 
-class GnnLayerBwdArgs(ctypes.Structure):  # ABI 11 dgppo_gnn_layer_bwd_args
-    _fields_ = [("a", GnnAttnArgs), ("dY", c_f32p), ("QBW", c_f32p), ("Wcat", c_f32p), ("Wu", c_f32p), ("mask", c_f32p)]
-
-
 ADAM_MAX_NETS = 4  # include/dgppo_hip.h DGPPO_ADAM_MAX_NETS
 
 
@@ -311,7 +307,6 @@ SIGNATURES = {
     "dgppo_gru_bwd": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _I32, _V]),
     "dgppo_gru_seq_blocks": (ctypes.c_int64, [_I32]),
     "dgppo_gnn_attn_partial_blocks": (ctypes.c_int64, [_V]),
-    "dgppo_gnn_set_attn_kernel": (ctypes.c_int, [ctypes.c_int]),
     "dgppo_gemm_partial_rows": (ctypes.c_int64, [ctypes.POINTER(GemmArgs)]),
     "dgppo_policy_step_supported": (ctypes.c_int, [_V]),
     "dgppo_policy_work_floats": (ctypes.c_int64, []),
@@ -346,15 +341,12 @@ SIGNATURES = {
     "dgppo_gather_env_steps": (ctypes.c_int, [ctypes.POINTER(GatherField), _I32, _V, _I32, _I32, _V]),
     "dgppo_gnn_layer_supported": (ctypes.c_int, [ctypes.POINTER(GnnLayerArgs)]),
     "dgppo_gnn_layer_fwd": (ctypes.c_int, [ctypes.POINTER(GnnLayerArgs), ctypes.c_void_p]),
-    "dgppo_gnn_layer_bwd_supported": (ctypes.c_int, [ctypes.POINTER(GnnLayerBwdArgs)]),
-    "dgppo_gnn_layer_bwd_partial_blocks": (ctypes.c_int64, [ctypes.POINTER(GnnLayerBwdArgs)]),
-    "dgppo_gnn_layer_bwd": (ctypes.c_int, [ctypes.POINTER(GnnLayerBwdArgs), ctypes.c_void_p]),
 }
 
 _LIB = None
 
 
-ABI_VERSION = 13  # include/dgppo_hip.h DGPPO_ABI_VERSION
+ABI_VERSION = 14  # include/dgppo_hip.h DGPPO_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

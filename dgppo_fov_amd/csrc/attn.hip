@@ -2998,13 +2998,7 @@ void gfwd_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
     hipLaunchKernelGGL(attn_fwd_graph_kernel<32>, dim3((unsigned)p->G), dim3(256), bytes, s, *p, pl.ns, pl.cp, pl.slots);
 }
 
-#include "attn_gm.h"
-
 int run(const dgppo_gnn_attn_args* p, bool bwd, hipStream_t s) {
-  if (gm_ok(p, bwd)) {  // graph-form MFMA kernels (attn_gm.h): N <= 96, n <= 10 (DGPPO_ATTN_GM=0: the others)
-    if (p->G > 0) gm_launch(p, bwd, s);
-    return 0;
-  }
   if (!bwd && gfwd_ok(p)) {
     if (p->G > 0) gfwd_launch(p, s);
     return 0;
@@ -3064,7 +3058,6 @@ extern "C" int dgppo_gnn_sender_table(int32_t G, int32_t n_agents, int32_t C, in
 
 extern "C" int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* p) {
   if (!dgppo::valid(p)) return 0;
-  if (dgppo::gm_ok(p, true)) return dgppo::gm_grid(p);
   if (dgppo::gbwd32_ok(p)) return dgppo::gbwd32_grid(p);
   if (dgppo::bwd2_ok(p)) {
     int64_t nblk;
@@ -3077,14 +3070,6 @@ extern "C" int dgppo_gnn_set_graph_otf(int32_t on) {
   if (on != 0 && on != 1) return DGPPO_EINVAL;
   dgppo::g_graph_otf = on;
   return 0;
-}
-
-extern "C" int dgppo_gnn_set_attn_kernel(int mode) {
-  if (mode < 0 || mode > 1) return DGPPO_EINVAL;
-  dgppo::gm_enabled();
-  const int prev = dgppo::g_attn_gm;
-  dgppo::g_attn_gm = mode;
-  return prev;
 }
 
 extern "C" int dgppo_gnn_attn_fwd(const dgppo_gnn_attn_args* p, void* stream) {

@@ -599,544 +599,3 @@ extern "C" int dgppo_gnn_layer_fwd(const dgppo_gnn_layer_args* p, void* stream) 
 #undef GL_LAUNCH
   return (int)hipGetLastError();
 }
-
-// ================================================================================================================
-// Backward (dgppo_gnn_layer_bwd): the row-block attention backward (attn.hip attn_bwd2r: softmax backward, dqt by
-// transposed DPP reductions, sender gradients, the never-receivers' Dense_4 gradient as MFMA [x_raw | 1]^T dz over
-// 16-pair chunks) on graphs staged in LDS as in the forward, with the GEMMs on each side in the kernel:
-//   prologue  dxcat = dY Wcat^T / H            (16 x 64 x 111 on MFMA; the unfused chain's dxcat GEMM + HBM trip)
-//   epilogue  dxa = agent senders' gradients + dY Wu^T + [dqt | dbeta] QBW[:D]^T, ReLU mask   (two GEMMs)
-// A persistent workgroup walks blocks of gpb = 16 / n whole graphs.  The agent senders' gradients of each
-// sub-round's 8 receiving rows go to an LDS image and are folded into the block's dxa accumulator in fixed
-// receiver order after each sub-round; the pre-gradient accumulators are combined over waves in fixed order into
-// one partial row per workgroup.  Deterministic, no atomics.
-// ================================================================================================================
-namespace dgppo {
-namespace {
-namespace lb {
-constexpr int kPS = 44;  // pre-gradient chunk staging row: dz (0..31) | x_raw (32..39) | 1 (40)
-template <int DM>
-struct Lay {
-  // GP: a dxcat row, then the row's [dqt | dbeta]; at DM = 32 wide enough (132 >= 128) to host the half-wave's
-  // 32 (dl, sender) pairs of the LDS-loop dqt sums in between
-  static constexpr int XP = DM + 4, HS = DM, QP = 3 * HS + 4, GP = DM == 32 ? 132 : 3 * HS + 16;
-};
-struct Carve {
-  int raw, qt, gs, img, acc, stg, pre, pa;
-  int floats;
-};
-template <int DM>
-Carve carve(int gpb, int N, int n, int F, bool stage) {
-  using L = Lay<DM>;
-  constexpr bool agent = DM == 32;
-  Carve c;
-  int o = stage ? (gpb * N * L::XP + 3) & ~3 : 0;
-  c.raw = o;
-  o += (agent && stage) ? gpb * N * kD0 : 0;
-  c.qt = o;
-  o += kRows * L::QP;
-  c.gs = o;
-  o += kRows * L::GP;
-  c.img = o;  // dY tile [16][F + 4] for the dxcat GEMM, then the agent-sender image [8][n][DM]
-  const int dz = kRows * (F + 4), im = agent ? 8 * n * DM : 0;
-  o += ((dz > im ? dz : im) + 3) & ~3;
-  c.acc = o;
-  o += agent ? kRows * DM : 0;
-  c.stg = o;  // per wave [16][kPS]; the epilogue's [2][16][32] partial products afterwards
-  o += agent ? 4 * 16 * kPS : 0;
-  c.pre = o;
-  o += agent ? kD0 * 32 + 32 : 0;
-  const bool pa_own = stage && wsum_lds() && L::GP < 128;  // else the pair slots live in the gs rows
-  c.pa = pa_own ? o : 0;
-  o += pa_own ? 4 * 64 * 4 : 0;
-  c.floats = o;
-  return c;
-}
-// staging the graphs (STAGE) or gathering per lane as attn_bwd2r does (the default: 3 workgroups per CU)
-static bool bwd_stage() {
-  static const bool v = [] {
-    const char* e = getenv("DGPPO_LAYER_BWD_STAGE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-template <int DM>
-int64_t grid_cap(bool stage) {
-  // resident workgroups: 2 per CU at the staged DM = 32 carve (~65 KB of LDS), 3 at the gather carve (~37 KB, VGPRs)
-  return DM == 32 ? (stage ? 512 : 768) : 2048;
-}
-}  // namespace lb
-
-template <int DM, bool WSL, bool STAGE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DM == 32 ? (STAGE ? 2 : 3) : 4, 8))) void
-gnn_layer_bwd_kernel(dgppo_gnn_layer_bwd_args p, int gpb, int64_t nblk, lb::Carve cv) {
-  static_assert(STAGE || !WSL, "the LDS-loop sums read the staged rows");
-  using L = lb::Lay<DM>;
-  constexpr int XP = L::XP, HS = L::HS, QP = L::QP, GP = L::GP, kPS = lb::kPS;
-  constexpr bool agent = DM == 32;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const dgppo_gnn_attn_args& a = p.a;
-  float* xs = lds;                // [gpb * N][XP]
-  float* raw = lds + cv.raw;      // agent mode: raw rows [gpb * N][8]
-  float* qts = lds + cv.qt;       // [16][QP]: qt_h (HS stride) | beta_h at 3 HS + h
-  float* gs = lds + cv.gs;        // [16][GP]: dxcat (dxbar_h HS stride | debar 3HS.. | dsig 3HS+12..); then [dqt | dbeta]
-  float* img = lds + cv.img;      // dY tile [16][F + 4]; then the agent-sender image [8][n][DM]
-  float* dxacc = lds + cv.acc;    // [16][DM] the block's dxa rows
-  float* stg = lds + cv.stg;      // per wave [16][kPS]
-  float* preW = lds + cv.pre;     // [8][32] | pre_b [32]
-  float* preb = preW + kD0 * 32;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int slot = lane >> 5, cc = lane & 31;
-  const int n = a.n_agents, N = a.N, D = a.D, F = a.F, C = a.C;
-  const int W = kH * D + kH, WX = kH * (D + 5), FP = F + 4;
-  const int64_t qld = a.qt_ld ? a.qt_ld : W;
-  const bool want_dxa = agent && a.dxa != nullptr;
-  const bool want_pre = agent && a.dpre_part != nullptr;
-  if constexpr (agent) {
-    const int k = tid >> 5, d = tid & 31;
-    preW[tid] = k < a.D0 ? a.pre_W[k * D + d] : 0.0f;
-    if (tid < 32) preb[tid] = a.pre_b[tid];
-  }
-  f32x4 gacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // [x_raw | 1]^T dz
-  float* ws = stg + wave * 16 * kPS;
-  const int TQ = (D + 3) >> 2;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int64_t g0 = blk * gpb;
-    const int ng = (int)((int64_t)a.G - g0 < gpb ? (int64_t)a.G - g0 : gpb);
-    const int nrec = ng * n;
-    const int64_t row0 = g0 * n;
-    // ---- stage 1: graphs (STAGE), [qt | beta] rows, dY rows into LDS; dxcat tile and dxa accumulator cleared
-    if constexpr (agent) {
-      const int D0 = a.D0;
-      for (int t = tid; t < (STAGE ? ng * N * kD0 : 0); t += 256) {
-        const int node = t >> 3, k = t & 7;
-        const int g = node / N, j = node - g * N;
-        raw[t] = k < D0 ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D0 + k] : 0.0f;
-      }
-      for (int t = tid; t < (STAGE ? nrec * (DM / 4) : 0); t += 256) {
-        const int r = t / (DM / 4), q = t - r * (DM / 4);
-        const int g = r / n, i = r - g * n;
-        *(f32x4*)(xs + (g * N + i) * XP + 4 * q) =
-            *(const f32x4*)(a.xa + (g0 + g) * a.xa_gstride + (int64_t)i * D + 4 * q);
-      }
-      for (int t = tid; t < kRows * DM; t += 256) dxacc[t] = 0.0f;
-    } else {
-      for (int t = tid; t < (STAGE ? ng * N * XP : 0); t += 256) {
-        const int node = t / XP, k = t - node * XP;
-        const int g = node / N, j = node - g * N;
-        xs[t] = k < D ? a.x[(g0 + g) * a.x_gstride + (int64_t)j * D + k] : 0.0f;
-      }
-    }
-    for (int t = tid; t < kRows * QP; t += 256) {
-      const int r = t / QP, k = t - r * QP;
-      int src = -1;
-      if (k < kH * HS) {
-        const int h = k / HS, d = k - h * HS;
-        src = d < D ? h * D + d : -1;
-      } else if (k - kH * HS < kH) {
-        src = kH * D + (k - kH * HS);
-      }
-      qts[t] = (r < nrec && src >= 0) ? a.qt[(row0 + r) * qld + src] : 0.0f;
-    }
-    for (int t = tid; t < kRows * F; t += 256) {
-      const int r = t / F, f = t - r * F;
-      img[r * FP + f] = r < nrec ? p.dY[(row0 + r) * F + f] : 0.0f;
-    }
-    for (int t = tid; t < kRows * GP; t += 256) gs[t] = 0.0f;
-    __syncthreads();
-    // ---- stage 2: never-receivers' rows (agent mode; the forward's order of operations) and dxcat = dY Wcat^T / H
-    if constexpr (agent && STAGE) {
-      const int nn = N - n;
-      for (int t = tid; t < ng * nn * (DM / 4); t += 256) {
-        const int q = t & (DM / 4 - 1), rr = t / (DM / 4);
-        const int g = rr / nn, j = n + rr - g * nn;
-        const float* xr = raw + (g * N + j) * kD0;
-        const f32x4 b = *(const f32x4*)(preb + 4 * q);
-        float v0 = b[0], v1 = b[1], v2 = b[2], v3 = b[3];
-#pragma unroll
-        for (int k = 0; k < kD0; ++k) {
-          const float xk = xr[k];
-          const f32x4 w = *(const f32x4*)(preW + k * 32 + 4 * q);
-          v0 += xk * w[0];
-          v1 += xk * w[1];
-          v2 += xk * w[2];
-          v3 += xk * w[3];
-        }
-        *(f32x4*)(xs + (g * N + j) * XP + 4 * q) =
-            f32x4{v0 > 0.0f ? v0 : 0.0f, v1 > 0.0f ? v1 : 0.0f, v2 > 0.0f ? v2 : 0.0f, v3 > 0.0f ? v3 : 0.0f};
-      }
-    }
-    {
-      constexpr int KS = 16;  // k-steps over F <= 64
-      const int ntile = (WX + 15) >> 4;
-      float bq[2][KS];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int col = 16 * (wave + 4 * t) + i16;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int k = 4 * ks + kq;
-          bq[t][ks] = (k < F && col < WX) ? p.Wcat[(int64_t)col * F + k] : 0.0f;
-        }
-      }
-      float aq[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int k = 4 * ks + kq;
-        aq[ks] = k < F ? img[i16 * FP + k] : 0.0f;
-      }
-      const float inv_h = 1.0f / (float)kH;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int ct = wave + 4 * t;
-        if (ct < ntile) {
-          const int col = 16 * ct + i16;
-          f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) acc = mma(aq[ks], bq[t][ks], acc);
-          if (col < WX) {
-            const int dst = col < kH * D ? (col / D) * HS + (col % D) : kH * HS + (col - kH * D);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) gs[(4 * kq + i) * GP + dst] = acc[i] * inv_h;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ---- stage 3: the pairs, two sub-rounds of 8 receiving rows
-#pragma unroll 1
-    for (int sr = 0; sr < 2; ++sr) {
-      const int rl = 2 * wave + 8 * sr + slot, lr = rl - 8 * sr;
-      const bool active = rl < nrec;
-      const int64_t row = row0 + rl;
-      const int gl = active ? rl / n : 0;
-      const int i = active ? rl - gl * n : 0;
-      if (want_dxa) {
-        for (int e = lane; e < 2 * n * DM; e += 64) img[2 * wave * n * DM + e] = 0.0f;
-        lanes::wave_sync();
-      }
-      int s = -1, e = 0;
-      if (active && cc < C) {
-        e = a.cand[i * C + cc];
-        s = a.sidx[row * C + cc];
-      }
-      const bool ok = s >= 0;
-      float av[kH];
-#pragma unroll
-      for (int h = 0; h < kH; ++h) av[h] = ok ? a.attn[(row * kH + h) * C + cc] : 0.0f;
-      f32x4 ef = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (ok) ef = *(const f32x4*)(a.ef + (g0 + gl) * a.ef_gstride + (int64_t)e * 4);
-      float x[DM];
-      float xg[kD0];  // the gather form's raw row of a never-receiving sender (its pre-gradient operand)
-      const bool viapre = agent && ok && s >= n;
-      if constexpr (STAGE) {
-        const float* xr = xs + (gl * N + (ok ? s : 0)) * XP;
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q) {
-          const f32x4 v = ok ? *(const f32x4*)(xr + 4 * q) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-          x[4 * q] = v[0], x[4 * q + 1] = v[1], x[4 * q + 2] = v[2], x[4 * q + 3] = v[3];
-        }
-      } else if (!agent || !viapre) {  // node rows (full mode) / agent senders' layer input rows (attn_bwd2r's gathers)
-        const float* xr = agent ? a.xa + (g0 + gl) * a.xa_gstride + (int64_t)(ok ? s : 0) * D
-                                : a.x + (g0 + gl) * a.x_gstride + (int64_t)(ok ? s : 0) * D;
-#pragma unroll
-        for (int d = 0; d < DM; ++d) x[d] = (ok && d < D) ? xr[d] : 0.0f;
-      } else {  // never-receiving sender: relu(x_raw pre_W + pre_b), attn_bwd2r's order of operations
-        const float* xr = a.x + (g0 + gl) * a.x_gstride + (int64_t)s * a.D0;
-#pragma unroll
-        for (int k = 0; k < kD0; ++k) xg[k] = k < a.D0 ? xr[k] : 0.0f;
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q) {
-          const f32x4 b = *(const f32x4*)(preb + 4 * q);
-          x[4 * q] = b[0], x[4 * q + 1] = b[1], x[4 * q + 2] = b[2], x[4 * q + 3] = b[3];
-        }
-#pragma unroll
-        for (int k = 0; k < kD0; ++k)
-#pragma unroll
-          for (int q = 0; q < DM / 4; ++q) {
-            const f32x4 w = *(const f32x4*)(preW + k * 32 + 4 * q);
-            x[4 * q] += xg[k] * w[0];
-            x[4 * q + 1] += xg[k] * w[1];
-            x[4 * q + 2] += xg[k] * w[2];
-            x[4 * q + 3] += xg[k] * w[3];
-          }
-#pragma unroll
-        for (int d = 0; d < DM; ++d) x[d] = x[d] > 0.0f ? x[d] : 0.0f;
-      }
-      // ---- softmax backward
-      const float* gv = gs + rl * GP;
-      float dl[kH], dbeta[kH];
-#pragma unroll
-      for (int h = 0; h < kH; ++h) {
-        float da = 0.0f;
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q)
-          if (q < TQ) {
-            const f32x4 gq = ((const f32x4*)(gv + HS * h))[q];
-            da += x[4 * q] * gq[0] + x[4 * q + 1] * gq[1] + x[4 * q + 2] * gq[2] + x[4 * q + 3] * gq[3];
-          }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) da += gv[3 * HS + 4 * h + j] * ef[j];
-        da += gv[3 * HS + 12 + h];
-        da = ok ? da : 0.0f;
-        const float dot = lanes::sum32(av[h] * da);
-        dl[h] = ok ? av[h] * (da - dot) * a.scale : 0.0f;
-        dbeta[h] = lanes::sum32(dl[h]);
-      }
-      // ---- dqt_h = sum_c dl_h x_c (DPP form: transposed reductions now, stored after the sender gradients have
-      // read this row's dxcat; LDS form: an LDS loop over the candidates once the row is free)
-      constexpr int TF = lanes::tr_final<DM>();
-      float dqv[kH][TF];
-      int dq_base = 0, dq_cnt = 0;
-      if constexpr (!WSL) {
-#pragma unroll
-        for (int h = 0; h < kH; ++h) {
-          float v[DM];
-#pragma unroll
-          for (int d = 0; d < DM; ++d) v[d] = dl[h] * x[d];
-          dq_base = lanes::treduce32(v, dq_cnt);
-#pragma unroll
-          for (int j = 0; j < TF; ++j) dqv[h][j] = v[j];
-        }
-      }
-      // ---- sender gradient of this pair: sum_h a_h dxbar_h + dl_h qt_h
-      f32x4 cq[DM / 4];
-      const float* qt = qts + rl * QP;
-#pragma unroll
-      for (int q = 0; q < DM / 4; ++q) {
-        cq[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (q < TQ)
-#pragma unroll
-          for (int h = 0; h < kH; ++h)
-            cq[q] += av[h] * ((const f32x4*)(gv + HS * h))[q] + dl[h] * ((const f32x4*)(qt + HS * h))[q];
-      }
-      lanes::wave_sync();  // every lane of the row has read its dxcat row: it becomes the row's [dqt | dbeta]
-      {
-        float* o = a.dqt + row * (a.dqt_ld ? a.dqt_ld : (int64_t)kH * D);
-        float* ot = gs + rl * GP;
-        if constexpr (WSL) {
-          f32x4* pr = GP >= 128 ? (f32x4*)ot : (f32x4*)(lds + cv.pa) + wave * 64 + slot * 32;
-          pr[cc] = f32x4{dl[0], dl[1], dl[2], __int_as_float(ok ? gl * N + s : -1)};
-          lanes::wave_sync();
-          const int d = cc < D ? cc : 0;
-          float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-#pragma unroll 8
-          for (int k = 0; k < 32; ++k) {
-            if (k < C) {
-              const f32x4 P = pr[k];
-              const int node = __float_as_int(P[3]);
-              const float xv = node >= 0 ? xs[node * XP + d] : 0.0f;
-              s0 += P[0] * xv;
-              s1 += P[1] * xv;
-              s2 += P[2] * xv;
-            }
-          }
-          lanes::wave_sync();  // the pair slots are read: the row becomes [dqt | dbeta]
-          if (active && cc < D) {
-            o[cc] = s0, o[D + cc] = s1, o[2 * D + cc] = s2;
-            ot[cc] = s0, ot[D + cc] = s1, ot[2 * D + cc] = s2;
-          }
-        } else {
-#pragma unroll
-          for (int h = 0; h < kH; ++h)
-#pragma unroll
-            for (int j = 0; j < TF; ++j) {
-              const int q = dq_base + j;
-              if (active && j < dq_cnt && q < D) {
-                o[h * D + q] = dqv[h][j];
-                ot[h * D + q] = dqv[h][j];
-              }
-            }
-        }
-        if (active && cc < kH) {
-          const float b = cc == 0 ? dbeta[0] : cc == 1 ? dbeta[1] : dbeta[2];
-          a.dbeta[row * (a.dbeta_ld ? a.dbeta_ld : kH) + cc] = b;
-          ot[kH * D + cc] = b;
-        }
-      }
-      if (want_dxa && ok && s < n) {
-        float* dst = img + (lr * n + s) * DM;
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q)
-          if (q < TQ) ((f32x4*)dst)[q] = cq[q];
-      }
-      // ---- never-receivers' Dense_4 gradient: gacc[ct] += [x_raw | 1]^T dz over 16-pair chunks
-      if (want_pre) {
-        float xraw[kD0];
-        if constexpr (STAGE) {
-          const float* xr = raw + (gl * N + (viapre ? s : 0)) * kD0;
-#pragma unroll
-          for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? xr[k] : 0.0f;
-        } else {
-#pragma unroll
-          for (int k = 0; k < kD0; ++k) xraw[k] = viapre ? xg[k] : 0.0f;
-        }
-#pragma unroll 1
-        for (int ch = 0; ch < 4; ++ch) {
-          if (kq == ch) {
-            float* sp = ws + i16 * kPS;
-#pragma unroll
-            for (int q = 0; q < DM / 4; ++q) {
-              f32x4 dz;
-#pragma unroll
-              for (int j = 0; j < 4; ++j) dz[j] = (viapre && x[4 * q + j] > 0.0f) ? cq[q][j] : 0.0f;
-              ((f32x4*)sp)[q] = dz;
-            }
-            ((f32x4*)(sp + 32))[0] = f32x4{xraw[0], xraw[1], xraw[2], xraw[3]};
-            ((f32x4*)(sp + 32))[1] = f32x4{xraw[4], xraw[5], xraw[6], xraw[7]};
-            sp[40] = viapre ? 1.0f : 0.0f;
-          }
-          lanes::wave_sync();
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int pp = 4 * ks + kq;
-            const float av2 = i16 <= kD0 ? ws[pp * kPS + 32 + i16] : 0.0f;
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) gacc[ct] = mma(av2, ws[pp * kPS + 16 * ct + i16], gacc[ct]);
-          }
-          lanes::wave_sync();
-        }
-      }
-      if (want_dxa) {
-        __syncthreads();
-        // fold this sub-round's image into the block's dxa rows: target (graph gl, agent j), receivers i ascending
-        for (int t = tid; t < nrec * DM; t += 256) {
-          const int r = t / DM, d = t - r * DM;
-          const int g = r / n, j = r - g * n;
-          float acc = dxacc[t];
-          for (int ii = 0; ii < n; ++ii) {
-            const int src = g * n + ii - 8 * sr;
-            if (src >= 0 && src < 8) acc += img[(src * n + j) * DM + d];
-          }
-          dxacc[t] = acc;
-        }
-        __syncthreads();
-      }
-    }
-    // ---- stage 4: dxa = (senders' image + dY Wu^T) + [dqt | dbeta] QBW[:D]^T, mask -> global (agent mode)
-    if (want_dxa) {
-      __syncthreads();  // every row's [dqt | dbeta] is in gs
-      constexpr int KS = 25;  // k-steps over max(F, W) <= 99
-      const int ct = wave & 1, part = wave >> 1;
-      const int col = 16 * ct + i16;
-      const int K = part == 0 ? F : W;
-      float bv[KS], avv[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int k = 4 * ks + kq;
-        bv[ks] = k >= K ? 0.0f : (part == 0 ? p.Wu[(int64_t)col * F + k] : p.QBW[(int64_t)col * W + k]);
-        avv[ks] = (k >= K || i16 >= nrec) ? 0.0f : (part == 0 ? p.dY[(row0 + i16) * F + k] : gs[i16 * GP + k]);
-      }
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = mma(avv[ks], bv[ks], acc);
-      float* px = stg + part * 512;
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) px[(4 * kq + ii) * 32 + col] = acc[ii];
-      __syncthreads();
-      for (int t = tid; t < nrec * DM; t += 256) {
-        const int r = t / DM, d = t - r * DM;
-        float v = dxacc[t] + stg[r * 32 + d];
-        v = v + stg[512 + r * 32 + d];
-        if (p.mask) v = p.mask[(row0 + r) * DM + d] > 0.0f ? v : 0.0f;
-        a.dxa[(row0 + r) * DM + d] = v;
-      }
-    }
-    __syncthreads();
-  }
-  if (want_pre) {  // fixed-order combine of the 4 waves' accumulators -> this workgroup's partial row
-    float* red = stg;
-    for (int w = 0; w < 4; ++w) {
-      if (wave == w) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            float* dst = red + (4 * kq + ii) * 33 + 16 * ct + i16;
-            *dst = (w == 0 ? 0.0f : *dst) + gacc[ct][ii];
-          }
-      }
-      __syncthreads();
-    }
-    const int PK = a.D0 * D + D;
-    for (int o = tid; o < PK; o += 256) {
-      const int m = o < a.D0 * D ? o / D : kD0;
-      const int d = o < a.D0 * D ? o - m * D : o - a.D0 * D;
-      a.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * 33 + d];
-    }
-  }
-}
-
-bool bwd_supported(const dgppo_gnn_layer_bwd_args* p) {
-  const dgppo_gnn_attn_args& a = p->a;
-  if (a.H != kH || a.C < 1 || a.C > 32 || a.n_agents < 1 || a.n_agents > kRows || a.F < 1 || a.F > 64 || !a.sidx ||
-      !a.cand || !a.x || !a.ef || !a.qt || !a.attn || !a.dqt || !a.dbeta || !p->dY || !p->Wcat || a.G < 0 ||
-      a.N < a.n_agents || a.da_add || a.dx || a.dq)
-    return false;
-  if (((uintptr_t)a.ef & 15) || (a.ef_gstride & 3)) return false;
-  const int W = kH * a.D + kH;
-  if (a.qt_ld != 0 && a.qt_ld != W) return false;
-  if (a.xa == nullptr) {
-    if (a.D < 1 || a.D > 8 || a.pre_W || a.dxa || a.dpre_part) return false;
-  } else {
-    if (a.D != 32 || a.D0 < 1 || a.D0 > kD0 || !a.pre_W || !a.pre_b) return false;
-    if (((uintptr_t)a.xa & 15) || a.xa_gstride != (int64_t)a.n_agents * 32) return false;
-    if (a.dxa && (a.dxa_gstride != (int64_t)a.n_agents * 32 || !p->Wu || !p->QBW)) return false;
-  }
-  const int gpb = kRows / a.n_agents;
-  const bool st = lb::bwd_stage();
-  const lb::Carve c =
-      a.xa ? lb::carve<32>(gpb, a.N, a.n_agents, a.F, st) : lb::carve<8>(gpb, a.N, a.n_agents, a.F, st);
-  return (size_t)c.floats * sizeof(float) <= 80 * 1024;
-}
-
-int64_t bwd_grid(const dgppo_gnn_layer_bwd_args* p, int64_t* nblk) {
-  const int gpb = kRows / p->a.n_agents;
-  *nblk = ((int64_t)p->a.G + gpb - 1) / gpb;
-  const int64_t cap = p->a.xa ? lb::grid_cap<32>(lb::bwd_stage()) : lb::grid_cap<8>(lb::bwd_stage());
-  return *nblk < cap ? *nblk : cap;
-}
-
-}  // namespace
-}  // namespace dgppo
-
-extern "C" int dgppo_gnn_layer_bwd_supported(const dgppo_gnn_layer_bwd_args* p) {
-  return p && dgppo::bwd_supported(p) ? 1 : 0;
-}
-
-extern "C" int64_t dgppo_gnn_layer_bwd_partial_blocks(const dgppo_gnn_layer_bwd_args* p) {
-  if (!p || !dgppo::bwd_supported(p)) return 0;
-  int64_t nblk;
-  return dgppo::bwd_grid(p, &nblk);
-}
-
-extern "C" int dgppo_gnn_layer_bwd(const dgppo_gnn_layer_bwd_args* p, void* stream) {
-  using namespace dgppo;
-  if (!p || !bwd_supported(p)) return DGPPO_EINVAL;
-  const dgppo_gnn_attn_args& a = p->a;
-  if (a.G == 0) return 0;
-  const int gpb = kRows / a.n_agents;
-  int64_t nblk;
-  const unsigned grid = (unsigned)bwd_grid(p, &nblk);
-  hipStream_t s = (hipStream_t)stream;
-  const bool st = lb::bwd_stage(), wsl = st && wsum_lds();
-  const lb::Carve c = a.xa ? lb::carve<32>(gpb, a.N, a.n_agents, a.F, st) : lb::carve<8>(gpb, a.N, a.n_agents, a.F, st);
-  const size_t bytes = (size_t)c.floats * sizeof(float);
-#define GLB_LAUNCH(DMv, WSLv, STv)                                                                              \
-  do {                                                                                                          \
-    if (bytes > 64 * 1024) allow_lds((const void*)gnn_layer_bwd_kernel<DMv, WSLv, STv>);                       \
-    hipLaunchKernelGGL((gnn_layer_bwd_kernel<DMv, WSLv, STv>), dim3(grid), dim3(256), bytes, s, *p, gpb, nblk, c); \
-  } while (0)
-  if (a.xa) {
-    if (!st) GLB_LAUNCH(32, false, false);
-    else if (wsl) GLB_LAUNCH(32, true, true);
-    else GLB_LAUNCH(32, false, true);
-  } else {
-    if (!st) GLB_LAUNCH(8, false, false);
-    else if (wsl) GLB_LAUNCH(8, true, true);
-    else GLB_LAUNCH(8, false, true);
-  }
-#undef GLB_LAUNCH
-  return (int)hipGetLastError();
-}

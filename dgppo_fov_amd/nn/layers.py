@@ -36,10 +36,6 @@ FUSE_LN = os.environ.get("DGPPO_FUSE_LN", "1") == "1"
 # one GraphTransformer layer forward as ONE kernel ([qt | beta] GEMM + attention + message / update GEMMs, ABI 11
 # dgppo_gnn_layer_fwd) where it applies; DGPPO_FUSED_LAYER=0 runs the unfused chain (A/B, parity tests)
 FUSED_LAYER = os.environ.get("DGPPO_FUSED_LAYER", "1") == "1"
-# the fused layer BACKWARD (dgppo_gnn_layer_bwd: dxcat GEMM + attention backward + d xa GEMMs in one kernel) is
-# measured slower than attn_bwd2r + its GEMMs (668 vs ~516 us per D = 32 call at 2 workgroups per CU);
-# DGPPO_FUSED_LAYER_BWD=1 selects it (A/B, parity tests)
-FUSED_LAYER_BWD = os.environ.get("DGPPO_FUSED_LAYER_BWD", "0") == "1"
 
 
 # ---- parameter space ------------------------------------------------------------------------
@@ -759,42 +755,6 @@ class GraphTransformer:
         x = xfull if xfull is not None else g.nodes
         return x, dict(lda=self.D, a_grp=g.n, a_gs=g.N * self.D)
 
-    def _fused_bwd(self, cache, dY, g: "GraphBatch", mask_dxa: bool):
-        """dgppo_gnn_layer_bwd (dxcat GEMM + attention backward + the d xa GEMMs in one kernel) where it applies:
-        returns (True, d xa or None) after every gradient of the layer is accumulated, or (False, None)."""
-        xa, pre, QBW, QB, attn, xcat, xcx, Y, xfull = cache
-        if (not FUSED_LAYER or not FUSED_LAYER_BWD or xfull is not None or self.EX or QB is None or
-                (xa is not None and pre is None)):
-            return False, None
-        G, n, D, F, H, C = g.G, g.n, self.D, self.F, self.H, g.C
-        R, WQ = G * n, H * D + H
-        dev = dY.device
-        if xa is None:
-            x, x_gs, D0, pre_W, pre_b = g.nodes, g.N * g.nodes.shape[2], 0, None, None
-        else:
-            raw, cols = g.sender_raw
-            if cols is not None:
-                return False, None
-            x, x_gs, D0, pre_W, pre_b = raw, g.N * raw.shape[2], raw.shape[2], pre.v("Wu"), pre.v("bu")
-        dQB = torch.empty((R, WQ), device=dev)
-        dXa = torch.empty((R, D), device=dev) if xa is not None else None
-        mask = xa if (xa is not None and mask_dxa) else None
-        head = [[G, g.N, g.E, n, D, F, H, C, D0], g.cand, g.receivers, g.senders, g.sidx, x, x_gs, g.edges_head, g.E * 4,
-                1.0 / math.sqrt(F), xa, n * D, pre_W, pre_b, QB, attn, dY, QBW, self.v("Wcat"), self.v("Wu"), mask]
-        PK = D0 * D + D
-        nb = ops.gnn_layer_bwd_plan(*head, dQB, dXa, QB if pre is not None else None)  # (any non-null dpre probe)
-        if nb == 0:
-            return False, None
-        part = K.workspace(nb * PK, dev, "attn_pre") if (xa is not None and pre is not None) else None
-        torch.ops.dgppo.gnn_layer_bwd(*head, dQB, dXa, part)
-        if part is not None:
-            self._pre_grads(pre, g, part, nb, PK, D0)
-        K.gemm(xcat, dY, self.v("Wcat", True), H * (D + 5), F, R, ta=True, lda=H * (D + 5), alpha=1.0 / H, beta=1.0)
-        A, akw = self._rows_in(g, xa, None)
-        self._qfree_grads(A, akw, dQB, R)  # parameter gradients only
-        K.gemm(A, dY, self.v("Wu", True), D, F, R, ta=True, beta=1.0, bias_grad=self.v("bu", True), **akw)
-        return True, dXa
-
     def _pre_grads(self, pre, g, part, nb, PK, D0):
         """Sum the per-workgroup [Wu (D0 x D) | bu (D)] partial rows of the pre layer (Wu rows = the raw columns used)."""
         D, dev = self.D, part.device
@@ -848,10 +808,6 @@ class GraphTransformer:
         A, akw = self._rows_in(g, xa, xfull)
         if not masked:
             K.relu_bwd_(dY, Y)  # dY := dZ
-        done, dXa = self._fused_bwd(cache, dY, g, mask_dxa)
-        self.last_fused_bwd = done
-        if done:
-            return dXa
         dxcat = torch.empty((R, W), device=dev)
         K.gemm(dY, self.v("Wcat"), dxcat, R, W, F, tb=True, ldb=F, alpha=1.0 / H)
         K.gemm(xcat, dY, self.v("Wcat", True), W, F, R, ta=True, lda=W, alpha=1.0 / H, beta=1.0)

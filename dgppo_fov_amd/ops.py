@@ -338,48 +338,6 @@ def _gnn_layer_fwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, 
     return None
 
 
-def _layer_bwd_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride, pre_W,
-                      pre_b, qb, attn, dY, QBW, Wcat, Wu, mask, dqb, dxa, dpre_part) -> _lib.GnnLayerBwdArgs:
-    la = _lib.GnnLayerBwdArgs()
-    la.a = _attn_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, None, qb, None, scale, xa,
-                        xa_gstride, pre_W, pre_b)
-    W = int(dims[6]) * int(dims[4]) + int(dims[6])
-    la.a.qt_ld, la.a.dqt_ld, la.a.dbeta_ld = W, W, W
-    la.a.attn, la.a.dqt = _p(attn), _p(dqb)
-    la.a.dbeta = (_p(dqb) + 4 * int(dims[6]) * int(dims[4])) if dqb is not None else None
-    la.a.dxa, la.a.dxa_gstride, la.a.dpre_part = _p(dxa), int(dims[3]) * int(dims[4]), _p(dpre_part)
-    la.dY, la.QBW, la.Wcat, la.Wu, la.mask = _p(dY), _p(QBW), _p(Wcat), _p(Wu), _p(mask)
-    return la
-
-
-def gnn_layer_bwd_plan(*args) -> int:
-    """Rows of the dpre_part workspace gnn_layer_bwd writes (0: the fused backward does not cover the call)."""
-    la = _layer_bwd_struct(*args)
-    lib = _lib.load()
-    return int(lib.dgppo_gnn_layer_bwd_partial_blocks(ctypes.byref(la))) if lib.dgppo_gnn_layer_bwd_supported(
-        ctypes.byref(la)) else 0
-
-
-@torch.library.custom_op("dgppo::gnn_layer_bwd", mutates_args=("dqb", "dxa", "dpre_part"))
-def gnn_layer_bwd(dims: List[int], cand: Tensor, receivers: Tensor, senders: Tensor, sidx: Tensor, x: Tensor,
-                  x_gstride: int, ef: Tensor, ef_gstride: int, scale: float, xa: Optional[Tensor], xa_gstride: int,
-                  pre_W: Optional[Tensor], pre_b: Optional[Tensor], qb: Tensor, attn: Tensor, dY: Tensor, QBW: Tensor,
-                  Wcat: Tensor, Wu: Tensor, mask: Optional[Tensor], dqb: Tensor, dxa: Optional[Tensor],
-                  dpre_part: Optional[Tensor]) -> None:
-    """Backward of gnn_layer_fwd's attention and dense layers given dY (ReLU gate applied): dqb = [dqt | dbeta] rows,
-    in agent mode dxa (overwritten; ReLU-masked by `mask`) and the pre-layer partial rows (nn/layers.py)."""
-    _lib.require_gpu(dY.device, "dgppo::gnn_layer_bwd")
-    la = _layer_bwd_struct(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride,
-                           pre_W, pre_b, qb, attn, dY, QBW, Wcat, Wu, mask, dqb, dxa, dpre_part)
-    _lib.check(_lib.load().dgppo_gnn_layer_bwd(ctypes.byref(la), _stream(dY)), "dgppo_gnn_layer_bwd")
-
-
-@gnn_layer_bwd.register_fake
-def _gnn_layer_bwd_fake(dims, cand, receivers, senders, sidx, x, x_gstride, ef, ef_gstride, scale, xa, xa_gstride,
-                        pre_W, pre_b, qb, attn, dY, QBW, Wcat, Wu, mask, dqb, dxa, dpre_part) -> None:
-    return None
-
-
 # ---- GAE, clip + Adam ------------------------------------------------------------------------------------
 @torch.library.custom_op("dgppo::gae", mutates_args=("Qh", "Ql"))
 def gae(hs: Tensor, l: Tensor, Vh: Tensor, Vl: Tensor, Qh: Tensor, Ql: Tensor, gamma: float, lam: float) -> None:

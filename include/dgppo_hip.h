@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DGPPO_ABI_VERSION 13  /* 13: dgppo_gemm_wgrad_grouped (a pass's weight gradients in one launch); 12: dgppo_adam_multi (the clipped Adam steps of several nets in two launches); 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
+#define DGPPO_ABI_VERSION 14  /* 14: dgppo_gnn_layer_bwd removed (the fused layer backward measured slower than the attention backward + GEMMs), dgppo_gnn_set_attn_kernel removed with the graph-form MFMA attention kernels (2-5x slower); 13: dgppo_gemm_wgrad_grouped (a pass's weight gradients in one launch); 12: dgppo_adam_multi (the clipped Adam steps of several nets in two launches); 11: dgppo_gnn_layer_fwd (fused GraphTransformer layer forward); 10: in-kernel policy-step noise, dgppo_gnn_set_graph_otf; 9: dgppo_gnn_set_attn_kernel (graph-form MFMA attention selector); 8: VMAS engines (DGPPO_ENGINE_VMAS_*) through the dgppo_env_* entry points; 7: dgppo_lstm_cell_fwd / _bwd; 6: env variants (dgppo_env_cfg variant fields); 5: Q-free attention args (beta, qt/dqt/dbeta strides), dgppo_gather_env_steps; 4: dgppo_env_rollout, dgppo_env_reset_states; 3: dgppo_adam takes double b1 / b2; 2: dgppo_gnn_attn_args.da_add, wide-edge entry points, env cfg Omni fields */
 #define DGPPO_EINVAL (-22)
 
 /* engines */
@@ -309,11 +309,6 @@ typedef struct dgppo_gnn_attn_args {
 } dgppo_gnn_attn_args;
 
 int64_t dgppo_gnn_attn_partial_blocks(const dgppo_gnn_attn_args* args);
-/* Attention-kernel selection (no reference counterpart; A/B and kernel-vs-kernel parity tests): 1 = the graph-form
- * MFMA kernels where they apply (graphs of N <= 96 nodes, n <= 10 agents), 0 = the row-block / graph / generic
- * kernels everywhere (the default: measured faster).  Returns the previous mode or DGPPO_EINVAL.  Initial mode:
- * DGPPO_ATTN_GM=1|0 (default 0). */
-int dgppo_gnn_set_attn_kernel(int mode);
 /* ABI 10, tuning / testing hook: 1 (default) = the graph-form forward computes each receiver's own
  * never-receiver rows on the fly (Lidar layout, D = 32 agent mode with pre_W: only agent and goal rows staged
  * in LDS), 0 = every row staged; bit-identical either way.  Process-wide; also DGPPO_ATTN_GRAPH_OTF=0|1. */
@@ -363,27 +358,6 @@ typedef struct dgppo_gnn_layer_args {
 } dgppo_gnn_layer_args;
 int dgppo_gnn_layer_supported(const dgppo_gnn_layer_args* args);
 int dgppo_gnn_layer_fwd(const dgppo_gnn_layer_args* args, void* stream);
-
-/* ABI 11: the backward of dgppo_gnn_layer_fwd's attention and of the two dense layers around it as ONE kernel,
- * given dY = dL/dY with the layer's ReLU gate applied: dxcat = dY Wcat^T / H (in the kernel, never stored), the
- * softmax / attention backward of dgppo_gnn_attn_bwd (a.dqt, a.dbeta written, [dqt | dbeta] rows with a.dqt_ld /
- * a.dbeta_ld), the never-receivers' pre_W / pre_b gradient partials (a.dpre_part, one row of D0*D + D per
- * workgroup: dgppo_gnn_layer_bwd_partial_blocks rows; sum them with dgppo_colsum) and, in agent mode with a.dxa,
- *   dxa = (sum of the agent senders' gradients) + dY Wu^T + [dqt | dbeta] QBW[:D]^T, then dxa *= (mask > 0)
- * (OVERWRITTEN, not accumulated; mask = the previous layer's ReLU output, or NULL).  a.qt = the forward's
- * [qt | beta] rows (a.qt_ld = H*D + H); a.attn = the forward's attention.  The weight gradients (xcat^T dY,
- * [x 1]^T [dqt | dbeta], x^T dY) stay GEMMs.  Same scope as dgppo_gnn_layer_fwd (dgppo_gnn_layer_bwd_supported). */
-typedef struct dgppo_gnn_layer_bwd_args {
-  dgppo_gnn_attn_args a;
-  const float* dY;    /* (G*n, F) */
-  const float* QBW;   /* (D+1, H*D + H) */
-  const float* Wcat;  /* (H*(D+5), F) */
-  const float* Wu;    /* (D, F) */
-  const float* mask;  /* optional (G*n, D) */
-} dgppo_gnn_layer_bwd_args;
-int dgppo_gnn_layer_bwd_supported(const dgppo_gnn_layer_bwd_args* args);
-int64_t dgppo_gnn_layer_bwd_partial_blocks(const dgppo_gnn_layer_bwd_args* args);
-int dgppo_gnn_layer_bwd(const dgppo_gnn_layer_bwd_args* args, void* stream);
 
 /* Edge features wider than 4 (LidarOmniTarget's 10-wide edges, lidar_omni_target.py edge_dim): the attention
  * kernels see columns 0..3, the remaining EX columns efx (G, E, EX) go through these two.

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.dgppo_abi_version() == 13
+    assert lib.dgppo_abi_version() == 14
     assert b"gfx950" in lib.dgppo_build_info()
 
 
@@ -56,7 +56,6 @@ def _c_layout(struct, fields):
                                             (_lib.GnnAttnArgs, "dgppo_gnn_attn_args"),
                                             (_lib.GnnLayerArgs, "dgppo_gnn_layer_args"),
                                             (_lib.GnnValueTail, "dgppo_gnn_value_tail"),
-                                            (_lib.GnnLayerBwdArgs, "dgppo_gnn_layer_bwd_args"),
                                             (_lib.TanhNormalArgs, "dgppo_tanh_normal_args"),
                                             (_lib.GaeArgs, "dgppo_gae_args"),
                                             (_lib.AdvArgs, "dgppo_adv_args"),

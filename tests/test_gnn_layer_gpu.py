@@ -83,26 +83,27 @@ def test_fused_layer_falls_back_outside_its_scope(cuda, eid, n, obs):
 
 
 def _grads(net, g, dz, fused):
-    old, oldb = layers.FUSED_LAYER, layers.FUSED_LAYER_BWD
-    layers.FUSED_LAYER = layers.FUSED_LAYER_BWD = fused
+    old = layers.FUSED_LAYER
+    layers.FUSED_LAYER = fused
     try:
         net.ps.zero_grad()
         z, c = net.gnn.fwd(g)
-        net.gnn.bwd(c, dz.clone(), g)
         for L in net.gnn.layers:
-            assert L.last_fused_bwd == fused, "fused backward not taken" if fused else "unfused backward expected"
+            assert L.last_fused == fused, "fused forward not taken" if fused else "unfused forward expected"
+        net.gnn.bwd(c, dz.clone(), g)
         torch.cuda.synchronize()
         return net.ps.grad.clone()
     finally:
-        layers.FUSED_LAYER, layers.FUSED_LAYER_BWD = old, oldb
+        layers.FUSED_LAYER = old
 
 
 @pytest.mark.parametrize("eid,n,obs", [("LidarSpread", 8, 3), ("LidarSpread", 3, 2), ("MPESpread", 3, 3),
                                        ("LidarBicycleTarget", 8, 3), ("LidarSpread", 5, 1)])
-def test_fused_layer_backward_matches_unfused_chain(cuda, eid, n, obs):
-    """dgppo_gnn_layer_bwd (dxcat GEMM + attention backward + d xa GEMMs in one kernel): every GNN parameter
-    gradient of the 2-layer actor GNN (agent-mode second layer: pre-layer partials, the previous layer's ReLU
-    mask, agent-sender sums) and the 1-layer Vh GNN within fp32 rounding of the unfused chain."""
+def test_backward_through_fused_forward_matches_unfused_chain(cuda, eid, n, obs):
+    """The backward (attn_bwd2r + GEMMs) from the fused forward's cache ([qt | beta], attention, xcat written by
+    dgppo_gnn_layer_fwd): every GNN parameter gradient of the 2-layer actor GNN (agent-mode second layer: the
+    compacted pre-layer gradient, the previous layer's ReLU mask, agent-sender sums) and the 1-layer Vh GNN within
+    fp32 rounding of the fully unfused chain."""
     env, g = _batch(cuda, eid, n, obs)
     gen = torch.Generator(device=cuda).manual_seed(5)
     for net in (ActorNet(env.node_dim, n, cuda, seed=3, edge_dim=env.edge_dim),
