@@ -1029,201 +1029,7 @@ constexpr size_t lds_floats() {
 }
 }  // namespace fwd2
 
-template <int DM>
-__global__ __launch_bounds__(256) void attn_fwd2_kernel(dgppo_gnn_attn_args p) {
-  using lanes::f32x4;
-  using lanes::wave_sync;
-  constexpr int kRows = fwd2::kRows, kSR = fwd2::kSR, kQP = fwd2::kQP;
-  constexpr int kXSP = fwd2::Pitch<DM>::XSP, EC = fwd2::Pitch<DM>::EC;
-  static_assert(DM == 8 || DM == 16 || DM == 32, "fwd2 instantiations");
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* qts = lds;                 // [16][100]: qt_h (32-float stride per head) | beta_h at 96 + h
-  float* preW = qts + kRows * kQP;  // [8][32]
-  float* preb = preW + kD0 * 32;    // [32]
-  float* att = preb + 32;           // per wave: xs [64][kXSP] | aa [64][4]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int slot = lane >> 5, c = lane & 31;
-  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = kH;
-  const int nrows = p.G * n;
-  const int row0 = blockIdx.x * kRows;
-  const bool agent = p.xa != nullptr;
-  const bool pre = DM == 32 && agent && p.pre_W != nullptr;  // the launcher sends pre mode to DM = 32
-  // ---- gathers of both sub-rounds
-  float xv[kSR][DM];
-  f32x4 efv[kSR];
-  int sv[kSR];
-#pragma unroll
-  for (int sr = 0; sr < kSR; ++sr) {
-    const int row = row0 + 2 * wave + 8 * sr + slot;
-    const bool active = row < nrows;
-    const int g = active ? row / n : 0;
-    const int i = active ? row - g * n : 0;
-    int s = -1, e = 0;
-    if (active && c < C) {
-      e = p.cand[i * C + c];
-      s = p.sidx[(int64_t)row * C + c];
-    }
-    const bool ok = s >= 0;
-    sv[sr] = s;
-    const float* er = p.ef + (int64_t)g * p.ef_gstride + (int64_t)(ok ? e : 0) * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) efv[sr][j] = ok ? er[j] : 0.0f;
-    if (!agent) {
-      load_row<DM>(p.x + (int64_t)g * p.x_gstride + (int64_t)(ok ? s : 0) * D, D, ok, xv[sr]);
-    } else if (!ok || s < n) {
-      load_row<DM>(p.xa + (int64_t)g * p.xa_gstride + (int64_t)(ok ? s : 0) * D, D, ok, xv[sr]);
-    } else {
-      const float* xr = p.x + (int64_t)g * p.x_gstride + (int64_t)s * p.D0;
-#pragma unroll
-      for (int k = 0; k < DM; ++k) xv[sr][k] = (k < kD0 && k < p.D0) ? xr[k < kD0 ? k : 0] : 0.0f;
-    }
-  }
-  // ---- stage qt (zero padded per head), beta_h = q_h . bk_h, pre weights
-  for (int e = threadIdx.x; e < kRows * 96; e += 256) {
-    const int r = e / 96, k = e - r * 96, h = k >> 5, d = k & 31;
-    qts[r * kQP + k] = (row0 + r < nrows && d < D) ? p.qt[(int64_t)(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
-  }
-  {
-    const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
-    const bool act = row0 + r < nrows;
-#pragma unroll
-    for (int h = 0; h < kH; ++h) {
-      float acc = 0.0f;
-      if (act)
-        acc = q_dot_bk(p, (int64_t)(row0 + r), h, j, 16);
-      acc = lanes::sum16(acc);
-      if (j == 0) qts[r * kQP + 96 + h] = acc;
-    }
-  }
-  if (pre) {
-    const int k = threadIdx.x >> 5, d = threadIdx.x & 31;
-    preW[threadIdx.x] = (k < p.D0 && d < D) ? p.pre_W[k * D + d] : 0.0f;
-    if (threadIdx.x < 32) preb[threadIdx.x] = threadIdx.x < D ? p.pre_b[threadIdx.x] : 0.0f;
-  }
-  __syncthreads();
-  float pw[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}}, pb[2] = {0.0f, 0.0f};
-  if (pre) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) pw[ks][ct] = preW[(4 * ks + kq) * 32 + 16 * ct + i16];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) pb[ct] = preb[16 * ct + i16];
-  }
-  float* xs = att + wave * fwd2::Pitch<DM>::AW;
-  float* aa = xs + 64 * kXSP;
-  const int pr = slot * 32 + c;
-  float* xp = xs + pr * kXSP;
-  const int TQ = (D + 3) >> 2, Th = TQ + 2, W = H * (D + 5);
-  int th = 0, tq = c;  // this lane's weighted-sum task: head th, column block tq
-  while (tq >= Th && th < kH) {
-    tq -= Th;
-    ++th;
-  }
-#pragma unroll
-  for (int sr = 0; sr < kSR; ++sr) {
-    const int rl = 2 * wave + 8 * sr + slot;
-    const int row = row0 + rl;
-    const bool active = row < nrows;
-    const int s = sv[sr];
-    const bool ok = s >= 0;
-    if (pre) {
-      const bool viapre = ok && s >= n;
-#pragma unroll
-      for (int k = 0; k < kD0; ++k) xp[k] = viapre ? xv[sr][k < DM ? k : 0] : 0.0f;
-      wave_sync();
-      float a[4][2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a[t][ks] = xs[(16 * t + i16) * kXSP + 4 * ks + kq];
-      f32x4 pacc[4][2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          pacc[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            pacc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][ks], pw[ks][ct], pacc[t][ct], 0, 0, 0);
-        }
-      wave_sync();
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float v = pacc[t][ct][i] + pb[ct];
-            xs[(16 * t + 4 * kq + i) * kXSP + 16 * ct + i16] = v > 0.0f ? v : 0.0f;
-          }
-      wave_sync();
-      if (!viapre) {
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q)
-          ((f32x4*)xp)[q] = f32x4{xv[sr][4 * q], xv[sr][4 * q + 1], xv[sr][4 * q + 2], xv[sr][4 * q + 3]};
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < DM / 4; ++q)
-        ((f32x4*)xp)[q] = f32x4{xv[sr][4 * q], xv[sr][4 * q + 1], xv[sr][4 * q + 2], xv[sr][4 * q + 3]};
-    }
-    *(f32x4*)(xp + EC) = efv[sr];
-    wave_sync();
-    // logits, softmax over the row's candidates, attention weights out
-    const float* qt = qts + rl * kQP;
-    float aw[kH];
-#pragma unroll
-    for (int h = 0; h < kH; ++h) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int q = 0; q < DM / 4; ++q)
-        if (q < TQ) {
-          const f32x4 xq = ((const f32x4*)xp)[q], qq = ((const f32x4*)(qt + 32 * h))[q];
-          acc += xq[0] * qq[0] + xq[1] * qq[1] + xq[2] * qq[2] + xq[3] * qq[3];
-        }
-      const float lg = ok ? (acc + qt[96 + h]) * p.scale : -INFINITY;
-      const float mx = lanes::max32(lg);
-      const float ex = ok ? expf(lg - mx) : 0.0f;
-      const float sm = lanes::sum32(ex);
-      aw[h] = ok ? ex / sm : 0.0f;
-      if (active && c < C && p.attn) p.attn[((int64_t)row * H + h) * C + c] = aw[h];
-    }
-#pragma unroll
-    for (int h = 0; h < kH; ++h) aa[pr * 4 + h] = aw[h];
-    wave_sync();
-    // xcat row = [xbar_h | ebar_h | sig_h]
-    if (active && th < kH) {
-      const float* xb = xs + slot * 32 * kXSP;
-      const float* ab = aa + slot * 32 * 4 + th;
-      float* o = p.xcat + (int64_t)row * W;
-      if (tq <= TQ) {
-        const int col = tq < TQ ? 4 * tq : EC;
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 8
-        for (int cc = 0; cc < 32; ++cc) acc += ab[cc * 4] * *(const f32x4*)(xb + cc * kXSP + col);
-        if (tq < TQ) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * tq + j < D) o[th * D + 4 * tq + j] = acc[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[H * D + 4 * th + j] = acc[j];
-        }
-      } else {
-        float acc = 0.0f;
-#pragma unroll 8
-        for (int cc = 0; cc < 32; ++cc) acc += ab[cc * 4];
-        o[H * D + 4 * H + th] = acc;
-      }
-    }
-    wave_sync();
-  }
-}
-
-// Register form of the row-block forward (the default; DGPPO_ATTN_FWD2=lds keeps the LDS-staged
-// kernel above): each lane's pair row x stays in registers (pre mode: relu(x_raw pre_W + pre_b) by VALU
+// Register form of the row-block forward (round 6: the LDS-staged form it replaced is removed): each lane's pair row x stays in registers (pre mode: relu(x_raw pre_W + pre_b) by VALU
 // FMAs against the LDS-resident pre_W), and the attention-weighted sums over the row's 32 candidates --
 // xbar_h per head, [ebar_h | sig_h] of all heads -- are transposed DPP reductions (lanes::treduce32)
 // whose totals each lane stores to its row of xcat.  LDS holds only the block's qt / beta rows and
@@ -1395,23 +1201,10 @@ void fwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const int64_t rows = (int64_t)p->G * p->n_agents;
   const unsigned grid = (unsigned)((rows + fwd2::kRows - 1) / fwd2::kRows);
   const bool no_pre = !(p->xa && p->pre_W);
-  static const bool reg = [] {
-    const char* e = getenv("DGPPO_ATTN_FWD2");
-    return !(e && strcmp(e, "lds") == 0);
-  }();
-  if (reg) {
-    const size_t bytes = ((size_t)fwd2::kRows * fwd2::kQP + kD0 * 32 + 32) * sizeof(float);
-    if (p->D <= 8 && no_pre) hipLaunchKernelGGL(attn_fwd2r_kernel<8>, dim3(grid), dim3(256), bytes, s, *p);
-    else if (p->D <= 16 && no_pre) hipLaunchKernelGGL(attn_fwd2r_kernel<16>, dim3(grid), dim3(256), bytes, s, *p);
-    else hipLaunchKernelGGL(attn_fwd2r_kernel<32>, dim3(grid), dim3(256), bytes, s, *p);
-    return;
-  }
-  if (p->D <= 8 && no_pre)
-    hipLaunchKernelGGL(attn_fwd2_kernel<8>, dim3(grid), dim3(256), fwd2::lds_floats<8>() * sizeof(float), s, *p);
-  else if (p->D <= 16 && no_pre)  // e.g. LidarOmniTarget's 10-wide first layer
-    hipLaunchKernelGGL(attn_fwd2_kernel<16>, dim3(grid), dim3(256), fwd2::lds_floats<16>() * sizeof(float), s, *p);
-  else
-    hipLaunchKernelGGL(attn_fwd2_kernel<32>, dim3(grid), dim3(256), fwd2::lds_floats<32>() * sizeof(float), s, *p);
+  const size_t bytes = ((size_t)fwd2::kRows * fwd2::kQP + kD0 * 32 + 32) * sizeof(float);
+  if (p->D <= 8 && no_pre) hipLaunchKernelGGL(attn_fwd2r_kernel<8>, dim3(grid), dim3(256), bytes, s, *p);
+  else if (p->D <= 16 && no_pre) hipLaunchKernelGGL(attn_fwd2r_kernel<16>, dim3(grid), dim3(256), bytes, s, *p);  // e.g. Omni's 10-wide first layer
+  else hipLaunchKernelGGL(attn_fwd2r_kernel<32>, dim3(grid), dim3(256), bytes, s, *p);
 }
 
 // ================================================================================================
@@ -1440,285 +1233,7 @@ size_t lds_floats(int n, int D) {
 }
 }  // namespace bwd2
 
-template <int DM>
-__global__ __launch_bounds__(256) void attn_bwd2_kernel(dgppo_gnn_attn_args p, int64_t nblk) {
-  using lanes::f32x4;
-  using lanes::wave_sync;
-  using LY = bwd2::Lay<DM>;
-  constexpr int kRows = bwd2::kRows, kSR = bwd2::kSR, HS = LY::HS, kQP = LY::QP, kGP = LY::GP, kXSP = LY::XSP;
-  static_assert(DM == 8 || DM == 16 || DM == 32, "bwd2 instantiations");
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* qts = lds;                 // [16][QP]: qt_h (HS-float stride per head)
-  float* gs = qts + kRows * kQP;    // [16][GP]: dxbar_h (HS stride) | debar (3HS..+12) | dsig (3HS+12..+3)
-  float* preW = gs + kRows * kGP;   // [8][32]
-  float* preb = preW + kD0 * 32;    // [32]
-  float* att = preb + 32;           // per wave: xs [64][XSP] (x | x_raw | 1) | aw [64][4]
-  float* cbi = att + 4 * LY::AW;    // [rows][n][D] agent-sender contributions
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int slot = lane >> 5, c = lane & 31;
-  const int n = p.n_agents, D = p.D, F = p.F, C = p.C, H = kH;
-  const int gpb = kRows / n;
-  const bool agent = p.xa != nullptr;
-  const bool pre = DM == 32 && agent && p.pre_W != nullptr;  // the launcher sends pre mode to DM = 32
-  const bool want_dxa = agent && p.dxa != nullptr;
-  const bool want_pre = pre && p.dpre_part != nullptr;
-  if (pre) {
-    const int k = threadIdx.x >> 5, d = threadIdx.x & 31;
-    preW[threadIdx.x] = (k < p.D0 && d < D) ? p.pre_W[k * D + d] : 0.0f;
-    if (threadIdx.x < 32) preb[threadIdx.x] = threadIdx.x < D ? p.pre_b[threadIdx.x] : 0.0f;
-  }
-  __syncthreads();
-  float pw[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}}, pb[2] = {0.0f, 0.0f};
-  if (pre) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) pw[ks][ct] = preW[(4 * ks + kq) * 32 + 16 * ct + i16];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) pb[ct] = preb[16 * ct + i16];
-  }
-  f32x4 gacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};  // [x_raw | 1]^T dz
-  float* xs = att + wave * LY::AW;
-  float* aw = xs + 64 * kXSP;
-  const int pr = slot * 32 + c;
-  float* xp = xs + pr * kXSP;
-  const int TQ = (D + 3) >> 2, W = H * (D + 5);
-  const int tk_h = c >> 3, tk_q = c & 7;  // dqt task: head, float4 column block
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int64_t g0 = blk * gpb;
-    const int ng = (int)((int64_t)p.G - g0 < gpb ? (int64_t)p.G - g0 : gpb);
-    const int nrec = ng * n;
-    const int64_t row0 = g0 * n;
-    // ---- per-lane pair data of both sub-rounds
-    float xv[kSR][DM];
-    f32x4 efv[kSR];
-    float av[kSR][kH];
-    int sv[kSR];
-#pragma unroll
-    for (int sr = 0; sr < kSR; ++sr) {
-      const int rl = 2 * wave + 8 * sr + slot;
-      const bool active = rl < nrec;
-      const int gl = active ? rl / n : 0;
-      const int i = active ? rl - gl * n : 0;
-      const int64_t g = g0 + gl, row = row0 + rl;
-      int s = -1, e = 0;
-      if (active && c < C) {
-        e = p.cand[i * C + c];
-        s = p.sidx[row * C + c];
-      }
-      const bool ok = s >= 0;
-      sv[sr] = s;
-#pragma unroll
-      for (int h = 0; h < kH; ++h) av[sr][h] = ok ? p.attn[(row * H + h) * C + c] : 0.0f;
-      const float* er = p.ef + g * p.ef_gstride + (int64_t)(ok ? e : 0) * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) efv[sr][j] = ok ? er[j] : 0.0f;
-      if (!agent) {
-        load_row<DM>(p.x + g * p.x_gstride + (int64_t)(ok ? s : 0) * D, D, ok, xv[sr]);
-      } else if (!ok || s < n) {
-        load_row<DM>(p.xa + g * p.xa_gstride + (int64_t)(ok ? s : 0) * D, D, ok, xv[sr]);
-      } else {
-        const float* xr = p.x + g * p.x_gstride + (int64_t)s * p.D0;
-#pragma unroll
-        for (int k = 0; k < DM; ++k) xv[sr][k] = (k < kD0 && k < p.D0) ? xr[k < kD0 ? k : 0] : 0.0f;
-      }
-    }
-    // ---- block staging: qt rows, dxcat rows (split at aligned offsets), agent image cleared
-    for (int e = threadIdx.x; e < kRows * 3 * HS; e += 256) {
-      const int r = e / (3 * HS), k = e - r * (3 * HS), h = k / HS, d = k - h * HS;
-      qts[r * kQP + k] = (r < nrec && d < D) ? p.qt[(row0 + r) * qt_ld(p) + h * D + d] : 0.0f;
-    }
-    for (int e = threadIdx.x; e < kRows * kGP; e += 256) {
-      const int r = e / kGP, k = e - r * kGP;
-      int src = -1;
-      if (k < 3 * HS) src = (k % HS) < D ? (k / HS) * D + (k % HS) : -1;
-      else if (k < 3 * HS + 12) src = H * D + (k - 3 * HS);
-      else if (k < 3 * HS + 15) src = H * D + 4 * H + (k - 3 * HS - 12);
-      gs[e] = (r < nrec && src >= 0) ? p.dxcat[(row0 + r) * W + src] : 0.0f;
-    }
-    if (want_dxa)
-      for (int e = threadIdx.x; e < kRows * n * D; e += 256) cbi[e] = 0.0f;
-    __syncthreads();
-#pragma unroll
-    for (int sr = 0; sr < kSR; ++sr) {
-      const int rl = 2 * wave + 8 * sr + slot;
-      const bool active = rl < nrec;
-      const int64_t row = row0 + rl;
-      const int s = sv[sr];
-      const bool ok = s >= 0;
-      const bool viapre = pre && ok && s >= n;
-      // x of the pair (transformed senders recomputed) and, in pre mode, its raw row
-      if (pre) {
-#pragma unroll
-        for (int k = 0; k < kD0; ++k) xp[k] = viapre ? xv[sr][k < DM ? k : 0] : 0.0f;
-        wave_sync();
-        float a[4][2];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) a[t][ks] = xs[(16 * t + i16) * kXSP + 4 * ks + kq];
-        f32x4 pacc[4][2];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) {
-            pacc[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-              pacc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][ks], pw[ks][ct], pacc[t][ct], 0, 0, 0);
-          }
-        wave_sync();
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float v = pacc[t][ct][i] + pb[ct];
-              xs[(16 * t + 4 * kq + i) * kXSP + 16 * ct + i16] = v > 0.0f ? v : 0.0f;
-            }
-        wave_sync();
-        if (!viapre) {
-#pragma unroll
-          for (int q = 0; q < DM / 4; ++q)
-            ((f32x4*)xp)[q] = f32x4{xv[sr][4 * q], xv[sr][4 * q + 1], xv[sr][4 * q + 2], xv[sr][4 * q + 3]};
-        }
-#pragma unroll
-        for (int k = 0; k < kD0; ++k) xp[32 + k] = viapre ? xv[sr][k < DM ? k : 0] : 0.0f;
-        xp[40] = viapre ? 1.0f : 0.0f;
-      } else {
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q)
-          ((f32x4*)xp)[q] = f32x4{xv[sr][4 * q], xv[sr][4 * q + 1], xv[sr][4 * q + 2], xv[sr][4 * q + 3]};
-      }
-      wave_sync();
-      // softmax backward
-      const float* gv = gs + rl * kGP;
-      float dl[kH], dbeta[kH];
-#pragma unroll
-      for (int h = 0; h < kH; ++h) {
-        float da = 0.0f;
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q)
-          if (q < TQ) {
-            const f32x4 xq = ((const f32x4*)xp)[q], gq = ((const f32x4*)(gv + HS * h))[q];
-            da += xq[0] * gq[0] + xq[1] * gq[1] + xq[2] * gq[2] + xq[3] * gq[3];
-          }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) da += gv[3 * HS + 4 * h + j] * efv[sr][j];
-        da += gv[3 * HS + 12 + h];
-        if (p.da_add && ok) da += p.da_add[(row * H + h) * C + c];
-        da = ok ? da : 0.0f;
-        const float dot = lanes::sum32(av[sr][h] * da);
-        dl[h] = ok ? av[sr][h] * (da - dot) * p.scale : 0.0f;
-        dbeta[h] = lanes::sum32(dl[h]);
-      }
-      if (active) {
-        if (c < kH) p.dbeta[row * dbeta_ld(p) + c] = c == 0 ? dbeta[0] : c == 1 ? dbeta[1] : dbeta[2];
-        for (int kk = c; kk < H * F; kk += 32) {
-          const int h = kk / F;
-          if (p.dq) p.dq[row * H * F + kk] = (h == 0 ? dbeta[0] : h == 1 ? dbeta[1] : dbeta[2]) * p.bk[kk];
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < kH; ++h) aw[pr * 4 + h] = dl[h];
-      // sender gradient of this pair
-      f32x4 cq[DM / 4];
-      const float* qt = qts + rl * kQP;
-#pragma unroll
-      for (int q = 0; q < DM / 4; ++q) {
-        cq[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (q < TQ)
-#pragma unroll
-          for (int h = 0; h < kH; ++h)
-            cq[q] += av[sr][h] * ((const f32x4*)(gv + HS * h))[q] + dl[h] * ((const f32x4*)(qt + HS * h))[q];
-      }
-      wave_sync();
-      // dqt_h = sum_c dl_h x_c
-      if (active && tk_h < kH && tk_q < TQ) {
-        const float* xb = xs + slot * 32 * kXSP;
-        const float* ab = aw + slot * 32 * 4 + tk_h;
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 8
-        for (int cc = 0; cc < 32; ++cc) acc += ab[cc * 4] * *(const f32x4*)(xb + cc * kXSP + 4 * tk_q);
-        float* o = p.dqt + row * dqt_ld(p) + tk_h * D;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (4 * tk_q + j < D) o[4 * tk_q + j] = acc[j];
-      }
-      if (want_dxa && ok && s < n) {
-        float* dst = cbi + (rl * n + s) * D;
-        if ((D & 3) == 0) {  // float4 rows (D-float stride): one wide store per column block
-#pragma unroll
-          for (int q = 0; q < DM / 4; ++q)
-            if (q < TQ) ((f32x4*)dst)[q] = cq[q];
-        } else {
-#pragma unroll
-          for (int q = 0; q < DM / 4; ++q)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (4 * q + j < D) dst[4 * q + j] = cq[q][j];
-        }
-      }
-      if (want_pre) {
-        wave_sync();  // the dqt readers of xs are done: x -> dz
-#pragma unroll
-        for (int q = 0; q < DM / 4; ++q) {
-          const f32x4 xq = ((const f32x4*)xp)[q];
-          f32x4 dz;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dz[j] = (viapre && xq[j] > 0.0f) ? cq[q][j] : 0.0f;
-          ((f32x4*)xp)[q] = dz;
-        }
-        wave_sync();
-        // gacc[ct] += [x_raw | 1]^T (rows m = i16: cols 32 + m, m <= 8) dz (cols 16 ct + i16), 64 pairs
-#pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
-          const int pp = 4 * ks + kq;
-          const float a = i16 <= kD0 ? xs[pp * kXSP + 32 + i16] : 0.0f;
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-            gacc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xs[pp * kXSP + 16 * ct + i16], gacc[ct], 0, 0, 0);
-        }
-      }
-      wave_sync();
-    }
-    __syncthreads();
-    if (want_dxa) {  // agent j of graph gl: sum over its receivers i in order
-      for (int e = threadIdx.x; e < nrec * D; e += 256) {
-        const int gl = e / (n * D), jd = e - gl * (n * D), j = jd / D, d = jd - j * D;
-        float acc = 0.0f;
-        for (int i = 0; i < n; ++i) acc += cbi[((gl * n + i) * n + j) * D + d];
-        p.dxa[(g0 + gl) * p.dxa_gstride + j * D + d] += acc;
-      }
-      __syncthreads();
-    }
-  }
-  if (want_pre) {  // fixed-order combine of the 4 waves' accumulators -> this workgroup's partial row
-    float* red = att;  // [16][33]
-    for (int w = 0; w < 4; ++w) {
-      if (wave == w) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float* dst = red + (4 * kq + i) * 33 + 16 * ct + i16;
-            *dst = (w == 0 ? 0.0f : *dst) + gacc[ct][i];
-          }
-      }
-      __syncthreads();
-    }
-    const int PK = p.D0 * D + D;
-    for (int o = threadIdx.x; o < PK; o += 256) {
-      const int m = o < p.D0 * D ? o / D : kD0;
-      const int d = o < p.D0 * D ? o - m * D : o - p.D0 * D;
-      p.dpre_part[(int64_t)blockIdx.x * PK + o] = red[m * 33 + d];
-    }
-  }
-}
-
-// Register form of the row-block backward (the default; DGPPO_ATTN_BWD2=lds keeps the kernel above): a
+// Register form of the row-block backward (round 6: the LDS-staged form it replaced is removed): a
 // lane's pair row x stays in registers (pre mode: relu(x_raw pre_W + pre_b) by VALU FMAs against the
 // LDS-resident pre_W), da / dl / dbeta and the sender gradient are lane-local math against the row's
 // LDS-staged dxbar / qt, dqt_h = sum_c dl_h x_c is one transposed DPP reduction per head, and the pre
@@ -2063,27 +1578,14 @@ bool bwd2_ok(const dgppo_gnn_attn_args* p) {
   if (p->xa == nullptr) return p->dx == nullptr && p->D <= 32;
   if (p->D0 > kD0) return false;
   if (p->pre_W && p->D > 32) return false;
-  return bwd2::lds_floats<32>(p->n_agents, p->D) * sizeof(float) <= 160 * 1024;
-}
-
-// the register form (default) or the LDS-staged kernel (DGPPO_ATTN_BWD2=lds)
-static bool bwd2_reg() {
-  static const bool reg = [] {
-    const char* e = getenv("DGPPO_ATTN_BWD2");
-    return !(e && strcmp(e, "lds") == 0);
-  }();
-  return reg;
+  return bwd2r::lds_floats<32>(p->n_agents, p->D) * sizeof(float) <= 160 * 1024;
 }
 
 int64_t bwd2_grid(const dgppo_gnn_attn_args* p, int64_t* nblk) {
-  // persistent-grid cap (A/B knob DGPPO_BWD2_BLOCKS): the resident workgroups of the chosen kernel, 3 per CU
-  // for the register form (42 KB of LDS, 3 waves per SIMD), 4 per CU for the LDS form
-  static const int64_t knob = [] {
-    const char* e = getenv("DGPPO_BWD2_BLOCKS");
-    return e ? (int64_t)atoi(e) : (int64_t)0;
-  }();
+  // persistent-grid cap: the resident workgroups, 3 per CU for the DM = 32 instantiation (47.7 KB of LDS, 3 waves per
+  // SIMD), 6 per CU for the narrower ones (512 / 2048 / 4096 measured no different)
   const bool wide = p->D > 16 || (p->xa && p->pre_W);  // the DM = 32 instantiation
-  const int64_t cap = knob > 0 ? knob : (bwd2_reg() ? (wide ? 768 : 1536) : (int64_t)bwd2::kMaxBlocks);
+  const int64_t cap = wide ? 768 : 1536;
   const int gpb = bwd2::kRows / p->n_agents;
   *nblk = (p->G + gpb - 1) / gpb;
   return *nblk < cap ? *nblk : cap;
@@ -2094,28 +1596,15 @@ void bwd2_launch(const dgppo_gnn_attn_args* p, hipStream_t s) {
   const unsigned grid = (unsigned)bwd2_grid(p, &nblk);
   const bool no_pre = !(p->xa && p->pre_W);
   const int v = p->D <= 8 && no_pre ? 0 : (p->D <= 16 && no_pre ? 1 : 2);  // DM 8 / 16 / 32
-  if (bwd2_reg()) {
-    const size_t bytes = (v == 0   ? bwd2r::lds_floats<8>(p->n_agents, p->D)
-                          : v == 1 ? bwd2r::lds_floats<16>(p->n_agents, p->D)
-                                   : bwd2r::lds_floats<32>(p->n_agents, p->D)) *
-                         sizeof(float);
-    const void* fn = v == 0 ? (const void*)attn_bwd2r_kernel<8>
-                            : (v == 1 ? (const void*)attn_bwd2r_kernel<16> : (const void*)attn_bwd2r_kernel<32>);
-    if (bytes > 64 * 1024) allow_lds(fn);
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(dgppo_gnn_attn_args, int64_t)>(const_cast<void*>(fn)), dim3(grid),
-                       dim3(256), bytes, s, *p, nblk);
-    return;
-  }
-  const size_t bytes = (v == 0   ? bwd2::lds_floats<8>(p->n_agents, p->D)
-                        : v == 1 ? bwd2::lds_floats<16>(p->n_agents, p->D)
-                                 : bwd2::lds_floats<32>(p->n_agents, p->D)) *
+  const size_t bytes = (v == 0   ? bwd2r::lds_floats<8>(p->n_agents, p->D)
+                        : v == 1 ? bwd2r::lds_floats<16>(p->n_agents, p->D)
+                                 : bwd2r::lds_floats<32>(p->n_agents, p->D)) *
                        sizeof(float);
-  const void* fn = v == 0 ? (const void*)attn_bwd2_kernel<8>
-                          : (v == 1 ? (const void*)attn_bwd2_kernel<16> : (const void*)attn_bwd2_kernel<32>);
+  const void* fn = v == 0 ? (const void*)attn_bwd2r_kernel<8>
+                          : (v == 1 ? (const void*)attn_bwd2r_kernel<16> : (const void*)attn_bwd2r_kernel<32>);
   if (bytes > 64 * 1024) allow_lds(fn);
-  if (v == 0) hipLaunchKernelGGL(attn_bwd2_kernel<8>, dim3(grid), dim3(256), bytes, s, *p, nblk);
-  else if (v == 1) hipLaunchKernelGGL(attn_bwd2_kernel<16>, dim3(grid), dim3(256), bytes, s, *p, nblk);
-  else hipLaunchKernelGGL(attn_bwd2_kernel<32>, dim3(grid), dim3(256), bytes, s, *p, nblk);
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(dgppo_gnn_attn_args, int64_t)>(const_cast<void*>(fn)), dim3(grid),
+                     dim3(256), bytes, s, *p, nblk);
 }
 
 struct Plan {

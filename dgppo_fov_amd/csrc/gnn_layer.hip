@@ -65,24 +65,13 @@ __device__ __forceinline__ void stage_copy(float* dst, int total, int tid, Ld ld
 
 struct Carve {
   // float offsets: node rows at 0 | raw rows / xcat tile | qt rows | pre_W, pre_b | Y tile (zmean, tail) | tail
-  // carries [16][kYP] | tail LayerNorm parameters [4][64] | per-wave pair weights [4][64] float4 (LDS-loop sums)
-  int rx, qt, pre, yt, hb, lnp, pa;
+  // carries [16][kYP] | tail LayerNorm parameters [4][64]
+  int rx, qt, pre, yt, hb, lnp;
   int floats;
 };
 
-// weighted sums xbar_h = sum_c a_hc x_c (and the backward's dqt) by an LDS loop over the candidates (one lane per
-// output column) instead of transposed DPP reductions: DGPPO_LAYER_WSUM=lds|dpp.  Default dpp: the LDS loop measured
-// slower (forward 241 vs 216 us per D = 32 call, backward 690 vs 668 us)
-static bool wsum_lds() {
-  static const bool v = [] {
-    const char* e = getenv("DGPPO_LAYER_WSUM");
-    return e && e[0] == 'l';
-  }();
-  return v;
-}
-
 template <int DM>
-Carve carve(int gpb, int N, bool agent, bool ytile, bool tail, bool wsl = wsum_lds()) {
+Carve carve(int gpb, int N, bool agent, bool ytile, bool tail) {
   using L = Lay<DM>;
   Carve c;
   const int xs = gpb * N * L::XP;
@@ -99,9 +88,6 @@ Carve carve(int gpb, int N, bool agent, bool ytile, bool tail, bool wsl = wsum_l
   o += tail ? kRows * kYP : 0;
   c.lnp = tail ? o : 0;
   o += tail ? 4 * 64 : 0;
-  const bool pa_own = wsl && L::XCP < 128;  // else the pairs live in the xcat tile's rows
-  c.pa = pa_own ? o : 0;
-  o += pa_own ? 4 * 64 * 4 : 0;
   c.floats = o;
   return c;
 }
@@ -159,7 +145,7 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 #ifndef DGPPO_DIAG_FWD
 #define DGPPO_DIAG_FWD 0  // diagnostic builds only (time attribution, results invalid): 1 no staging loads, 2 no xbar
 #endif                    // reductions, 4 no [qt | beta] / message GEMMs, 8 no attn / xcat / qb stores
-template <int DM, bool TAIL, bool WSL>
+template <int DM, bool TAIL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 4, 8))) void gnn_layer_fwd_kernel(
     dgppo_gnn_layer_args p, int gpb, Carve cv) {
   const int o_rx = cv.rx, o_qt = cv.qt, o_pre = cv.pre;
@@ -343,32 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 3 : 
       }
       float* o = (a.xcat && !(DGPPO_DIAG_FWD & 8)) ? a.xcat + row * WX : nullptr;
       float* ot = xc + rl * XCP;
-      if constexpr (WSL) {
-        // xbar_h[d] = sum_c a_hc x_c[d]: the row's (a, sender) pairs through the wave's LDS slots, lane c of the
-        // half-wave owns column d = c and walks the candidates (sender row reads: consecutive columns of one row)
-        // the half-wave's 32 slots: its own xcat row (written only after the loop) or, for narrow rows, a region
-        f32x4* pr = XCP >= 128 ? (f32x4*)ot : (f32x4*)(lds + cv.pa) + wave * 64 + slot * 32;
-        pr[c] = f32x4{aw[0], aw[1], aw[2], __int_as_float(ok ? gl * N + s : -1)};
-        lanes::wave_sync();
-        const int d = c < D ? c : 0;
-        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-#pragma unroll 8
-        for (int cc = 0; cc < 32; ++cc) {
-          if (cc < C) {
-            const f32x4 P = pr[cc];
-            const int node = __float_as_int(P[3]);
-            const float xv = node >= 0 ? xs[node * XP + d] : 0.0f;
-            s0 += P[0] * xv;
-            s1 += P[1] * xv;
-            s2 += P[2] * xv;
-          }
-        }
-        if (active && c < D) {
-          ot[c] = s0, ot[D + c] = s1, ot[2 * D + c] = s2;
-          if (o) o[c] = s0, o[D + c] = s1, o[2 * D + c] = s2;
-        }
-        lanes::wave_sync();  // the slots are rewritten next sub-round
-      } else {
+      {  // xbar_h = sum_c a_hc x_c by transposed DPP reductions (an LDS loop over the candidates measured slower)
 #pragma unroll
         for (int h = 0; h < ((DGPPO_DIAG_FWD & 2) ? 0 : kH); ++h) {
           float v[DM];
@@ -580,22 +541,15 @@ extern "C" int dgppo_gnn_layer_fwd(const dgppo_gnn_layer_args* p, void* stream) 
   const int gpb = kRows / a.n_agents;
   const unsigned grid = (unsigned)((a.G + gpb - 1) / gpb);
   hipStream_t s = (hipStream_t)stream;
-  const bool yt = p->zmean != nullptr, tail = p->tail.on != 0, wsl = wsum_lds();
+  const bool yt = p->zmean != nullptr, tail = p->tail.on != 0;
   const size_t b32 = (size_t)carve<32>(gpb, a.N, true, yt, false).floats * sizeof(float);
   const size_t b8 = (size_t)carve<8>(gpb, a.N, false, yt, tail).floats * sizeof(float);
-#define GL_LAUNCH(DMv, TAILv, WSLv, bytes)                                                                        \
-  hipLaunchKernelGGL((gnn_layer_fwd_kernel<DMv, TAILv, WSLv>), dim3(grid), dim3(256), bytes, s, *p, gpb,          \
+#define GL_LAUNCH(DMv, TAILv, bytes)                                                                               \
+  hipLaunchKernelGGL((gnn_layer_fwd_kernel<DMv, TAILv>), dim3(grid), dim3(256), bytes, s, *p, gpb,                  \
                      carve<DMv>(gpb, a.N, DMv == 32, yt, TAILv))
-  if (a.xa) {
-    if (wsl) GL_LAUNCH(32, false, true, b32);
-    else GL_LAUNCH(32, false, false, b32);
-  } else if (tail) {
-    if (wsl) GL_LAUNCH(8, true, true, b8);
-    else GL_LAUNCH(8, true, false, b8);
-  } else {
-    if (wsl) GL_LAUNCH(8, false, true, b8);
-    else GL_LAUNCH(8, false, false, b8);
-  }
+  if (a.xa) GL_LAUNCH(32, false, b32);
+  else if (tail) GL_LAUNCH(8, true, b8);
+  else GL_LAUNCH(8, false, b8);
 #undef GL_LAUNCH
   return (int)hipGetLastError();
 }

@@ -175,28 +175,6 @@ __device__ __forceinline__ void acc_store(const f32x4 (&acc)[CT][kRT], float* ds
   }
 }
 
-// one GraphTransformer layer's operands: [QT | beta] (K = D), Wcat (K = 3 (D + 5)), Wex (K = 3 EX, the
-// edge columns past 4; rows read as 0 without them), Wu (K = D)
-template <int KQ, int KC, int KX, int KU>
-struct LayerW {
-  Frag<KQ, 2> qk;
-  Frag<KC, 1> wc;
-  Frag<KX, 1> wx;
-  Frag<KU, 1> wu;
-  float bqk[2], bu[1];
-};
-
-template <int KQ, int KC, int KX, int KU>
-__device__ __forceinline__ void layer_load(LayerW<KQ, KC, KX, KU>& w, const dgppo_gt_layer& ly, const float* qk,
-                                           int EX) {
-  frag_load(w.qk, qk, kQKCols, ly.D);
-  frag_load(w.wc, ly.Wcat, ly.F, kHeads * (ly.D + 5));
-  frag_load(w.wx, ly.Wex, ly.F, EX > 0 ? kHeads * EX : 0);
-  frag_load(w.wu, ly.Wu, ly.F, ly.D);
-  bias_load(w.bqk, qk + 32 * kQKCols, kQKCols);
-  bias_load(w.bu, ly.bu, ly.F);
-}
-
 // layer-1 features relu(x_raw Wu0 + bu0) of a workgroup's never-receiving nodes, computed once per node (MFMA) into
 // LDS when the group has at most kPreMax of them (LidarSpread n = 8: 2 graphs x 73 nodes); rows of 32 floats, each
 // row's float4 quads stored XOR-swizzled by (row & 7) so that lanes reading different rows spread over the banks
@@ -207,12 +185,11 @@ struct Lds {
   float* hb;          // aliases att: the carries are written there after the GNN
 };
 
-constexpr int kAttPerWave = 2 * kCP * (kXSP + 4);
 // the register form's att region only hosts the pair tables (before the GNN) and the carries (after it)
 constexpr int kAttReg = kRowsG * kYP > 2 * kRowsG * kCP ? kRowsG * kYP : 2 * kRowsG * kCP;
-constexpr size_t lds_floats(bool reg) {
+constexpr size_t lds_floats() {
   return (size_t)kRowsG * (kX0P + kQTP + kXCP + kY0P + kYP) + kMaxD0 * 32 + 32 + 4 * kHid + 2 * kHid * 4 + 8 +
-         (reg ? kAttReg + kPreMax * 32 : 4 * kAttPerWave);
+         kAttReg + kPreMax * 32;
 }
 
 __device__ __forceinline__ Lds carve(float* base) {
@@ -293,166 +270,7 @@ __device__ __forceinline__ void pair_gather(const dgppo_policy_step_args& p, con
   for (int k = 0; k < MD0; ++k) o.xr[k] = (ok && k < p.D0) ? xr[k] : 0.0f;
 }
 
-// One GraphTransformer layer for the group's rows: A (32 x D, LDS) = this layer's agent rows;
-// senders: agents -> A rows of the same graph (layer 1) or their raw rows (layer 0); others -> raw
-// node rows (layer 0) or relu(raw Wu0 + bu0) (layer 1, agent mode).  Output relu(M/H + A Wu + bu)
-// into out (kRowsG x F).  pg[k] = the lane's pair of sub-round k (rows 2 wave + 8 k + (lane >> 5)).
-template <int MD0, int MEX, int KQ, int KC, int KX, int KU>
-__device__ __forceinline__ void gt_layer(const dgppo_policy_step_args& p, const dgppo_gt_layer& ly,
-                                         const LayerW<KQ, KC, KX, KU>& w, const PairG<MD0, MEX> (&pg)[kSR], const Lds& L,
-                                         const float* A, int lda, bool layer0, float* out, int ldo, int nmag,
-                                         int pk) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int n = p.n_agents, D = ly.D, F = ly.F, H = kHeads;
-  // [QT_h | beta_h] = A QK + qk_bias (kRowsG x 100)
-  {
-    f32x4 acc[2][kRT];
-    acc_zero(acc);
-    frag_mma(acc, A, lda, D, w.qk);
-    acc_store(acc, L.qt, kQTP, kQKCols, w.bqk, 1.0f, false);
-  }
-  // pre-transform operands (layer 1): B[k][d] = Wu0[k][d], k = 4 ks + kq, d = 16 ct + i16
-  constexpr int kPK = MD0 / 4;
-  const int EX = MEX > 0 ? p.ED - 4 : 0;
-  float pw[kPK][2], pb[2];
-#pragma unroll
-  for (int ks = 0; ks < kPK; ++ks)
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) pw[ks][ct] = layer0 ? 0.0f : L.preW[(4 * ks + kq) * 32 + 16 * ct + i16];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) pb[ct] = layer0 ? 0.0f : L.preb[16 * ct + i16];
-  __syncthreads();
-  PROBE(pk);
-  // attention: each wave two rows (32-lane groups) per sub-round
-  float* xs = L.att + wave * kAttPerWave;  // [64 pairs][kXSP]: x (cols 0..31), edge feats (32..35)
-  float* aa = xs + 2 * kCP * kXSP;         // [64 pairs][4]: attention weights
-  const int slot = lane >> 5, c = lane & 31;
-  const int pr = slot * kCP + c;
-  float* xp = xs + pr * kXSP;
-  const float scale = rsqrtf((float)F);
-  const int TQ = (D + 3) >> 2, Th = TQ + 2;
-  // rolled loop (keeps the code small); the sub-round's pair is selected out of the registers
-#pragma unroll 1
-  for (int sr = 0; sr < kSR; ++sr) {
-    PairG<MD0, MEX> cur;
-    pair_pick(pg, sr, cur);
-    const int r = 2 * wave + 8 * sr + slot;
-    const bool ok = cur.s >= 0;
-#pragma unroll
-    for (int k = 0; k < MD0; ++k) xp[k] = cur.xr[k];
-    if (!layer0) {
-      wave_sync();
-      // relu(x_raw Wu0 + bu0) for the wave's 64 pairs: 4 row tiles x 2 column tiles x 2 k-steps
-      float a[4][kPK];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ks = 0; ks < kPK; ++ks) a[t][ks] = xs[(16 * t + i16) * kXSP + 4 * ks + kq];
-      f32x4 pacc[4][2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          pacc[t][ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int ks = 0; ks < kPK; ++ks)
-            pacc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][ks], pw[ks][ct], pacc[t][ct], 0, 0, 0);
-        }
-      wave_sync();
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float v = pacc[t][ct][i] + pb[ct];
-            xs[(16 * t + 4 * kq + i) * kXSP + 16 * ct + i16] = v > 0.0f ? v : 0.0f;
-          }
-      wave_sync();
-      if (ok && cur.s < n) {  // agent sender: the layer input row of the same graph
-        const f32x4* src = (const f32x4*)(A + (div_n(r, nmag) * n + cur.s) * lda);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) ((f32x4*)xp)[q] = src[q];
-      }
-    }
-    *(f32x4*)(xp + 32) = cur.ef;
-#pragma unroll
-    for (int j = 0; j < MEX; ++j) xp[36 + j] = cur.ex[j];
-    wave_sync();
-    // logits (QT_h . x + beta_h) / sqrt(F) and the softmax over the row's 32 candidates
-    const float* qt = L.qt + r * kQTP;
-    float aw[kHeads];
-#pragma unroll
-    for (int h = 0; h < kHeads; ++h) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (q < TQ) {
-          const f32x4 xv = ((const f32x4*)xp)[q], qv = ((const f32x4*)(qt + 32 * h))[q];
-          acc += xv[0] * qv[0] + xv[1] * qv[1] + xv[2] * qv[2] + xv[3] * qv[3];
-        }
-      const float lg = ok ? (acc + qt[96 + h]) * scale : -INFINITY;
-      const float mx = gmax32(lg);
-      const float ex = ok ? expf(lg - mx) : 0.0f;
-      const float sm = gsum32(ex);
-      aw[h] = ok ? ex / sm : 0.0f;
-    }
-#pragma unroll
-    for (int h = 0; h < kHeads; ++h) aa[pr * 4 + h] = aw[h];
-    wave_sync();
-    // xcat row = [xbar_h (D each) | ebar_h (4 each) | sig_h | ebar_x_h (EX each)]: lane tasks (head, float4
-    // column block), a second pass when they outnumber the row's 32 lanes (wide edges)
-    const int EXQ = (EX + 3) >> 2, Tw = Th + EXQ;
-    for (int task = c; task < H * Tw; task += 32) {
-      const int h = task / Tw, q = task - h * Tw;
-      const float* xb = xs + slot * kCP * kXSP;
-      const float* ab = aa + slot * kCP * 4 + h;
-      float* o = L.xc + r * kXCP;
-      if (q == TQ + 1) {
-        float acc = 0.0f;
-#pragma unroll 8
-        for (int cc = 0; cc < kCP; ++cc) acc += ab[cc * 4];
-        o[H * D + 4 * H + h] = acc;
-      } else {
-        const int col = q < TQ ? 4 * q : (q == TQ ? 32 : 36 + 4 * (q - TQ - 2));
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 8
-        for (int cc = 0; cc < kCP; ++cc) acc += ab[cc * 4] * *(const f32x4*)(xb + cc * kXSP + col);
-        if (q < TQ) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * q + j < D) o[h * D + 4 * q + j] = acc[j];
-        } else if (q == TQ) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[H * D + 4 * h + j] = acc[j];
-        } else {
-          const int j0 = 4 * (q - TQ - 2);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (j0 + j < EX) o[H * (D + 5) + h * EX + j0 + j] = acc[j];
-        }
-      }
-    }
-    wave_sync();
-  }
-  __syncthreads();
-  PROBE(pk + 1);
-  // out = relu(xcat Wcat / H + A Wu + bu)
-  {
-    f32x4 acc[1][kRT];
-    acc_zero(acc);
-    frag_mma(acc, L.xc, kXCP, H * (D + 5), w.wc);
-    if (EX > 0) frag_mma(acc, L.xc + H * (D + 5), kXCP, H * EX, w.wx);
-#pragma unroll
-    for (int rt = 0; rt < kRT; ++rt) acc[0][rt] *= 1.0f / H;
-    frag_mma(acc, A, lda, D, w.wu);
-    acc_store(acc, out, ldo, F, w.bu, 1.0f, true);
-  }
-  __syncthreads();
-}
-
-// Register form of the same layer (the default): a lane's pair keeps its sender row x in registers
+// One GraphTransformer layer for the group's rows (register form; round 6 removed the LDS-staged form): a lane's pair keeps its sender row x in registers
 // (layer 0: the raw row; layer 1: relu(x_raw Wu0 + bu0) by VALU FMAs against the LDS-resident Wu0, or
 // the agent's layer-0 output row from LDS), the logits are lane-local dots against the row's QT_h, and
 // the attention-weighted sums over the row's 32 candidates -- [xbar_h | ebar_h | sig_h | ebar_x_h] --
@@ -655,8 +473,8 @@ __device__ __forceinline__ void ln_relu64(float* Y, const float* scale, const fl
 // NP: the per-node layer-1 pre-transform table (narrow register form, two layers, <= kPreMax never-receiving nodes
 // per group: the host picks this instantiation, node_pre_ok); its own instantiation, so that the raw sender rows die
 // after layer 0 instead of staying live through layer 1 for the per-lane fallback
-template <int MD0, int MEX, bool REG, bool NP = false>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG && MD0 <= kNarrowD0 ? kRegWaves : 1, 8))) void policy_step_kernel(dgppo_policy_step_args p) {
+template <int MD0, int MEX, bool NP = false>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MD0 <= kNarrowD0 ? kRegWaves : 1, 8))) void policy_step_kernel(dgppo_policy_step_args p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Lds L = carve(lds);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -720,7 +538,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
   // xcat region (free until layer 0's attention) for the per-node layer-1 pre-transform
   constexpr int kPreLd = kPreMax * kNarrowD0 / kThreads;
   const int nnr = p.N - n;
-  constexpr bool node_pre = NP && REG && MD0 <= kNarrowD0;
+  constexpr bool node_pre = NP && MD0 <= kNarrowD0;
   float prv[kPreLd];
   if constexpr (node_pre) {
 #pragma unroll
@@ -784,7 +602,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
   __syncthreads();  // the pair tables alias the attention scratch
   PROBE(1);
   // ---- GNN
-  if (REG) {
+  {
     constexpr int KX = MEX > 0 ? (kHeads * MEX + 3) / 4 : 1;
     gt_layer_reg<MD0, true, MD0, MEX, (MD0 + 3) / 4, (kHeads * (MD0 + 5) + 3) / 4, KX, (MD0 + 3) / 4>(
         p, p.layer[0], pg, L, p.work, L.x0, kX0P, two ? L.y0 : L.yb, two ? kY0P : kYP, nmag, 2);
@@ -795,24 +613,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
       PROBE(7);
     }
   }
-#pragma unroll 1
-  for (int l = 0; l < (REG ? 0 : p.n_layers); ++l) {
-    const bool last = l == p.n_layers - 1;
-    const dgppo_gt_layer& ly = l == 0 ? p.layer[0] : p.layer[1];
-    // one operand shape for both layers (layer 0's extra k-steps read as zeros): one copy of the code
-    LayerW<8, 28, (MEX > 0 ? 5 : 1), 8> w;
-    layer_load(w, ly, p.work + l * kQKStride, p.ED - 4);
-    gt_layer(p, ly, w, pg, L, l == 0 ? L.x0 : L.y0, l == 0 ? kX0P : kY0P, l == 0, last ? L.yb : L.y0,
-             last ? kYP : kY0P, nmag, 2 + 3 * l);
-    PROBE(4 + 3 * l);
-  }
 #pragma unroll
   for (int u = 0; u < kHT; ++u) {
     const int e = threadIdx.x + u * kThreads;
     L.hb[(e / kHid) * kYP + e % kHid] = hreg[u];
   }
   // head / GRU / ScaleHid operands: loaded after the GNN (holding them through the attention would
-  // spill).  LDS form: all in flight at once; register form: each loaded one phase ahead of its GEMM
+  // spill); each loaded one phase ahead of its GEMM
   // (fi during the second head layer, fh after gi, fs during the gate math) so that at most ~100
   // registers of fragments are live and the kernel fits 3-4 waves per SIMD
   Frag<16, 1> fh0, fh1, fs;
@@ -820,11 +627,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
   float bh0[1], bh1[1], bs[1], bi[3], bhn[1];
   frag_load(fh0, p.head_W0, kHid, kHid);
   frag_load(fh1, p.head_W1, kHid, kHid);
-  if (!REG) {
-    frag_load(fi, p.gru_Wi, 3 * kHid, kHid);
-    frag_load(fh, p.gru_Wh, 3 * kHid, kHid);
-    frag_load(fs, p.Ws, kHid, kHid);
-  }
   bias_load(bh0, p.head_b0, kHid);
   bias_load(bh1, p.head_b1, kHid);
   bias_load(bi, p.gru_bi, 3 * kHid);
@@ -841,7 +643,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
     __syncthreads();
     ln_relu64(L.yb, L.lnp, L.lnp + kHid);
     __syncthreads();
-    if (REG) frag_load(fi, p.gru_Wi, 3 * kHid, kHid);
+    frag_load(fi, p.gru_Wi, 3 * kHid, kHid);
     acc_zero(acc);
     frag_mma(acc, L.yb, kYP, kHid, fh1);
     __syncthreads();
@@ -857,9 +659,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(REG &&
     acc_zero(gi);
     acc_zero(gh);
     frag_mma(gi, L.yb, kYP, kHid, fi);
-    if (REG) frag_load(fh, p.gru_Wh, 3 * kHid, kHid);
+    frag_load(fh, p.gru_Wh, 3 * kHid, kHid);
     frag_mma(gh, L.hb, kYP, kHid, fh);
-    if (REG) frag_load(fs, p.Ws, kHid, kHid);
+    frag_load(fs, p.Ws, kHid, kHid);
     const int col = wave * 16 + i16;
     float hn[kRT][4];
 #pragma unroll
@@ -968,7 +770,7 @@ __global__ __launch_bounds__(256) void policy_prepare_kernel(dgppo_policy_step_a
   p.work[(int64_t)l * kQKStride + idx] = v;
 }
 
-size_t lds_bytes(bool reg) { return lds_floats(reg) * sizeof(float); }
+size_t lds_bytes() { return lds_floats() * sizeof(float); }
 
 }  // namespace
 }  // namespace dgppo
@@ -1006,25 +808,16 @@ extern "C" int dgppo_policy_step(const dgppo_policy_step_args* p, void* stream) 
   if (ngroups > INT32_MAX) return DGPPO_EINVAL;
   const int64_t grid = ngroups;
   const bool wide = p->D0 > dgppo::kNarrowD0 || p->ED > 4;
-  // DGPPO_POLICY_ATTN=lds selects the LDS-staged attention (A/B); default: the register form
-  static const bool reg = [] {
-    const char* e = getenv("DGPPO_POLICY_ATTN");
-    return !(e && strcmp(e, "lds") == 0);
-  }();
-  const bool np = !wide && reg && p->n_layers == 2 && (int64_t)gpg * (p->N - p->n_agents) <= dgppo::kPreMax;
-  const void* fn = wide ? (reg ? (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, true>
-                               : (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, false>)
-                        : (np ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true, true>
-                              : reg ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>
-                                    : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>);
-  const size_t bytes = dgppo::lds_bytes(reg);
+  const bool np = !wide && p->n_layers == 2 && (int64_t)gpg * (p->N - p->n_agents) <= dgppo::kPreMax;
+  const void* fn = wide ? (const void*)dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX>
+                        : (np ? (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>
+                              : (const void*)dgppo::policy_step_kernel<dgppo::kNarrowD0, 0>);
+  const size_t bytes = dgppo::lds_bytes();
   if (bytes > 64 * 1024) dgppo::allow_lds(fn);
   const dim3 g((unsigned)grid), b(dgppo::kThreads);
   const hipStream_t s = (hipStream_t)stream;
-  if (wide && reg) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, true>), g, b, bytes, s, *p);
-  else if (wide) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX, false>), g, b, bytes, s, *p);
-  else if (np) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true, true>), g, b, bytes, s, *p);
-  else if (reg) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>), g, b, bytes, s, *p);
-  else hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, false>), g, b, bytes, s, *p);
+  if (wide) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kMaxD0, dgppo::kMaxEX>), g, b, bytes, s, *p);
+  else if (np) hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0, true>), g, b, bytes, s, *p);
+  else hipLaunchKernelGGL((dgppo::policy_step_kernel<dgppo::kNarrowD0, 0>), g, b, bytes, s, *p);
   return (int)hipGetLastError();
 }

@@ -1,6 +1,5 @@
 """Per-call time of the fused policy step (ActorNet.act, mode 1) for LidarSpread n=8 obs=3 at B envs:
-HIP events around 50 back-to-back calls on the current stream.  DGPPO_POLICY_ATTN=lds selects the
-LDS-staged attention; DGPPO_HIP_LIB another build (e.g. lib/libdgppo_hip_w3.so)."""
+HIP events around 50 back-to-back calls on the current stream.  DGPPO_HIP_LIB selects another build (e.g. lib/libdgppo_hip_w3.so)."""
 import json
 import os
 import sys
@@ -41,7 +40,7 @@ def main():
         ts.append(e0.elapsed_time(e1) / 50 * 1e3)
     a, lp, h2 = algo.actor.act(gb, h, 1, noise=noise, h_out=hout, prepare=False)
     torch.cuda.synchronize()
-    print(json.dumps({"env": eid, "n": n, "B": B, "attn": os.environ.get("DGPPO_POLICY_ATTN", "reg"),
+    print(json.dumps({"env": eid, "n": n, "B": B, "attn": "reg",
                       "lib": os.path.basename(os.environ.get("DGPPO_HIP_LIB", "libdgppo_hip.so")),
                       "act_us_median": round(sorted(ts)[2], 2), "act_us_all": [round(t, 2) for t in ts],
                       "checksum": [float(a.double().sum()), float(lp.double().sum()), float(h2.double().sum())]}))

@@ -1,5 +1,5 @@
 """Median DGPPO update time at the bench config (LidarSpread n8 o3, 4096 envs x 128 steps, batch 16384 -> 32
-minibatches) after two warm-up updates; knobs come from the environment (DGPPO_FUSE_LN, DGPPO_ATTN_GM, ...).
+minibatches) after two warm-up updates; knobs come from the environment (DGPPO_FUSE_LN, DGPPO_FUSED_LAYER, ...).
 Prints one JSON line.  --envs / --batch select other shares (e.g. --envs 512 --batch 2048: config 4's per-rank
 plan), --env / -n / --obs other configs."""
 import argparse
