@@ -227,6 +227,61 @@ __device__ __forceinline__ void write_graph(const dgppo_env_cfg& cfg, const D& d
   }
   // edges: [agent-agent n*n][agent-goal][agent-lidar n*k | agent-obstacle n*O]
   const int n_aa = n * n;
+  // Lidar double-integrator rows (SD = 4) with nthr a multiple of n (the n = 32 block kernel): a thread's sender
+  // column j = tid % n is the same in every agent-agent / agent-goal iteration, so its agent and goal rows stay in
+  // registers as float4s and each edge reads only the receiver's row (one broadcast float4 per wave and half-wave)
+  // instead of eight scalar LDS reads; receiver i advances by nthr / n without a division.  Same arithmetic.
+  if (SD == 4 && ENGINE != DGPPO_ENGINE_BICYCLE && !mpe && edges_vec4 && nthr % n == 0) {
+    const int j = tid % n, di = nthr / n;
+    float4* eo4 = reinterpret_cast<float4*>(out.edges);
+    {
+      const float4 sj = *reinterpret_cast<const float4*>(nxt + j * SD);
+#pragma unroll 1
+      for (int i = tid / n; i < n; i += di) {
+        const float4 si = *reinterpret_cast<const float4*>(nxt + i * SD);
+        const int e = i * n + j;
+        const float d2 = sq2(si.x - sj.x, si.y - sj.y);
+        const bool m = i == j ? ((d2 == 0.0f) & (cfg.c_self_dist < comm)) : (d2 < cfg.t2_comm);
+        eo4[e] = make_float4(si.x - sj.x, si.y - sj.y, si.z - sj.z, si.w - sj.w);
+        out.recv[e] = m ? i : pad;
+        out.send[e] = m ? j : pad;
+      }
+    }
+    if (GOAL == DGPPO_GOAL_SPREAD) {
+      const float4 gj = *reinterpret_cast<const float4*>(goal + j * SD);
+#pragma unroll 1
+      for (int i = tid / n; i < n; i += di) {
+        const float4 si = *reinterpret_cast<const float4*>(nxt + i * SD);
+        const int eg = n_aa + i * n + j;
+        eo4[eg] = make_float4(si.x - gj.x, si.y - gj.y, si.z - gj.z, si.w - gj.w);
+        out.recv[eg] = i;
+        out.send[eg] = n + j;
+      }
+    }
+    if (GOAL != DGPPO_GOAL_SPREAD) {
+#pragma unroll 1
+      for (int q = tid; q < n; q += nthr) {
+        const float4 si = *reinterpret_cast<const float4*>(nxt + q * SD);
+        const float4 gq = *reinterpret_cast<const float4*>(goal + q * SD);
+        eo4[n_aa + q] = make_float4(si.x - gq.x, si.y - gq.y, si.z - gq.z, si.w - gq.w);
+        out.recv[n_aa + q] = q;
+        out.send[n_aa + q] = n + q;
+      }
+    }
+#pragma unroll 1
+    for (int q = tid; q < n_third; q += nthr) {  // agent-lidar blocks (1, k) per agent
+      const int i = q / k;
+      const float2 si = *reinterpret_cast<const float2*>(nxt + i * SD);
+      const float2 hq = *reinterpret_cast<const float2*>(third + 2 * q);
+      const float f0 = si.x - hq.x, f1 = si.y - hq.y;
+      const bool m = sq2(f0, f1) < cfg.t2_lidar;
+      const int e = n_aa + n_ag + q;
+      eo4[e] = make_float4(f0, f1, 0.0f, 0.0f);
+      out.recv[e] = m ? i : pad;
+      out.send[e] = m ? 2 * n + q : pad;
+    }
+    return;
+  }
 #pragma unroll 1
   for (int e = tid; e < E; e += nthr) {
     float f0, f1, f2, f3;
@@ -929,8 +984,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(dgppo_env_cfg cfg, dgpp
 // workgroup, step t reading graph t's rows from LDS (graph 0 from HBM) and writing graph t + 1 into the
 // time-major (T + 1) buffers, reward[t], cost[t] -- the same arithmetic as T per-step launches, without their
 // launch floor and their re-reads of every graph.
+// (n = 32: at most 128 VGPRs, so the 1024 envs of BASELINE config 5's share are resident in one round, 4 per CU)
 template <int ENGINE, int GOAL, int SD, int BLOCK, int NA, int NO, int NR, int NK>
-__global__ __launch_bounds__(BLOCK) void env_rollout_block_kernel(dgppo_env_cfg cfg, dgppo_env_rollout_io r,
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NA == 32 ? 4 : 1, 8))) void env_rollout_block_kernel(dgppo_env_cfg cfg, dgppo_env_rollout_io r,
                                                                    int stage_acts) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool mpe = ENGINE == DGPPO_ENGINE_MPE;
