@@ -1,6 +1,6 @@
 """Vl (16-step sequences) and Vh (one GRU step per graph) forward + backward time of one DGPPO minibatch
-(LidarSpread n8, 16384 graphs) for A/B runs of kernel knobs set through the environment (e.g. DGPPO_BWD2_BLOCKS,
-the attention backward's persistent-grid cap) or of two library builds (DGPPO_HIP_LIB)."""
+(LidarSpread n8, 16384 graphs) for A/B runs of kernel knobs set through the environment (e.g. DGPPO_FUSE_LN,
+the LayerNorm epilogues) or of two library builds (DGPPO_HIP_LIB)."""
 import os
 import sys
 import time
